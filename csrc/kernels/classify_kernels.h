@@ -1,0 +1,249 @@
+// embed_pool: hashed-token embedding gather -> bf16 MFMA GEMM -> GELU ->
+// masked mean-pool per message (N4), plus the tiny classifier head.
+//
+// A NEW capability relative to the reference (which only has keyword regexes,
+// `internal/preprocessor/preprocessor.go:117-168`): a random-init priority /
+// sentiment / question classifier whose hot path is a gather + GEMM on the
+// matrix cores.
+//
+// Shapes: token rows are the batch's tokens compacted message-major
+// (row_off = exclusive scan of ntok), X[row] = E[hash & (V-1)] (D = 256 bf16),
+// Hid = GELU(X . W1^T + b1) (H = 1024), pooled[msg] = mean over the message's
+// rows.  W1 is stored transposed, W1t[H][D], so a B fragment is 16 contiguous
+// bytes of one W1t row.
+//
+// Tiling (gfx950): one 256-thread workgroup (4 waves) per 64-row tile.
+//   * the 64 x 256 bf16 A tile (32 KiB) is gathered ONCE into LDS with 16-byte
+//     loads; its 16-byte chunks are XOR-swizzled (chunk ^ (row & 15)) so the
+//     v_mfma_f32_16x16x32_bf16 A-fragment reads (16 rows x one chunk per lane
+//     group) are bank-conflict free for every ds_read_b128 lane group;
+//   * the tile stays resident while the 4 waves sweep H in 256-column chunks
+//     (64 columns per wave = 4x4 16x16 accumulators, K = 256 = 8 MFMA k-steps);
+//   * B fragments stream from L2 (W1t is 512 KiB, resident);
+//   * epilogue: bias + tanh-GELU into a 64 x 256 f32 LDS slab, then one thread
+//     per column walks the 64 rows, sums runs of equal message id and writes
+//     sum/ntok -- a plain store when the message lies wholly inside the tile,
+//     an f32 atomic add otherwise (pooled is zeroed before the launch).
+// Grid: ceil(rows_upper / 64) tiles; tiles past the device-side row total
+// exit immediately (rows_upper is a host bound from byte lengths).
+
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace llmq {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int EP_TM = 64;      // rows per tile
+constexpr int EP_D = 256;      // embedding dim (K)
+constexpr int EP_NCHUNK = 256; // columns per sweep step
+constexpr int EP_CHUNKS_PER_ROW = EP_D / 8;  // 16-byte chunks per A row
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t b) {
+  return __uint_as_float(((uint32_t)b) << 16);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float y = k0 * (x + k1 * x * x * x);
+  // tanh(y) = 1 - 2 / (exp(2y) + 1)
+  const float t = 1.0f - 2.0f / (__expf(2.0f * y) + 1.0f);
+  return 0.5f * x * (1.0f + t);
+}
+
+// Exclusive scan of ntok (stats[:, ST_NTOK], row stride `stride`) into
+// row_off[0..B]; single workgroup of 1024 threads.
+__global__ void __launch_bounds__(1024)
+scan_rows_kernel(const int32_t* __restrict__ ntok, int stride, int B, int32_t* __restrict__ row_off) {
+  __shared__ int32_t part[1024];
+  __shared__ int32_t carry;
+  const int t = threadIdx.x;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < B; base += 1024) {
+    const int i = base + t;
+    const int v = (i < B) ? ntok[(int64_t)i * stride] : 0;
+    part[t] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int x = (t >= off) ? part[t - off] : 0;
+      __syncthreads();
+      part[t] += x;
+      __syncthreads();
+    }
+    if (i < B) row_off[i] = carry + part[t] - v;
+    __syncthreads();
+    if (t == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (t == 0) row_off[B] = carry;
+}
+
+__global__ void __launch_bounds__(256)
+embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __restrict__ row_off,
+                  int B, const uint16_t* __restrict__ E, uint32_t vmask,
+                  const uint16_t* __restrict__ W1t, const float* __restrict__ b1, int H,
+                  float* __restrict__ pooled) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  uint16_t* At = reinterpret_cast<uint16_t*>(smem);                       // 64 x 256 bf16 (32 KiB)
+  float* Hs = reinterpret_cast<float*>(smem + EP_TM * EP_D * 2);          // 64 x 256 f32 (64 KiB)
+  int32_t* rmsg = reinterpret_cast<int32_t*>(smem + EP_TM * EP_D * 2 + EP_TM * EP_NCHUNK * 4);
+  int32_t* rinfo = rmsg + EP_TM;  // [0]=rows in tile
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int total = row_off[B];
+  const int tile0 = blockIdx.x * EP_TM;
+  if (tile0 >= total) return;  // uniform across the block
+  const int rows = min(EP_TM, total - tile0);
+
+  // ---- row -> (message, token) by binary search over row_off
+  if (tid < EP_TM) {
+    int m = -1;
+    const int g = tile0 + tid;
+    if (tid < rows) {
+      int lo = 0, hi = B - 1;
+      while (lo < hi) {  // largest m with row_off[m] <= g
+        const int mid = (lo + hi + 1) >> 1;
+        if (row_off[mid] <= g) lo = mid; else hi = mid - 1;
+      }
+      m = lo;
+    }
+    rmsg[tid] = m;
+  }
+  if (tid == 0) rinfo[0] = rows;
+  __syncthreads();
+
+  // ---- gather the A tile: 64 rows x 32 chunks of 16 B, swizzled chunk ^ (row & 15)
+  for (int c = tid; c < EP_TM * EP_CHUNKS_PER_ROW; c += 256) {
+    const int r = c / EP_CHUNKS_PER_ROW;
+    const int ch = c % EP_CHUNKS_PER_ROW;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    const int m = rmsg[r];
+    if (m >= 0) {
+      const int tok = tile0 + r - row_off[m];
+      const uint32_t bucket = hashes[(int64_t)m * L + tok] & vmask;
+      v = *reinterpret_cast<const uint4*>(E + (int64_t)bucket * EP_D + ch * 8);
+    }
+    const int pch = ch ^ (r & 15);
+    *reinterpret_cast<uint4*>(At + r * EP_D + pch * 8) = v;
+  }
+  __syncthreads();
+
+  const int fr = lane & 15;   // fragment row / col within a 16x16 tile
+  const int fq = lane >> 4;   // k-quarter (A/B), row-quad (C)
+
+  for (int n0 = 0; n0 < H; n0 += EP_NCHUNK) {
+    const int wc0 = n0 + wv * 64;  // this wave's 64 output columns
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 2
+    for (int ks = 0; ks < EP_D / 32; ++ks) {
+      bf16x8 bfrag[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = wc0 + j * 16 + fr;
+        bfrag[j] = *reinterpret_cast<const bf16x8*>(W1t + (int64_t)col * EP_D + ks * 32 + fq * 8);
+      }
+      bf16x8 afrag[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = i * 16 + fr;
+        const int ch = ks * 4 + fq;
+        afrag[i] = *reinterpret_cast<const bf16x8*>(At + r * EP_D + ((ch ^ (r & 15)) * 8));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[i], bfrag[j], acc[i][j], 0, 0, 0);
+    }
+
+    // ---- epilogue 1: bias + GELU into the f32 slab (C map: row = 4*fq + k, col = fr)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int lc = wv * 64 + j * 16 + fr;          // column within the 256-wide chunk
+      const float bias = b1[n0 + lc];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = i * 16 + fq * 4 + k;
+          Hs[r * EP_NCHUNK + lc] = gelu_tanh(acc[i][j][k] + bias);
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- epilogue 2: segmented mean over rows (one thread per column)
+    {
+      const int col = tid;  // 256 threads == 256 columns
+      float run = 0.f;
+      int cur = rmsg[0];
+      for (int r = 0; r < rows; ++r) {
+        const int m = rmsg[r];
+        if (m != cur) {
+          const int a = row_off[cur], b = row_off[cur + 1];
+          const float v = run / (float)(b - a);
+          float* dst = pooled + (int64_t)cur * H + n0 + col;
+          if (a >= tile0 && b <= tile0 + rows) *dst = v; else atomicAdd(dst, v);
+          run = 0.f;
+          cur = m;
+        }
+        run += Hs[r * EP_NCHUNK + col];
+      }
+      if (cur >= 0) {
+        const int a = row_off[cur], b = row_off[cur + 1];
+        const float v = run / (float)(b - a);
+        float* dst = pooled + (int64_t)cur * H + n0 + col;
+        if (a >= tile0 && b <= tile0 + rows) *dst = v; else atomicAdd(dst, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// logits[b, 0:8] = pooled[b] . W2 + b2 ; pred[b] = 1 + argmax(logits[b, 0:4])
+// One wave per message; lane l covers 16 hidden units.
+__global__ void __launch_bounds__(256)
+classify_head_kernel(const float* __restrict__ pooled, int B, int H, const float* __restrict__ W2,
+                     const float* __restrict__ b2, float* __restrict__ logits, int32_t* __restrict__ pred) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float part[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) part[o] = 0.f;
+  for (int h = lane; h < H; h += 64) {
+    const float x = pooled[(int64_t)b * H + h];
+    const float4 wa = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8);
+    const float4 wb = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8 + 4);
+    part[0] += x * wa.x; part[1] += x * wa.y; part[2] += x * wa.z; part[3] += x * wa.w;
+    part[4] += x * wb.x; part[5] += x * wb.y; part[6] += x * wb.z; part[7] += x * wb.w;
+  }
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) part[o] += __shfl_xor(part[o], off, 64);
+  }
+  if (lane == 0) {
+    int best = 0;
+    float bv = -3.4e38f;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      const float v = part[o] + b2[o];
+      logits[(int64_t)b * 8 + o] = v;
+      if (o < 4 && v > bv) { bv = v; best = o; }
+    }
+    pred[b] = best + 1;
+  }
+}
+
+}  // namespace llmq

@@ -1,0 +1,218 @@
+// pybind11 bindings for every HIP kernel of llm_message_queue_amd (gfx950).
+//
+// Python passes raw device pointers (tensor.data_ptr()) plus the HIP stream
+// handle (torch.cuda.current_stream().cuda_stream); shapes are re-validated
+// here before every launch so a bad call raises instead of faulting the GPU.
+
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "classify_kernels.h"
+#include "llama_kernels.h"
+#include "summarise_kernels.h"
+#include "text_kernels.h"
+
+namespace py = pybind11;
+using namespace llmq;
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(_e));       \
+  } while (0)
+
+template <typename T>
+static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void check_launch() { HIP_CHECK(hipGetLastError()); }
+
+static void require(bool cond, const char* what) {
+  if (!cond) throw std::invalid_argument(what);
+}
+
+// ---------------------------------------------------------------------- text
+static void text_analyze(uintptr_t bytes, uintptr_t offsets, int B, int L, py::bytes table,
+                         uintptr_t stats, uintptr_t hashes, uintptr_t stream) {
+  std::string t = table;
+  require(t.size() == sizeof(PatternTable), "pattern table size mismatch");
+  require(B >= 0 && L > 0, "bad B/L");
+  PatternTable pt;
+  std::memcpy(&pt, t.data(), sizeof(pt));
+  require(pt.npat >= 0 && pt.npat <= TA_MAX_PAT, "npat out of range");
+  for (int j = 0; j < pt.npat; ++j) {
+    require(pt.len[j] >= 1 && pt.len[j] <= 16, "pattern length out of range");
+    require(pt.slot[j] >= 0 && pt.slot[j] < TA_SLOTS, "pattern slot out of range");
+  }
+  if (B == 0) return;
+  const int grid = (B + TA_WAVES - 1) / TA_WAVES;
+  hipLaunchKernelGGL(text_analyze_kernel, dim3(grid), dim3(256), 0, S(stream), P<const uint8_t>(bytes),
+                     P<const int64_t>(offsets), B, L, pt, P<int32_t>(stats), P<uint32_t>(hashes));
+  check_launch();
+}
+
+static void scan_rows(uintptr_t ntok, int stride, int B, uintptr_t row_off, uintptr_t stream) {
+  require(B >= 0 && stride >= 1, "bad scan args");
+  hipLaunchKernelGGL(scan_rows_kernel, dim3(1), dim3(1024), 0, S(stream), P<const int32_t>(ntok), stride,
+                     B, P<int32_t>(row_off));
+  check_launch();
+}
+
+static bool g_embed_attr = false;
+static void embed_pool(uintptr_t hashes, int L, uintptr_t row_off, int B, int rows_upper, uintptr_t E,
+                       int V, uintptr_t W1t, uintptr_t b1, int H, uintptr_t pooled, uintptr_t stream) {
+  require(V > 0 && (V & (V - 1)) == 0, "vocab buckets must be a power of two");
+  require(H % EP_NCHUNK == 0, "hidden dim must be a multiple of 256");
+  require(B >= 0 && rows_upper >= 0, "bad sizes");
+  if (B == 0 || rows_upper == 0) return;
+  const size_t smem = EP_TM * EP_D * 2 + EP_TM * EP_NCHUNK * 4 + 2 * EP_TM * 4 + 16;
+  if (!g_embed_attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)embed_pool_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    g_embed_attr = true;
+  }
+  const int grid = (rows_upper + EP_TM - 1) / EP_TM;
+  hipLaunchKernelGGL(embed_pool_kernel, dim3(grid), dim3(256), smem, S(stream), P<const uint32_t>(hashes),
+                     L, P<const int32_t>(row_off), B, P<const uint16_t>(E), (uint32_t)(V - 1),
+                     P<const uint16_t>(W1t), P<const float>(b1), H, P<float>(pooled));
+  check_launch();
+}
+
+static void classify_head(uintptr_t pooled, int B, int H, uintptr_t W2, uintptr_t b2, uintptr_t logits,
+                          uintptr_t pred, uintptr_t stream) {
+  if (B == 0) return;
+  hipLaunchKernelGGL(classify_head_kernel, dim3((B + 3) / 4), dim3(256), 0, S(stream), P<const float>(pooled),
+                     B, H, P<const float>(W2), P<const float>(b2), P<float>(logits), P<int32_t>(pred));
+  check_launch();
+}
+
+// ---------------------------------------------------------------------- summarise
+static void summarise_project(uintptr_t pooled, uintptr_t seg_off, int C, uintptr_t Pt, float alpha,
+                              uintptr_t state, uintptr_t first_flag, int H, int DS, uintptr_t stream) {
+  require(H == SM_H && DS == SM_DS, "summarise expects H=1024, DS=256");
+  if (C == 0) return;
+  hipLaunchKernelGGL(summarise_project_kernel, dim3((C + SM_ROWS - 1) / SM_ROWS), dim3(256), 0, S(stream),
+                     P<const float>(pooled), P<const int32_t>(seg_off), C, P<const uint16_t>(Pt), alpha,
+                     P<float>(state), P<int32_t>(first_flag));
+  check_launch();
+}
+
+static void salient_topk(uintptr_t hashes, int L, uintptr_t ntok, int stride, uintptr_t seg_off, int C,
+                         uintptr_t stop, int nstop, int K, uintptr_t out_hash, uintptr_t out_cnt,
+                         uintptr_t stream) {
+  require(K >= 0 && K <= 64, "K out of range");
+  if (C == 0 || K == 0) return;
+  hipLaunchKernelGGL(salient_topk_kernel, dim3(C), dim3(256), 0, S(stream), P<const uint32_t>(hashes), L,
+                     P<const int32_t>(ntok), stride, P<const int32_t>(seg_off), P<const uint32_t>(stop),
+                     nstop, K, P<uint32_t>(out_hash), P<int32_t>(out_cnt));
+  check_launch();
+}
+
+// ---------------------------------------------------------------------- llama stub
+static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T, int D, float eps,
+                    uintptr_t stream) {
+  require(D % 2048 == 0 && D <= 8192, "rmsnorm expects D % 2048 == 0 and D <= 8192");
+  if (T == 0) return;
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3(T), dim3(256), 0, S(stream), P<const uint16_t>(x),
+                     res ? P<uint16_t>(res) : nullptr, P<const uint16_t>(w), P<uint16_t>(y), D, eps);
+  check_launch();
+}
+
+static void silu_mul(uintptr_t gu, uintptr_t out, int T, int F, uintptr_t stream) {
+  require(F % 8 == 0, "F must be a multiple of 8");
+  const int64_t total = (int64_t)T * F / 8;
+  if (total == 0) return;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream),
+                     P<const uint16_t>(gu), P<uint16_t>(out), T, F);
+  check_launch();
+}
+
+static void rope_kv(uintptr_t qkv, uintptr_t pos, uintptr_t slot, uintptr_t cos_t, uintptr_t sin_t, int T,
+                    int Hq, int Hkv, int max_ctx, uintptr_t q_out, uintptr_t kc, uintptr_t vc,
+                    uintptr_t stream) {
+  require(Hq % 4 == 0 && Hkv >= 1, "bad head counts");
+  if (T == 0) return;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, S(stream), P<const uint16_t>(qkv),
+                     P<const int32_t>(pos), P<const int32_t>(slot), P<const float>(cos_t),
+                     P<const float>(sin_t), Hq, Hkv, max_ctx, P<uint16_t>(q_out), P<uint16_t>(kc),
+                     P<uint16_t>(vc));
+  check_launch();
+}
+
+static void attention(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, uintptr_t slot, int T, int Hq,
+                      int Hkv, int max_ctx, float scale, uintptr_t out, uintptr_t stream) {
+  require(Hq % Hkv == 0 && Hq / Hkv <= 4, "attention expects a GQA group of <= 4 heads");
+  if (T == 0) return;
+  hipLaunchKernelGGL(attention_kernel, dim3(T * Hkv), dim3(256), 0, S(stream), P<const uint16_t>(q),
+                     P<const uint16_t>(kc), P<const uint16_t>(vc), P<const int32_t>(pos),
+                     P<const int32_t>(slot), Hq, Hkv, max_ctx, scale, P<uint16_t>(out));
+  check_launch();
+}
+
+// ---------------------------------------------------------------------- N9 slot page
+struct MappedPage {
+  void* host = nullptr;
+  void* dev = nullptr;
+};
+
+static py::tuple register_host_page(uintptr_t host_ptr, size_t bytes) {
+  HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(host_ptr), bytes, hipHostRegisterMapped));
+  void* dev = nullptr;
+  HIP_CHECK(hipHostGetDevicePointer(&dev, reinterpret_cast<void*>(host_ptr), 0));
+  return py::make_tuple((uintptr_t)host_ptr, (uintptr_t)dev);
+}
+
+static void unregister_host_page(uintptr_t host_ptr) {
+  HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(host_ptr)));
+}
+
+static void slot_census(uintptr_t slot_state, int S_, int tokens, uint32_t step, uintptr_t page_dev,
+                        uintptr_t stream) {
+  hipLaunchKernelGGL(slot_census_kernel, dim3(1), dim3(256), 0, S(stream), P<const int32_t>(slot_state), S_,
+                     tokens, step, P<uint32_t>(page_dev));
+  check_launch();
+}
+
+static py::dict device_info(int dev) {
+  hipDeviceProp_t p;
+  HIP_CHECK(hipGetDeviceProperties(&p, dev));
+  py::dict d;
+  d["name"] = std::string(p.name);
+  d["gcn_arch"] = std::string(p.gcnArchName);
+  d["cus"] = p.multiProcessorCount;
+  d["lds_per_cu"] = (int64_t)p.maxSharedMemoryPerMultiProcessor;
+  d["lds_per_block"] = (int64_t)p.sharedMemPerBlock;
+  d["hbm_bytes"] = (int64_t)p.totalGlobalMem;
+  d["clock_khz"] = p.clockRate;
+  d["warp_size"] = p.warpSize;
+  return d;
+}
+
+PYBIND11_MODULE(_hipops, m) {
+  m.doc() = "llm_message_queue_amd HIP kernels (gfx950)";
+  m.attr("PATTERN_TABLE_BYTES") = (int)sizeof(PatternTable);
+  m.attr("MAX_PATTERNS") = TA_MAX_PAT;
+  m.attr("STAT_COLS") = TA_STAT_COLS;
+  m.attr("SLOTS") = TA_SLOTS;
+  m.attr("MAX_TOKEN_BYTES") = TA_MAX_TOKEN_BYTES;
+  m.def("text_analyze", &text_analyze);
+  m.def("scan_rows", &scan_rows);
+  m.def("embed_pool", &embed_pool);
+  m.def("classify_head", &classify_head);
+  m.def("summarise_project", &summarise_project);
+  m.def("salient_topk", &salient_topk);
+  m.def("rmsnorm", &rmsnorm);
+  m.def("silu_mul", &silu_mul);
+  m.def("rope_kv", &rope_kv);
+  m.def("attention", &attention);
+  m.def("register_host_page", &register_host_page);
+  m.def("unregister_host_page", &unregister_host_page);
+  m.def("slot_census", &slot_census);
+  m.def("device_info", &device_info);
+}

@@ -1,0 +1,138 @@
+"""Llama-3-8B-shaped backend stub (N12): random-init bf16 weights, one
+instance per GPU, serving the gateway's dispatched requests.
+
+The reference never calls its endpoints (`internal/loadbalancer/load_balancer.go:35-49`,
+URLs from `internal/scheduler/scheduler.go:299-301`); here each endpoint is a
+real GPU worker so load signals (in-flight slots, HBM) are live.
+
+Forward = one continuous-batching step over T tokens (chunked-prefill and
+decode tokens mixed).  GEMMs: ``torch.nn.functional.linear`` (hipBLASLt).
+Everything else: hand-written HIP kernels (``ops.llama_ops.HipOps``):
+residual-add+RMSNorm, RoPE + KV-cache write, unified GQA attention over the
+slot KV cache, SiLU*up.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..ops.llama_ops import get_ops, rope_tables
+
+
+@dataclass
+class LlamaConfig:
+    vocab: int = 128256
+    dim: int = 4096
+    layers: int = 32
+    heads: int = 32
+    kv_heads: int = 8
+    head_dim: int = 128
+    ffn: int = 14336
+    rope_theta: float = 500000.0
+    eps: float = 1e-5
+
+    @classmethod
+    def llama3_8b(cls) -> "LlamaConfig":
+        return cls()
+
+    @classmethod
+    def tiny(cls) -> "LlamaConfig":
+        """Smoke/CPU-test size (same kernels, same head_dim=128, GQA 4)."""
+        return cls(vocab=1024, dim=2048, layers=2, heads=16, kv_heads=4, ffn=2048)
+
+    @classmethod
+    def by_name(cls, name: str) -> "LlamaConfig":
+        n = name.lower().replace("_", "-")
+        if n in ("llama3-8b", "llama-3-8b", "llama3_8b", "8b"):
+            return cls.llama3_8b()
+        if n == "tiny":
+            return cls.tiny()
+        raise ValueError(f"unknown backend model {name!r}")
+
+    def param_count(self) -> int:
+        d, f = self.dim, self.ffn
+        qkv = d * (self.heads + 2 * self.kv_heads) * self.head_dim
+        per = qkv + d * d + 2 * d * f + d * f + 2 * d
+        return self.layers * per + 2 * self.vocab * d + d
+
+
+class LlamaStub:
+    def __init__(self, cfg: LlamaConfig, slots: int, max_ctx: int, device="cuda", impl: str = "hip",
+                 seed: int = 0, dtype=torch.bfloat16):
+        if cfg.head_dim != 128:
+            raise ValueError("kernels assume head_dim = 128")
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.ops = get_ops(impl)
+        self.impl = impl
+        self.slots = slots
+        self.max_ctx = max_ctx
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        std = 0.02
+
+        def w(*shape):
+            return (torch.randn(*shape, generator=g, device=self.device, dtype=torch.float32) * std).to(dtype)
+
+        d, hq, hkv, hd = cfg.dim, cfg.heads, cfg.kv_heads, cfg.head_dim
+        self.embed = w(cfg.vocab, d)
+        self.lm_head = w(cfg.vocab, d)
+        self.final_norm = torch.ones(d, dtype=dtype, device=self.device)
+        self.layers = []
+        for _ in range(cfg.layers):
+            self.layers.append({
+                "attn_norm": torch.ones(d, dtype=dtype, device=self.device),
+                "wqkv": w((hq + 2 * hkv) * hd, d),
+                "wo": w(d, hq * hd),
+                "mlp_norm": torch.ones(d, dtype=dtype, device=self.device),
+                "w_gu": w(2 * cfg.ffn, d),
+                "w_down": w(d, cfg.ffn),
+            })
+        # KV cache: per layer [slots, kv_heads, max_ctx, head_dim]
+        self.kcache = [torch.zeros((slots, hkv, max_ctx, hd), dtype=dtype, device=self.device)
+                       for _ in range(cfg.layers)]
+        self.vcache = [torch.zeros((slots, hkv, max_ctx, hd), dtype=dtype, device=self.device)
+                       for _ in range(cfg.layers)]
+        self.cos, self.sin = rope_tables(max_ctx, cfg.rope_theta, self.device)
+        self.scale = 1.0 / math.sqrt(hd)
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
+        for L in self.layers:
+            n += sum(t.numel() for t in L.values())
+        return n * 2
+
+    def kv_bytes(self) -> int:
+        return sum(t.numel() * 2 for t in self.kcache) * 2
+
+    @torch.no_grad()
+    def forward(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
+                sample_idx: torch.Tensor) -> torch.Tensor:
+        """One step over T tokens; returns greedy next-token ids for the rows
+        in ``sample_idx`` (the last token of each request's chunk)."""
+        cfg, ops = self.cfg, self.ops
+        T = tokens.shape[0]
+        h = F.embedding(tokens, self.embed)              # [T, d]
+        res = h.clone()
+        x = ops.rmsnorm(h, self.layers[0]["attn_norm"], cfg.eps)
+        out = None
+        for i, L in enumerate(self.layers):
+            if i > 0:
+                x = ops.rmsnorm(out, L["attn_norm"], cfg.eps, residual=res)
+            qkv = F.linear(x, L["wqkv"])
+            q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
+                            self.kcache[i], self.vcache[i])
+            a = ops.attention(q, self.kcache[i], self.vcache[i], pos, slot, cfg.heads, cfg.kv_heads,
+                              self.scale)
+            ao = F.linear(a, L["wo"])
+            x2 = ops.rmsnorm(ao, L["mlp_norm"], cfg.eps, residual=res)
+            gu = F.linear(x2, L["w_gu"])
+            act = ops.silu_mul(gu)
+            out = F.linear(act, L["w_down"])
+        xf = ops.rmsnorm(out, self.final_norm, cfg.eps, residual=res)
+        sel = xf.index_select(0, sample_idx)
+        logits = F.linear(sel, self.lm_head)
+        return torch.argmax(logits, dim=-1).to(torch.int32)

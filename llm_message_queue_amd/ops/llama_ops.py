@@ -1,0 +1,162 @@
+"""Backend-stub decode ops: HIP kernels (``_hipops``) and plain-PyTorch fp32
+reference implementations of the same math (used by the numerics tests and,
+explicitly requested, by CPU-only engine tests -- never as a silent fallback
+on a GPU host).
+
+KV cache layout per layer: ``[slots, kv_heads, max_ctx, 128]`` bf16.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import _native
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check(t: torch.Tensor, dtype, name: str):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+class HipOps:
+    """Thin validated wrappers over the HIP kernels."""
+
+    def __init__(self):
+        self.k = _native.require_hipops()
+
+    def rmsnorm(self, x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        _check(x, torch.bfloat16, "x")
+        _check(w, torch.bfloat16, "w")
+        T, D = x.shape
+        if w.numel() != D:
+            raise ValueError("rmsnorm weight size mismatch")
+        if residual is not None:
+            _check(residual, torch.bfloat16, "residual")
+            if residual.shape != x.shape:
+                raise ValueError("residual shape mismatch")
+        y = out if out is not None else torch.empty_like(x)
+        self.k.rmsnorm(x.data_ptr(), residual.data_ptr() if residual is not None else 0, w.data_ptr(),
+                       y.data_ptr(), T, D, float(eps), _stream(x))
+        return y
+
+    def silu_mul(self, gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        _check(gu, torch.bfloat16, "gu")
+        T, F2 = gu.shape
+        F = F2 // 2
+        y = out if out is not None else torch.empty((T, F), dtype=gu.dtype, device=gu.device)
+        self.k.silu_mul(gu.data_ptr(), y.data_ptr(), T, F, _stream(gu))
+        return y
+
+    def rope_kv(self, qkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, q_out=None):
+        _check(qkv, torch.bfloat16, "qkv")
+        _check(pos, torch.int32, "pos")
+        _check(slot, torch.int32, "slot")
+        T = qkv.shape[0]
+        if qkv.shape[1] != (Hq + 2 * Hkv) * 128:
+            raise ValueError("qkv width mismatch")
+        S, hk, max_ctx, hd = kc.shape
+        if hk != Hkv or hd != 128 or vc.shape != kc.shape:
+            raise ValueError("kv cache shape mismatch")
+        q = q_out if q_out is not None else torch.empty((T, Hq * 128), dtype=qkv.dtype, device=qkv.device)
+        self.k.rope_kv(qkv.data_ptr(), pos.data_ptr(), slot.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), T,
+                       Hq, Hkv, max_ctx, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), _stream(qkv))
+        return q
+
+    def attention(self, q, kc, vc, pos, slot, Hq, Hkv, scale, out=None):
+        _check(q, torch.bfloat16, "q")
+        T = q.shape[0]
+        max_ctx = kc.shape[2]
+        o = out if out is not None else torch.empty_like(q)
+        self.k.attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), pos.data_ptr(), slot.data_ptr(), T, Hq, Hkv,
+                         max_ctx, float(scale), o.data_ptr(), _stream(q))
+        return o
+
+
+class RefOps:
+    """fp32 PyTorch reference of the same math (bf16 in / bf16 out)."""
+
+    def rmsnorm(self, x, w, eps, residual=None, out=None):
+        xf = x.float()
+        if residual is not None:
+            r = (xf + residual.float()).to(torch.bfloat16)
+            residual.copy_(r)
+            xf = r.float()
+        y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+        y = y.to(torch.bfloat16)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def silu_mul(self, gu, out=None):
+        F = gu.shape[1] // 2
+        g, u = gu[:, :F].float(), gu[:, F:].float()
+        y = (torch.nn.functional.silu(g) * u).to(torch.bfloat16)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def rope_kv(self, qkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, q_out=None):
+        T = qkv.shape[0]
+        x = qkv.float().view(T, Hq + 2 * Hkv, 128)
+        c = cos_t[pos.long()].unsqueeze(1)   # [T,1,64]
+        s = sin_t[pos.long()].unsqueeze(1)
+
+        def rot(v):
+            a, b = v[..., :64], v[..., 64:]
+            return torch.cat([a * c - b * s, b * c + a * s], dim=-1)
+
+        q = rot(x[:, :Hq]).to(torch.bfloat16).reshape(T, Hq * 128)
+        k = rot(x[:, Hq:Hq + Hkv]).to(torch.bfloat16)
+        v = x[:, Hq + Hkv:].to(torch.bfloat16)
+        for t in range(T):
+            kc[slot[t], :, pos[t]] = k[t]
+            vc[slot[t], :, pos[t]] = v[t]
+        if q_out is not None:
+            q_out.copy_(q)
+            return q_out
+        return q
+
+    def attention(self, q, kc, vc, pos, slot, Hq, Hkv, scale, out=None):
+        T = q.shape[0]
+        G = Hq // Hkv
+        res = torch.empty_like(q)
+        qf = q.float().view(T, Hq, 128)
+        for t in range(T):
+            n = int(pos[t]) + 1
+            K = kc[slot[t], :, :n].float()       # [Hkv, n, 128]
+            V = vc[slot[t], :, :n].float()
+            Kx = K.repeat_interleave(G, dim=0)   # [Hq, n, 128]
+            Vx = V.repeat_interleave(G, dim=0)
+            sc = torch.einsum("hd,hnd->hn", qf[t], Kx) * scale
+            p = torch.softmax(sc, dim=-1)
+            res[t] = torch.einsum("hn,hnd->hd", p, Vx).reshape(-1).to(torch.bfloat16)
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
+
+
+def rope_tables(max_pos: int, theta: float = 500000.0, device="cpu"):
+    inv = 1.0 / (theta ** (torch.arange(0, 64, dtype=torch.float64) / 64.0))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return f.cos().float().to(device).contiguous(), f.sin().float().to(device).contiguous()
+
+
+def get_ops(impl: str):
+    if impl == "hip":
+        return HipOps()
+    if impl == "ref":
+        return RefOps()
+    raise ValueError(f"unknown op implementation {impl!r}")

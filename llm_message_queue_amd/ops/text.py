@@ -1,0 +1,271 @@
+"""GPU preprocess pipeline: ``text_analyze`` (N1-N3) + ``embed_pool`` /
+``classify_head`` (N4) HIP kernels, driven from PyTorch-ROCm.
+
+One ``TextPipeline.run(contents, patterns)`` call does, on the current HIP
+stream:
+  1. pack the micro-batch's UTF-8 bytes + offsets into a pinned staging
+     buffer and copy them to the device in one transfer;
+  2. ``text_analyze`` -> per-message stats [B,16] + token hashes [B,L];
+  3. ``scan_rows`` -> compacted token row offsets;
+  4. ``embed_pool`` -> pooled [B,H] (bf16 MFMA GEMM over gathered rows);
+  5. ``classify_head`` -> logits [B,8], predicted priority;
+  6. one D2H copy of stats + predictions (one sync per micro-batch).
+Pooled vectors and hashes stay on the device for context summarisation (N5).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .. import _native
+from ..preprocess import oracle
+
+MAX_PATTERNS = 32
+STAT_COLS = 16
+ST_WORDS, ST_POS, ST_NEG, ST_QUESTION, ST_FLAGS, ST_NTOK, ST_SCORES = 0, 1, 2, 3, 4, 5, 8
+FLAG_FOLD = 1
+
+
+def _has_border(b: bytes) -> bool:
+    n = len(b)
+    return any(b[:k] == b[n - k:] for k in range(1, n))
+
+
+def gpu_eligible(p) -> bool:
+    """Literal patterns the kernel matches exactly (see text_kernels.h)."""
+    if not isinstance(p, oracle.LiteralPattern):
+        return False
+    if "�" in p.text or "\x00" in p.text:
+        return False
+    b = p.text.encode("utf-8")
+    if not (1 <= len(b) <= 16):
+        return False
+    if p.ci:
+        for ch in p.text:
+            if ord(ch) >= 0x80 and (ch.lower() != ch or ch.upper() != ch):
+                return False
+            if ch in oracle.FOLD_SPECIAL:
+                return False
+    return True
+
+
+@dataclass
+class PackedPatterns:
+    table: bytes
+    slot_prio: List[int]                   # slot index -> priority value
+    cpu_patterns: List[Tuple[int, object]]  # (slot, pattern) scored on the host
+    version: int
+
+
+def pack_patterns(patterns: Dict[int, list], version: int = 0) -> PackedPatterns:
+    prios = sorted(patterns)
+    if len(prios) > 8:
+        raise ValueError("at most 8 distinct keyword priorities are supported")
+    slot_of = {p: i for i, p in enumerate(prios)}
+    text = np.zeros((MAX_PATTERNS, 4), dtype=np.uint32)
+    mask = np.zeros((MAX_PATTERNS, 4), dtype=np.uint32)
+    lens = np.zeros(MAX_PATTERNS, dtype=np.int32)
+    slots = np.zeros(MAX_PATTERNS, dtype=np.int32)
+    flags = np.zeros(MAX_PATTERNS, dtype=np.int32)
+    n = 0
+    cpu: List[Tuple[int, object]] = []
+    for prio in prios:
+        for p in patterns[prio]:
+            if n >= MAX_PATTERNS or not gpu_eligible(p):
+                cpu.append((slot_of[prio], p))
+                continue
+            raw = p.text.encode("utf-8")
+            if p.ci:
+                raw = bytes((c + 32) if 65 <= c <= 90 else c for c in raw)
+            buf = raw.ljust(16, b"\x00")
+            mbuf = (b"\xff" * len(raw)).ljust(16, b"\x00")
+            text[n] = np.frombuffer(buf, dtype="<u4")
+            mask[n] = np.frombuffer(mbuf, dtype="<u4")
+            lens[n] = len(raw)
+            slots[n] = slot_of[prio]
+            flags[n] = (1 if p.ci else 0) | (2 if _has_border(raw) else 0)
+            n += 1
+    table = (text.tobytes() + mask.tobytes() + lens.tobytes() + slots.tobytes() + flags.tobytes()
+             + np.int32(n).tobytes())
+    return PackedPatterns(table, prios, cpu, version)
+
+
+class ClassifierWeights:
+    """Random-init weights of the hashed-token priority classifier (N4)."""
+
+    def __init__(self, vocab: int = 65536, dim: int = 256, hidden: int = 1024, seed: int = 1234,
+                 device="cuda"):
+        import torch
+        if vocab & (vocab - 1):
+            raise ValueError("vocab_buckets must be a power of two")
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        self.vocab, self.dim, self.hidden = vocab, dim, hidden
+        self.E = (torch.randn(vocab, dim, generator=g) * 0.5).to(torch.bfloat16).to(device)
+        self.W1t = (torch.randn(hidden, dim, generator=g) / dim ** 0.5).to(torch.bfloat16).to(device)
+        self.b1 = (torch.randn(hidden, generator=g) * 0.02).float().to(device)
+        self.W2 = (torch.randn(hidden, 8, generator=g) / hidden ** 0.5).float().to(device).contiguous()
+        self.b2 = torch.zeros(8, dtype=torch.float32, device=device)
+
+
+class TextResult:
+    __slots__ = ("stats", "pred", "elapsed_ms", "has_classifier", "slot_prio", "extra_scores",
+                 "pooled", "hashes", "L", "prompt_hashes")
+
+    def __init__(self, stats, pred, elapsed_ms, has_classifier, slot_prio, extra_scores, pooled, hashes, L,
+                 prompt_hashes=None):
+        self.stats = stats
+        self.pred = pred
+        self.elapsed_ms = elapsed_ms
+        self.has_classifier = has_classifier
+        self.slot_prio = slot_prio
+        self.extra_scores = extra_scores
+        self.pooled = pooled      # device tensor [B, H] (or None)
+        self.hashes = hashes      # device tensor [B, L] int32 view of uint32
+        self.L = L
+        self.prompt_hashes = prompt_hashes   # host [B, prompt_cap] uint32 (or None)
+
+    def prompt_ids(self, j: int):
+        n = min(int(self.stats[j, ST_NTOK]), self.prompt_hashes.shape[1])
+        return self.prompt_hashes[j, :n]
+
+    @property
+    def word_count(self):
+        return self.stats[:, ST_WORDS]
+
+    @property
+    def question(self):
+        return self.stats[:, ST_QUESTION]
+
+    @property
+    def ntok(self):
+        return self.stats[:, ST_NTOK]
+
+    @property
+    def fallback(self):
+        return (self.stats[:, ST_FLAGS] & FLAG_FOLD) != 0
+
+    @property
+    def ml_priority(self):
+        return self.pred
+
+    def scores(self, j: int) -> Dict[int, int]:
+        row = self.stats[j, ST_SCORES:ST_SCORES + 8]
+        out = {p: int(row[s]) for s, p in enumerate(self.slot_prio)}
+        if self.extra_scores is not None:
+            for s, p in enumerate(self.slot_prio):
+                out[p] += int(self.extra_scores[j, s])
+        return out
+
+    def priority(self, j: int, default_priority: int) -> int:
+        return oracle.pick_priority(self.scores(j), default_priority)
+
+    def sentiment(self, j: int) -> str:
+        pos, neg = self.stats[j, ST_POS], self.stats[j, ST_NEG]
+        return "positive" if pos > neg else ("negative" if neg > pos else "neutral")
+
+
+class TextPipeline:
+    def __init__(self, cfg=None, device: str = "cuda"):
+        import torch
+        from ..utils.config import PreprocessorConfig
+        self.torch = torch
+        self.cfg = cfg or PreprocessorConfig()
+        self.ops = _native.require_hipops()
+        assert self.ops.PATTERN_TABLE_BYTES == 4 * (MAX_PATTERNS * 8 + MAX_PATTERNS * 3 + 1)
+        self.device = torch.device(device)
+        self.L = int(self.cfg.max_tokens)
+        self.weights: Optional[ClassifierWeights] = None
+        self._packed: Optional[PackedPatterns] = None
+        self._pin = torch.empty(0, dtype=torch.uint8).pin_memory()
+        self._dev_bytes = torch.empty(0, dtype=torch.uint8, device=self.device)
+        # own HIP stream: preprocess kernels run concurrently with the
+        # backend forward on the default stream
+        self.stream = torch.cuda.Stream(device=self.device)
+
+    def _ensure_weights(self) -> ClassifierWeights:
+        if self.weights is None:
+            c = self.cfg
+            self.weights = ClassifierWeights(c.vocab_buckets, c.embed_dim, c.hidden_dim, c.seed,
+                                             device=self.device)
+        return self.weights
+
+    def _patterns(self, patterns, version) -> PackedPatterns:
+        if self._packed is None or self._packed.version != version or version < 0:
+            self._packed = pack_patterns(patterns, version)
+        return self._packed
+
+    def pack(self, contents: Sequence[str]):
+        """UTF-8 bytes + offsets for a batch (host side)."""
+        enc = [oracle.sanitize(c).encode("utf-8") for c in contents]
+        lens = np.fromiter((len(b) for b in enc), dtype=np.int64, count=len(enc))
+        offsets = np.zeros(len(enc) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        blob = b"".join(enc) + b"\x00" * 16
+        return blob, offsets, lens
+
+    def run(self, contents: Sequence[str], patterns: Dict[int, list], version: int = -1,
+            classify: bool = True, keep_device: bool = False, prompt_cap: int = 0) -> TextResult:
+        with self.torch.cuda.stream(self.stream):
+            return self._run(contents, patterns, version, classify, keep_device, prompt_cap)
+
+    def _run(self, contents, patterns, version, classify, keep_device, prompt_cap) -> TextResult:
+        torch = self.torch
+        t0 = time.perf_counter()
+        B = len(contents)
+        pk = self._patterns(patterns, version)
+        blob, offsets, lens = self.pack(contents)
+        ob = len(blob) + (-len(blob)) % 8        # offsets 8-byte aligned after the bytes
+        nb = ob + offsets.nbytes
+        if self._pin.numel() < nb:
+            self._pin = torch.empty(max(nb, 2 * self._pin.numel()), dtype=torch.uint8).pin_memory()
+        pin = self._pin
+        pnp = pin.numpy()
+        pnp[:len(blob)] = np.frombuffer(blob, dtype=np.uint8)
+        pnp[ob:ob + offsets.nbytes] = offsets.view(np.uint8)
+        total = ob + offsets.nbytes
+        if self._dev_bytes.numel() < total:
+            self._dev_bytes = torch.empty(max(total, 2 * self._dev_bytes.numel()), dtype=torch.uint8,
+                                          device=self.device)
+        dev = self._dev_bytes
+        dev[:total].copy_(pin[:total], non_blocking=True)
+        d_off = dev[ob:ob + offsets.nbytes].view(torch.int64)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        L = self.L
+        stats = torch.empty((B, STAT_COLS), dtype=torch.int32, device=self.device)
+        hashes = torch.zeros((B, L), dtype=torch.int32, device=self.device)
+        self.ops.text_analyze(dev.data_ptr(), d_off.data_ptr(), B, L, pk.table, stats.data_ptr(),
+                              hashes.data_ptr(), stream)
+        pooled = pred = None
+        if classify and B:
+            w = self._ensure_weights()
+            row_off = torch.empty(B + 1, dtype=torch.int32, device=self.device)
+            self.ops.scan_rows(stats.data_ptr() + 4 * ST_NTOK, STAT_COLS, B, row_off.data_ptr(), stream)
+            # host bound on token rows: a token needs >= 1 byte plus a separator
+            rows_upper = int(np.minimum((lens + 1) // 2, L).sum())
+            pooled = torch.zeros((B, w.hidden), dtype=torch.float32, device=self.device)
+            self.ops.embed_pool(hashes.data_ptr(), L, row_off.data_ptr(), B, rows_upper, w.E.data_ptr(),
+                                w.vocab, w.W1t.data_ptr(), w.b1.data_ptr(), w.hidden, pooled.data_ptr(),
+                                stream)
+            logits = torch.empty((B, 8), dtype=torch.float32, device=self.device)
+            pred = torch.empty(B, dtype=torch.int32, device=self.device)
+            self.ops.classify_head(pooled.data_ptr(), B, w.hidden, w.W2.data_ptr(), w.b2.data_ptr(),
+                                   logits.data_ptr(), pred.data_ptr(), stream)
+        ph = None
+        if prompt_cap > 0 and B:
+            ph = hashes[:, :min(prompt_cap, L)].to("cpu", non_blocking=True)
+        stats_h = stats.to("cpu")   # synchronises the stream
+        pred_h = pred.to("cpu").numpy() if pred is not None else None
+        if ph is not None:
+            ph = ph.numpy().view(np.uint32)
+        extra = None
+        if pk.cpu_patterns:
+            extra = np.zeros((B, 8), dtype=np.int64)
+            for j, c in enumerate(contents):
+                for slot, p in pk.cpu_patterns:
+                    extra[j, slot] += p.count(c)
+        el = (time.perf_counter() - t0) * 1e3
+        return TextResult(stats_h.numpy(), pred_h, el, pred is not None, pk.slot_prio, extra,
+                          pooled if keep_device else None, hashes if keep_device else None, L, ph)

@@ -1,0 +1,208 @@
+"""Control-plane communication between GPU backend processes (N10, N11).
+
+One process per GPU, ``torch.distributed`` with the ``nccl`` backend (= RCCL
+on ROCm, over xGMI).  The reference has no inter-service transport at all
+(its three microservices each own a private queue); here
+every scheduler tick does
+  * ``all_gather`` of a fixed-size int64 load vector per rank (latency-bound,
+    ~1 KiB total: free slots, in-flight, per-tier queue depth/age, HBM), so
+    every rank computes the SAME dispatch/rebalance plan deterministically
+    (no leader round-trip, collectives issued in the same order everywhere);
+  * ``all_to_all_single`` of fixed-width int32 request descriptors for the
+    requests a router hands to a backend on another GPU (sizes are known on
+    every rank from the plan, so no size exchange is needed);
+  * ``send``/``recv`` point-to-point for conversation KV/context migration
+    (N11) -- one direct xGMI link per GPU pair, not a ring.
+
+``FakeComm`` runs the same API between threads of one process so the
+multi-rank logic is testable on a CPU box at world sizes 2/4/8.
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+
+class Comm:
+    rank: int = 0
+    world: int = 1
+
+    def all_gather_i64(self, vec: np.ndarray) -> np.ndarray:
+        raise NotImplementedError
+
+    def all_to_all_rows(self, send: Sequence[np.ndarray], recv_counts: Sequence[int], width: int) -> List[np.ndarray]:
+        raise NotImplementedError
+
+    def broadcast_i64(self, vec: np.ndarray, root: int = 0) -> np.ndarray:
+        raise NotImplementedError
+
+    def send_tensor(self, t, dst: int) -> None:
+        raise NotImplementedError
+
+    def recv_tensor(self, t, src: int) -> None:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        pass
+
+    def max_f64(self, x: float) -> float:
+        v = self.all_gather_i64(np.array([int(x * 1e6)], dtype=np.int64))
+        return float(v.max()) / 1e6
+
+
+class SoloComm(Comm):
+    """world_size == 1."""
+
+    def all_gather_i64(self, vec):
+        return np.asarray(vec, dtype=np.int64).reshape(1, -1).copy()
+
+    def all_to_all_rows(self, send, recv_counts, width):
+        return [np.asarray(send[0], dtype=np.int32).reshape(-1, width).copy()]
+
+    def broadcast_i64(self, vec, root=0):
+        return np.asarray(vec, dtype=np.int64).copy()
+
+    def send_tensor(self, t, dst):
+        raise RuntimeError("no peer in a world of one")
+
+    recv_tensor = send_tensor
+
+
+class TorchComm(Comm):
+    """torch.distributed process group (nccl=RCCL on GPU tensors, gloo on CPU)."""
+
+    def __init__(self, device=None, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        backend = dist.get_backend(group)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        self.device = torch.device(device)
+
+    def all_gather_i64(self, vec):
+        torch = self.torch
+        v = torch.as_tensor(np.asarray(vec, dtype=np.int64)).to(self.device)
+        out = torch.empty((self.world, v.numel()), dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(out, v.reshape(-1), group=self.group)
+        return out.cpu().numpy()
+
+    def all_to_all_rows(self, send, recv_counts, width):
+        torch = self.torch
+        send_counts = [int(np.asarray(s).size // width) for s in send]
+        flat = np.concatenate([np.asarray(s, dtype=np.int32).reshape(-1) for s in send]) \
+            if sum(send_counts) else np.zeros(0, dtype=np.int32)
+        total_in = int(sum(recv_counts))
+        inp = torch.as_tensor(flat).to(self.device)
+        out = torch.empty(total_in * width, dtype=torch.int32, device=self.device)
+        self.dist.all_to_all_single(out, inp, output_split_sizes=[c * width for c in recv_counts],
+                                    input_split_sizes=[c * width for c in send_counts], group=self.group)
+        o = out.cpu().numpy().reshape(-1, width) if total_in else np.zeros((0, width), dtype=np.int32)
+        res, a = [], 0
+        for c in recv_counts:
+            res.append(o[a:a + c])
+            a += c
+        return res
+
+    def broadcast_i64(self, vec, root=0):
+        torch = self.torch
+        v = torch.as_tensor(np.asarray(vec, dtype=np.int64)).to(self.device).clone()
+        self.dist.broadcast(v, src=root, group=self.group)
+        return v.cpu().numpy()
+
+    def send_tensor(self, t, dst):
+        self.dist.send(t, dst=dst, group=self.group)
+
+    def recv_tensor(self, t, src):
+        self.dist.recv(t, src=src, group=self.group)
+
+    def barrier(self):
+        if self.dist.get_backend(self.group) == "nccl":
+            self.dist.barrier(group=self.group, device_ids=[self.device.index])
+        else:
+            self.dist.barrier(group=self.group)
+
+
+class _Hub:
+    def __init__(self, world: int):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots: List[object] = [None] * world
+        self.mail = {}
+        self.cv = threading.Condition()
+
+
+class FakeComm(Comm):
+    """In-process multi-rank comm (threads); same semantics as TorchComm."""
+
+    def __init__(self, hub: _Hub, rank: int):
+        self.hub, self.rank, self.world = hub, rank, hub.world
+
+    @staticmethod
+    def make(world: int) -> List["FakeComm"]:
+        hub = _Hub(world)
+        return [FakeComm(hub, r) for r in range(world)]
+
+    def _exchange(self, obj):
+        h = self.hub
+        h.bar.wait()
+        h.slots[self.rank] = obj
+        h.bar.wait()
+        got = list(h.slots)
+        h.bar.wait()
+        return got
+
+    def all_gather_i64(self, vec):
+        got = self._exchange(np.asarray(vec, dtype=np.int64).reshape(-1).copy())
+        return np.stack(got)
+
+    def all_to_all_rows(self, send, recv_counts, width):
+        got = self._exchange([np.asarray(s, dtype=np.int32).reshape(-1, width).copy() for s in send])
+        out = [got[src][self.rank] for src in range(self.world)]
+        for src, c in enumerate(recv_counts):
+            if out[src].shape[0] != c:
+                raise RuntimeError(f"rank {self.rank}: expected {c} rows from {src}, got {out[src].shape[0]}")
+        return out
+
+    def broadcast_i64(self, vec, root=0):
+        got = self._exchange(np.asarray(vec, dtype=np.int64).copy())
+        return got[root].copy()
+
+    def send_tensor(self, t, dst):
+        h = self.hub
+        with h.cv:
+            h.mail.setdefault((self.rank, dst), []).append(t.clone())
+            h.cv.notify_all()
+
+    def recv_tensor(self, t, src):
+        h = self.hub
+        with h.cv:
+            h.cv.wait_for(lambda: h.mail.get((src, self.rank)))
+            t.copy_(h.mail[(src, self.rank)].pop(0))
+
+    def barrier(self):
+        self.hub.bar.wait()
+
+
+def init_from_env(backend: Optional[str] = None):
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...)."""
+    import os
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return SoloComm()
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, **kw)
+    return TorchComm()

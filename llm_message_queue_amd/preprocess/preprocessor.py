@@ -1,0 +1,245 @@
+"""Preprocessor (component C10): content-based priority + analysis metadata.
+
+Reference: `internal/preprocessor/preprocessor.go`.  ``process_message``
+follows `:56-114` step by step (explicit non-normal priority respected and NOT
+analysed; ``metadata.user_priority`` override; per-user default; keyword
+scoring; content analysis; ``analyzed=true``; queue name = ``priority.String()``).
+
+Two execution paths with identical results:
+  * ``process_message`` / ``process_batch(..., use_gpu=False)``: the exact CPU
+    oracle (`oracle.py`);
+  * ``process_batch(..., use_gpu=True)``: one fused ``text_analyze`` HIP launch
+    for the whole micro-batch (word count, sentiment, question, keyword
+    scores, token hashes) followed by the MFMA embedding classifier
+    (``embed_classify``).  Messages containing the three fold-special
+    characters (U+017F, U+212A, U+0130) are flagged by the kernel and
+    re-scored by the oracle, so GPU results are bit-identical to the oracle.
+
+Thread-safety: user priorities and patterns are guarded by a lock (the
+reference's map writes are unguarded).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Any, Dict, List, Optional, Sequence
+
+from ..models.message import (Message, PRIORITY_NORMAL, level_priority_from_name,
+                              priority_name)
+from . import oracle
+
+
+class Preprocessor:
+    def __init__(self, cfg=None, *, use_gpu: Optional[bool] = None, device: str = "cuda"):
+        """``cfg`` is a ``PreprocessorConfig`` (or None for defaults)."""
+        from ..utils.config import PreprocessorConfig
+        self.cfg = cfg or PreprocessorConfig()
+        self._lock = threading.RLock()
+        self._patterns: Dict[int, list] = oracle.default_patterns()
+        self._user_priorities: Dict[str, int] = {}
+        self.default_priority = PRIORITY_NORMAL
+        self.positive_words = list(oracle.POSITIVE_WORDS)
+        self.negative_words = list(oracle.NEGATIVE_WORDS)
+        self.question_words = list(oracle.QUESTION_WORDS)
+        self._want_gpu = self.cfg.use_gpu if use_gpu is None else use_gpu
+        self._device = device
+        self._gpu = None           # lazily-built ops.text.TextPipeline
+        self._pattern_version = 0
+        self.stats = {"gpu_batches": 0, "gpu_messages": 0, "oracle_fallbacks": 0,
+                      "cpu_messages": 0, "last_gpu_ms": 0.0}
+
+    # ------------------------------------------------------------------ admin
+    def set_user_priority(self, user_id: str, priority: int) -> None:
+        with self._lock:
+            self._user_priorities[user_id] = int(priority)
+
+    def user_priorities(self) -> Dict[str, int]:
+        with self._lock:
+            return dict(self._user_priorities)
+
+    def add_keyword_pattern(self, priority: int, pattern: str) -> None:
+        """``AddKeywordPattern`` (`:176-184`): raises ``re.error`` on a bad regex."""
+        compiled = oracle.compile_pattern(pattern)
+        with self._lock:
+            self._patterns.setdefault(int(priority), []).append(compiled)
+            self._pattern_version += 1
+
+    def remove_keyword_pattern(self, priority: int, pattern: str) -> bool:
+        with self._lock:
+            pats = self._patterns.get(int(priority), [])
+            for i, p in enumerate(pats):
+                if p.source == pattern:
+                    del pats[i]
+                    self._pattern_version += 1
+                    return True
+        return False
+
+    def set_default_priority(self, priority: int) -> None:
+        with self._lock:
+            self.default_priority = int(priority)
+
+    def get_keyword_patterns(self, priority: int) -> List[str]:
+        with self._lock:
+            return [p.source for p in self._patterns.get(int(priority), [])]
+
+    def all_patterns(self) -> Dict[int, List[str]]:
+        with self._lock:
+            return {k: [p.source for p in v] for k, v in sorted(self._patterns.items())}
+
+    def patterns_snapshot(self):
+        with self._lock:
+            return {k: list(v) for k, v in self._patterns.items()}, self._pattern_version
+
+    # ------------------------------------------------------------------ single message (CPU)
+    def _resolve_priority_head(self, msg: Message) -> Optional[bool]:
+        """Steps 1-3 of ProcessMessage that need no content analysis.
+        Returns None if the message must be returned unchanged, True if the
+        priority still needs content analysis, False if it was decided."""
+        if msg.metadata is None:
+            msg.metadata = {}
+        if msg.priority != PRIORITY_NORMAL and msg.priority != 0:
+            return None
+        up = msg.metadata.get("user_priority")
+        if isinstance(up, str):
+            p = level_priority_from_name(up)
+            if p is not None:
+                msg.priority = p
+                msg.metadata["priority_reason"] = "user_override"
+            return False
+        with self._lock:
+            udef = self._user_priorities.get(msg.user_id)
+        if udef is not None:
+            msg.priority = udef
+            msg.metadata["priority_reason"] = "user_default"
+            return False
+        return True
+
+    def _finish(self, msg: Message, now_ns: int) -> None:
+        msg.metadata["analyzed"] = True
+        if not msg.queue_name:
+            msg.queue_name = priority_name(msg.priority)
+        if not msg.created_at:
+            msg.created_at = now_ns
+        msg.updated_at = now_ns
+
+    def _analyze_priority_cpu(self, msg: Message) -> int:
+        content = msg.content
+        if content == "":
+            ps = msg.metadata.get("priority")
+            if isinstance(ps, str):
+                p = level_priority_from_name(ps)
+                if p is not None:
+                    return p
+            return self.default_priority
+        pats, _ = self.patterns_snapshot()
+        return oracle.pick_priority(oracle.keyword_scores(content, pats), self.default_priority)
+
+    @staticmethod
+    def _content_metadata(msg: Message, word_count: int, sentiment: str, question: bool) -> None:
+        if msg.content == "":
+            return
+        msg.metadata["word_count"] = word_count
+        msg.metadata["sentiment"] = sentiment
+        msg.metadata["contains_question"] = "true" if question else "false"
+
+    def process_message(self, msg: Message) -> Message:
+        """``ProcessMessage`` (`preprocessor.go:56-114`) on the CPU oracle."""
+        head = self._resolve_priority_head(msg)
+        if head is None:
+            return msg
+        if head:
+            original = msg.priority
+            msg.priority = self._analyze_priority_cpu(msg)
+            if msg.priority != original:
+                msg.metadata["priority_reason"] = "content_keywords"
+        if msg.content:
+            wc, sent, q = oracle.content_analysis(msg.content)
+            self._content_metadata(msg, wc, sent, q)
+        self._finish(msg, time.time_ns())
+        self.stats["cpu_messages"] += 1
+        return msg
+
+    def analyze_message_content(self, content: str) -> Dict[str, Any]:
+        """``AnalyzeMessageContent`` (`:253-298`)."""
+        wc, sent, q = oracle.content_analysis(content)
+        return {"word_count": wc, "sentiment": sent, "is_question": q}
+
+    # ------------------------------------------------------------------ batch (GPU)
+    def gpu_pipeline(self):
+        """The HIP text pipeline, built on first use.  Raises if the HIP
+        extension is missing on a GPU host (never a silent fallback)."""
+        if self._gpu is None:
+            from ..ops.text import TextPipeline
+            self._gpu = TextPipeline(self.cfg, device=self._device)
+        return self._gpu
+
+    def gpu_enabled(self) -> bool:
+        if not self._want_gpu:
+            return False
+        try:
+            import torch
+            return torch.cuda.is_available()
+        except Exception:
+            return False
+
+    def process_batch(self, msgs: Sequence[Message], use_gpu: Optional[bool] = None,
+                      classify: Optional[bool] = None, prompt_cap: int = 0) -> Sequence[Message]:
+        """Process a micro-batch.  Same results as ``process_message`` per
+        message; on the GPU path one fused launch covers the whole batch."""
+        use_gpu = self.gpu_enabled() if use_gpu is None else use_gpu
+        if not use_gpu:
+            for m in msgs:
+                self.process_message(m)
+                if prompt_cap:
+                    m.prompt_ids = oracle.token_hashes(m.content, prompt_cap)
+            return msgs
+        heads = [self._resolve_priority_head(m) for m in msgs]
+        work = [i for i, h in enumerate(heads) if h is not None and msgs[i].content]
+        now = time.time_ns()
+        if work:
+            pipe = self.gpu_pipeline()
+            pats, ver = self.patterns_snapshot()
+            res = pipe.run([msgs[i].content for i in work], pats, ver,
+                           classify=self.cfg.classifier if classify is None else classify,
+                           prompt_cap=prompt_cap)
+            self.stats["gpu_batches"] += 1
+            self.stats["gpu_messages"] += len(work)
+            self.stats["last_gpu_ms"] = res.elapsed_ms
+            for j, i in enumerate(work):
+                m = msgs[i]
+                if res.fallback[j]:
+                    # fold-special characters / non-literal patterns: oracle
+                    self.stats["oracle_fallbacks"] += 1
+                    if heads[i]:
+                        original = m.priority
+                        m.priority = self._analyze_priority_cpu(m)
+                        if m.priority != original:
+                            m.metadata["priority_reason"] = "content_keywords"
+                    wc, sent, q = oracle.content_analysis(m.content)
+                else:
+                    if heads[i]:
+                        original = m.priority
+                        m.priority = res.priority(j, self.default_priority)
+                        if m.priority != original:
+                            m.metadata["priority_reason"] = "content_keywords"
+                    wc, sent, q = res.word_count[j], res.sentiment(j), bool(res.question[j])
+                self._content_metadata(m, int(wc), sent, q)
+                if prompt_cap:
+                    m.prompt_ids = res.prompt_ids(j)
+                if res.has_classifier:
+                    m.metadata["ml_priority"] = int(res.ml_priority[j])
+                    if (self.cfg.use_classifier_priority and heads[i]
+                            and m.metadata.get("priority_reason") is None):
+                        m.priority = int(res.ml_priority[j])
+                        m.metadata["priority_reason"] = "classifier"
+        for i, m in enumerate(msgs):
+            h = heads[i]
+            if h is None:
+                continue
+            if h and not m.content:
+                original = m.priority
+                m.priority = self._analyze_priority_cpu(m)
+                if m.priority != original:
+                    m.metadata["priority_reason"] = "content_keywords"
+            self._finish(m, now)
+        return msgs

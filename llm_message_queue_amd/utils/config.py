@@ -1,0 +1,360 @@
+"""Configuration tree (component C2).
+
+Loads the reference's YAML schema unchanged (`configs/config.yaml`, key names
+from `pkg/config/config.go:9-104`) with three fixes over the reference:
+
+  * defaults from ``default_config()`` (= ``GetDefaultConfig``,
+    `config.go:127-203`) are MERGED under the file values -- the reference does
+    not merge them, so the shipped yaml yields ``time.NewTicker(0)`` panics
+    (defect D3);
+  * environment overrides ``LLMQ_<SECTION>__<KEY>[__<SUBKEY>]`` actually bind
+    nested keys (viper's ``AutomaticEnv`` without a key replacer does not);
+  * validation: every interval must be > 0, level priorities unique, etc.
+
+MI355X-specific sections (``gpu``, ``backend``, ``preprocessor``,
+``conversation``) are additions; they have defaults so reference yaml files
+load unchanged.
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+from .duration import parse_duration_ns
+
+S = 1_000_000_000
+MS = 1_000_000
+
+
+@dataclass
+class ServerConfig:
+    port: int = 8080
+    host: str = "0.0.0.0"
+    mode: str = "debug"
+
+
+@dataclass
+class PostgresConfig:
+    host: str = "localhost"
+    port: int = 5432
+    user: str = "postgres"
+    password: str = "password"
+    dbname: str = "llm_queue"
+    sslmode: str = "disable"
+
+
+@dataclass
+class RedisConfig:
+    addr: str = "localhost:6379"
+    password: str = ""
+    db: int = 0
+    pool_size: int = 100
+
+
+@dataclass
+class DatabaseConfig:
+    postgres: PostgresConfig = field(default_factory=PostgresConfig)
+    redis: RedisConfig = field(default_factory=RedisConfig)
+    # MI355X build: persistence backend for conversations: memory|sqlite|redis|postgres
+    backend: str = "memory"
+    sqlite_path: str = "llmq_state.sqlite3"
+
+
+@dataclass
+class QueueLevel:
+    name: str = ""
+    priority: int = 0
+    max_wait_time: int = 0      # ns; used as the tier's aging deadline (anti-starvation)
+    max_concurrent: int = 0     # used as the tier's admission cap (in-flight)
+
+
+@dataclass
+class WorkerConfig:
+    max_batch_size: int = 10
+    process_interval: int = 100 * MS
+    max_concurrent: int = 50
+
+
+@dataclass
+class RetryConfig:
+    initial_backoff: int = 1 * S
+    max_backoff: int = 60 * S
+    factor: float = 2.0
+    max_retries: int = 3
+
+
+def _default_levels() -> List[QueueLevel]:
+    return [
+        QueueLevel("realtime", 1, 1 * S, 100),
+        QueueLevel("high", 2, 5 * S, 200),
+        QueueLevel("normal", 3, 30 * S, 500),
+        QueueLevel("low", 4, 300 * S, 1000),
+    ]
+
+
+@dataclass
+class QueueConfig:
+    levels: List[QueueLevel] = field(default_factory=_default_levels)
+    default_max_size: int = 10000
+    monitor_interval: int = 5 * S
+    cleanup_interval: int = 60 * S
+    max_retention_period: int = 24 * 3600 * S
+    enable_metrics: bool = True
+    enable_auto_scaling: bool = True
+    scaling_thresholds: Dict[str, int] = field(default_factory=lambda: {
+        "realtime": 100, "high": 500, "normal": 1000, "low": 5000})
+    worker: WorkerConfig = field(default_factory=WorkerConfig)
+    retry: RetryConfig = field(default_factory=RetryConfig)
+    # MI355X build additions
+    enable_aging: bool = True          # promote a tier head past its max_wait_time
+    dead_letter_max_size: int = 10000
+
+
+@dataclass
+class SchedulerConfig:
+    strategy: str = "priority_weighted"
+    check_interval: int = 100 * MS
+    max_retries: int = 3
+    timeout: int = 30 * S
+    # reference hardcodes these in cmd/scheduler/main.go:68-74
+    min_endpoints: int = 1
+    max_endpoints: int = 10
+    scale_up_threshold: int = 100
+    scale_down_threshold: int = 10
+    heartbeat_timeout: int = 30 * S
+    enable_auto_scaling: bool = False
+    autoscale_cooldown: int = 300 * S
+
+
+@dataclass
+class LoadBalancerConfig:
+    algorithm: str = "weighted_round_robin"
+    health_check_interval: int = 30 * S
+    max_failures: int = 3
+    enable_session_affinity: bool = True
+    session_timeout: int = 0           # 0 = never expires (reference behaviour)
+    healthy_threshold: int = 2
+
+
+@dataclass
+class LoggingConfig:
+    level: str = "info"
+    format: str = "json"
+    output: str = "stdout"
+
+
+@dataclass
+class MetricsConfig:
+    enabled: bool = True
+    port: int = 9090
+    path: str = "/metrics"
+
+
+@dataclass
+class PreprocessorConfig:
+    """GPU preprocess pipeline (N1-N4)."""
+    use_gpu: bool = True               # fall back to the CPU oracle when no GPU
+    batch_window_us: int = 500         # ingress micro-batch flush window
+    max_batch: int = 4096
+    max_tokens: int = 128              # tokens per message fed to the classifier
+    classifier: bool = True            # run the MFMA embedding classifier
+    use_classifier_priority: bool = False  # let the classifier decide no-keyword msgs
+    vocab_buckets: int = 65536
+    embed_dim: int = 256
+    hidden_dim: int = 1024
+    seed: int = 1234
+
+
+@dataclass
+class GPUConfig:
+    devices: List[int] = field(default_factory=list)   # empty = all visible
+    slots_per_gpu: int = 256
+    hbm_reserve_gb: float = 16.0
+    telemetry_period_ms: int = 20
+    comm_backend: str = "nccl"        # RCCL on ROCm; "gloo" for CPU tests
+    rebalance_interval_ms: int = 100
+
+
+@dataclass
+class BackendConfig:
+    model: str = "llama3-8b"
+    max_ctx: int = 512
+    prompt_tokens: int = 32            # prompt tokens prefilled per request (cap)
+    gen_tokens: int = 4                # decode steps per request
+    dtype: str = "bf16"
+
+
+@dataclass
+class ConversationConfig:
+    max_conversations: int = 1000      # per user (cmd/server/main.go:75)
+    max_context_length: int = 4096     # messages (cmd/server/main.go:76)
+    max_idle_time: int = 30 * 60 * S
+    summarise_on_evict: bool = True
+    summary_dim: int = 256
+    salient_tokens: int = 8
+    summary_alpha: float = 0.8
+
+
+@dataclass
+class Config:
+    server: ServerConfig = field(default_factory=ServerConfig)
+    database: DatabaseConfig = field(default_factory=DatabaseConfig)
+    queue: QueueConfig = field(default_factory=QueueConfig)
+    scheduler: SchedulerConfig = field(default_factory=SchedulerConfig)
+    loadbalancer: LoadBalancerConfig = field(default_factory=LoadBalancerConfig)
+    logging: LoggingConfig = field(default_factory=LoggingConfig)
+    metrics: MetricsConfig = field(default_factory=MetricsConfig)
+    preprocessor: PreprocessorConfig = field(default_factory=PreprocessorConfig)
+    gpu: GPUConfig = field(default_factory=GPUConfig)
+    backend: BackendConfig = field(default_factory=BackendConfig)
+    conversation: ConversationConfig = field(default_factory=ConversationConfig)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+
+# Fields holding Go durations (ns ints) -- decoded from strings like "100ms".
+_DURATION_FIELDS = {
+    "max_wait_time", "monitor_interval", "cleanup_interval", "max_retention_period",
+    "process_interval", "initial_backoff", "max_backoff", "check_interval", "timeout",
+    "health_check_interval", "session_timeout", "heartbeat_timeout", "autoscale_cooldown",
+    "max_idle_time",
+}
+
+
+class ConfigError(ValueError):
+    pass
+
+
+def default_config() -> Config:
+    """``GetDefaultConfig`` (`config.go:127-203`)."""
+    return Config()
+
+
+def _coerce(name: str, current: Any, value: Any, ftype: Any) -> Any:
+    if name in _DURATION_FIELDS:
+        try:
+            return parse_duration_ns(value)
+        except ValueError as e:
+            raise ConfigError(f"{name}: {e}") from None
+    if isinstance(current, bool) or ftype is bool:
+        if isinstance(value, str):
+            return value.strip().lower() in ("1", "true", "yes", "on")
+        return bool(value)
+    if isinstance(current, int) and not isinstance(current, bool):
+        try:
+            return int(value)
+        except (TypeError, ValueError):
+            raise ConfigError(f"{name}: expected int, got {value!r}") from None
+    if isinstance(current, float):
+        return float(value)
+    if isinstance(current, str):
+        return str(value)
+    return value
+
+
+def _merge(obj: Any, data: Dict[str, Any], path: str = "") -> None:
+    if not isinstance(data, dict):
+        raise ConfigError(f"{path or 'config'}: expected a mapping")
+    fields = {f.name: f for f in dataclasses.fields(obj)}
+    for key, value in data.items():
+        k = str(key).lower()
+        if k not in fields:
+            continue  # unknown keys are ignored, as viper does
+        cur = getattr(obj, k)
+        full = f"{path}.{k}" if path else k
+        if dataclasses.is_dataclass(cur):
+            _merge(cur, value or {}, full)
+        elif k == "levels":
+            levels = []
+            for i, lv in enumerate(value or []):
+                q = QueueLevel()
+                _merge(q, lv, f"{full}[{i}]")
+                levels.append(q)
+            setattr(obj, k, levels)
+        elif isinstance(cur, dict):
+            if not isinstance(value, dict):
+                raise ConfigError(f"{full}: expected a mapping")
+            setattr(obj, k, {str(a): int(b) for a, b in value.items()})
+        elif isinstance(cur, list):
+            if isinstance(value, str):
+                value = [int(x) for x in value.split(",") if x.strip()]
+            setattr(obj, k, list(value or []))
+        else:
+            setattr(obj, k, _coerce(k, cur, value, fields[k].type))
+
+
+def _apply_env(cfg: Config, environ: Dict[str, str], prefix: str = "LLMQ_") -> None:
+    for key, value in environ.items():
+        if not key.startswith(prefix):
+            continue
+        parts = [p.lower() for p in key[len(prefix):].split("__") if p]
+        if not parts:
+            continue
+        nested: Dict[str, Any] = {}
+        cur = nested
+        for p in parts[:-1]:
+            cur = cur.setdefault(p, {})
+        cur[parts[-1]] = value
+        _merge(cfg, nested)
+
+
+def validate(cfg: Config) -> Config:
+    q = cfg.queue
+    for name in ("monitor_interval", "cleanup_interval"):
+        if getattr(q, name) <= 0:
+            raise ConfigError(f"queue.{name} must be > 0")
+    if q.worker.process_interval <= 0:
+        raise ConfigError("queue.worker.process_interval must be > 0")
+    if q.worker.max_batch_size <= 0 or q.worker.max_concurrent <= 0:
+        raise ConfigError("queue.worker.max_batch_size/max_concurrent must be > 0")
+    if cfg.scheduler.check_interval <= 0:
+        raise ConfigError("scheduler.check_interval must be > 0")
+    if q.retry.factor < 1.0:
+        raise ConfigError("queue.retry.factor must be >= 1")
+    seen = set()
+    for lv in q.levels:
+        if not lv.name:
+            raise ConfigError("queue.levels[*].name must be set")
+        if lv.priority in seen:
+            raise ConfigError(f"duplicate level priority {lv.priority}")
+        seen.add(lv.priority)
+    if cfg.gpu.slots_per_gpu <= 0:
+        raise ConfigError("gpu.slots_per_gpu must be > 0")
+    return cfg
+
+
+def load_config(config_path: Optional[str] = None, *, environ: Optional[Dict[str, str]] = None,
+                validate_config: bool = True) -> Config:
+    """``LoadConfig`` with defaults merged.
+
+    ``config_path`` may be a directory (searched for ``config.yaml`` like viper's
+    ``AddConfigPath``) or a file.  Search order: arg, ``.``, ``./configs``.
+    A missing file is an error only when a path was given explicitly.
+    """
+    import yaml
+
+    cfg = default_config()
+    candidates: List[str] = []
+    if config_path:
+        if os.path.isdir(config_path):
+            candidates.append(os.path.join(config_path, "config.yaml"))
+        else:
+            candidates.append(config_path)
+    candidates += [os.path.join(".", "config.yaml"), os.path.join(".", "configs", "config.yaml")]
+    found = next((c for c in candidates if os.path.isfile(c)), None)
+    if found is None and config_path:
+        raise ConfigError(f"config file not found under {config_path!r}")
+    if found:
+        with open(found, "r", encoding="utf-8") as fh:
+            data = yaml.safe_load(fh) or {}
+        _merge(cfg, data)
+    _apply_env(cfg, dict(os.environ if environ is None else environ))
+    return validate(cfg) if validate_config else cfg
+
+
+def clone(cfg: Config) -> Config:
+    return copy.deepcopy(cfg)

@@ -1,0 +1,294 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 / Python oracle.
+
+Run on the MI355X box: ``pytest -m gpu``.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from llm_message_queue_amd.preprocess import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+# ----------------------------------------------------------------------------- text_analyze
+ADVERSARIAL = [
+    "", "?", " ", "URGENT", "urgent urgent", "aſap please", "KELVIN K and İstanbul good",
+    "somewhat unclear", "what is this", "WHAT is", "How are you", "who", "who ",
+    "good", "GOOD bad", "good! bad", "good bad", "good　happy sad", "tab\tgood\nbad\rterrible",
+    "\x1cgood\x1c", "emergency emergency asap immediate right now now", "right  now",
+    "critical soon important priority urgent", "prioritySetting", "immediately", "ASAPasap",
+    "\xff\xfe invalid?", "é good é", "good\u0085bad", " good ", " why  ",
+    "x" * 1000 + " urgent " + "y" * 1000, " ".join(["good"] * 300), "where where where? ",
+    "frustrated frustrated happy", "satisfied excellent great happy good", "awful angry",
+    "why　 not", "when ", "emergencyemergency", "soonsoon", "a" * 70 + "urgent",
+    "日本語 urgent 中文 good", "Ünïcödé ÉMERGENCY",
+]
+
+WORDS = ["good", "bad", "urgent", "asap", "what", "how", "why", "soon", "right", "now", "happy",
+         "angry", "critical", "emergency", "priority", "terrible", "who", "where", "é", "日本", "Good",
+         "URGENT", "Now", "x", "test", "important", "immediate"]
+SEPS = [" ", "  ", "\t", "\n", " ", "　", " ", ",", ".", "?", "!", "\u0085", "\x1c"]
+
+
+def _random_texts(n, seed=0):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        k = rng.randint(0, 40)
+        parts = []
+        for _ in range(k):
+            parts.append(rng.choice(WORDS))
+            parts.append(rng.choice(SEPS))
+        s = "".join(parts)
+        if rng.random() < 0.2:
+            s += "?"
+        out.append(s)
+    return out
+
+
+def _check_batch(texts, patterns=None, L=64):
+    from llm_message_queue_amd.ops.text import TextPipeline
+    from llm_message_queue_amd.utils.config import PreprocessorConfig
+    cfg = PreprocessorConfig(max_tokens=L)
+    pipe = TextPipeline(cfg, device=DEV)
+    pats = patterns or oracle.default_patterns()
+    res = pipe.run(texts, pats, classify=False, keep_device=True)
+    hashes = res.hashes.cpu().numpy().view(np.uint32)
+    for j, t in enumerate(texts):
+        t = oracle.sanitize(t)
+        wc, sent, q = oracle.content_analysis(t)
+        pos, neg = oracle.sentiment_counts(t)
+        fold = any(c in oracle.FOLD_SPECIAL for c in t)
+        assert bool(res.fallback[j]) == fold, (t, res.stats[j])
+        assert res.stats[j, 0] == wc, (repr(t), res.stats[j, 0], wc)
+        assert bool(res.question[j]) == q, (repr(t),)
+        if not fold:
+            assert (res.stats[j, 1], res.stats[j, 2]) == (pos, neg), (repr(t), res.stats[j])
+            assert res.scores(j) == oracle.keyword_scores(t, pats), (repr(t), res.scores(j))
+        th = oracle.token_hashes(t, L)
+        assert res.stats[j, 5] == len(th)
+        assert list(hashes[j, :len(th)]) == th, repr(t)
+
+
+def test_text_analyze_adversarial():
+    _check_batch(ADVERSARIAL)
+
+
+def test_text_analyze_random():
+    _check_batch(_random_texts(777, seed=3))
+
+
+def test_text_analyze_custom_patterns():
+    pats = oracle.default_patterns()
+    pats.setdefault(4, []).append(oracle.compile_pattern("(?i)later"))
+    pats[2].append(oracle.compile_pattern("aa"))           # self-overlapping (bordered)
+    pats[2].append(oracle.compile_pattern("Case"))         # case-sensitive
+    pats[1].append(oracle.compile_pattern("紧急"))          # non-ASCII literal
+    pats[4].append(oracle.compile_pattern("(?i)l[a-z]+r"))  # regex -> host path
+    texts = ["aaaa later LATER Case case", "紧急 紧急紧急", "aaa", "lover later", "CASE"] + _random_texts(50, 9)
+    _check_batch(texts, pats)
+
+
+def test_preprocessor_gpu_matches_cpu():
+    from llm_message_queue_amd.gateway.workload import Workload
+    from llm_message_queue_amd.preprocess.preprocessor import Preprocessor
+    msgs_a = Workload(seed=5).make(300)
+    msgs_b = [m.copy() for m in msgs_a]
+    extra = [("aſap now", 0), ("", 0), ("help", 2), ("x", 3)]
+    from llm_message_queue_amd.models.message import Message
+    for c, p in extra:
+        msgs_a.append(Message(id="e", content=c, priority=p))
+        msgs_b.append(Message(id="e", content=c, priority=p))
+    pre = Preprocessor(use_gpu=True)
+    pre.process_batch(msgs_a, use_gpu=True, classify=True)
+    pre2 = Preprocessor(use_gpu=False)
+    for m in msgs_b:
+        pre2.process_message(m)
+    for a, b in zip(msgs_a, msgs_b):
+        assert a.priority == b.priority
+        ma = {k: v for k, v in a.metadata.items() if k != "ml_priority"}
+        assert ma == b.metadata, (a.content, ma, b.metadata)
+        assert a.queue_name == b.queue_name
+
+
+# ----------------------------------------------------------------------------- classifier
+def test_embed_pool_matches_torch():
+    from llm_message_queue_amd.ops.text import TextPipeline
+    from llm_message_queue_amd.utils.config import PreprocessorConfig
+    texts = _random_texts(200, seed=11) + ["", "one", "two words"] + ["w " * 200]
+    cfg = PreprocessorConfig(max_tokens=64)
+    pipe = TextPipeline(cfg, device=DEV)
+    res = pipe.run(texts, oracle.default_patterns(), classify=True, keep_device=True)
+    w = pipe.weights
+    hashes = res.hashes.cpu().numpy().view(np.uint32)
+    ntok = res.stats[:, 5]
+    E = w.E.float()
+    pooled_ref = torch.zeros((len(texts), w.hidden), device=DEV)
+    for j in range(len(texts)):
+        n = int(ntok[j])
+        if n == 0:
+            continue
+        idx = torch.as_tensor((hashes[j, :n] & (w.vocab - 1)).astype(np.int64), device=DEV)
+        X = E[idx]
+        Hd = X @ w.W1t.float().t() + w.b1
+        Hd = 0.5 * Hd * (1 + torch.tanh(0.7978845608028654 * (Hd + 0.044715 * Hd ** 3)))
+        pooled_ref[j] = Hd.mean(0)
+    err = (res.pooled - pooled_ref).abs().max().item()
+    scale = pooled_ref.abs().max().item()
+    assert err <= 2e-2 * max(1.0, scale), (err, scale)
+    logits_ref = pooled_ref @ w.W2 + w.b2
+    pred_ref = logits_ref[:, :4].argmax(1).cpu().numpy() + 1
+    agree = (pred_ref == res.pred).mean()
+    assert agree > 0.97, agree
+
+
+def test_embed_pool_large_batch_spans_tiles():
+    from llm_message_queue_amd.ops.text import TextPipeline
+    from llm_message_queue_amd.utils.config import PreprocessorConfig
+    texts = [" ".join(f"w{i}_{k}" for k in range(1 + (i * 7) % 90)) for i in range(1500)]
+    pipe = TextPipeline(PreprocessorConfig(max_tokens=128), device=DEV)
+    res = pipe.run(texts, oracle.default_patterns(), classify=True, keep_device=True)
+    assert torch.isfinite(res.pooled).all()
+    w = pipe.weights
+    hashes = res.hashes.cpu().numpy().view(np.uint32)
+    for j in (0, 1, 77, 999, 1499):
+        n = int(res.stats[j, 5])
+        idx = torch.as_tensor((hashes[j, :n] & (w.vocab - 1)).astype(np.int64), device=DEV)
+        Hd = w.E.float()[idx] @ w.W1t.float().t() + w.b1
+        Hd = 0.5 * Hd * (1 + torch.tanh(0.7978845608028654 * (Hd + 0.044715 * Hd ** 3)))
+        assert torch.allclose(res.pooled[j], Hd.mean(0), atol=2e-2, rtol=2e-2)
+
+
+# ----------------------------------------------------------------------------- llama ops
+@pytest.fixture(scope="module")
+def ops():
+    from llm_message_queue_amd.ops.llama_ops import HipOps, RefOps
+    return HipOps(), RefOps()
+
+
+def test_rmsnorm(ops):
+    hip, ref = ops
+    torch.manual_seed(0)
+    x = torch.randn(37, 4096, device=DEV).to(torch.bfloat16)
+    r = torch.randn(37, 4096, device=DEV).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(4096, device=DEV)).to(torch.bfloat16)
+    r1, r2 = r.clone(), r.clone()
+    y1 = hip.rmsnorm(x, w, 1e-5, residual=r1)
+    y2 = ref.rmsnorm(x, w, 1e-5, residual=r2)
+    assert torch.equal(r1, r2)
+    assert (y1.float() - y2.float()).abs().max().item() < 3e-2
+    y3 = hip.rmsnorm(x, w, 1e-5)
+    y4 = ref.rmsnorm(x, w, 1e-5)
+    assert (y3.float() - y4.float()).abs().max().item() < 3e-2
+
+
+def test_silu_mul(ops):
+    hip, ref = ops
+    gu = torch.randn(19, 2 * 1024, device=DEV).to(torch.bfloat16)
+    assert (hip.silu_mul(gu).float() - ref.silu_mul(gu).float()).abs().max().item() < 2e-2
+
+
+def test_rope_kv_and_attention(ops):
+    from llm_message_queue_amd.ops.llama_ops import rope_tables
+    hip, ref = ops
+    torch.manual_seed(1)
+    Hq, Hkv, S, C = 32, 8, 6, 200
+    cos, sin = rope_tables(C, device=DEV)
+    kc1 = torch.zeros(S, Hkv, C, 128, device=DEV, dtype=torch.bfloat16)
+    vc1 = torch.zeros_like(kc1)
+    kc2, vc2 = kc1.clone(), vc1.clone()
+    # slot s has a context of lens[s]; write all positions in one call (prefill)
+    lens = [1, 5, 64, 65, 130, 200]
+    slot = torch.tensor(sum([[s] * n for s, n in enumerate(lens)], []), dtype=torch.int32, device=DEV)
+    pos = torch.tensor(sum([list(range(n)) for n in lens], []), dtype=torch.int32, device=DEV)
+    T = slot.numel()
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * 128, device=DEV).to(torch.bfloat16)
+    q1 = hip.rope_kv(qkv, pos, slot, cos, sin, Hq, Hkv, kc1, vc1)
+    q2 = ref.rope_kv(qkv, pos, slot, cos, sin, Hq, Hkv, kc2, vc2)
+    assert (q1.float() - q2.float()).abs().max().item() < 2e-2
+    assert (kc1.float() - kc2.float()).abs().max().item() < 2e-2
+    assert torch.equal(vc1, vc2)
+    sel = torch.arange(0, T, 7, device=DEV)
+    o1 = hip.attention(q1[sel].contiguous(), kc1, vc1, pos[sel].contiguous(), slot[sel].contiguous(), Hq, Hkv, 128 ** -0.5)
+    o2 = ref.attention(q1[sel].contiguous(), kc1, vc1, pos[sel], slot[sel], Hq, Hkv, 128 ** -0.5)
+    assert (o1.float() - o2.float()).abs().max().item() < 2e-2
+
+
+def test_tiny_model_forward_hip_vs_ref():
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
+    cfg = LlamaConfig.tiny()
+    m1 = LlamaStub(cfg, slots=4, max_ctx=64, device=DEV, impl="hip", seed=3)
+    m2 = LlamaStub(cfg, slots=4, max_ctx=64, device=DEV, impl="ref", seed=3)
+    tok = torch.randint(0, cfg.vocab, (20,), device=DEV)
+    slot = torch.tensor([0] * 10 + [1] * 10, dtype=torch.int32, device=DEV)
+    pos = torch.tensor(list(range(10)) * 2, dtype=torch.int32, device=DEV)
+    samp = torch.tensor([9, 19], device=DEV)
+    a = m1.forward(tok, pos, slot, samp)
+    b = m2.forward(tok, pos, slot, samp)
+    assert a.shape == (2,)
+    # greedy tokens may differ on near-ties; hidden-state agreement is checked per op above
+    assert (a == b).float().mean().item() >= 0.5
+
+
+# ----------------------------------------------------------------------------- summarise
+def test_summarise_project_and_salient():
+    from llm_message_queue_amd.ops.summarise import Summariser
+    torch.manual_seed(4)
+    C = 37
+    counts = [1 + (c * 5) % 9 for c in range(C)]
+    M = sum(counts)
+    pooled = torch.randn(M, 1024, device=DEV)
+    seg = torch.tensor([0] + list(np.cumsum(counts)), dtype=torch.int32, device=DEV)
+    sm = Summariser(dim=256, hidden=1024, alpha=0.75, device=DEV)
+    state = torch.randn(C, 256, device=DEV)
+    first = torch.zeros(C, dtype=torch.int32, device=DEV)
+    first[::5] = 1
+    ref_state = state.clone()
+    sm.project(pooled, seg, state, first)
+    Pt = sm.Pt.float()
+    for c in range(C):
+        a, b = int(seg[c]), int(seg[c + 1])
+        mean = pooled[a:b].mean(0).to(torch.bfloat16).float()
+        proj = Pt @ mean
+        exp = proj if first[c] else 0.75 * ref_state[c] + 0.25 * proj
+        assert torch.allclose(state[c], exp, atol=3e-2, rtol=3e-2), c
+    # salient tokens
+    L = 16
+    hashes = torch.randint(1, 50, (M, L), dtype=torch.int32, device=DEV)
+    ntok = torch.randint(0, L + 1, (M,), dtype=torch.int32, device=DEV)
+    stop = torch.tensor([3, 4], dtype=torch.int32, device=DEV)
+    hs, cs = sm.salient(hashes, ntok, seg, k=5, stop=stop)
+    hh, nn = hashes.cpu().numpy(), ntok.cpu().numpy()
+    for c in range(C):
+        a, b = int(seg[c]), int(seg[c + 1])
+        toks = [int(x) for m in range(a, b) for x in hh[m, :nn[m]] if int(x) not in (3, 4)]
+        exp = oracle_salient(toks, 5)
+        got = [(int(h), int(n)) for h, n in zip(hs[c], cs[c]) if n > 0]
+        assert got == exp, (c, got, exp)
+
+
+def oracle_salient(toks, k):
+    cnt, first = {}, {}
+    for i, t in enumerate(toks):
+        cnt[t] = cnt.get(t, 0) + 1
+        first.setdefault(t, i)
+    return sorted(cnt.items(), key=lambda kv: (-kv[1], first[kv[0]]))[:k]
+
+
+def test_slot_census_page():
+    from llm_message_queue_amd.backend.slot_page import SlotPage
+    from llm_message_queue_amd import _native
+    page = SlotPage("pytest", 0)
+    page.register_device()
+    st = torch.zeros(100, dtype=torch.int32, device=DEV)
+    st[::3] = 1
+    _native.require_hipops().slot_census(st.data_ptr(), 100, 77, 5, page.dev_ptr,
+                                         torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    r = page.read()
+    assert r["active"] == 34 and r["free"] == 66 and r["tokens"] == 77 and r["step"] == 5
+    page.close(unlink=True)
