@@ -1,0 +1,436 @@
+"""REST API (component C17): the reference's 21 routes with the same
+payloads (`api/handlers.go:75-118`), plus ``/metrics`` (D6) and the doc-only
+extras of `docs/api.md` that the gateway can actually serve
+(``GET /api/v1/queues/status``, ``GET /api/v1/config``,
+``PUT /api/v1/messages/:id/status``, ``DELETE /api/v1/messages/:id``,
+``GET /api/v1/conversations``, ``PUT /api/v1/conversations/:id``).
+
+Behaviour notes vs the reference:
+  * ``priority`` accepts ints or level names (D4); timeouts default to 30 s (D16);
+  * stub routes are implemented (D24): get/list messages, preprocessor rule
+    admin, remove message, dead-letter requeue by id / all;
+  * ``GET /conversations/:id`` returns 404 for unknown ids (D19, the docs'
+    contract); POST paths keep get-or-create;
+  * ``setUserPriority`` accepts ``realtime`` (D18);
+  * ``estimated_wait`` comes from live queue depth / dispatch rate;
+  * CORS: echo an allowed Origin (or any, with "*"), allow credentials,
+    OPTIONS -> 204 (`:121-148`).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, Response
+
+from ..balancer.load_balancer import Endpoint, LoadBalancerError
+from ..models.message import (ConversationNotFound, ConversationState, Message, MessageStatus,
+                              PriorityParseError, format_time, level_priority_from_name, parse_priority,
+                              priority_name)
+from ..preprocess import oracle
+from ..queue.core import QueueError
+from ..scheduler.resource_scheduler import Resource, ResourceError
+from ..utils.metrics import CONTENT_TYPE_LATEST
+
+VERSION = "1.0.0"
+
+
+def _err(code: int, msg: str) -> JSONResponse:
+    return JSONResponse({"error": msg}, status_code=code)
+
+
+async def _json(request: Request) -> Any:
+    raw = await request.body()
+    if not raw:
+        raise ValueError("EOF")
+    return json.loads(raw)
+
+
+def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
+    """``gw_app`` is a ``gateway.app.GatewayApp``."""
+    app = FastAPI(title="llm_message_queue_amd", version=VERSION)
+    origins = allowed_origins if allowed_origins is not None else ["*"]
+    G = gw_app
+
+    # ------------------------------------------------------------------ CORS
+    @app.middleware("http")
+    async def cors(request: Request, call_next):
+        origin = request.headers.get("origin", "")
+        if request.method == "OPTIONS":
+            resp: Response = Response(status_code=204)
+        else:
+            resp = await call_next(request)
+        if origin and ("*" in origins or origin in origins):
+            resp.headers["Access-Control-Allow-Origin"] = origin
+            resp.headers["Access-Control-Allow-Credentials"] = "true"
+            resp.headers["Access-Control-Allow-Headers"] = \
+                "Content-Type, Content-Length, Accept-Encoding, X-CSRF-Token, Authorization, accept, origin, Cache-Control, X-Requested-With"
+            resp.headers["Access-Control-Allow-Methods"] = "POST, OPTIONS, GET, PUT, DELETE"
+        return resp
+
+    # ------------------------------------------------------------------ health / metrics
+    @app.get("/health")
+    def health():
+        return {"status": "ok", "version": VERSION, "time": format_time(time.time_ns())}
+
+    @app.get("/metrics")
+    def metrics():
+        return Response(G.metrics.render(), media_type=CONTENT_TYPE_LATEST)
+
+    # ------------------------------------------------------------------ messages
+    def _bind_message(body: Any) -> Message:
+        m = Message.from_dict(body)
+        if not m.id:
+            m.id = str(uuid.uuid4())
+        now = time.time_ns()
+        m.created_at = m.updated_at = now
+        return m
+
+    def _enqueue(m: Message) -> Optional[JSONResponse]:
+        if G.cfg.queue.enable_metrics:
+            m.metadata["analysis"] = json.dumps(G.preprocessor.analyze_message_content(m.content),
+                                                separators=(",", ":"))
+        try:
+            err = G.submit(m)
+        except Exception as e:
+            return _err(500, f"Failed to queue message: {e}")
+        if err is not None:
+            return _err(500, "Failed to queue message")
+        return None
+
+    @app.post("/api/v1/messages")
+    async def submit_message(request: Request):
+        try:
+            m = _bind_message(await _json(request))
+        except (ValueError, PriorityParseError, TypeError) as e:
+            return _err(400, f"Invalid message format: {e}")
+        bad = _enqueue(m)
+        if bad is not None:
+            return bad
+        if m.conversation_id:
+            G.state.get_conversation(m.conversation_id, m.user_id)
+            try:
+                G.state.add_message(m.conversation_id, m)
+            except ConversationNotFound:
+                pass
+        return JSONResponse({"message_id": m.id, "priority": int(m.priority),
+                             "queue_time": format_time(time.time_ns()),
+                             "estimated_wait": G.estimated_wait_ns(m)}, status_code=202)
+
+    @app.get("/api/v1/messages/{mid}")
+    def get_message(mid: str):
+        m = G.messages.get(mid)
+        if m is None:
+            return _err(404, "Message not found")
+        return m.to_dict()
+
+    @app.get("/api/v1/messages")
+    def list_messages(user_id: str = "", conversation_id: str = "", status: str = "", limit: int = 10,
+                      offset: int = 0):
+        total, msgs = G.messages.query(user_id, conversation_id, status, max(0, limit), max(0, offset))
+        return {"messages": [m.to_dict() for m in msgs], "total": total, "limit": limit, "offset": offset}
+
+    @app.put("/api/v1/messages/{mid}/status")
+    async def update_message_status(mid: str, request: Request):
+        try:
+            body = await _json(request)
+            status = str(body["status"])
+        except Exception as e:
+            return _err(400, f"Invalid request format: {e}")
+        if status not in MessageStatus.ALL:
+            return _err(400, f"invalid status {status!r}")
+        m = G.messages.get(mid)
+        if m is None:
+            return _err(404, "Message not found")
+        m.status = status
+        m.updated_at = time.time_ns()
+        return {"status": "updated", "message_id": mid}
+
+    @app.delete("/api/v1/messages/{mid}")
+    def delete_message(mid: str):
+        m = G.messages.get(mid)
+        if m is None:
+            return _err(404, "Message not found")
+        removed = m.queue_name and G.standard.has_queue(m.queue_name) and G.standard.mlq.remove(m.queue_name, m)
+        G.messages.remove(mid)
+        return {"status": "deleted", "message_id": mid, "dequeued": bool(removed)}
+
+    # ------------------------------------------------------------------ conversations
+    @app.post("/api/v1/conversations")
+    async def create_conversation(request: Request):
+        try:
+            body = await _json(request)
+            user_id = body.get("user_id")
+            if not user_id:
+                raise ValueError("Key: 'user_id' Error:Field validation for 'user_id' failed on the 'required' tag")
+            md = body.get("metadata") or {}
+            if not isinstance(md, dict):
+                raise ValueError("metadata must be an object")
+        except Exception as e:
+            return _err(400, f"Invalid request format: {e}")
+        conv = G.state.create_conversation(str(user_id), md)
+        return JSONResponse({"conversation_id": conv.id, "user_id": conv.user_id,
+                             "created_at": format_time(conv.created_at), "state": conv.state}, status_code=201)
+
+    @app.get("/api/v1/conversations")
+    def list_conversations(user_id: str = "", state: str = "", limit: int = 20, offset: int = 0):
+        if user_id:
+            convs = G.state.get_user_conversations(user_id)
+        else:
+            with G.state._lock:
+                convs = list(G.state._convs.values())
+        if state:
+            convs = [c for c in convs if c.state == state]
+        return {"conversations": [c.to_dict(False) for c in convs[offset:offset + limit]], "total": len(convs)}
+
+    @app.get("/api/v1/conversations/{cid}")
+    def get_conversation(cid: str):
+        conv = G.state.find_conversation(cid)
+        if conv is None:
+            return _err(404, "Conversation not found")
+        return conv.to_dict()
+
+    @app.put("/api/v1/conversations/{cid}")
+    async def update_conversation(cid: str, request: Request):
+        try:
+            body = await _json(request)
+        except Exception as e:
+            return _err(400, f"Invalid request format: {e}")
+        conv = G.state.find_conversation(cid)
+        if conv is None:
+            return _err(404, "Conversation not found")
+        if "metadata" in body:
+            G.state.update_conversation_metadata(cid, body.get("metadata") or {})
+        if "state" in body:
+            G.state.update_conversation_state(cid, str(body["state"]))
+        if "title" in body:
+            conv.title = str(body["title"])
+        return conv.to_dict(False)
+
+    @app.post("/api/v1/conversations/{cid}/messages")
+    async def add_message_to_conversation(cid: str, request: Request):
+        try:
+            m = _bind_message(await _json(request))
+        except (ValueError, PriorityParseError, TypeError) as e:
+            return _err(400, f"Invalid message format: {e}")
+        m.conversation_id = cid
+        # route sticky to the GPU holding this conversation's KV (residency hint)
+        home = G.state.home_gpu(cid)
+        if home >= 0:
+            m.metadata.setdefault("home_gpu", home)
+        try:
+            G.state.add_message(cid, m)
+        except ConversationNotFound:
+            return _err(500, "Failed to add message to conversation")
+        bad = _enqueue(m)
+        if bad is not None:
+            return bad
+        return JSONResponse({"message_id": m.id, "conversation_id": cid, "priority": int(m.priority),
+                             "queue_time": format_time(time.time_ns()),
+                             "estimated_wait": G.estimated_wait_ns(m)}, status_code=202)
+
+    @app.put("/api/v1/conversations/{cid}/state")
+    async def update_conversation_state(cid: str, request: Request):
+        try:
+            body = await _json(request)
+            state = body.get("state")
+            if not state:
+                raise ValueError("Key: 'state' Error:Field validation for 'state' failed on the 'required' tag")
+        except Exception as e:
+            return _err(400, f"Invalid request format: {e}")
+        try:
+            G.state.update_conversation_state(cid, str(state))
+        except ConversationNotFound:
+            return _err(500, "Failed to update conversation state")
+        if isinstance(body.get("metadata"), dict):
+            G.state.update_conversation_metadata(cid, body["metadata"])
+        return {"status": "updated"}
+
+    @app.get("/api/v1/users/{user_id}/conversations")
+    def list_user_conversations(user_id: str):
+        return {"conversations": [c.to_dict() for c in G.state.get_user_conversations(user_id)]}
+
+    # ------------------------------------------------------------------ queues
+    @app.get("/api/v1/queues/stats")
+    def queue_stats():
+        return G.queue_stats()
+
+    @app.get("/api/v1/queues/status")
+    def queue_status():
+        tiers = []
+        for t, name in enumerate(G.gateway.tiers):
+            st = G.standard.get_queue_stats(name)
+            tiers.append({"name": name, "priority": G.gateway.tier_prio[t], "pending": st.pending_count,
+                          "processing": st.processing_count, "completed": st.completed_count,
+                          "failed": st.failed_count,
+                          "avg_wait_ms": (st.total_wait_time / max(1, st.completed_count + st.processing_count
+                                                                   + st.failed_count)) / 1e6})
+        lat = G.gateway.rec.summary()
+        return {"queues": tiers, "total_pending": G.standard.total_pending(), "latency": lat,
+                "dead_letter": G.factory.dead_letter_queue.size(), "delayed": G.factory.delayed_queue.size()}
+
+    # ------------------------------------------------------------------ resources
+    @app.post("/api/v1/resources")
+    async def register_resource(request: Request):
+        try:
+            r = Resource.from_dict(await _json(request))
+        except Exception as e:
+            return _err(400, f"Invalid resource format: {e}")
+        try:
+            G.resources.register_resource(r)
+        except ResourceError as e:
+            return _err(500, f"Failed to register resource: {e}")
+        return JSONResponse({"resource_id": r.id, "status": "registered"}, status_code=201)
+
+    @app.get("/api/v1/resources")
+    def list_resources():
+        return {"resources": [r.to_dict() for r in G.resources.get_all_resources()]}
+
+    @app.get("/api/v1/resources/stats")
+    def resource_stats():
+        return G.resources.get_resource_stats()
+
+    # ------------------------------------------------------------------ endpoints
+    @app.post("/api/v1/endpoints")
+    async def register_endpoint(request: Request):
+        try:
+            ep = Endpoint.from_dict(await _json(request))
+        except Exception as e:
+            return _err(400, f"Invalid endpoint format: {e}")
+        try:
+            G.lb.add_endpoint(ep)
+        except LoadBalancerError as e:
+            return _err(500, f"Failed to register endpoint: {e}")
+        return JSONResponse({"endpoint_id": ep.id, "status": "registered"}, status_code=201)
+
+    @app.delete("/api/v1/endpoints/{eid}")
+    def remove_endpoint(eid: str):
+        try:
+            G.lb.remove_endpoint(eid)
+        except LoadBalancerError:
+            return _err(404, "endpoint not found")
+        return {"endpoint_id": eid, "status": "removed"}
+
+    @app.put("/api/v1/endpoints/{eid}/status")
+    async def update_endpoint_status(eid: str, request: Request):
+        try:
+            status = str((await _json(request))["status"])
+            G.lb.update_endpoint_status(eid, status)
+        except LoadBalancerError:
+            return _err(404, "endpoint not found")
+        except Exception as e:
+            return _err(400, f"Invalid request format: {e}")
+        return {"endpoint_id": eid, "status": status}
+
+    @app.get("/api/v1/endpoints")
+    def list_endpoints():
+        return {"endpoints": [e.to_dict() for e in G.lb.get_all_endpoints()]}
+
+    @app.get("/api/v1/endpoints/stats")
+    def endpoint_stats():
+        return G.lb.get_endpoint_stats()
+
+    # ------------------------------------------------------------------ admin
+    @app.post("/api/v1/admin/preprocessor/rules")
+    async def add_priority_rule(request: Request):
+        try:
+            body = await _json(request)
+            pattern = str(body.get("pattern") or body.get("rule") or "")
+            if not pattern:
+                raise ValueError("pattern is required")
+            prio = parse_priority(body.get("priority"), 0)
+            if prio <= 0:
+                raise ValueError("priority is required")
+        except Exception as e:
+            return _err(400, f"Invalid rule format: {e}")
+        try:
+            G.preprocessor.add_keyword_pattern(prio, pattern)
+        except Exception as e:
+            return _err(400, f"Invalid pattern: {e}")
+        return JSONResponse({"status": "rule added"}, status_code=201)
+
+    @app.get("/api/v1/admin/preprocessor/rules")
+    def list_priority_rules():
+        rules = [{"priority": p, "priority_name": priority_name(p), "pattern": s}
+                 for p, pats in G.preprocessor.all_patterns().items() for s in pats]
+        return {"rules": rules}
+
+    @app.delete("/api/v1/admin/preprocessor/rules")
+    async def remove_priority_rule(request: Request):
+        try:
+            body = await _json(request)
+            ok = G.preprocessor.remove_keyword_pattern(parse_priority(body.get("priority")), str(body["pattern"]))
+        except Exception as e:
+            return _err(400, f"Invalid rule format: {e}")
+        return {"status": "rule removed"} if ok else _err(404, "rule not found")
+
+    @app.post("/api/v1/admin/preprocessor/user-priorities")
+    async def set_user_priority(request: Request):
+        try:
+            body = await _json(request)
+            user_id = body.get("user_id")
+            pstr = body.get("priority")
+            if not user_id or pstr in (None, ""):
+                raise ValueError("user_id and priority are required")
+        except Exception as e:
+            return _err(400, f"Invalid request format: {e}")
+        p = level_priority_from_name(pstr) if isinstance(pstr, str) else None
+        if p is None:
+            try:
+                p = parse_priority(pstr)
+            except PriorityParseError:
+                p = 3
+        if p not in (1, 2, 3, 4):
+            p = 3
+        G.preprocessor.set_user_priority(str(user_id), p)
+        return {"status": "user priority set"}
+
+    @app.delete("/api/v1/admin/queues/{queue_type}/{mid}")
+    def remove_message(queue_type: str, mid: str):
+        if queue_type not in ("standard", "delayed", "dead_letter", "priority"):
+            return _err(400, "Invalid queue type")
+        if queue_type == "dead_letter":
+            dlq = G.factory.dead_letter_queue
+            i = dlq.index_of(mid)
+            if i < 0:
+                return _err(404, "Message not found")
+            dlq.remove(i)
+            return {"status": "removed", "message_id": mid}
+        if queue_type == "delayed":
+            return _err(404, "Message not found")
+        mgr = G.factory.get_queue_manager(queue_type)
+        m = G.messages.get(mid)
+        if mgr is None or m is None or not m.queue_name or not mgr.has_queue(m.queue_name) \
+                or not mgr.mlq.remove(m.queue_name, m):
+            return _err(404, "Message not found")
+        return {"status": "removed", "message_id": mid}
+
+    @app.post("/api/v1/admin/dead-letter/requeue/{mid}")
+    def requeue_dead_letter(mid: str):
+        try:
+            G.factory.dead_letter_queue.requeue_by_id(mid, G.standard)
+        except QueueError as e:
+            return _err(404 if e.code == "INDEX_OUT_OF_RANGE" else 500, str(e))
+        return {"status": "requeued", "message_id": mid}
+
+    @app.post("/api/v1/admin/dead-letter/requeue-all")
+    def requeue_all_dead_letter():
+        n = G.factory.dead_letter_queue.requeue_all(G.standard)
+        return {"status": "requeued", "count": n}
+
+    @app.get("/api/v1/admin/dead-letter")
+    def list_dead_letter():
+        return {"items": [it.to_dict() for it in G.factory.dead_letter_queue.get_all()]}
+
+    @app.get("/api/v1/config")
+    def get_config():
+        d = dataclasses.asdict(G.cfg)
+        d["database"]["postgres"]["password"] = "***"
+        d["database"]["redis"]["password"] = "***"
+        return d
+
+    return app

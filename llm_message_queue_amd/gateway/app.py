@@ -1,0 +1,228 @@
+"""Monolith wiring (component C18, `cmd/server/main.go`), fixed:
+  * the four level queues exist before the first request (D1);
+  * a dispatcher always runs (D2): with a GPU, the gateway tick loop feeds
+    the local Llama-stub backend (and, under torchrun, the other ranks' GPUs
+    via the RCCL planner); without a GPU, QueueFactory workers drain the level
+    queues with a simulated LLM call that goes through the LoadBalancer's
+    GetEndpoint/ReleaseEndpoint (what `cmd/queue-manager/main.go:141-166`
+    simulates);
+  * defaults merged / intervals validated (D3) by ``utils.config``.
+"""
+from __future__ import annotations
+
+import collections
+import threading
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..balancer.load_balancer import Endpoint, LoadBalancer
+from ..conversation.persistence import make_store
+from ..conversation.state_manager import StateManager
+from ..models.message import Message, MessageStatus, priority_name
+from ..preprocess.preprocessor import Preprocessor
+from ..queue.core import QueueError
+from ..queue.factory import QueueFactory, QueueType
+from ..scheduler.resource_scheduler import ResourceScheduler
+from ..utils.logging import get_logger
+from ..utils.metrics import QueueMetrics, default_metrics
+from .ingress import MicroBatcher
+from .router import Gateway
+
+# reference fixed estimates (api/handlers.go:729-744), used before rates exist
+_REF_WAIT_NS = {1: 1_000_000_000, 2: 5_000_000_000, 3: 15_000_000_000, 4: 30_000_000_000}
+
+
+class MessageStore:
+    """Bounded id -> Message index for GET /messages (stubs in the reference)."""
+
+    def __init__(self, max_items: int = 200_000):
+        self._d: "collections.OrderedDict[str, Message]" = collections.OrderedDict()
+        self._lock = threading.Lock()
+        self.max_items = max_items
+
+    def put(self, m: Message) -> None:
+        with self._lock:
+            self._d[m.id] = m
+            self._d.move_to_end(m.id)
+            while len(self._d) > self.max_items:
+                self._d.popitem(last=False)
+
+    def get(self, mid: str) -> Optional[Message]:
+        with self._lock:
+            return self._d.get(mid)
+
+    def remove(self, mid: str) -> Optional[Message]:
+        with self._lock:
+            return self._d.pop(mid, None)
+
+    def query(self, user_id: str = "", conversation_id: str = "", status: str = "", limit: int = 10,
+              offset: int = 0) -> Tuple[int, List[Message]]:
+        with self._lock:
+            items = list(self._d.values())
+        sel = [m for m in items if (not user_id or m.user_id == user_id)
+               and (not conversation_id or m.conversation_id == conversation_id)
+               and (not status or m.status == status)]
+        return len(sel), sel[offset:offset + limit]
+
+
+class GatewayApp:
+    def __init__(self, cfg, *, use_gpu: Optional[bool] = None, engine=None, comm=None,
+                 simulate_ms: Sequence[float] = (5, 10, 20, 30), start: bool = True):
+        import torch
+        self.cfg = cfg
+        self.log = get_logger("app")
+        self.metrics: QueueMetrics = default_metrics()
+        gpu = torch.cuda.is_available() if use_gpu is None else use_gpu
+        self.gpu = gpu
+        self.preprocessor = Preprocessor(cfg.preprocessor, use_gpu=gpu and cfg.preprocessor.use_gpu)
+        self.factory = QueueFactory(cfg.queue, metrics=self.metrics)
+        self.standard = self.factory.create_queue_manager("standard", QueueType.STANDARD)
+        self.factory.create_queue_manager("delayed", QueueType.DELAYED)
+        self.factory.create_queue_manager("dead_letter", QueueType.DEAD_LETTER)
+        self.factory.create_queue_manager("priority", QueueType.PRIORITY)
+        self.lb = LoadBalancer(cfg.loadbalancer)
+        self.resources = ResourceScheduler.from_config(cfg.scheduler)
+        store = make_store(cfg)
+        summary = None
+        if cfg.conversation.summarise_on_evict:
+            from ..conversation.summarise import SummaryEngine
+            summary = SummaryEngine(cfg.preprocessor, device="cuda" if gpu else "cpu",
+                                    k=cfg.conversation.salient_tokens, alpha=cfg.conversation.summary_alpha)
+        self.state = StateManager.from_config(cfg, persistence=store, summary_engine=summary)
+        self.messages = MessageStore()
+        self.engine = engine
+        self.gateway = Gateway(cfg, preprocessor=self.preprocessor, engine=engine, comm=comm,
+                               load_balancer=self.lb if engine is not None else None, metrics=self.metrics,
+                               state_manager=self.state, use_gpu_preprocess=self.preprocessor.gpu_enabled(),
+                               queue_manager=self.standard)
+        self.gateway.on_complete = self._on_complete
+        self.batcher = MicroBatcher(self._flush, cfg.preprocessor.batch_window_us, cfg.preprocessor.max_batch)
+        self._stop = threading.Event()
+        self._wake = threading.Event()
+        self._loop_thread: Optional[threading.Thread] = None
+        self.simulate_ns = [int(x * 1e6) for x in simulate_ms]
+        self._workers = []
+        self._dispatch_times: "collections.deque[Tuple[float, int]]" = collections.deque(maxlen=64)
+        if start:
+            self.start()
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> None:
+        self.state.start()
+        if self.engine is not None:
+            self._loop_thread = threading.Thread(target=self._serve_loop, name="gateway-loop", daemon=True)
+            self._loop_thread.start()
+        else:
+            if not self.lb.get_all_endpoints():
+                self.lb.add_endpoint(Endpoint(id="local-sim", url="", name="simulated LLM", type="llm",
+                                              max_connections=self.cfg.queue.worker.max_concurrent))
+            for tier in self.gateway.tiers:
+                self._workers += self.factory.create_workers("standard", 1, self._simulate, queue_name=tier) or []
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._wake.set()
+        if self._loop_thread is not None:
+            self._loop_thread.join(timeout=10)
+        self.batcher.close()
+        self.factory.close()
+        self.state.stop()
+        self.resources.stop()
+        self.lb.stop()
+
+    # ------------------------------------------------------------------ ingest
+    def _flush(self, msgs: Sequence[Message]) -> List[Optional[QueueError]]:
+        self.preprocessor.process_batch(msgs, use_gpu=self.preprocessor.gpu_enabled(),
+                                        prompt_cap=self.gateway.prompt_cap)
+        for m in msgs:
+            if not m.queue_name:
+                m.queue_name = priority_name(m.priority)
+        errs = self.standard.push_routed(msgs)
+        for m, e in zip(msgs, errs):
+            if e is None:
+                self.messages.put(m)
+        self._wake.set()
+        return errs
+
+    def submit(self, msg: Message, timeout_s: float = 30.0) -> Optional[QueueError]:
+        """Preprocess (micro-batched on the GPU) and enqueue one message."""
+        if not msg.arrival_ns:
+            msg.arrival_ns = time.monotonic_ns()
+        return self.batcher.submit(msg).result(timeout=timeout_s)
+
+    def estimated_wait_ns(self, msg: Message) -> int:
+        """Requests ahead of this one / observed dispatch rate (reference:
+        fixed per-tier constants, used until a rate is known)."""
+        rate = self._dispatch_rate()
+        if rate <= 0:
+            return _REF_WAIT_NS.get(msg.priority, 15_000_000_000)
+        ahead = 0
+        for t, name in enumerate(self.gateway.tiers):
+            if self.gateway.tier_prio[t] <= msg.priority:
+                ahead += self.standard.size(name)
+        return int(ahead / rate * 1e9)
+
+    def _dispatch_rate(self) -> float:
+        d = list(self._dispatch_times)
+        if len(d) < 2 or d[-1][0] <= d[0][0]:
+            return 0.0
+        return (d[-1][1] - d[0][1]) / (d[-1][0] - d[0][0])
+
+    # ------------------------------------------------------------------ dispatch
+    def _serve_loop(self) -> None:
+        gw = self.gateway
+        while not self._stop.is_set():
+            gw.tick()
+            self._dispatch_times.append((time.monotonic(), gw.counters["dispatched"]))
+            if self.engine.inflight() == 0 and gw.pending() == 0:
+                self._wake.wait(0.01)
+                self._wake.clear()
+
+    def _simulate(self, ctx, msg: Message):
+        """CPU mode process function: LB pick -> simulated LLM latency -> release."""
+        ep = self.lb.get_endpoint(msg, msg.conversation_id)
+        msg.endpoint_id = ep.id
+        t0 = time.monotonic_ns()
+        if msg.dispatched_at == 0:
+            msg.dispatched_at = t0
+            self.gateway.rec.record(np.array([min(max(msg.priority, 1), 4) - 1]),
+                                    np.array([t0 - (msg.arrival_ns or t0)]),
+                                    np.array([t0 - (msg.enqueued_at or t0)]))
+            self.gateway.counters["dispatched"] += 1
+            self._dispatch_times.append((time.monotonic(), self.gateway.counters["dispatched"]))
+        dur = self.simulate_ns[min(max(msg.priority, 1), 4) - 1] / 1e9
+        err = None
+        if ctx.err() is None:
+            time.sleep(dur)
+        fail = msg.metadata.get("simulate_error") if isinstance(msg.metadata, dict) else None
+        if fail:
+            err = RuntimeError(str(fail))
+        self.lb.release_endpoint(ep.id, time.monotonic_ns() - t0, err is not None)
+        if err is None:
+            self._on_complete(msg)
+        return err
+
+    def _on_complete(self, msg: Message) -> None:
+        msg.status = MessageStatus.COMPLETED
+        msg.completed_at = time.time_ns()
+        if msg.conversation_id:
+            conv = self.state.find_conversation(msg.conversation_id)
+            if conv is not None and msg.endpoint_id.startswith("gpu"):
+                try:
+                    self.state.set_home_gpu(msg.conversation_id, int(msg.endpoint_id[3:]))
+                except ValueError:
+                    pass
+
+    # ------------------------------------------------------------------ stats
+    def queue_stats(self) -> Dict[str, object]:
+        out: Dict[str, object] = {}
+        for name, mgr in self.factory.managers().items():
+            out[name] = {q: s.to_dict() for q, s in mgr.get_all_queue_stats().items()}
+        out["workers"] = {q: [w.to_dict() for w in ws] for q, ws in self.factory.get_worker_stats().items()}
+        out["dispatch"] = dict(self.gateway.counters)
+        out["latency"] = self.gateway.rec.summary()
+        out["dead_letter"] = self.factory.dead_letter_queue.size()
+        out["delayed"] = self.factory.delayed_queue.size()
+        return out

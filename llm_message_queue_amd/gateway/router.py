@@ -113,7 +113,8 @@ class Gateway:
     def __init__(self, cfg, *, preprocessor=None, engine: Optional[BackendEngine] = None,
                  comm: Optional[Comm] = None, load_balancer=None, metrics=None, state_manager=None,
                  use_gpu_preprocess: Optional[bool] = None, prompt_cap: Optional[int] = None,
-                 gen_tokens: Optional[int] = None, name: str = "gateway"):
+                 gen_tokens: Optional[int] = None, name: str = "gateway",
+                 queue_manager: Optional[QueueManager] = None):
         from ..preprocess.preprocessor import Preprocessor
         self.cfg = cfg
         self.log = get_logger("gateway")
@@ -129,7 +130,7 @@ class Gateway:
         self.prompt_cap = int(prompt_cap if prompt_cap is not None else cfg.backend.prompt_tokens)
         self.gen_tokens = int(gen_tokens if gen_tokens is not None else cfg.backend.gen_tokens)
         q = cfg.queue
-        self.qm = QueueManager(QueueManagerConfig(
+        self.qm = queue_manager or QueueManager(QueueManagerConfig(
             default_max_size=q.default_max_size, monitor_interval=q.monitor_interval,
             cleanup_interval=q.cleanup_interval, max_retention_period=q.max_retention_period,
             enable_metrics=q.enable_metrics and metrics is not None, enable_auto_scaling=q.enable_auto_scaling,

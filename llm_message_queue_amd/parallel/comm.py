@@ -87,9 +87,9 @@ class TorchComm(Comm):
     def all_gather_i64(self, vec):
         torch = self.torch
         v = torch.as_tensor(np.asarray(vec, dtype=np.int64)).to(self.device)
-        out = torch.empty((self.world, v.numel()), dtype=torch.int64, device=self.device)
+        out = torch.empty(self.world * v.numel(), dtype=torch.int64, device=self.device)
         self.dist.all_gather_into_tensor(out, v.reshape(-1), group=self.group)
-        return out.cpu().numpy()
+        return out.cpu().numpy().reshape(self.world, -1)
 
     def all_to_all_rows(self, send, recv_counts, width):
         torch = self.torch

@@ -338,16 +338,13 @@ def load_config(config_path: Optional[str] = None, *, environ: Optional[Dict[str
     import yaml
 
     cfg = default_config()
-    candidates: List[str] = []
     if config_path:
-        if os.path.isdir(config_path):
-            candidates.append(os.path.join(config_path, "config.yaml"))
-        else:
-            candidates.append(config_path)
-    candidates += [os.path.join(".", "config.yaml"), os.path.join(".", "configs", "config.yaml")]
-    found = next((c for c in candidates if os.path.isfile(c)), None)
-    if found is None and config_path:
-        raise ConfigError(f"config file not found under {config_path!r}")
+        found = os.path.join(config_path, "config.yaml") if os.path.isdir(config_path) else config_path
+        if not os.path.isfile(found):
+            raise ConfigError(f"config file not found under {config_path!r}")
+    else:
+        candidates = [os.path.join(".", "config.yaml"), os.path.join(".", "configs", "config.yaml")]
+        found = next((c for c in candidates if os.path.isfile(c)), None)
     if found:
         with open(found, "r", encoding="utf-8") as fh:
             data = yaml.safe_load(fh) or {}

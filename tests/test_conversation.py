@@ -1,0 +1,193 @@
+"""Conversation state (C14), persistence stores (C15), DB-backed manager (C16)
+and the summarise-on-evict engine (N5, CPU reference path here; the HIP path
+is in test_gpu_kernels.py)."""
+import time
+
+import numpy as np
+import pytest
+
+from llm_message_queue_amd.conversation.db_state import DBStateManager
+from llm_message_queue_amd.conversation.persistence import (MemoryPersistenceStore, PostgresPersistenceStore,
+                                                            RedisPersistenceStore, SQLitePersistenceStore)
+from llm_message_queue_amd.conversation.resp import MiniRedis, RespClient
+from llm_message_queue_amd.conversation.state_manager import DAY_NS, StateManager
+from llm_message_queue_amd.conversation.summarise import SummaryEngine
+from llm_message_queue_amd.models.message import (Conversation, ConversationNotFound, MessageStatus,
+                                                  new_message)
+
+
+def sm(**kw):
+    kw.setdefault("cleanup_interval", 0)
+    return StateManager(**kw)
+
+
+def test_get_or_create_and_find():
+    s = sm()
+    c = s.get_conversation("c1", "u1")
+    assert c.id == "c1" and c.user_id == "u1" and c.state == "active"
+    assert s.get_conversation("c1") is c
+    assert s.find_conversation("nope") is None
+
+
+def test_add_message_truncates_and_queues_evictions():
+    s = sm(max_context_length=3)
+    s.get_conversation("c", "u")
+    for i in range(5):
+        s.add_message("c", new_message("c", "u", f"m{i}", 3))
+    msgs = s.get_conversation_context("c")
+    assert [m.content for m in msgs] == ["m2", "m3", "m4"]
+    assert [m.content for m in s.get_conversation_context("c", 2)] == ["m3", "m4"]
+    assert s.pending_evictions() == 2
+    with pytest.raises(ConversationNotFound):
+        s.add_message("missing", new_message("x", "u", "m", 3))
+
+
+def test_state_metadata_delete_and_user_index():
+    s = sm()
+    c = s.create_conversation("u", {"a": 1})
+    s.update_conversation_state(c.id, "completed")
+    assert c.state == "completed" and c.completed_at > 0
+    s.update_conversation_metadata(c.id, {"b": 2})
+    assert c.metadata == {"a": 1, "b": 2}
+    assert [x.id for x in s.get_user_conversations("u")] == [c.id]
+    s.delete_conversation(c.id)
+    assert s.get_user_conversations("u") == []
+    with pytest.raises(ConversationNotFound):
+        s.delete_conversation(c.id)
+
+
+def test_user_cap_archives_oldest():
+    s = sm(max_conversations=2)
+    a = s.create_conversation("u")
+    b = s.create_conversation("u")
+    c = s.create_conversation("u")
+    assert a.state == "archived" and b.state == "active" and c.state == "active"
+
+
+def test_cleanup_rules():
+    s = sm(conversation_ttl=1000 * DAY_NS, max_idle_time=60 * 1_000_000_000)
+    old = s.create_conversation("u")
+    idle = s.create_conversation("u")
+    done = s.create_conversation("u")
+    fresh = s.create_conversation("u")
+    now = time.time_ns()
+    idle.last_active_time = now - 120 * 1_000_000_000
+    done.state, done.completed_at = "completed", now - 2 * DAY_NS
+    old.created_at = now - 1001 * DAY_NS
+    assert s.cleanup_expired_conversations(now) == 3
+    assert s.find_conversation(fresh.id) is fresh
+
+
+@pytest.mark.parametrize("kind", ["memory", "sqlite", "redis"])
+def test_persistence_roundtrip(kind, tmp_path):
+    srv = None
+    if kind == "memory":
+        store = MemoryPersistenceStore()
+    elif kind == "sqlite":
+        store = SQLitePersistenceStore(str(tmp_path / "s.db"))
+    else:
+        srv = MiniRedis()
+        store = RedisPersistenceStore(RespClient(srv.addr), "conversation:", 3600 * 1_000_000_000)
+    try:
+        c = Conversation("c1", "u1")
+        c.messages.append(new_message("c1", "u1", "hello", 2))
+        c.summary_vec = [0.5] * 4
+        store.save_conversation(c)
+        got = store.load_conversation("c1")
+        assert got.user_id == "u1" and got.messages[0].content == "hello" and got.summary_vec == [0.5] * 4
+        assert store.list_user_conversations("u1") == ["c1"]
+        store.delete_conversation("c1")
+        assert store.list_user_conversations("u1") == []
+        with pytest.raises(ConversationNotFound):
+            store.load_conversation("c1")
+    finally:
+        if srv is not None:
+            srv.close()
+
+
+def test_postgres_store_gated():
+    try:
+        import psycopg2  # noqa: F401
+        pytest.skip("psycopg2 present")
+    except ImportError:
+        with pytest.raises(RuntimeError):
+            PostgresPersistenceStore("host=localhost")
+
+
+def test_async_write_behind_and_reload():
+    store = MemoryPersistenceStore()
+    s = sm(persistence=store)
+    s.start()
+    c = s.create_conversation("u")
+    for i in range(50):
+        s.add_message(c.id, new_message(c.id, "u", f"m{i}", 3))
+    s.stop()
+    assert store.saves < 51                        # coalesced
+    loaded = store.load_conversation(c.id)
+    assert len(loaded.messages) == 50
+    s2 = sm(persistence=store)
+    assert s2.find_conversation(c.id).message_count == 50
+    assert [x.id for x in s2.get_user_conversations("u")] == [c.id]
+
+
+def test_summarise_on_evict_cpu_reference():
+    eng = SummaryEngine(device="cpu", k=4)
+    s = sm(max_context_length=2, summary_engine=eng)
+    c = s.get_conversation("c", "u")
+    for i in range(6):
+        s.add_message("c", new_message("c", "u", f"apple banana apple cherry {i}", 3))
+    assert s.summarise_pending() == 1
+    assert c.summary_vec is not None and np.asarray(c.summary_vec).shape == (256,)
+    assert c.evicted_count == 4
+    from llm_message_queue_amd.preprocess.oracle import fnv1a32
+    assert c.summary_tokens[0] == fnv1a32(b"apple")
+    v1 = np.asarray(c.summary_vec).copy()
+    for i in range(3):
+        s.add_message("c", new_message("c", "u", f"zebra quartz {i}", 3))
+    s.summarise_pending()
+    assert c.evicted_count == 7 and not np.allclose(v1, c.summary_vec)
+    assert s.pending_evictions() == 0
+
+
+def test_db_state_manager_with_redis_cache():
+    srv = MiniRedis()
+    try:
+        db = DBStateManager(":memory:", redis=RespClient(srv.addr))
+        c = db.create_conversation("u1", "title", 2)
+        assert c.id.startswith("conv_") and c.status == "active"
+        m = new_message(c.id, "u1", "first answer", 3)
+        m.status = MessageStatus.COMPLETED
+        db.add_message(c.id, m)
+        db.add_message(c.id, new_message(c.id, "u1", "pending q", 3))
+        got = db.get_conversation(c.id)
+        assert got.message_count == 2 and got.context == "\nfirst answer"
+        assert len(db.get_conversation_messages(c.id, 10)) == 2
+        db.update_conversation_priority(c.id, 1)
+        assert db.get_conversation(c.id).priority == 1
+        assert [x.id for x in db.get_active_conversations()] == [c.id]
+        db.archive_conversation(c.id)
+        assert db.get_active_conversations() == []
+        assert db.get_conversation_context(c.id) == "\nfirst answer"
+        assert [x.id for x in db.get_user_conversations("u1")] == [c.id]
+        m.content = "edited"
+        db.update_message(m)
+        assert db.get_message(m.id).content == "edited"
+        db.delete_conversation(c.id)
+        with pytest.raises(ConversationNotFound):
+            db.get_conversation(c.id)
+    finally:
+        srv.close()
+
+
+def test_resp_client_ttl_and_sets():
+    srv = MiniRedis()
+    try:
+        r = RespClient(srv.addr)
+        assert r.ping()
+        r.set("k", b"v", 1)
+        assert r.get("k") == b"v"
+        assert r.sadd("s", "a", "b") == 2 and r.smembers("s") == ["a", "b"]
+        assert r.srem("s", "a") == 1 and r.delete("k", "s") == 2
+        assert r.get("k") is None
+    finally:
+        srv.close()

@@ -1,0 +1,126 @@
+"""Ports of reference tests/queue_factory_test.go + config and model coverage."""
+import json
+import os
+import time
+
+import pytest
+
+from llm_message_queue_amd.models.message import (Conversation, Message, PriorityParseError, format_time,
+                                                  new_message, parse_priority, parse_time, priority_name)
+from llm_message_queue_amd.queue import QueueFactory, QueueType
+from llm_message_queue_amd.utils.config import ConfigError, QueueConfig, default_config, load_config
+from llm_message_queue_amd.utils.duration import format_duration_ns, parse_duration_ns
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ---------------------------------------------------------------- factory (:42-211)
+@pytest.fixture
+def factory():
+    f = QueueFactory(QueueConfig(enable_metrics=False))
+    yield f
+    f.close()
+
+
+def test_factory_create_and_get(factory):
+    m = factory.create_queue_manager("q1", QueueType.STANDARD)
+    assert factory.create_queue_manager("q1", QueueType.STANDARD) is m      # idempotent
+    assert factory.get_queue_manager("q1") is m
+    assert factory.get_queue_manager("nope") is None
+
+
+@pytest.mark.parametrize("qt", QueueType.ALL)
+def test_factory_push_on_each_type(factory, qt):
+    m = factory.create_queue_manager(f"m-{qt}", qt)
+    m.create_queue("x")
+    m.push_message("x", new_message("c", "u", "hi", 3))
+    assert m.size("x") == 1
+
+
+def test_factory_workers(factory):
+    m = factory.create_queue_manager("wq", QueueType.STANDARD)
+    done = []
+    ws = factory.create_workers("wq", 2, lambda ctx, msg: done.append(msg.id))
+    assert len(ws) == 2 and ws[0].id == "wq-worker-0" and ws[1].id == "wq-worker-1"
+    m.push_message("wq", new_message("c", "u", "x", 3))
+    t0 = time.time()
+    while not done and time.time() - t0 < 2:
+        time.sleep(0.01)
+    assert len(done) == 1
+    assert factory.create_workers("missing", 1, lambda c, m: None) is None
+    stats = factory.get_worker_stats()
+    assert sum(s.processed_count for s in stats["wq"]) == 1
+    factory.stop_all()
+    assert factory.get_queue_manager("wq") is None
+
+
+# ---------------------------------------------------------------- config
+def test_shipped_yaml_loads_with_defaults_merged():
+    cfg = load_config(os.path.join(ROOT, "configs"))
+    assert cfg.queue.monitor_interval == 5_000_000_000       # D3: from defaults, not 0
+    assert cfg.queue.cleanup_interval == 60_000_000_000
+    assert [lv.name for lv in cfg.queue.levels] == ["realtime", "high", "normal", "low"]
+    assert cfg.queue.levels[3].max_wait_time == 300_000_000_000
+    assert cfg.scheduler.check_interval == 100_000_000
+
+
+def test_env_override_nested(tmp_path):
+    cfg = load_config(os.path.join(ROOT, "configs"), environ={"LLMQ_SERVER__PORT": "9999",
+                                                               "LLMQ_QUEUE__WORKER__MAX_BATCH_SIZE": "64",
+                                                               "LLMQ_QUEUE__MONITOR_INTERVAL": "250ms"})
+    assert cfg.server.port == 9999 and cfg.queue.worker.max_batch_size == 64
+    assert cfg.queue.monitor_interval == 250_000_000
+
+
+def test_validation(tmp_path):
+    p = tmp_path / "config.yaml"
+    p.write_text("queue:\n  monitor_interval: 0s\n")
+    with pytest.raises(ConfigError):
+        load_config(str(tmp_path))
+    with pytest.raises(ConfigError):
+        load_config(str(tmp_path / "missing"))
+
+
+def test_durations():
+    assert parse_duration_ns("1h30m") == 5_400_000_000_000
+    assert parse_duration_ns("100ms") == 100_000_000
+    assert parse_duration_ns("1.5s") == 1_500_000_000
+    assert format_duration_ns(90_000_000_000) == "1m30s"
+    with pytest.raises(ValueError):
+        parse_duration_ns("10 parsecs")
+
+
+# ---------------------------------------------------------------- models
+def test_priority_names_and_parsing():
+    assert [priority_name(p) for p in (1, 2, 3, 4, 0, 9)] == ["realtime", "high", "normal", "low", "unknown",
+                                                               "unknown"]
+    assert parse_priority("high") == 2 and parse_priority("URGENT") == 1 and parse_priority(3) == 3
+    assert parse_priority("4") == 4
+    with pytest.raises(PriorityParseError):
+        parse_priority("soonish")
+
+
+def test_message_json_roundtrip_and_defaults():
+    m = Message.from_dict({"content": "x", "priority": "low", "metadata": {"a": 1}})
+    assert m.priority == 4 and m.timeout == 30_000_000_000 and m.max_retries == 3   # D16
+    d = m.to_dict()
+    assert d["priority"] == 4 and isinstance(d["priority"], int)
+    m2 = Message.from_dict(json.loads(json.dumps(d)))
+    assert m2.metadata == {"a": 1}
+    nm = new_message("c", "u", "hi", 2)
+    assert nm.status == "pending" and len(nm.id) == 36
+
+
+def test_time_format_roundtrip():
+    t = 1_700_000_000_123_456_789
+    assert parse_time(format_time(t)) == t
+    assert format_time(0) == "0001-01-01T00:00:00Z"
+
+
+def test_conversation_roundtrip():
+    c = Conversation("c1", "u1")
+    c.messages.append(new_message("c1", "u1", "hi", 3))
+    c.summary_tokens = [1, 2]
+    c.evicted_count = 3
+    c2 = Conversation.from_dict(json.loads(json.dumps(c.to_dict())))
+    assert c2.id == "c1" and len(c2.messages) == 1 and c2.summary_tokens == [1, 2] and c2.evicted_count == 3

@@ -1,0 +1,184 @@
+"""Gateway data path on CPU (reference-op engine), the deterministic RCCL
+planner, and multi-rank dispatch: threads with FakeComm (world 2/4/8) and
+real torch.distributed gloo processes (world 2)."""
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from llm_message_queue_amd.backend.engine import BackendEngine
+from llm_message_queue_amd.gateway.router import Gateway, LatencyRecorder, hist_percentile
+from llm_message_queue_amd.gateway.workload import PoissonArrivals, Workload
+from llm_message_queue_amd.models.llama_stub import LlamaConfig
+from llm_message_queue_amd.parallel import planner
+from llm_message_queue_amd.parallel.comm import FakeComm, SoloComm
+from llm_message_queue_amd.utils.config import default_config
+
+MICRO = LlamaConfig(vocab=512, dim=2048, layers=1, heads=16, kv_heads=4, ffn=256)
+
+
+def cfg():
+    c = default_config()
+    c.queue.enable_metrics = False
+    return c
+
+
+def engine(slots=8, seed=0):
+    return BackendEngine(MICRO, slots=slots, max_ctx=64, token_budget=64, device="cpu", impl="ref", seed=seed)
+
+
+def run_until_done(gws, n_expected, max_ticks=400):
+    for _ in range(max_ticks):
+        if len(gws) == 1:
+            gws[0].tick()
+        else:
+            ths = [threading.Thread(target=g.tick) for g in gws]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+        if sum(g.counters["completed"] for g in gws) >= n_expected:
+            return True
+    return False
+
+
+# ---------------------------------------------------------------- single rank
+def test_gateway_cpu_end_to_end_and_priority_order():
+    gw = Gateway(cfg(), engine=engine(slots=4), use_gpu_preprocess=False, prompt_cap=8, gen_tokens=2)
+    msgs = Workload(seed=2).make(40)
+    gw.submit(msgs)
+    gw.ingest()
+    # one dispatch: the 4 free slots go to the most urgent tier present
+    n = gw.dispatch()
+    assert n == 4
+    dispatched = [m for m in msgs if m.dispatched_at]
+    assert sorted(m.priority for m in dispatched) == sorted(m.priority for m in msgs)[:4]
+    assert run_until_done([gw], 40)
+    assert gw.counters["dispatched"] == 40 and gw.pending() == 0
+    st = gw.qm.get_all_queue_stats()
+    assert sum(s.completed_count for s in st.values()) == 40
+    assert sum(s.processing_count for s in st.values()) == 0
+    summ = gw.rec.summary()
+    assert summ["count"] == 40 and summ["p99_ms"] >= summ["p50_ms"] > 0
+
+
+def test_latency_histogram_percentiles():
+    rec = LatencyRecorder(4)
+    v = np.array([1_000_000] * 98 + [400_000_000, 900_000_000])
+    rec.record(np.zeros(100, dtype=np.int64), v, v)
+    s = rec.summary()
+    assert 0.9 < s["p50_ms"] < 1.1 and 390 < s["p99_ms"] < 410
+
+
+def test_poisson_arrivals_rate():
+    a = PoissonArrivals(1000.0, seed=1)
+    a.reset(0.0)
+    assert abs(len(a.due(10.0)) - 10000) < 400
+
+
+# ---------------------------------------------------------------- planner
+def load(free, depth, age=(0, 0, 0, 0), healthy=True):
+    return planner.make_load(free, 0, depth, age, healthy=healthy)
+
+
+def test_plan_local_first_then_least_loaded():
+    loads = np.stack([load(2, [0, 0, 10, 0]), load(8, [0, 0, 0, 0]), load(5, [0, 0, 0, 0])])
+    q = planner.plan_dispatch(loads, [0] * 4)
+    assert q[0, 0, 2] == 2 and q[0, 1, 2] == 8 and q[0, 2, 2] == 0
+    assert q.sum() == 10
+
+
+def test_plan_strict_priority_and_proportional_split():
+    loads = np.stack([load(3, [4, 0, 10, 0]), load(3, [2, 0, 10, 0])])
+    q = planner.plan_dispatch(loads, [0] * 4)
+    assert q[:, :, 0].sum() == 6 and q[:, :, 2].sum() == 0           # realtime takes every slot
+    assert q[0, :, 0].sum() == 4 and q[1, :, 0].sum() == 2
+    loads = np.stack([load(2, [0, 0, 30, 0]), load(2, [0, 0, 10, 0])])
+    q = planner.plan_dispatch(loads, [0] * 4)
+    assert q[0, :, 2].sum() == 3 and q[1, :, 2].sum() == 1           # 4 slots split 3:1
+
+
+def test_plan_aging_and_unhealthy():
+    loads = np.stack([load(2, [5, 0, 0, 3], age=(0, 0, 0, 9_000_000)), load(4, [0, 0, 0, 0], healthy=False)])
+    q = planner.plan_dispatch(loads, [0, 0, 0, 5_000_000])
+    assert q[0, 0, 3] == 2 and q[:, 1].sum() == 0                     # overdue low first; no unhealthy target
+
+
+# ---------------------------------------------------------------- multi-rank (threads)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_fakecomm_multirank_dispatch(world):
+    comms = FakeComm.make(world)
+    gws = [Gateway(cfg(), engine=engine(slots=4, seed=r), comm=comms[r], use_gpu_preprocess=False, prompt_cap=8,
+                   gen_tokens=2) for r in range(world)]
+    # all demand on rank 0: the planner must spread it over every GPU
+    gws[0].submit(Workload(seed=7).make(12 * world))
+    assert run_until_done(gws, 12 * world)
+    assert all(g.pending() == 0 for g in gws)
+    assert gws[0].counters["completed"] == 12 * world
+    assert gws[0].counters["remote_sent"] > 0
+    assert sum(g.counters["remote_recv"] for g in gws[1:]) == gws[0].counters["remote_sent"]
+    assert all(g.engine.completed_total > 0 for g in gws)
+    assert not gws[0].remote_out and all(not g.foreign for g in gws)
+
+
+# ---------------------------------------------------------------- multi-process gloo
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from llm_message_queue_amd.parallel.comm import TorchComm
+    comm = TorchComm()
+    gw = Gateway(cfg(), engine=engine(slots=4, seed=rank), comm=comm, use_gpu_preprocess=False, prompt_cap=8,
+                 gen_tokens=2)
+    if rank == 0:
+        gw.submit(Workload(seed=11).make(24))
+    done = False
+    for _ in range(300):
+        gw.tick()
+        tot = comm.all_gather_i64(np.array([gw.counters["completed"]]))
+        if tot.sum() >= 24:
+            done = True
+            break
+    g = comm.all_gather_i64(np.array([gw.counters["completed"], gw.counters["remote_recv"],
+                                      gw.engine.completed_total]))
+    b = comm.broadcast_i64(np.array([rank * 10 + 5]), root=1)
+    if rank == 0:
+        out.put((done, g.tolist(), int(b[0])))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_dispatch():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    import queue as _q
+    res = None
+    for _ in range(240):
+        try:
+            res = q.get(timeout=1)
+            break
+        except _q.Empty:
+            if any(p.exitcode not in (None, 0) for p in ps):
+                break
+    for p in ps:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert res is not None, [p.exitcode for p in ps]
+    done, g, b = res
+    assert done and g[0][0] == 24 and g[1][1] > 0 and g[1][2] > 0 and b == 15
