@@ -1,0 +1,108 @@
+"""Telemetry service (N8 + failure detection): publishes the native amd-smi
+poller's snapshot to the node-shared load pages (HBM used/total, busy %), the
+Prometheus gauges, and the ResourceScheduler (``Heartbeat`` with used HBM),
+and flags GPUs as unhealthy when amd-smi stops answering or the uncorrectable
+ECC count rises -- the reference's health check is a stub that always
+succeeds (`internal/loadbalancer/load_balancer.go:588-616`, D9).
+
+GPU index mapping: amd-smi enumerates every GPU of the node in PCI order,
+which is also HIP's default order; a process restricted with
+``HIP_VISIBLE_DEVICES`` passes an explicit ``gpu_map``.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Callable, Dict, List, Optional
+
+from .. import _native
+from ..utils.logging import get_logger
+
+
+class TelemetryService:
+    def __init__(self, period_ms: int = 20, pages: Optional[Dict[int, object]] = None, metrics=None,
+                 resource_scheduler=None, on_unhealthy: Optional[Callable[[int, str], None]] = None,
+                 synthetic: int = 0, gpu_map: Optional[Dict[int, int]] = None):
+        self.native = _native.telemetry().Telemetry(int(period_ms))
+        self.period_s = period_ms / 1e3
+        self.pages = pages or {}
+        self.metrics = metrics
+        self.rs = resource_scheduler
+        self.on_unhealthy = on_unhealthy
+        self.synthetic = synthetic
+        self.gpu_map = gpu_map or {}
+        self.log = get_logger("telemetry")
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._ecc0: Dict[int, int] = {}
+        self.unhealthy: Dict[int, str] = {}
+        self.last: List[dict] = []
+
+    @property
+    def available(self) -> bool:
+        return self.native.available()
+
+    def start(self) -> None:
+        self.native.start()
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._loop, name="telemetry", daemon=True)
+            self._thread.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=2)
+        self.native.stop()
+
+    def _loop(self) -> None:
+        while not self._stop.wait(self.period_s):
+            self.publish()
+
+    def inject(self, gpu: int, field: str, value: float) -> None:
+        """Fault injection: override a telemetry field (e.g. valid=0, ecc_uncorrectable=5)."""
+        self.native.inject(gpu, field, float(value))
+
+    def publish(self) -> List[dict]:
+        snap = self.native.snapshot(self.synthetic)
+        self.last = snap
+        for s in snap:
+            g = self.gpu_map.get(s["gpu"], s["gpu"])
+            page = self.pages.get(g)
+            if page is not None:
+                page.set_telemetry(int(s["hbm_used_mb"]), int(s["hbm_total_mb"]), int(s["gfx_pct"]))
+            if self.metrics is not None:
+                self.metrics.hbm_used.labels(str(g)).set(int(s["hbm_used_mb"]) << 20)
+                if page is not None:
+                    self.metrics.inflight.labels(str(g)).set(page.active())
+            if self.rs is not None and s["valid"]:
+                try:
+                    r = self.rs.get_resource(f"gpu{g}")
+                    used = dict(r.used)
+                    used["memory"] = int(s["hbm_used_mb"]) << 20
+                    self.rs.heartbeat(f"gpu{g}", used=used)
+                except Exception:
+                    pass
+            self._health(g, s)
+        return snap
+
+    def _health(self, g: int, s: dict) -> None:
+        reason = ""
+        if not s["valid"] and (self.available or self.synthetic):
+            reason = "telemetry unavailable"
+        ecc = int(s["ecc_uncorrectable"])
+        base = self._ecc0.setdefault(g, ecc)
+        if ecc > base:
+            reason = f"uncorrectable ECC errors: {ecc - base}"
+        if reason and g not in self.unhealthy:
+            self.unhealthy[g] = reason
+            self.log.warning("GPU unhealthy", gpu=g, reason=reason)
+            page = self.pages.get(g)
+            if page is not None:
+                page.set_health(False)
+            if self.on_unhealthy is not None:
+                self.on_unhealthy(g, reason)
+        elif not reason and g in self.unhealthy:
+            del self.unhealthy[g]
+            page = self.pages.get(g)
+            if page is not None:
+                page.set_health(True)

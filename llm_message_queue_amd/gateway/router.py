@@ -147,6 +147,7 @@ class Gateway:
         self._inbox: List[Message] = []
         self._inbox_lock = threading.Lock()
         self.inflight_by_tier = np.zeros(len(self.tiers), dtype=np.int64)
+        self.pinned = np.zeros(self.world, dtype=np.int64)   # queued requests per home GPU
         self.local: Dict[int, Message] = {}          # handle -> msg dispatched to my engine (my origin)
         self.remote_out: Dict[int, Message] = {}      # handle -> msg I sent to another rank
         self.foreign: Dict[int, Tuple[int, int, int]] = {}  # my engine req id -> (origin, handle, tier)
@@ -179,6 +180,10 @@ class Gateway:
         errs = self.qm.push_routed(batch)
         out = []
         for m, e in zip(batch, errs):
+            if e is None and self.world > 1:
+                h = self._home(m)
+                if 0 <= h < self.world:
+                    self.pinned[h] += 1
             if e is not None:
                 m.status = MessageStatus.FAILED
                 self.counters["rejected"] += 1
@@ -268,7 +273,7 @@ class Gateway:
         inflight = self.engine.inflight() if self.engine is not None else 0
         done_for = [len(self._done_owed[r]) for r in range(W)]
         load = planner.make_load(free, inflight, depth, age, healthy=self.engine is not None,
-                                 done_for=done_for)
+                                 done_for=done_for, pinned=[int(x) for x in self.pinned])
         loads = self.comm.all_gather_i64(load)
         quota = planner.plan_dispatch(loads, [a // 1000 for a in self.aging_ns])
         # pop exactly my per-tier grant
@@ -280,6 +285,9 @@ class Gateway:
         for m, t in zip(msgs, tier_idx):
             m.tier = int(t)
             by_tier[int(t)].append(m)
+            h = self._home(m)
+            if 0 <= h < W and self.pinned[h] > 0:
+                self.pinned[h] -= 1
         cap = self.prompt_cap
         width = DESC_HDR + cap
         send = []
@@ -288,7 +296,17 @@ class Gateway:
             rows = []
             for t in range(len(self.tiers)):
                 n = int(mine[j, t])
-                take, by_tier[t] = by_tier[t][:n], by_tier[t][n:]
+                if n <= 0:
+                    continue
+                # KV-residency affinity: fill destination j's quota with the
+                # conversations homed on GPU j first, then in queue order
+                pool = by_tier[t]
+                pref = [m for m in pool if self._home(m) == j][:n]
+                if len(pref) < n:
+                    pick = set(id(m) for m in pref)
+                    pref += [m for m in pool if id(m) not in pick][:n - len(pref)]
+                chosen = set(id(m) for m in pref)
+                take, by_tier[t] = pref, [m for m in pool if id(m) not in chosen]
                 if j == me:
                     local_msgs.extend(take)
                 else:
@@ -348,6 +366,12 @@ class Gateway:
             raise RuntimeError(f"rank {me}: plan over-committed backend ({len(reqs)} > {len(admitted)})")
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
+
+    def _home(self, m: Message) -> int:
+        h = m.metadata.get("home_gpu") if m.metadata else None
+        if h is None and self.state_manager is not None and m.conversation_id:
+            h = self.state_manager.home_gpu(m.conversation_id)
+        return -1 if h is None else int(h)
 
     def _fill_desc(self, row: np.ndarray, m: Message, origin: int, cap: int) -> None:
         row[0] = K_DISPATCH

@@ -22,7 +22,10 @@ from typing import List, Sequence
 import numpy as np
 
 MAX_WORLD = 8
-LOAD_WIDTH = 16 + MAX_WORLD   # [16 + r] = completion records this rank owes router r
+# [16 + r] = completion records this rank owes router r
+# [24 + j] = queued requests at this router whose conversation is homed on GPU j
+LOAD_WIDTH = 16 + 2 * MAX_WORLD
+L_PIN = 16 + MAX_WORLD
 L_FREE, L_INFLIGHT = 0, 1
 L_DEPTH = 2          # 4 tiers: 2..5
 L_AGE_US = 6         # 4 tiers: 6..9 (oldest head wait, microseconds)
@@ -33,7 +36,7 @@ NTIERS = 4
 
 def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[int], hbm_used_mib: int = 0,
               hbm_total_mib: int = 0, healthy: bool = True, epoch: int = 0,
-              done_for: Sequence[int] = ()) -> np.ndarray:
+              done_for: Sequence[int] = (), pinned: Sequence[int] = ()) -> np.ndarray:
     v = np.zeros(LOAD_WIDTH, dtype=np.int64)
     v[L_FREE], v[L_INFLIGHT] = free, inflight
     v[L_DEPTH:L_DEPTH + NTIERS] = list(depth)[:NTIERS]
@@ -41,6 +44,8 @@ def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[i
     v[L_HBM_USED], v[L_HBM_TOTAL], v[L_HEALTHY], v[L_EPOCH] = hbm_used_mib, hbm_total_mib, int(healthy), epoch
     for r, n in enumerate(done_for):
         v[L_DONE + r] = n
+    for j, n in enumerate(pinned):
+        v[L_PIN + j] = n
     return v
 
 
@@ -67,6 +72,7 @@ def plan_dispatch(loads: np.ndarray, aging_us: Sequence[int]) -> np.ndarray:
     depth = loads[:, L_DEPTH:L_DEPTH + NTIERS].copy()
     age = loads[:, L_AGE_US:L_AGE_US + NTIERS]
     quota = np.zeros((W, W, NTIERS), dtype=np.int64)
+    pin = loads[:, L_PIN:L_PIN + W].copy() if loads.shape[1] >= L_PIN + W else np.zeros((W, W), np.int64)
     overdue = [t for t in range(NTIERS)
                if aging_us[t] > 0 and (age[:, t] > aging_us[t]).any() and depth[:, t].sum() > 0]
     order = overdue + [t for t in range(NTIERS) if t not in overdue]
@@ -79,7 +85,17 @@ def plan_dispatch(loads: np.ndarray, aging_us: Sequence[int]) -> np.ndarray:
             g = int(grant[i])
             if g <= 0:
                 continue
-            # local first
+            # KV-residency affinity: conversations homed on GPU j go to j
+            for j in range(W):
+                if g <= 0:
+                    break
+                take = min(g, int(pin[i, j]), int(cap[j]))
+                if take > 0:
+                    quota[i, j, t] += take
+                    cap[j] -= take
+                    pin[i, j] -= take
+                    g -= take
+            # then local first
             take = min(g, int(cap[i]))
             if take:
                 quota[i, i, t] += take

@@ -182,3 +182,57 @@ def test_gloo_world2_dispatch():
     assert res is not None, [p.exitcode for p in ps]
     done, g, b = res
     assert done and g[0][0] == 24 and g[1][1] > 0 and g[1][2] > 0 and b == 15
+
+
+# ---------------------------------------------------------------- affinity + KV migration
+def test_affinity_routes_to_home_gpu():
+    comms = FakeComm.make(2)
+    gws = [Gateway(cfg(), engine=engine(slots=8, seed=r), comm=comms[r], use_gpu_preprocess=False, prompt_cap=8,
+                   gen_tokens=1) for r in range(2)]
+    msgs = Workload(seed=5).make(6)
+    for m in msgs:
+        m.priority = 3
+        m.metadata["home_gpu"] = 1
+    gws[0].submit(msgs)
+    assert run_until_done(gws, 6)
+    assert gws[1].counters["remote_recv"] == 6          # all went to their home GPU despite local capacity
+
+
+def test_kv_migration_fakecomm():
+    from llm_message_queue_amd.models.llama_stub import LlamaStub
+    from llm_message_queue_amd.parallel.migration import KVMigrator
+    comms = FakeComm.make(2)
+    a = LlamaStub(MICRO, slots=2, max_ctx=16, device="cpu", impl="ref", seed=1)
+    b = LlamaStub(MICRO, slots=2, max_ctx=16, device="cpu", impl="ref", seed=2)
+    for L in range(MICRO.layers):
+        a.kcache[L][1, :, :5].normal_()
+        a.vcache[L][1, :, :5].normal_()
+    ma, mb = KVMigrator(a, comms[0]), KVMigrator(b, comms[1])
+    t = threading.Thread(target=lambda: ma.send(1, 1, 5))
+    t.start()
+    nb = mb.recv(0, 0, 5)
+    t.join()
+    assert nb == MICRO.layers * 2 * MICRO.kv_heads * 5 * 128 * 2
+    for L in range(MICRO.layers):
+        assert torch.equal(b.kcache[L][0, :, :5], a.kcache[L][1, :, :5])
+        assert torch.equal(b.vcache[L][0, :, :5], a.vcache[L][1, :, :5])
+
+
+def test_telemetry_fault_injection_marks_unhealthy():
+    from llm_message_queue_amd.backend.slot_page import SlotPage
+    from llm_message_queue_amd.backend.telemetry import TelemetryService
+    page = SlotPage("pytest-telem", 0)
+    try:
+        page.set_health(True)
+        bad = []
+        ts = TelemetryService(pages={0: page}, synthetic=1, on_unhealthy=lambda g, r: bad.append((g, r)))
+        ts.inject(0, "valid", 1)
+        ts.inject(0, "hbm_used_mb", 1000)
+        ts.inject(0, "hbm_total_mb", 288000)
+        ts.publish()
+        assert page.read()["hbm_used_mib"] == 1000 and not bad
+        ts.inject(0, "ecc_uncorrectable", 3)
+        ts.publish()
+        assert bad and bad[0][0] == 0 and "ECC" in bad[0][1] and page.read()["healthy"] == 0
+    finally:
+        page.close(unlink=True)
