@@ -1,23 +1,33 @@
 """GPU backend engine: continuous batching over fixed batch slots (N12 + N9).
 
 One engine per GPU process.  ``admit`` places dispatched requests into free
-slots; ``step`` runs ONE model forward over a token batch made of
+slots; ``launch`` enqueues ONE model forward over a token batch made of
   * one decode token for every slot that is generating, then
-  * chunked-prefill tokens of newly admitted prompts, up to ``token_budget``;
-samples the next token for every slot whose chunk ended its prompt or that
-decoded, retires requests that reached ``gen_tokens``, and publishes the
-slot census to the node-shared load page (``slot_census`` kernel -> mapped
-host page, read zero-copy by routers).
+  * chunked-prefill tokens of admitted prompts, up to ``token_budget``;
+and returns immediately.  The pipeline is fully asynchronous:
+  * a decode token's id is the previous step's greedy output, which stays on
+    the device -- the next step gathers it there (``index_select``), so the
+    host never waits for token values;
+  * completions are deterministic (greedy decode always yields a token), so
+    a request's slot is freed at launch of its last step and can be re-admitted
+    into the NEXT step (same-stream ordering keeps its KV rows safe);
+  * at most ``max_inflight`` (2) steps are queued on the GPU; ``finish`` reaps
+    finished steps (blocking only when the queue is full), so host work of the
+    next tick overlaps the current forward and the GPU never idles between
+    steps.
+The slot census of every step is written by the ``slot_census`` kernel into
+the node-shared load page (zero-copy for routers, N9).
 
-Request cost model (documented in README/bench): prompt = the message's
-tokens from the GPU tokenizer (capped), generation = ``gen_tokens`` greedy
-tokens.  This is real work on the full 32-layer stub, never skipped.
+Request cost model (README/bench): prompt = the message's tokens from the
+GPU tokenizer (capped), generation = ``gen_tokens`` greedy tokens, all 32
+layers of the stub, never skipped.
 """
 from __future__ import annotations
 
+import collections
 import time
-from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from dataclasses import dataclass
+from typing import Deque, Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -34,11 +44,12 @@ class Request:
     slot: int = -1
     prefilled: int = 0
     generated: int = 0
-    last_token: int = 0
     admitted_ns: int = 0
     first_token_ns: int = 0
     done_ns: int = 0
     meta: object = None
+    out_idx: int = -1             # row of the previous step's output holding my last token
+    out_step: int = -1
 
 
 @dataclass
@@ -51,38 +62,59 @@ class StepResult:
     elapsed_ms: float
 
 
+@dataclass
+class _Inflight:
+    step: int
+    event: object
+    T: int
+    n_pre: int
+    n_dec: int
+    completed: List[Request]
+    firsts: List[Request]
+    t0: float
+    out: object                   # device tensor of sampled tokens (kept alive for the next gather)
+
+
 class BackendEngine:
     def __init__(self, model_cfg: LlamaConfig, slots: int = 256, max_ctx: int = 512,
                  token_budget: int = 2048, device="cuda", impl: str = "hip", seed: int = 0,
-                 page=None, gpu_index: int = 0):
+                 page=None, gpu_index: int = 0, max_inflight: int = 2):
         self.cfg = model_cfg
         self.slots = slots
         self.max_ctx = max_ctx
-        self.token_budget = token_budget
+        # every generating slot gets its decode token each step (the on-device
+        # token gather reads the previous step's output only)
+        self.token_budget = max(token_budget, slots)
         self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
         self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed)
         self.impl = impl
         self.active: Dict[int, Request] = {}            # slot -> request
         self.free: List[int] = list(range(slots - 1, -1, -1))
-        self.waiting: List[Request] = []                 # admitted, prefill not started/finished
         self.page = page
         self.gpu_index = gpu_index
+        self.max_inflight = max(1, max_inflight)
         self.step_id = 0
-        self._pending = None
         self.total_tokens = 0
-        self.completed_tokens = 0
         self.completed_total = 0
-        self._slot_state_h = torch.zeros(slots, dtype=torch.int32).pin_memory() if self.device.type == "cuda" \
-            else torch.zeros(slots, dtype=torch.int32)
+        self.completed_tokens = 0
+        self._q: Deque[_Inflight] = collections.deque()
+        self._reaped: List[_Inflight] = []               # reaped by launch(), not yet returned
+        self._prev_out = None                            # device int32 [n_samples] of the last launched step
+        # double-buffered pinned staging (a buffer is reused only after the
+        # step that read it has finished: <= 2 steps in flight)
+        self._pins = [self._alloc_pin(4 * (3 * token_budget + 2 * slots + 64)) for _ in range(2)]
+        self._state_pins = [self._alloc_pin(4 * slots) for _ in range(2)]
         self._slot_state_d = torch.zeros(slots, dtype=torch.int32, device=self.device)
-        self._pin = torch.empty(4 * (token_budget * 4 + 16), dtype=torch.uint8)
-        if self.device.type == "cuda":
-            self._pin = self._pin.pin_memory()
-            if page is not None and page.dev_ptr is None:
-                page.register_device()
+        if self.cuda and page is not None and page.dev_ptr is None:
+            page.register_device()
         if page is not None:
             page.set_health(True)
-            self._publish(0)
+            page.write_host(0, slots, 0, 0)
+
+    def _alloc_pin(self, nbytes: int) -> torch.Tensor:
+        t = torch.empty(nbytes, dtype=torch.uint8)
+        return t.pin_memory() if self.cuda else t
 
     # ------------------------------------------------------------------ admission
     def free_slots(self) -> int:
@@ -101,12 +133,13 @@ class BackendEngine:
             if r.gen_tokens < 1:
                 r.gen_tokens = 1
             plen = max(1, min(len(r.prompt), cap - r.gen_tokens + 1))
-            r.prompt = np.asarray(r.prompt[:plen], dtype=np.int32) % self.cfg.vocab
+            r.prompt = np.asarray(r.prompt[:plen], dtype=np.int64) % self.cfg.vocab
             if len(r.prompt) == 0:
-                r.prompt = np.zeros(1, dtype=np.int32)
+                r.prompt = np.zeros(1, dtype=np.int64)
             r.slot = self.free.pop()
             r.prefilled = 0
             r.generated = 0
+            r.out_idx = r.out_step = -1
             r.admitted_ns = now
             self.active[r.slot] = r
             out.append(r)
@@ -115,13 +148,19 @@ class BackendEngine:
     # ------------------------------------------------------------------ step
     def _build(self):
         toks, pos, slot, samp, sample_reqs = [], [], [], [], []
+        dec_rows, dec_src = [], []
         budget = self.token_budget
         n_dec = n_pre = 0
-        # decode tokens first (in-flight generations keep their cadence)
+        # decode tokens first (in-flight generations keep their cadence);
+        # their ids are gathered on the device from the previous output
         for s, r in self.active.items():
-            if r.prefilled >= len(r.prompt) and budget > 0:
+            if r.prefilled >= len(r.prompt):
+                if r.out_step != self.step_id - 1:
+                    raise RuntimeError("decode token source is not the previous step")
                 ctx = len(r.prompt) + r.generated - 1
-                toks.append(r.last_token)
+                dec_rows.append(len(toks))
+                dec_src.append(r.out_idx)
+                toks.append(0)
                 pos.append(ctx)
                 slot.append(s)
                 samp.append(len(toks) - 1)
@@ -146,103 +185,120 @@ class BackendEngine:
             if r.prefilled >= len(r.prompt):
                 samp.append(len(toks) - 1)
                 sample_reqs.append(r)
-        return toks, pos, slot, samp, sample_reqs, n_pre, n_dec
-
-    def step(self) -> StepResult:
-        """Synchronous step: launch + finish."""
-        self.launch()
-        return self.finish()
+        return toks, pos, slot, samp, sample_reqs, dec_rows, dec_src, n_pre, n_dec
 
     def launch(self) -> None:
-        """Build the token batch and enqueue the forward on the current HIP
-        stream WITHOUT waiting for it; ``finish`` collects the result.  The
-        gateway overlaps its host work (ingest, preprocess on a side stream)
-        with the forward between the two calls."""
-        if self._pending is not None:
-            raise RuntimeError("launch() called twice without finish()")
+        """Build the next token batch and enqueue its forward (async)."""
+        while len(self._q) >= self.max_inflight:       # bound the run-ahead (and staging reuse)
+            self._reaped.append(self._reap(block=True))  # handed to the next finish()
         t0 = time.perf_counter()
-        toks, pos, slot, samp, sample_reqs, n_pre, n_dec = self._build()
+        toks, pos, slot, samp, sample_reqs, dec_rows, dec_src, n_pre, n_dec = self._build()
         T = len(toks)
-        nxt = None
-        if T:
-            dev = self.device
-            S = len(samp)
-            buf = np.empty(3 * T + S, dtype=np.int32)
-            buf[:T] = toks
-            buf[T:2 * T] = pos
-            buf[2 * T:3 * T] = slot
-            buf[3 * T:] = samp
-            nbytes = buf.nbytes
-            if self._pin.numel() < nbytes:
-                self._pin = torch.empty(2 * nbytes, dtype=torch.uint8)
-                if dev.type == "cuda":
-                    self._pin = self._pin.pin_memory()
-            self._pin[:nbytes].numpy()[:] = buf.view(np.uint8)
-            d = self._pin[:nbytes].to(dev, non_blocking=True).view(torch.int32)
-            tok_d = d[:T].long()
-            pos_d, slot_d = d[T:2 * T], d[2 * T:3 * T]
-            samp_d = d[3 * T:].long()
-            nxt = self.model.forward(tok_d, pos_d, slot_d, samp_d)
-            self.step_id += 1
-            self._publish(T, device_side=True)
-            if dev.type == "cuda":
-                nxt_h = torch.empty(nxt.shape, dtype=nxt.dtype).pin_memory()
-                nxt_h.copy_(nxt, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record()
-            else:
-                nxt_h, ev = nxt, None
-            nxt = (nxt_h, ev)
-        self._pending = (t0, T, n_pre, n_dec, sample_reqs, nxt)
+        if T == 0:
+            return
+        dev = self.device
+        S, D = len(samp), len(dec_rows)
+        buf = np.empty(3 * T + S + 2 * D, dtype=np.int32)
+        buf[:T] = toks
+        buf[T:2 * T] = pos
+        buf[2 * T:3 * T] = slot
+        buf[3 * T:3 * T + S] = samp
+        buf[3 * T + S:3 * T + S + D] = dec_rows
+        buf[3 * T + S + D:] = dec_src
+        nbytes = buf.nbytes
+        pin = self._pins[self.step_id % 2]
+        if pin.numel() < nbytes:
+            pin = self._pins[self.step_id % 2] = self._alloc_pin(2 * nbytes)
+        pin[:nbytes].numpy()[:] = buf.view(np.uint8)
+        d = pin[:nbytes].to(dev, non_blocking=True).view(torch.int32)
+        tok_d = d[:T].long()
+        if D:
+            if self._prev_out is None:
+                raise RuntimeError("decode token without a previous step output")
+            rows = d[3 * T + S:3 * T + S + D].long()
+            src = d[3 * T + S + D:].long()
+            tok_d.index_copy_(0, rows, self._prev_out.index_select(0, src).long())
+        out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:3 * T + S].long())
+        self._census(T)
+        ev = None
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        # deterministic bookkeeping: every sampled request gets one token
+        completed, firsts = [], []
+        for i, r in enumerate(sample_reqs):
+            r.generated += 1
+            r.out_idx, r.out_step = i, self.step_id
+            if r.generated == 1:
+                firsts.append(r)
+            if r.generated >= r.gen_tokens:
+                completed.append(r)
+        for r in completed:
+            del self.active[r.slot]
+            self.free.append(r.slot)
+        self._prev_out = out
+        self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out))
+        self.step_id += 1
+        self.total_tokens += T
+        self.completed_total += len(completed)
+        self.completed_tokens += sum(len(r.prompt) + r.gen_tokens - 1 for r in completed)
 
-    def finish(self) -> StepResult:
-        if self._pending is None:
-            return StepResult(0, 0, 0, [], [], 0.0)
-        t0, T, n_pre, n_dec, sample_reqs, nxt = self._pending
-        self._pending = None
-        completed: List[Request] = []
-        firsts: List[Request] = []
-        if T:
-            nxt_h, ev = nxt
-            if ev is not None:
-                ev.synchronize()
-            nxt_h = nxt_h.numpy()
-            now = time.monotonic_ns()
-            for r, t in zip(sample_reqs, nxt_h):
-                r.last_token = int(t)
-                r.generated += 1
-                if r.generated == 1:
-                    r.first_token_ns = now
-                    firsts.append(r)
-                if r.generated >= r.gen_tokens:
-                    r.done_ns = now
-                    completed.append(r)
-            for r in completed:
-                del self.active[r.slot]
-                self.free.append(r.slot)
-            self.total_tokens += T
-            self.completed_total += len(completed)
-            self.completed_tokens += sum(len(r.prompt) + r.gen_tokens - 1 for r in completed)
-            if completed:
-                self._publish(T, device_side=False)
-        return StepResult(T, n_pre, n_dec, completed, firsts, (time.perf_counter() - t0) * 1e3)
+    def _reap(self, block: bool) -> Optional[_Inflight]:
+        if not self._q:
+            return None
+        f = self._q[0]
+        if f.event is not None:
+            if block:
+                f.event.synchronize()
+            elif not f.event.query():
+                return None
+        self._q.popleft()
+        now = time.monotonic_ns()
+        for r in f.firsts:
+            r.first_token_ns = now
+        for r in f.completed:
+            r.done_ns = now
+        if self.page is not None and not self.cuda:
+            self.page.write_host(self.inflight(), self.free_slots(), f.T, f.step)
+        return f
+
+    def finish(self, block: bool = False) -> StepResult:
+        """Reap finished steps.  Non-blocking unless ``block`` (then waits for
+        every queued step)."""
+        done: List[_Inflight] = self._reaped
+        self._reaped = []
+        while self._q:
+            f = self._reap(block=block)
+            if f is None:
+                break
+            done.append(f)
+        comp = [r for f in done for r in f.completed]
+        firsts = [r for f in done for r in f.firsts]
+        return StepResult(sum(f.T for f in done), sum(f.n_pre for f in done), sum(f.n_dec for f in done),
+                          comp, firsts, (time.perf_counter() - done[0].t0) * 1e3 if done else 0.0)
+
+    def step(self) -> StepResult:
+        """Synchronous step: launch + wait."""
+        self.launch()
+        return self.finish(block=True)
+
+    def sync(self) -> None:
+        self.finish(block=True)
 
     # ------------------------------------------------------------------ N9 page
-    def _publish(self, tokens: int, device_side: bool = False) -> None:
-        if self.page is None:
+    def _census(self, tokens: int) -> None:
+        if self.page is None or not self.cuda or self.page.dev_ptr is None:
             return
-        if device_side and self.device.type == "cuda" and self.page.dev_ptr is not None:
-            st = self._slot_state_h.numpy()
-            st[:] = 0
-            for s in self.active:
-                st[s] = 1
-            self._slot_state_d.copy_(self._slot_state_h, non_blocking=True)
-            from .. import _native
-            _native.require_hipops().slot_census(self._slot_state_d.data_ptr(), self.slots, int(tokens),
-                                                 int(self.step_id) & 0xFFFFFFFF, self.page.dev_ptr,
-                                                 torch.cuda.current_stream(self.device).cuda_stream)
-        else:
-            self.page.write_host(self.inflight(), self.free_slots(), tokens, self.step_id)
+        pin = self._state_pins[self.step_id % 2]
+        st = pin.numpy().view(np.int32)
+        st[:] = 0
+        if self.active:
+            st[np.fromiter(self.active.keys(), dtype=np.int64)] = 1
+        self._slot_state_d.copy_(pin.view(torch.int32), non_blocking=True)
+        from .. import _native
+        _native.require_hipops().slot_census(self._slot_state_d.data_ptr(), self.slots, int(tokens),
+                                             int(self.step_id) & 0xFFFFFFFF, self.page.dev_ptr,
+                                             torch.cuda.current_stream(self.device).cuda_stream)
 
     def drain(self, max_steps: int = 10000) -> List[Request]:
         out = []
@@ -250,4 +306,5 @@ class BackendEngine:
             if not self.active:
                 break
             out.extend(self.step().completed)
+        out.extend(self.finish(block=True).completed)
         return out

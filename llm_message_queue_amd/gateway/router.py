@@ -421,12 +421,14 @@ class Gateway:
         if self.engine is None:
             return None
         self.engine.launch()
-        return self.finish_backend()
+        return self.finish_backend(block=True)
 
-    def finish_backend(self):
+    def finish_backend(self, block: bool = False):
+        """Reap finished backend steps (non-blocking by default: the engine
+        bounds its own run-ahead) and complete their requests."""
         if self.engine is None:
             return None
-        res = self.engine.finish()
+        res = self.engine.finish(block=block)
         for r in res.completed:
             if isinstance(r.meta, Message):
                 m = r.meta

@@ -65,6 +65,19 @@ def test_gateway_cpu_end_to_end_and_priority_order():
     assert summ["count"] == 40 and summ["p99_ms"] >= summ["p50_ms"] > 0
 
 
+def test_engine_async_launch_never_drops_completions():
+    from llm_message_queue_amd.backend.engine import Request
+    eng = engine(slots=8)
+    eng.admit([Request(i, np.arange(3, dtype=np.int32), gen_tokens=2) for i in range(8)])
+    # 4 launches with no finish in between: launch() itself reaps the full queue
+    for _ in range(4):
+        eng.launch()
+    res = eng.finish(block=True)
+    assert len(res.completed) == 8 and eng.completed_total == 8
+    assert sorted(r.req_id for r in res.completed) == list(range(8))
+    assert eng.free_slots() == 8 and not eng.finish(block=True).completed
+
+
 def test_latency_histogram_percentiles():
     rec = LatencyRecorder(4)
     v = np.array([1_000_000] * 98 + [400_000_000, 900_000_000])
