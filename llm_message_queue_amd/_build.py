@@ -43,6 +43,13 @@ def _targets() -> Dict[str, dict]:
             flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
             libs=[],
         ),
+        "_shmring": dict(
+            compiler="g++",
+            sources=[os.path.join(CSRC, "queue", "shm_ring.cpp")],
+            deps=[],
+            flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
+            libs=["-lrt"],
+        ),
         "_hipops": dict(
             compiler=os.path.join(ROCM, "bin", "hipcc"),
             sources=[os.path.join(k, "hipops.hip")],

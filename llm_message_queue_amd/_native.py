@@ -61,3 +61,7 @@ def require_hipops():
 
 def telemetry():
     return load("_telemetry", autobuild=True)
+
+
+def shmring():
+    return load("_shmring", autobuild=True)

@@ -11,9 +11,11 @@ of one entry point.
 Multi-GPU: launch under ``torch.distributed.run`` (one rank per GPU, RCCL).
 Rank 0 hosts HTTP; every rank runs the gateway tick loop and the ranks share
 work through the RCCL planner (all_gather of load vectors + all_to_all of
-request descriptors) -- the microservices of the reference never shared
-their queues (D14).  ``api-gateway`` on rank 0 plus ``queue-manager`` on the
-other ranks is the split deployment.
+request descriptors).  Split deployment: any number of ``api-gateway``
+processes (HTTP + preprocess) push into a shared-memory request ring that the
+``queue-manager`` process (dispatcher + GPU backend) drains, with status
+events flowing back -- the reference's microservices never shared their
+queues (D14).
 """
 from __future__ import annotations
 
@@ -62,7 +64,13 @@ def cmd_serve(a, role: str = "serve") -> int:
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         engine, page = _build_engine(cfg, a.model, torch.device("cuda", local))
-    gapp = GatewayApp(cfg, use_gpu=use_gpu, engine=engine, comm=comm, start=False)
+    ring, app_role = None, "serve"
+    if role in ("api-gateway", "queue-manager") and not a.no_ring:
+        # the split deployment shares ONE request queue through shared memory (D14)
+        from ..gateway.shm_bridge import RingPair
+        ring = RingPair(a.ring or cfg.server.shared_ring, cfg.server.shared_ring_bytes, "open")
+        app_role = "ingress" if role == "api-gateway" else "dispatcher"
+    gapp = GatewayApp(cfg, use_gpu=use_gpu, engine=engine, comm=comm, start=False, role=app_role, ring=ring)
     if engine is not None:
         gapp.lb.add_endpoint(Endpoint(id=f"gpu{rank}", type="llm", gpu_index=rank, page=page,
                                       max_connections=cfg.gpu.slots_per_gpu))
@@ -171,6 +179,8 @@ def main(argv=None) -> int:
         p.add_argument("--port", type=int, default=0)
         p.add_argument("--model", default="llama3-8b")
         p.add_argument("--no-gpu", action="store_true")
+        p.add_argument("--ring", default="", help="shared request ring name (api-gateway/queue-manager)")
+        p.add_argument("--no-ring", action="store_true", help="api-gateway/queue-manager without the shared ring")
     p = sub.add_parser("scheduler")
     p.add_argument("--config", default=None)
     p.add_argument("--gateway", default="http://127.0.0.1:8080")

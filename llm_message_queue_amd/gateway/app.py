@@ -22,7 +22,7 @@ from ..conversation.persistence import make_store
 from ..conversation.state_manager import StateManager
 from ..models.message import Message, MessageStatus, priority_name
 from ..preprocess.preprocessor import Preprocessor
-from ..queue.core import QueueError
+from ..queue.core import QueueError, QueueFull
 from ..queue.factory import QueueFactory, QueueType
 from ..scheduler.resource_scheduler import ResourceScheduler
 from ..utils.logging import get_logger
@@ -69,8 +69,20 @@ class MessageStore:
 
 class GatewayApp:
     def __init__(self, cfg, *, use_gpu: Optional[bool] = None, engine=None, comm=None,
-                 simulate_ms: Sequence[float] = (5, 10, 20, 30), start: bool = True):
+                 simulate_ms: Sequence[float] = (5, 10, 20, 30), start: bool = True,
+                 role: str = "serve", ring=None):
+        """``role``: "serve" (monolith), "ingress" (HTTP + preprocess, pushes
+        into the shared request ring ``ring``), or "dispatcher" (pops the ring
+        into its queue and runs the backend; reports status via the event
+        ring).  See ``shm_bridge``."""
         import torch
+        if role not in ("serve", "ingress", "dispatcher"):
+            raise ValueError(f"unknown gateway role {role!r}")
+        if role != "serve" and ring is None:
+            raise ValueError(f"role {role!r} needs a shared ring")
+        self.role = role
+        self.ring = ring
+        self._ring_thread: Optional[threading.Thread] = None
         self.cfg = cfg
         self.log = get_logger("app")
         self.metrics: QueueMetrics = default_metrics()
@@ -111,6 +123,13 @@ class GatewayApp:
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> None:
         self.state.start()
+        if self.role == "ingress":
+            self._ring_thread = threading.Thread(target=self._event_loop, name="ring-events", daemon=True)
+            self._ring_thread.start()
+            return
+        if self.role == "dispatcher":
+            self._ring_thread = threading.Thread(target=self._ring_loop, name="ring-ingest", daemon=True)
+            self._ring_thread.start()
         if self.engine is not None:
             self._loop_thread = threading.Thread(target=self._serve_loop, name="gateway-loop", daemon=True)
             self._loop_thread.start()
@@ -124,8 +143,11 @@ class GatewayApp:
     def stop(self) -> None:
         self._stop.set()
         self._wake.set()
-        if self._loop_thread is not None:
-            self._loop_thread.join(timeout=10)
+        if self.ring is not None:
+            self.ring.wake_all()
+        for t in (self._loop_thread, self._ring_thread):
+            if t is not None:
+                t.join(timeout=10)
         self.batcher.close()
         self.factory.close()
         self.state.stop()
@@ -139,7 +161,11 @@ class GatewayApp:
         for m in msgs:
             if not m.queue_name:
                 m.queue_name = priority_name(m.priority)
-        errs = self.standard.push_routed(msgs)
+        if self.role == "ingress":
+            n = self.ring.put_messages(msgs)
+            errs = [None] * n + [QueueFull(f"shared request ring {self.ring.name} is full")] * (len(msgs) - n)
+        else:
+            errs = self.standard.push_routed(msgs)
         for m, e in zip(msgs, errs):
             if e is None:
                 self.messages.put(m)
@@ -169,6 +195,43 @@ class GatewayApp:
         if len(d) < 2 or d[-1][0] <= d[0][0]:
             return 0.0
         return (d[-1][1] - d[0][1]) / (d[-1][0] - d[0][0])
+
+    # ------------------------------------------------------------------ shared rings
+    def _ring_loop(self) -> None:
+        """Dispatcher: drain the request ring into the local queue."""
+        while not self._stop.is_set():
+            msgs = self.ring.get_messages(self.cfg.preprocessor.max_batch, timeout_ms=100)
+            if not msgs:
+                continue
+            for m in msgs:
+                if not m.queue_name:
+                    m.queue_name = priority_name(m.priority)
+            errs = self.standard.push_routed(msgs)
+            bad = []
+            for m, e in zip(msgs, errs):
+                if e is None:
+                    self.messages.put(m)
+                else:
+                    m.status = MessageStatus.FAILED
+                    bad.append(m)
+            if bad:
+                self.ring.put_events(bad, error="queue full")
+            self._wake.set()
+
+    def _event_loop(self) -> None:
+        """Ingress: apply status events from the dispatcher to the message store."""
+        while not self._stop.is_set():
+            for ev in self.ring.get_events(4096, timeout_ms=100):
+                m = self.messages.get(ev["id"])
+                if m is None:
+                    continue
+                m.status = ev["status"]
+                m.endpoint_id = ev["endpoint_id"]
+                m.dispatched_at = ev["dispatched_at"]
+                m.completed_at = ev["completed_at"]
+                m.retry_count = ev["retry_count"]
+                if ev["error"]:
+                    m.metadata["error"] = ev["error"]
 
     # ------------------------------------------------------------------ dispatch
     def _serve_loop(self) -> None:
@@ -207,6 +270,8 @@ class GatewayApp:
     def _on_complete(self, msg: Message) -> None:
         msg.status = MessageStatus.COMPLETED
         msg.completed_at = time.time_ns()
+        if self.role == "dispatcher":
+            self.ring.put_events([msg])
         if msg.conversation_id:
             conv = self.state.find_conversation(msg.conversation_id)
             if conv is not None and msg.endpoint_id.startswith("gpu"):
@@ -224,5 +289,7 @@ class GatewayApp:
         out["dispatch"] = dict(self.gateway.counters)
         out["latency"] = self.gateway.rec.summary()
         out["dead_letter"] = self.factory.dead_letter_queue.size()
+        if self.ring is not None:
+            out["rings"] = self.ring.stats()
         out["delayed"] = self.factory.delayed_queue.size()
         return out

@@ -1,0 +1,101 @@
+"""Cross-process request/event rings (fixes D14: the reference's api-gateway
+and queue-manager never shared a queue, `cmd/api-gateway/main.go:66`,
+`cmd/queue-manager/main.go:58`).
+
+Ingress processes (HTTP workers, `cli api-gateway`) preprocess messages and
+push them into the *request* ring; the dispatcher process (`cli
+queue-manager`, owner of the GPU backend) pops them into its native
+MultiLevelQueue and reports status changes back through the *event* ring.
+Both rings are ``_shmring.ShmRing`` (POSIX shm, MPMC, futex wake-ups).
+
+Wire format: msgpack.  A message travels with its preprocessing results
+(priority, analysis metadata, GPU-tokenizer prompt ids), so the dispatcher
+never re-runs the preprocessor, and with its monotonic arrival timestamp
+(CLOCK_MONOTONIC is system-wide), so enqueue->dispatch latency is measured
+from the moment the ingress process received the request.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import msgpack
+import numpy as np
+
+from .. import _native
+from ..models.message import Message
+
+TAG_MESSAGE = 1
+TAG_EVENT = 2
+
+_FIELDS = ("id", "conversation_id", "user_id", "content", "priority", "status", "queue_name",
+           "retry_count", "max_retries", "timeout", "created_at", "updated_at", "scheduled_at",
+           "completed_at", "metadata", "arrival_ns")
+
+
+def encode_message(m: Message) -> bytes:
+    rec = [getattr(m, f) for f in _FIELDS]
+    p = m.prompt_ids
+    rec.append(None if p is None else np.ascontiguousarray(p, dtype=np.uint32).tobytes())
+    return msgpack.packb(rec, use_bin_type=True)
+
+
+def decode_message(b: bytes) -> Message:
+    rec = msgpack.unpackb(b, raw=False, strict_map_key=False)
+    m = Message()
+    for f, v in zip(_FIELDS, rec):
+        setattr(m, f, v)
+    if m.metadata is None:
+        m.metadata = {}
+    p = rec[len(_FIELDS)]
+    m.prompt_ids = None if p is None else np.frombuffer(p, dtype=np.uint32).copy()
+    return m
+
+
+def encode_event(m: Message, error: str = "") -> bytes:
+    return msgpack.packb([m.id, m.status, m.endpoint_id, int(m.dispatched_at or 0), m.completed_at,
+                          int(m.retry_count), error], use_bin_type=True)
+
+
+def decode_event(b: bytes) -> dict:
+    i, st, ep, disp, comp, retries, err = msgpack.unpackb(b, raw=False)
+    return {"id": i, "status": st, "endpoint_id": ep, "dispatched_at": disp, "completed_at": comp,
+            "retry_count": retries, "error": err}
+
+
+class RingPair:
+    """The request ring and the event ring of one gateway deployment."""
+
+    def __init__(self, name: str, capacity: int = 64 << 20, mode: str = "open"):
+        R = _native.shmring().ShmRing
+        self.name = name
+        self.requests = R(f"llmq-{name}-req", capacity, mode)
+        self.events = R(f"llmq-{name}-evt", max(capacity // 4, 1 << 20), mode)
+
+    # ingress side
+    def put_messages(self, msgs: Sequence[Message]) -> int:
+        """Push; returns how many fit (the rest were rejected: ring full)."""
+        return self.requests.push_many([encode_message(m) for m in msgs], TAG_MESSAGE)
+
+    def get_events(self, max_n: int = 4096, timeout_ms: int = 0) -> List[dict]:
+        return [decode_event(b) for _, b in self.events.pop(max_n, timeout_ms)]
+
+    # dispatcher side
+    def get_messages(self, max_n: int = 4096, timeout_ms: int = 0) -> List[Message]:
+        return [decode_message(b) for _, b in self.requests.pop(max_n, timeout_ms)]
+
+    def put_events(self, msgs: Iterable[Message], error: str = "") -> int:
+        recs = [encode_event(m, error) for m in msgs]
+        return self.events.push_many(recs, TAG_EVENT) if recs else 0
+
+    def stats(self) -> dict:
+        return {"requests": self.requests.stats(), "events": self.events.stats()}
+
+    def wake_all(self) -> None:
+        self.requests.wake_all()
+        self.events.wake_all()
+
+    def close(self, unlink: bool = False) -> None:
+        for r in (self.requests, self.events):
+            if unlink:
+                r.unlink()
+            r.close()

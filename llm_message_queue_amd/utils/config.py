@@ -34,6 +34,10 @@ class ServerConfig:
     port: int = 8080
     host: str = "0.0.0.0"
     mode: str = "debug"
+    # split deployment (api-gateway + queue-manager): name and size of the
+    # shared-memory request ring the two modes exchange messages through
+    shared_ring: str = "default"
+    shared_ring_bytes: int = 64 << 20
 
 
 @dataclass

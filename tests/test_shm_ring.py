@@ -1,0 +1,163 @@
+"""Process-shared request ring (native ``_shmring``) and the split
+ingress/dispatcher deployment built on it (fix for D14: the reference's
+api-gateway and queue-manager never shared a queue)."""
+import os
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from llm_message_queue_amd import _native
+from llm_message_queue_amd.gateway.shm_bridge import RingPair, decode_message, encode_message
+from llm_message_queue_amd.models.message import Message, new_message
+
+
+def ring_name(tag):
+    return f"pytest-{tag}-{os.getpid()}"
+
+
+@pytest.fixture
+def ring():
+    R = _native.shmring().ShmRing
+    r = R(ring_name("basic"), 8192, "create")
+    yield r
+    r.unlink()
+    r.close()
+
+
+def test_fifo_wrap_and_full(ring):
+    R = _native.shmring().ShmRing
+    other = R(ring.name, 0, "attach")                 # a second handle on the same segment
+    rng = random.Random(1)
+    sent, got = [], []
+    for i in range(3000):                              # many wrap-arounds of an 8 KiB ring
+        rec = bytes([i % 251]) * rng.randint(0, 300)
+        if ring.push(rec, i % 7):
+            sent.append((i % 7, rec))
+        if rng.random() < 0.5:
+            got += other.pop(rng.randint(1, 8), 0)
+    got += other.pop(100000, 0)
+    assert got == sent and len(sent) > 2000
+    st = ring.stats()
+    assert st["pushed"] == st["popped"] == len(sent) and st["size"] == 0 and st["bytes_used"] == 0
+    # full ring rejects (and counts) instead of overwriting
+    n = ring.push_many([b"x" * 1000] * 20)
+    assert 0 < n < 20 and ring.stats()["dropped_full"] >= 20 - n
+    assert not ring.push(b"y" * 5000)                  # larger than half the ring: never fits
+    assert len(other.pop(100, 0)) == n
+
+
+def test_pop_timeout_and_wake(ring):
+    t0 = time.monotonic()
+    assert ring.pop(10, 30) == []
+    assert 0.02 < time.monotonic() - t0 < 1.0
+    out = []
+    th = threading.Thread(target=lambda: out.append(ring.pop(10, 5000)))
+    th.start()
+    time.sleep(0.05)
+    ring.push(b"wake", 9)
+    th.join(2)
+    assert out == [[(9, b"wake")]]
+    th = threading.Thread(target=lambda: out.append(ring.pop(10, 5000)))
+    th.start()
+    time.sleep(0.05)
+    t0 = time.monotonic()
+    ring.wake_all()                                    # empty wake: returns [] promptly
+    th.join(2)
+    assert out[-1] == [] and time.monotonic() - t0 < 1.0
+
+
+def _producer(name, k, n):
+    R = _native.shmring().ShmRing
+    r = R(name, 0, "attach")
+    i = 0
+    while i < n:
+        if r.push(f"{k}:{i}".encode() + b"." * (i % 50), k):
+            i += 1
+        else:
+            time.sleep(0.0005)
+
+
+def test_multiprocess_mpmc_exactly_once():
+    import multiprocessing as mp
+    name = ring_name("mpmc")
+    R = _native.shmring().ShmRing
+    r = R(name, 1 << 16, "create")
+    try:
+        ctx = mp.get_context("spawn")
+        ps = [ctx.Process(target=_producer, args=(name, k, 3000)) for k in range(3)]
+        for p in ps:
+            p.start()
+        seen = {k: [] for k in range(3)}
+        lock = threading.Lock()
+        stop = threading.Event()
+
+        def consume():
+            c = R(name, 0, "attach")
+            while not stop.is_set() or c.size():
+                for tag, b in c.pop(64, 20):
+                    with lock:
+                        seen[tag].append(int(b.split(b":")[1].split(b".")[0]))
+
+        cs = [threading.Thread(target=consume) for _ in range(2)]
+        for c in cs:
+            c.start()
+        for p in ps:
+            p.join(120)
+            assert p.exitcode == 0
+        stop.set()
+        for c in cs:
+            c.join(30)
+        for k in range(3):
+            assert sorted(seen[k]) == list(range(3000))
+    finally:
+        r.unlink()
+
+
+def test_message_wire_roundtrip():
+    m = new_message("c1", "u1", "urgent: is it down?", 2)
+    m.metadata = {"analyzed": "true", "score": 3, "nested": {"a": [1, 2]}}
+    m.prompt_ids = np.array([5, 7, 2**31 + 3], dtype=np.uint32)
+    m.arrival_ns = 123456789
+    m.queue_name = "high"
+    d = decode_message(encode_message(m))
+    assert d.to_dict() == m.to_dict()
+    assert d.arrival_ns == m.arrival_ns and np.array_equal(d.prompt_ids, m.prompt_ids)
+    m.prompt_ids = None
+    assert decode_message(encode_message(m)).prompt_ids is None
+
+
+def test_split_ingress_and_dispatcher_share_queue():
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    from llm_message_queue_amd.utils.config import default_config
+    cfg = default_config()
+    cfg.queue.worker.process_interval = 5_000_000
+    cfg.preprocessor.batch_window_us = 200
+    name = ring_name("split")
+    disp_ring = RingPair(name, 1 << 20, "create")
+    ing_ring = RingPair(name, 0, "attach")
+    disp = GatewayApp(cfg, use_gpu=False, simulate_ms=(1, 1, 1, 1), role="dispatcher", ring=disp_ring)
+    ing = GatewayApp(cfg, use_gpu=False, role="ingress", ring=ing_ring)
+    try:
+        msgs = [new_message("", f"u{i}", "EMERGENCY now" if i % 4 == 0 else f"hello {i}", 0) for i in range(40)]
+        for m in msgs:
+            assert ing.submit(m) is None
+        assert ing.standard.get_all_queue_stats()["realtime"].pending_count == 0   # nothing queued locally
+        t0 = time.time()
+        while time.time() - t0 < 10:
+            if all(ing.messages.get(m.id).status == "completed" for m in msgs):
+                break
+            time.sleep(0.02)
+        assert all(ing.messages.get(m.id).status == "completed" for m in msgs)
+        assert all(ing.messages.get(m.id).endpoint_id for m in msgs)
+        got = [disp.messages.get(m.id) for m in msgs]
+        assert all(g is not None for g in got)
+        assert [g.priority for g in got[::4]] == [1] * 10           # preprocessing travelled with the message
+        assert disp.gateway.counters["dispatched"] == 40
+    finally:
+        ing.stop()
+        disp.stop()
+        disp_ring.close(unlink=True)
+        ing_ring.close()
