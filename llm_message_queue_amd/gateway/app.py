@@ -11,6 +11,7 @@
 from __future__ import annotations
 
 import collections
+import os
 import threading
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -53,6 +54,10 @@ class MessageStore:
         with self._lock:
             return self._d.get(mid)
 
+    def values(self) -> List[Message]:
+        with self._lock:
+            return list(self._d.values())
+
     def remove(self, mid: str) -> Optional[Message]:
         with self._lock:
             return self._d.pop(mid, None)
@@ -83,6 +88,7 @@ class GatewayApp:
         self.role = role
         self.ring = ring
         self._ring_thread: Optional[threading.Thread] = None
+        self._snap_thread: Optional[threading.Thread] = None
         self.cfg = cfg
         self.log = get_logger("app")
         self.metrics: QueueMetrics = default_metrics()
@@ -123,6 +129,21 @@ class GatewayApp:
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> None:
         self.state.start()
+        snap = self.cfg.queue.snapshot_path
+        if snap and self.role != "ingress":
+            from ..queue.snapshot import read_snapshot
+            counts = read_snapshot(self.factory, snap)
+            if counts is not None:
+                self.log.info("Resumed queue snapshot", path=snap, **counts)
+                os.replace(snap, snap + ".resumed")
+                for mgr in self.factory.managers().values():
+                    for q in mgr.queue_names():
+                        for m in mgr.mlq.messages(q):
+                            self.messages.put(m)
+            if self.cfg.queue.snapshot_interval > 0:
+                self._snap_thread = threading.Thread(target=self._snapshot_loop, name="queue-snapshot",
+                                                     daemon=True)
+                self._snap_thread.start()
         if self.role == "ingress":
             self._ring_thread = threading.Thread(target=self._event_loop, name="ring-events", daemon=True)
             self._ring_thread.start()
@@ -145,9 +166,11 @@ class GatewayApp:
         self._wake.set()
         if self.ring is not None:
             self.ring.wake_all()
-        for t in (self._loop_thread, self._ring_thread):
+        for t in (self._loop_thread, self._ring_thread, self._snap_thread):
             if t is not None:
                 t.join(timeout=10)
+        if self.cfg.queue.snapshot_path and self.role != "ingress":
+            self.snapshot()
         self.batcher.close()
         self.factory.close()
         self.state.stop()
@@ -195,6 +218,21 @@ class GatewayApp:
         if len(d) < 2 or d[-1][0] <= d[0][0]:
             return 0.0
         return (d[-1][1] - d[0][1]) / (d[-1][0] - d[0][0])
+
+    # ------------------------------------------------------------------ checkpoint
+    def snapshot(self, path: str = "") -> Dict[str, int]:
+        """Write queued + in-flight + delayed + dead-lettered messages (JSONL)."""
+        from ..queue.snapshot import write_snapshot
+        inflight = [m for m in self.messages.values() if m.status == MessageStatus.PROCESSING]
+        return write_snapshot(self.factory, path or self.cfg.queue.snapshot_path, inflight)
+
+    def _snapshot_loop(self) -> None:
+        period = self.cfg.queue.snapshot_interval / 1e9
+        while not self._stop.wait(period):
+            try:
+                self.snapshot()
+            except OSError as e:
+                self.log.error("Queue snapshot failed", error=str(e))
 
     # ------------------------------------------------------------------ shared rings
     def _ring_loop(self) -> None:

@@ -76,6 +76,11 @@ class DeadLetterQueue:
             except _pyqueue.Full:
                 self.dropped_notifications += 1
 
+    def restore(self, item: DeadLetterItem) -> None:
+        """Re-insert an item from a snapshot (no handlers/notifications fire)."""
+        with self._lock:
+            self._items.append(item)
+
     def _run_handler(self, h: DeadLetterHandler, item: DeadLetterItem) -> None:
         try:
             err = h(item)

@@ -110,6 +110,11 @@ class DelayedQueue:
             return None, 0, False
         return item[0], item[1], True
 
+    def items(self):
+        """[(msg, ready_at wall ns, target)] of every scheduled item (snapshot)."""
+        with self._lock:
+            return list(self._items.values())
+
     def clear(self) -> None:
         for h in self._native.clear():
             with self._lock:

@@ -115,6 +115,11 @@ class QueueConfig:
     # MI355X build additions
     enable_aging: bool = True          # promote a tier head past its max_wait_time
     dead_letter_max_size: int = 10000
+    # checkpoint/resume of queue contents (doc-only in the reference,
+    # docs/configuration.md:290-309): JSONL snapshot of queued, in-flight,
+    # delayed and dead-lettered messages; replayed on start.  "" disables.
+    snapshot_path: str = ""
+    snapshot_interval: int = 0         # ns; 0 = only at shutdown
 
 
 @dataclass
