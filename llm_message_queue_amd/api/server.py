@@ -319,7 +319,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
     async def update_endpoint_status(eid: str, request: Request):
         try:
             status = str((await _json(request))["status"])
-            G.lb.update_endpoint_status(eid, status)
+            G.set_endpoint_status(eid, status)
         except LoadBalancerError:
             return _err(404, "endpoint not found")
         except Exception as e:

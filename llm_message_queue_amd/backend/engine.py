@@ -106,6 +106,10 @@ class BackendEngine:
         self._pins = [self._alloc_pin(4 * (3 * token_budget + 2 * slots + 64)) for _ in range(2)]
         self._state_pins = [self._alloc_pin(4 * slots) for _ in range(2)]
         self._slot_state_d = torch.zeros(slots, dtype=torch.int32, device=self.device)
+        # fault injection: {"fail_launch": n} raises on the next
+        # n launches (a HIP error / OOM), {"slow_ms": x} stalls every launch,
+        # {"drop_heartbeat": True} stops the load-page census
+        self.fault: Dict[str, float] = {}
         if self.cuda and page is not None and page.dev_ptr is None:
             page.register_device()
         if page is not None:
@@ -187,8 +191,42 @@ class BackendEngine:
                 sample_reqs.append(r)
         return toks, pos, slot, samp, sample_reqs, dec_rows, dec_src, n_pre, n_dec
 
+    def inject(self, **fault) -> None:
+        """Fault injection: ``fail_launch=n``, ``slow_ms=x``, ``drop_heartbeat=True``
+        (0/False clears one)."""
+        for k, v in fault.items():
+            if k not in ("fail_launch", "slow_ms", "drop_heartbeat"):
+                raise ValueError(f"unknown fault {k!r}")
+            if v:
+                self.fault[k] = v
+            else:
+                self.fault.pop(k, None)
+
+    def abort_all(self) -> List[Request]:
+        """Evacuate: drop every queued step and active request (slots are
+        freed) and return the unfinished requests so the caller can re-route
+        them.  Steps not yet reaped by ``finish`` count as unfinished (their
+        completions were never reported): at-least-once.  Makes no GPU call,
+        so it is safe after a device error; reap first if the GPU is fine."""
+        out = [r for f in list(self._q) + self._reaped for r in f.completed]
+        out += list(self.active.values())
+        self._q.clear()
+        self._reaped = []
+        self._prev_out = None
+        self.active.clear()
+        self.free = list(range(self.slots - 1, -1, -1))
+        return out
+
     def launch(self) -> None:
         """Build the next token batch and enqueue its forward (async)."""
+        if self.fault:
+            if self.fault.get("fail_launch", 0) > 0:
+                self.fault["fail_launch"] -= 1
+                if self.fault["fail_launch"] <= 0:
+                    del self.fault["fail_launch"]
+                raise RuntimeError("HIP error: out of memory (injected fault)")
+            if self.fault.get("slow_ms"):
+                time.sleep(self.fault["slow_ms"] / 1e3)
         while len(self._q) >= self.max_inflight:       # bound the run-ahead (and staging reuse)
             self._reaped.append(self._reap(block=True))  # handed to the next finish()
         t0 = time.perf_counter()
@@ -258,7 +296,7 @@ class BackendEngine:
             r.first_token_ns = now
         for r in f.completed:
             r.done_ns = now
-        if self.page is not None and not self.cuda:
+        if self.page is not None and not self.cuda and not self.fault.get("drop_heartbeat"):
             self.page.write_host(self.inflight(), self.free_slots(), f.T, f.step)
         return f
 
@@ -287,7 +325,7 @@ class BackendEngine:
 
     # ------------------------------------------------------------------ N9 page
     def _census(self, tokens: int) -> None:
-        if self.page is None or not self.cuda or self.page.dev_ptr is None:
+        if self.page is None or not self.cuda or self.page.dev_ptr is None or self.fault.get("drop_heartbeat"):
             return
         pin = self._state_pins[self.step_id % 2]
         st = pin.numpy().view(np.int32)

@@ -77,6 +77,8 @@ def cmd_serve(a, role: str = "serve") -> int:
         gapp.resources.register_gpu(rank, a.model, cfg.gpu.slots_per_gpu,
                                     torch.cuda.get_device_properties(engine.device).total_memory,
                                     cfg.gpu.slots_per_gpu * cfg.backend.max_ctx)
+    if page is not None:
+        gapp.start_telemetry({rank: page})
     gapp.start()
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())

@@ -89,6 +89,7 @@ class GatewayApp:
         self.ring = ring
         self._ring_thread: Optional[threading.Thread] = None
         self._snap_thread: Optional[threading.Thread] = None
+        self.telemetry = None
         self.cfg = cfg
         self.log = get_logger("app")
         self.metrics: QueueMetrics = default_metrics()
@@ -166,6 +167,8 @@ class GatewayApp:
         self._wake.set()
         if self.ring is not None:
             self.ring.wake_all()
+        if self.telemetry is not None:
+            self.telemetry.stop()
         for t in (self._loop_thread, self._ring_thread, self._snap_thread):
             if t is not None:
                 t.join(timeout=10)
@@ -218,6 +221,32 @@ class GatewayApp:
         if len(d) < 2 or d[-1][0] <= d[0][0]:
             return 0.0
         return (d[-1][1] - d[0][1]) / (d[-1][0] - d[0][0])
+
+    # ------------------------------------------------------------------ health
+    def set_endpoint_status(self, eid: str, status: str) -> None:
+        """LB endpoint status; for this process's own GPU endpoint also the
+        gateway's health (unhealthy evacuates the backend, healthy re-admits)."""
+        self.lb.update_endpoint_status(eid, status)
+        if self.engine is not None and eid == f"gpu{self.gateway.rank}":
+            self.gateway.set_healthy(status == "healthy", f"operator set {status}")
+
+    def _gpu_unhealthy(self, gpu: int, reason: str) -> None:
+        """Telemetry callback (ECC / amd-smi failure)."""
+        try:
+            self.lb.update_endpoint_status(f"gpu{gpu}", "unhealthy")
+        except Exception:
+            pass
+        if self.engine is not None and gpu == getattr(self.engine, "gpu_index", -1):
+            self.gateway.set_healthy(False, reason)
+
+    def start_telemetry(self, pages: Dict[int, object]):
+        """N8 amd-smi poller -> load pages, metrics, ResourceScheduler, health."""
+        from ..backend.telemetry import TelemetryService
+        self.telemetry = TelemetryService(self.cfg.gpu.telemetry_period_ms, pages=pages, metrics=self.metrics,
+                                          resource_scheduler=self.resources, on_unhealthy=self._gpu_unhealthy)
+        if self.telemetry.available:
+            self.telemetry.start()
+        return self.telemetry
 
     # ------------------------------------------------------------------ checkpoint
     def snapshot(self, path: str = "") -> Dict[str, int]:

@@ -96,7 +96,7 @@ class LatencyRecorder:
 
 
 # --------------------------------------------------------------------------- descriptors
-K_DISPATCH, K_DONE = 1, 2
+K_DISPATCH, K_DONE, K_FAIL = 1, 2, 3     # K_FAIL: an evacuating backend hands a request back
 DESC_HDR = 12
 
 
@@ -154,7 +154,15 @@ class Gateway:
         self._done_owed: Dict[int, List[Tuple[int, int, int, int]]] = {r: [] for r in range(self.world)}
         self.rec = LatencyRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
-                         "remote_sent": 0, "remote_recv": 0}
+                         "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0}
+        # failure detection: a backend error (HIP error / OOM), the telemetry
+        # poller (ECC, amd-smi gone) or an operator marks this GPU unhealthy;
+        # it then takes no new work, its in-flight requests are re-routed and
+        # conversations homed on it are re-homed wherever they land next
+        self.healthy = True
+        self.health_reason = ""
+        self._tick_lock = threading.RLock()     # set_healthy from a telemetry thread waits for the tick
+        self.unhealthy_peers: set = set()
         self.on_complete = None     # optional callback(msg)
         self._next_req = 1 << 40
 
@@ -231,7 +239,7 @@ class Gateway:
         return self._dispatch_global()
 
     def _dispatch_local(self) -> int:
-        if self.engine is None:
+        if self.engine is None or not self.healthy:
             return 0
         free = self.engine.free_slots()
         if free <= 0:
@@ -272,9 +280,10 @@ class Gateway:
         free = self.engine.free_slots() if self.engine is not None else 0
         inflight = self.engine.inflight() if self.engine is not None else 0
         done_for = [len(self._done_owed[r]) for r in range(W)]
-        load = planner.make_load(free, inflight, depth, age, healthy=self.engine is not None,
+        load = planner.make_load(free, inflight, depth, age, healthy=self.engine is not None and self.healthy,
                                  done_for=done_for, pinned=[int(x) for x in self.pinned])
         loads = self.comm.all_gather_i64(load)
+        self.unhealthy_peers = {i for i in range(W) if loads[i, planner.L_HEALTHY] == 0}
         quota = planner.plan_dispatch(loads, [a // 1000 for a in self.aging_ns])
         # pop exactly my per-tier grant
         mine = quota[me]                              # [W, 4]
@@ -301,7 +310,7 @@ class Gateway:
                 # KV-residency affinity: fill destination j's quota with the
                 # conversations homed on GPU j first, then in queue order
                 pool = by_tier[t]
-                pref = [m for m in pool if self._home(m) == j][:n]
+                pref = [m for m in pool if self._home(m, effective=True) == j][:n]
                 if len(pref) < n:
                     pick = set(id(m) for m in pref)
                     pref += [m for m in pool if id(m) not in pick][:n - len(pref)]
@@ -320,7 +329,7 @@ class Gateway:
                 m.dispatched_at = time.monotonic_ns()
             for k, rec in enumerate(self._done_owed[j]):
                 row = buf[len(rows) + k]
-                row[0] = K_DONE
+                row[0] = rec[4]
                 row[1], row[2] = _split64(np.array([rec[0]]))[0][0], _split64(np.array([rec[0]]))[1][0]
                 row[3], row[4] = me, rec[1]
                 row[5], row[6] = _split64(np.array([rec[2]]))[0][0], _split64(np.array([rec[2]]))[1][0]
@@ -343,6 +352,8 @@ class Gateway:
                     reqs.append(self._foreign_request(row, cap))
                 elif row[0] == K_DONE:
                     self._remote_done(row)
+                elif row[0] == K_FAIL:
+                    self._remote_fail(row)
         admitted = self.engine.admit(reqs) if (self.engine is not None and reqs) else []
         now = time.monotonic_ns()
         tiers, arr, enqs = [], [], []
@@ -367,11 +378,16 @@ class Gateway:
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
 
-    def _home(self, m: Message) -> int:
+    def _home(self, m: Message, effective: bool = False) -> int:
+        """GPU holding the conversation's KV (-1: none).  ``effective``: -1
+        as well when that GPU is unhealthy (the conversation is re-homed)."""
         h = m.metadata.get("home_gpu") if m.metadata else None
         if h is None and self.state_manager is not None and m.conversation_id:
             h = self.state_manager.home_gpu(m.conversation_id)
-        return -1 if h is None else int(h)
+        h = -1 if h is None else int(h)
+        if effective and (h in self.unhealthy_peers or (h == self.rank and not self.healthy)):
+            return -1
+        return h
 
     def _fill_desc(self, row: np.ndarray, m: Message, origin: int, cap: int) -> None:
         row[0] = K_DISPATCH
@@ -394,6 +410,57 @@ class Gateway:
         self._next_req += 1
         return Request(req_id=self._next_req, prompt=prompt, gen_tokens=gen, tier=tier,
                        meta=(origin, handle, tier, arrival, enq))
+
+    def _remote_fail(self, row: np.ndarray) -> None:
+        """The backend my request was sent to evacuated it: queue it again."""
+        handle = int(_join64(row[1:2], row[2:3])[0])
+        m = self.remote_out.pop(handle, None)
+        if m is None:
+            return
+        self.inflight_by_tier[m.tier] -= 1
+        self._requeue(m)
+        self.counters["handed_back"] += 1
+
+    def _requeue(self, m: Message) -> None:
+        m.status = MessageStatus.PENDING
+        m.endpoint_id = ""
+        m.dispatched_at = 0
+        self.qm.requeue_after_failure(m.queue_name, m)
+        h = self._home(m)
+        if self.world > 1 and 0 <= h < self.world:
+            self.pinned[h] += 1
+
+    # ------------------------------------------------------------------ health
+    def set_healthy(self, healthy: bool, reason: str = "") -> int:
+        """Mark this rank's GPU (un)healthy.  Going unhealthy evacuates the
+        backend: local requests are re-queued here (the planner then places
+        them on healthy GPUs), foreign ones are handed back to their origin
+        router (K_FAIL).  Returns the number of evacuated requests."""
+        with self._tick_lock:
+            return self._set_healthy(healthy, reason)
+
+    def _set_healthy(self, healthy: bool, reason: str) -> int:
+        was = self.healthy
+        self.healthy, self.health_reason = bool(healthy), ("" if healthy else reason)
+        if healthy or not was or self.engine is None:
+            return 0
+        self.log.warning("GPU backend unhealthy; evacuating", rank=self.rank, reason=reason)
+        n = 0
+        for r in self.engine.abort_all():
+            n += 1
+            if isinstance(r.meta, Message):
+                m = r.meta
+                self.local.pop(m.handle, None)
+                if 0 <= r.tier < len(self.inflight_by_tier):
+                    self.inflight_by_tier[r.tier] -= 1
+                if m.metadata and m.metadata.get("home_gpu") == self.rank:
+                    del m.metadata["home_gpu"]
+                self._requeue(m)
+            else:
+                origin, handle, tier = self.foreign.pop(r.req_id)
+                self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
+        self.counters["evacuated"] += n
+        return n
 
     def _remote_done(self, row: np.ndarray) -> None:
         handle = int(_join64(row[1:2], row[2:3])[0])
@@ -438,7 +505,7 @@ class Gateway:
                 self._complete(m, r.done_ns - r.admitted_ns)
             else:
                 origin, handle, tier = self.foreign.pop(r.req_id)
-                self._done_owed[origin].append((handle, tier, r.admitted_ns, r.done_ns))
+                self._done_owed[origin].append((handle, tier, r.admitted_ns, r.done_ns, K_DONE))
         return res
 
     def tick(self):
@@ -446,10 +513,20 @@ class Gateway:
         launch the backend forward (async) -> ingest + GPU preprocess on a
         side stream -> collect the forward (completions free slots) ->
         dispatch queued requests into free slots for the next forward."""
-        if self.engine is not None:
-            self.engine.launch()
-        self.ingest()
-        res = self.finish_backend()
+        with self._tick_lock:
+            return self._tick()
+
+    def _tick(self):
+        res = None
+        if self.engine is not None and self.healthy:
+            try:
+                self.engine.launch()
+                self.ingest()
+                res = self.finish_backend()
+            except RuntimeError as e:           # HIP error / OOM from the backend
+                self._set_healthy(False, f"backend error: {e}")
+        if res is None:
+            self.ingest()
         n = self.dispatch()
         self.counters["ticks"] += 1
         return n, res

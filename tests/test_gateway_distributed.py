@@ -249,3 +249,54 @@ def test_telemetry_fault_injection_marks_unhealthy():
         assert bad and bad[0][0] == 0 and "ECC" in bad[0][1] and page.read()["healthy"] == 0
     finally:
         page.close(unlink=True)
+
+
+# ---------------------------------------------------------------- failure detection / evacuation
+@pytest.mark.parametrize("world", [2, 4])
+def test_backend_fault_evacuates_and_reroutes(world):
+    comms = FakeComm.make(world)
+    gws = [Gateway(cfg(), engine=engine(slots=4, seed=r), comm=comms[r], use_gpu_preprocess=False, prompt_cap=8,
+                   gen_tokens=3) for r in range(world)]
+    n = 16 * world
+    msgs = Workload(seed=3).make(n)
+    for i, m in enumerate(msgs):                      # half the conversations live on the GPU that will fail
+        if i % 2:
+            m.metadata["home_gpu"] = 1
+    gws[0].submit(msgs)
+    for _ in range(3):                                # get work in flight everywhere
+        ths = [threading.Thread(target=g.tick) for g in gws]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+    assert gws[1].engine.inflight() > 0
+    gws[1].engine.inject(fail_launch=1)               # next forward on GPU 1 raises (HIP OOM)
+    assert run_until_done(gws, n)
+    assert not gws[1].healthy and "out of memory" in gws[1].health_reason
+    assert gws[1].counters["evacuated"] > 0 and gws[0].counters["handed_back"] > 0
+    assert gws[0].counters["completed"] == n and all(g.pending() == 0 for g in gws)
+    assert not gws[0].remote_out and all(not g.foreign for g in gws)
+    # after the fault GPU 1 got no new work
+    before = gws[1].engine.completed_total
+    gws[0].submit(Workload(seed=4).make(8))
+    assert run_until_done(gws, n + 8)
+    assert gws[1].engine.completed_total == before
+    # operator brings it back: it is used again
+    gws[1].set_healthy(True)
+    gws[0].submit(Workload(seed=5).make(8 * world))
+    assert run_until_done(gws, n + 8 + 8 * world)
+    assert gws[1].engine.completed_total > before
+
+
+def test_single_rank_fault_requeues_and_recovers():
+    gw = Gateway(cfg(), engine=engine(slots=4), use_gpu_preprocess=False, prompt_cap=8, gen_tokens=3)
+    gw.submit(Workload(seed=8).make(10))
+    gw.tick(); gw.tick()
+    gw.engine.inject(fail_launch=1)
+    gw.tick()
+    assert not gw.healthy and gw.counters["evacuated"] > 0 and gw.engine.inflight() == 0
+    for _ in range(5):
+        gw.tick()
+    assert gw.counters["completed"] < 10 and gw.pending() > 0      # no healthy backend: requests wait
+    gw.set_healthy(True)
+    assert run_until_done([gw], 10)
+    st = gw.qm.get_all_queue_stats()
+    assert sum(s.processing_count for s in st.values()) == 0
