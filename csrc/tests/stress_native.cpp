@@ -1,0 +1,211 @@
+// Multi-threaded stress of the native host runtime, built WITHOUT Python so it
+// can run under ThreadSanitizer / AddressSanitizer+UBSan (SURVEY.md §5 "race
+// detection": the reference relies on `go test -race`, .github/workflows/go.yml:27).
+//
+//   g++ -std=c++17 -O1 -g -fsanitize=thread -Icsrc csrc/tests/stress_native.cpp -o /tmp/stress -lrt -pthread
+//   /tmp/stress            # exit 0 = every invariant held (sanitizer reports fail the run)
+//
+// Covers: MultiLevelQueue (concurrent push/push_batch/pop_tiers/pop_batch/
+// stats/complete across 4 tiers, exactly-once delivery, FIFO per producer
+// within a tier), DelayedQueue (concurrent schedule + wait_ready, no early
+// delivery), ShmRing (2 handles on one segment, MPMC exactly-once).
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "queue/mlq_core.h"
+#include "queue/shm_ring.h"
+
+#define CHECK(c)                                                              \
+  do {                                                                        \
+    if (!(c)) {                                                               \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      std::exit(1);                                                           \
+    }                                                                         \
+  } while (0)
+
+static void stress_mlq() {
+  using namespace llmq;
+  MultiLevelQueue q(0);
+  const std::vector<std::string> tiers = {"realtime", "high", "normal", "low"};
+  for (auto& t : tiers) q.add_queue(t, -1);
+  constexpr int P = 4, N = 20000;
+  std::atomic<int> done_producers{0};
+  std::vector<std::thread> th;
+  for (int p = 0; p < P; ++p) {
+    th.emplace_back([&, p] {
+      // handles are pushed in increasing order: runs of 64 via push_batch,
+      // then 32 single pushes
+      std::vector<int32_t> qi, pr;
+      std::vector<int64_t> hs;
+      for (int i = 0; i < N;) {
+        if ((i / 32) % 3 != 2) {
+          for (int k = 0; k < 64 && i < N; ++k, ++i) {
+            int64_t h = (int64_t)p * N + i;
+            qi.push_back((int32_t)(h % 4));
+            hs.push_back(h);
+            pr.push_back((int32_t)(h % 4) + 1);
+          }
+          auto st = q.push_batch(tiers, qi.data(), hs.data(), pr.data(), (int64_t)qi.size());
+          for (int s : st) CHECK(s == OK);
+          qi.clear(); hs.clear(); pr.clear();
+        } else {
+          for (int k = 0; k < 32 && i < N; ++k, ++i) {
+            int64_t h = (int64_t)p * N + i;
+            CHECK(q.push(tiers[h % 4], h, (int32_t)(h % 4) + 1).first == OK);
+          }
+        }
+      }
+      done_producers++;
+    });
+  }
+  std::vector<std::vector<int64_t>> got(3);
+  for (int c = 0; c < 3; ++c) {
+    th.emplace_back([&, c] {
+      std::vector<int64_t> hs, enq;
+      std::vector<int32_t> ti;
+      while (true) {
+        bool fin = done_producers.load() == P;
+        hs.clear(); ti.clear(); enq.clear();
+        if (c == 2) {
+          for (auto& t : tiers) {
+            auto v = q.pop_batch(t, 17);
+            for (auto h : v) { hs.push_back(h); ti.push_back((int32_t)(h % 4)); }
+          }
+        } else {
+          q.pop_tiers(tiers, 97, {1000000, 0, 0, 5000000}, {-1, 50, -1, 20}, hs, ti, enq);
+        }
+        for (size_t k = 0; k < hs.size(); ++k) {
+          CHECK(hs[k] % 4 == ti[k]);
+          got[c].push_back(hs[k]);
+          CHECK(q.complete(tiers[ti[k]], 10));
+        }
+        Stats s;
+        CHECK(q.stats(tiers[c], &s));
+        CHECK(s.pending >= 0);
+        if (fin && hs.empty() && q.total_size() == 0) break;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  std::vector<int64_t> all;
+  for (auto& g : got) all.insert(all.end(), g.begin(), g.end());
+  std::sort(all.begin(), all.end());
+  CHECK((int)all.size() == P * N);
+  for (int i = 0; i < P * N; ++i) CHECK(all[i] == i);
+  // per consumer: handles of one producer within one tier arrive in push order
+  for (auto& g : got) {
+    std::map<std::pair<int64_t, int64_t>, int64_t> last;
+    for (auto h : g) {
+      auto key = std::make_pair(h / N, h % 4);
+      auto it = last.find(key);
+      CHECK(it == last.end() || it->second < h);
+      last[key] = h;
+    }
+  }
+  int64_t completed = 0;
+  for (auto& t : tiers) {
+    Stats s;
+    CHECK(q.stats(t, &s));
+    CHECK(s.pending == 0 && s.processing == 0);
+    completed += s.completed;
+  }
+  CHECK(completed == (int64_t)P * N);
+  std::printf("mlq: %d items, 4 producers / 3 consumers OK\n", P * N);
+}
+
+static void stress_delayed() {
+  using namespace llmq;
+  DelayedQueue d;
+  constexpr int P = 4, N = 500;
+  std::vector<std::thread> th;
+  std::vector<int64_t> due((size_t)P * N);
+  for (int p = 0; p < P; ++p) {
+    th.emplace_back([&, p] {
+      for (int i = 0; i < N; ++i) {
+        int64_t h = (int64_t)p * N + i;
+        int64_t at = mono_ns() + (h % 37) * 200000;   // 0..7.2 ms
+        due[h] = at;
+        d.schedule(h, at);
+      }
+    });
+  }
+  std::set<int64_t> seen;
+  std::thread cons([&] {
+    while ((int)seen.size() < P * N) {
+      auto v = d.wait_ready(64, 0.05);
+      int64_t now = mono_ns();
+      for (auto h : v) {
+        CHECK(seen.insert(h).second);
+        CHECK(now >= due[h] - 1000000);          // 1 ms early-fire tolerance
+      }
+    }
+  });
+  for (auto& t : th) t.join();
+  cons.join();
+  CHECK(d.size() == 0);
+  d.shutdown();
+  std::printf("delayed: %d items OK\n", P * N);
+}
+
+static void stress_ring() {
+  using llmq::ShmRing;
+  std::string name = "/llmq-stress-" + std::to_string(getpid());
+  ShmRing a(name, 1 << 14, "create");
+  ShmRing b(name, 0, "attach");
+  constexpr int P = 3, N = 20000;
+  std::vector<std::thread> th;
+  for (int p = 0; p < P; ++p) {
+    th.emplace_back([&, p] {
+      ShmRing& r = (p % 2) ? a : b;
+      for (int i = 0; i < N;) {
+        std::string rec = std::to_string(p * N + i) + std::string(i % 40, '.');
+        if (r.push(rec, (uint32_t)p)) ++i;
+        else std::this_thread::yield();
+      }
+    });
+  }
+  std::atomic<int> total{0};
+  std::vector<std::vector<int>> got(2);
+  for (int c = 0; c < 2; ++c) {
+    th.emplace_back([&, c] {
+      ShmRing& r = c ? a : b;
+      while (total.load() < P * N) {
+        auto v = r.pop(32, 5);
+        for (auto& kv : v) {
+          int id = std::atoi(kv.second.c_str());
+          CHECK((int)kv.first == id / N);
+          got[c].push_back(id);
+        }
+        total += (int)v.size();
+      }
+      r.wake_all();
+    });
+  }
+  for (auto& t : th) t.join();
+  std::vector<int> all;
+  for (auto& g : got) all.insert(all.end(), g.begin(), g.end());
+  std::sort(all.begin(), all.end());
+  CHECK((int)all.size() == P * N);
+  for (int i = 0; i < P * N; ++i) CHECK(all[i] == i);
+  auto s = a.stats();
+  CHECK(s.size == 0 && s.pushed == (uint64_t)P * N && s.popped == (uint64_t)P * N);
+  a.unlink();
+  std::printf("shm ring: %d records, 3 producers / 2 consumers OK\n", P * N);
+}
+
+int main() {
+  stress_mlq();
+  stress_delayed();
+  stress_ring();
+  std::printf("ALL OK\n");
+  return 0;
+}

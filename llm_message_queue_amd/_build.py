@@ -39,14 +39,14 @@ def _targets() -> Dict[str, dict]:
         "_mlq": dict(
             compiler="g++",
             sources=[os.path.join(CSRC, "queue", "mlq.cpp")],
-            deps=[],
+            deps=[os.path.join(CSRC, "queue", "mlq_core.h")],
             flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
             libs=[],
         ),
         "_shmring": dict(
             compiler="g++",
             sources=[os.path.join(CSRC, "queue", "shm_ring.cpp")],
-            deps=[],
+            deps=[os.path.join(CSRC, "queue", "shm_ring.h")],
             flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
             libs=["-lrt"],
         ),
