@@ -122,7 +122,7 @@ def main(argv=None) -> int:
     # token throughput over the second half and convert it to requests/s with
     # the measured tokens per completed request (robust to the prefill/decode
     # waves a saturated start produces).
-    warm = max(a.warmup, 12)
+    warm = max(a.warmup, 40)
     t_c0 = None
     tok0 = rt0 = done0 = 0
     for i in range(warm):
@@ -135,8 +135,15 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(dev)
             t_c0 = time.perf_counter()
             tok0, rt0, done0 = engine.total_tokens, engine.completed_tokens, engine.completed_total
+            gw.host_profile(reset=True)
+            sat_eng0 = engine.host_ns.copy()
     torch.cuda.synchronize(dev)
     t_c1 = time.perf_counter()
+    n_sat = warm - 1 - warm // 3
+    host_sat = dict(gw.host_profile(), engine_build=round(float(engine.host_ns[0] - sat_eng0[0]) / n_sat / 1e6, 3),
+                    engine_sync=round(float(engine.host_ns[1] - sat_eng0[1]) / n_sat / 1e6, 3),
+                    tick_ms=round((t_c1 - t_c0) * 1e3 / n_sat, 3),
+                    tokens_per_tick=round((engine.total_tokens - tok0) / n_sat, 1))
     tok_rate = (engine.total_tokens - tok0) / max(1e-9, t_c1 - t_c0)
     done = max(1, engine.completed_total - done0)
     tok_per_req = max(1.0, (engine.completed_tokens - rt0) / done)
@@ -164,6 +171,8 @@ def main(argv=None) -> int:
     gc.collect()
     gc.freeze()
     gc.disable()
+    gw.host_profile(reset=True)
+    eng_host0 = engine.host_ns.copy()
     d0 = gw.counters["dispatched"]
     tok0 = engine.total_tokens
     sync_all()
@@ -234,6 +243,10 @@ def main(argv=None) -> int:
         "calibrated_capacity_per_gpu": round(capacity, 2),
         "backend_tokens_per_s": round(tokens / elapsed, 1) if elapsed > 0 else 0.0,
         "dispatched": dispatched,
+        "host_ms_per_tick_saturated": host_sat,
+        "host_ms_per_tick": dict(gw.host_profile(), engine_build=round(
+            float(engine.host_ns[0] - eng_host0[0]) / max(1, a.steps) / 1e6, 3), engine_sync=round(
+            float(engine.host_ns[1] - eng_host0[1]) / max(1, a.steps) / 1e6, 3)),
     }
     if a.gateway_only_s > 0:
         # Secondary, untimed-by-contract measurement: the gateway path alone

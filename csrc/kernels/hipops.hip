@@ -155,6 +155,18 @@ static void attention(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, ui
   check_launch();
 }
 
+// tiles: int32 [n_tiles][4] = {first token row, n (<= 16), slot, first position}
+static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t tiles, int n_tiles, int Hq,
+                            int Hkv, int max_ctx, float scale, uintptr_t out, uintptr_t stream) {
+  require(Hq == 4 * Hkv, "attention_tiles expects a GQA group of exactly 4 heads");
+  if (n_tiles == 0) return;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attention_seg_kernel, dim3(n_tiles * Hkv), dim3(256), 0, S(stream), P<const uint16_t>(q),
+                     P<const uint16_t>(kc), P<const uint16_t>(vc), P<const int32_t>(tiles), Hq, Hkv, max_ctx,
+                     scale_log2, P<uint16_t>(out));
+  check_launch();
+}
+
 // ---------------------------------------------------------------------- N9 slot page
 struct MappedPage {
   void* host = nullptr;
@@ -211,6 +223,7 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("silu_mul", &silu_mul);
   m.def("rope_kv", &rope_kv);
   m.def("attention", &attention);
+  m.def("attention_tiles", &attention_tiles);
   m.def("register_host_page", &register_host_page);
   m.def("unregister_host_page", &unregister_host_page);
   m.def("slot_census", &slot_census);

@@ -227,6 +227,163 @@ attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc
   }
 }
 
+// ---------------------------------------------------------------------------
+// Segment-tiled MFMA attention (the serving path).  A step's tokens come in
+// SEGMENTS: a run of consecutive positions of one slot (a prefill chunk; a
+// decode token is a segment of 1).  The engine cuts segments into tiles of
+// <= 16 tokens: tiles[i] = {first token row, n, slot, first position}.
+//
+// One 256-thread workgroup per (tile, kv head); wave w = query head g*4+w of
+// the GQA group, so every wave owns a 16-token x 128 Q block (A operand, kept
+// in registers) and the 4 waves share the K/V block staged in LDS -- K/V of a
+// slot are read ONCE per tile instead of once per token (a 12-token prefill
+// chunk reads its context 12x less than the per-token kernel above).
+//   S = Q K^T : v_mfma_f32_16x16x32_bf16, 4 key tiles x 4 k-steps per 64 keys;
+//               K rows staged with 16-B chunks XOR-swizzled by (key & 15) so
+//               the B-fragment reads (16 keys, one chunk each) hit 16 banks;
+//   softmax   : online, causal mask key <= pos0 + row, exp2 with the scale
+//               folded into log2(e); row max/sum reduced over the 16 lanes
+//               that hold a row (C layout: lane = (row quad fq, key fr));
+//   O += P V  : P goes through a per-wave LDS tile (C layout -> A layout),
+//               V is staged TRANSPOSED (Vt[dim][key], 2 keys packed per
+//               dword write) so B fragments are 16-B reads; 8 dim tiles x
+//               2 k-steps per 64 keys, O in 32 accumulator VGPRs.
+constexpr int SA_KEYS = 64;
+constexpr int SA_VROW = 72;   // Vt row: 64 keys + 8 pad (144 B)
+constexpr int SA_PROW = 72;   // P row : 64 keys + 8 pad
+
+__global__ void __launch_bounds__(256)
+attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                     const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int Hq, int Hkv,
+                     int max_ctx, float scale_log2, uint16_t* __restrict__ out) {
+  __shared__ __align__(16) uint16_t Ks[SA_KEYS * 128];
+  __shared__ __align__(16) uint16_t Vt[128 * SA_VROW];
+  __shared__ __align__(16) uint16_t Ps[4][16 * SA_PROW];
+  const int tile = blockIdx.x / Hkv;
+  const int g = blockIdx.x % Hkv;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tok0 = tiles[tile * 4 + 0];
+  const int n = tiles[tile * 4 + 1];
+  const int s = tiles[tile * 4 + 2];
+  const int pos0 = tiles[tile * 4 + 3];
+  const int h = g * 4 + wv;
+  const int ctx = pos0 + n;
+  const int64_t kvbase = ((int64_t)s * Hkv + g) * max_ctx * 128;
+
+  // Q fragments (A operand): row = token fr of the tile, dims ks*32 + fq*8 .. +7
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (fr < n) qf[ks] = *reinterpret_cast<const bf16x8*>(q + ((int64_t)(tok0 + fr) * Hq + h) * 128 + ks * 32 + fq * 8);
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt) o[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrow[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
+  float lrow[4] = {0.f, 0.f, 0.f, 0.f};
+  uint16_t* P = Ps[wv];
+
+  for (int k0 = 0; k0 < ctx; k0 += SA_KEYS) {
+    __syncthreads();
+    // K: 64 keys x 16 chunks, row-coalesced, chunk-swizzled
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = tid + r * 256;
+      const int key = c >> 4, ch = c & 15;
+      uint4 kv = make_uint4(0u, 0u, 0u, 0u);
+      if (k0 + key < ctx) kv = *reinterpret_cast<const uint4*>(kc + kvbase + (int64_t)(k0 + key) * 128 + ch * 8);
+      *reinterpret_cast<uint4*>(Ks + key * 128 + ((ch ^ (key & 15)) * 8)) = kv;
+    }
+    // V^T: item = (key pair kp, chunk ch); two keys per dword store
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + r * 256;
+      const int kp = c & 31, ch = c >> 5;
+      const int ka = k0 + 2 * kp;
+      uint4 va = make_uint4(0u, 0u, 0u, 0u), vb = make_uint4(0u, 0u, 0u, 0u);
+      if (ka < ctx) va = *reinterpret_cast<const uint4*>(vc + kvbase + (int64_t)ka * 128 + ch * 8);
+      if (ka + 1 < ctx) vb = *reinterpret_cast<const uint4*>(vc + kvbase + (int64_t)(ka + 1) * 128 + ch * 8);
+      const uint16_t* ea = reinterpret_cast<const uint16_t*>(&va);
+      const uint16_t* eb = reinterpret_cast<const uint16_t*>(&vb);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        *reinterpret_cast<uint32_t*>(Vt + (ch * 8 + i) * SA_VROW + 2 * kp) = (uint32_t)ea[i] | ((uint32_t)eb[i] << 16);
+    }
+    __syncthreads();
+
+    // ---- S = Q K^T (C layout: sc[j][k] = S[row 4fq+k][key k0 + 16j + fr])
+    f32x4 sc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (j * 16 + fr) * 128 + (((ks * 4 + fq) ^ fr) * 8));
+        sc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[ks], kf, sc[j], 0, 0, 0);
+      }
+    }
+    // ---- online softmax over this block (rows 4fq+k live in the 16 lanes of quad fq)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = 4 * fq + k;
+      const int lim = (row < n) ? pos0 + row : -1;       // causal: key <= position
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + j * 16 + fr;
+        const float v = (key <= lim) ? sc[j][k] * scale_log2 : -3.0e38f;
+        sc[j][k] = v;
+        mx = fmaxf(mx, v);
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+      const float mn = fmaxf(mrow[k], mx);
+      const float corr = exp2f(mrow[k] - mn);
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + j * 16 + fr;
+        const float p = (key <= lim) ? exp2f(sc[j][k] - mn) : 0.f;
+        sum += p;
+        P[row * SA_PROW + j * 16 + fr] = f32_to_bf16_rne(p);
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
+      lrow[k] = lrow[k] * corr + sum;
+      mrow[k] = mn;
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) o[nt][k] *= corr;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's P stores landed (lgkmcnt 0)
+    __builtin_amdgcn_wave_barrier();
+    // ---- O += P V
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pf = *reinterpret_cast<const bf16x8*>(P + fr * SA_PROW + ks * 32 + fq * 8);
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) {
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vt + (nt * 16 + fr) * SA_VROW + ks * 32 + fq * 8);
+        o[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf, o[nt], 0, 0, 0);
+      }
+    }
+  }
+  // ---- epilogue: o[nt][k] = O[row 4fq+k][dim 16nt + fr]
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = 4 * fq + k;
+    if (row < n) {
+      const float inv = 1.0f / lrow[k];
+      uint16_t* dst = out + ((int64_t)(tok0 + row) * Hq + h) * 128;
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) dst[nt * 16 + fr] = f32_to_bf16_rne(o[nt][k] * inv);
+    }
+  }
+}
+
 // N9: device-side slot census -> host-mapped load page (zero-copy for the
 // router).  page layout (uint32): [0]=seq, [1]=active slots, [2]=free slots,
 // [3]=tokens this step, [4]=step id lo.  Stores are system-scope so a host

@@ -91,6 +91,17 @@ class BackendEngine:
         self.impl = impl
         self.active: Dict[int, Request] = {}            # slot -> request
         self.free: List[int] = list(range(slots - 1, -1, -1))
+        # per-slot host state (the batch builder is vectorised over these)
+        self.s_prompt = np.zeros((slots, max_ctx), dtype=np.int32)
+        self.s_plen = np.zeros(slots, dtype=np.int64)
+        self.s_pref = np.zeros(slots, dtype=np.int64)       # prompt tokens prefilled
+        self.s_gen = np.zeros(slots, dtype=np.int64)        # tokens generated
+        self.s_gmax = np.zeros(slots, dtype=np.int64)       # tokens to generate
+        self.s_seq = np.zeros(slots, dtype=np.int64)        # admission order
+        self.s_out_idx = np.zeros(slots, dtype=np.int64)    # row of my last token in the step output
+        self.s_out_step = np.full(slots, -2, dtype=np.int64)
+        self.s_active = np.zeros(slots, dtype=bool)
+        self._admit_seq = 0
         self.page = page
         self.gpu_index = gpu_index
         self.max_inflight = max(1, max_inflight)
@@ -100,10 +111,13 @@ class BackendEngine:
         self.completed_tokens = 0
         self._q: Deque[_Inflight] = collections.deque()
         self._reaped: List[_Inflight] = []               # reaped by launch(), not yet returned
+        self.host_ns = np.zeros(2, dtype=np.int64)       # [batch build, wait for GPU] host time
         self._prev_out = None                            # device int32 [n_samples] of the last launched step
         # double-buffered pinned staging (a buffer is reused only after the
         # step that read it has finished: <= 2 steps in flight)
-        self._pins = [self._alloc_pin(4 * (3 * token_budget + 2 * slots + 64)) for _ in range(2)]
+        self._pins = [self._alloc_pin(4 * (7 * self.token_budget + 2 * slots + 64)) for _ in range(2)]
+        # segment-tiled MFMA attention on the HIP path (per-token otherwise)
+        self.use_tiles = impl == "hip"
         self._state_pins = [self._alloc_pin(4 * slots) for _ in range(2)]
         self._slot_state_d = torch.zeros(slots, dtype=torch.int32, device=self.device)
         # fault injection: {"fail_launch": n} raises on the next
@@ -140,56 +154,86 @@ class BackendEngine:
             r.prompt = np.asarray(r.prompt[:plen], dtype=np.int64) % self.cfg.vocab
             if len(r.prompt) == 0:
                 r.prompt = np.zeros(1, dtype=np.int64)
-            r.slot = self.free.pop()
+            s = r.slot = self.free.pop()
             r.prefilled = 0
             r.generated = 0
             r.out_idx = r.out_step = -1
             r.admitted_ns = now
-            self.active[r.slot] = r
+            self.active[s] = r
+            n = len(r.prompt)
+            self.s_prompt[s, :n] = r.prompt
+            self.s_plen[s] = n
+            self.s_pref[s] = 0
+            self.s_gen[s] = 0
+            self.s_gmax[s] = r.gen_tokens
+            self.s_seq[s] = self._admit_seq
+            self._admit_seq += 1
+            self.s_active[s] = True
             out.append(r)
         return out
 
     # ------------------------------------------------------------------ step
     def _build(self):
-        toks, pos, slot, samp, sample_reqs = [], [], [], [], []
-        dec_rows, dec_src = [], []
-        budget = self.token_budget
-        n_dec = n_pre = 0
-        # decode tokens first (in-flight generations keep their cadence);
-        # their ids are gathered on the device from the previous output
-        for s, r in self.active.items():
-            if r.prefilled >= len(r.prompt):
-                if r.out_step != self.step_id - 1:
-                    raise RuntimeError("decode token source is not the previous step")
-                ctx = len(r.prompt) + r.generated - 1
-                dec_rows.append(len(toks))
-                dec_src.append(r.out_idx)
-                toks.append(0)
-                pos.append(ctx)
-                slot.append(s)
-                samp.append(len(toks) - 1)
-                sample_reqs.append(r)
-                budget -= 1
-                n_dec += 1
-        # then chunked prefill in admission order
-        for s, r in sorted(self.active.items(), key=lambda kv: kv[1].admitted_ns):
-            if budget <= 0:
-                break
-            rem = len(r.prompt) - r.prefilled
-            if rem <= 0:
-                continue
-            n = min(rem, budget)
-            a = r.prefilled
-            toks.extend(r.prompt[a:a + n].tolist())
-            pos.extend(range(a, a + n))
-            slot.extend([s] * n)
-            r.prefilled += n
-            budget -= n
-            n_pre += n
-            if r.prefilled >= len(r.prompt):
-                samp.append(len(toks) - 1)
-                sample_reqs.append(r)
-        return toks, pos, slot, samp, sample_reqs, dec_rows, dec_src, n_pre, n_dec
+        """Vectorised batch construction over the per-slot state arrays:
+        decode rows first (one token per generating slot, ids gathered on the
+        device from the previous step's output), then chunked prefill in
+        admission order up to the token budget.  Returns int32 arrays."""
+        act = np.flatnonzero(self.s_active)
+        plen, pref = self.s_plen[act], self.s_pref[act]
+        is_dec = pref >= plen
+        dec = act[is_dec]
+        D = len(dec)
+        if D and (self.s_out_step[dec] != self.step_id - 1).any():
+            raise RuntimeError("decode token source is not the previous step")
+        pre = act[~is_dec]
+        if len(pre):
+            pre = pre[np.argsort(self.s_seq[pre], kind="stable")]
+        rem = self.s_plen[pre] - self.s_pref[pre]
+        budget = self.token_budget - D
+        before = np.cumsum(rem) - rem
+        take = np.clip(budget - before, 0, rem)
+        keep = take > 0
+        pre, take = pre[keep], take[keep]
+        n_pre = int(take.sum())
+        T = D + n_pre
+        a0 = self.s_pref[pre]
+        # prefill token rows: slot pre[i] contributes prompt[a0:a0+take]
+        start = D + np.cumsum(take) - take                   # first row of each chunk
+        rep = np.repeat(np.arange(len(pre)), take)
+        off = np.arange(n_pre) - (start[rep] - D) if n_pre else np.zeros(0, np.int64)
+        p_slot = pre[rep]
+        p_pos = a0[rep] + off
+        toks = np.zeros(T, dtype=np.int32)
+        pos = np.empty(T, dtype=np.int32)
+        slot = np.empty(T, dtype=np.int32)
+        d_pos = self.s_plen[dec] + self.s_gen[dec] - 1
+        pos[:D] = d_pos
+        slot[:D] = dec
+        if n_pre:
+            toks[D:] = self.s_prompt[p_slot, p_pos]
+            pos[D:] = p_pos
+            slot[D:] = p_slot
+        fin = a0 + take >= self.s_plen[pre]                   # chunk completes the prompt
+        samp = np.concatenate([np.arange(D), (start + take - 1)[fin]]).astype(np.int32)
+        samp_slots = np.concatenate([dec, pre[fin]])
+        dec_rows = np.arange(D, dtype=np.int32)
+        dec_src = self.s_out_idx[dec].astype(np.int32)
+        # attention tiles: decode rows are 1-token tiles; chunks cut at 16
+        nt = (take + 15) // 16
+        trep = np.repeat(np.arange(len(pre)), nt)
+        toff = (np.arange(int(nt.sum())) - np.repeat(np.cumsum(nt) - nt, nt)) * 16
+        tiles = np.empty((D + len(trep), 4), dtype=np.int32)
+        tiles[:D, 0] = dec_rows
+        tiles[:D, 1] = 1
+        tiles[:D, 2] = dec
+        tiles[:D, 3] = d_pos
+        if len(trep):
+            tiles[D:, 0] = start[trep] + toff
+            tiles[D:, 1] = np.minimum(16, take[trep] - toff)
+            tiles[D:, 2] = pre[trep]
+            tiles[D:, 3] = a0[trep] + toff
+        self.s_pref[pre] += take
+        return toks, pos, slot, samp, samp_slots, dec_rows, dec_src, tiles, n_pre, D
 
     def inject(self, **fault) -> None:
         """Fault injection: ``fail_launch=n``, ``slow_ms=x``, ``drop_heartbeat=True``
@@ -214,6 +258,7 @@ class BackendEngine:
         self._reaped = []
         self._prev_out = None
         self.active.clear()
+        self.s_active[:] = False
         self.free = list(range(self.slots - 1, -1, -1))
         return out
 
@@ -227,53 +272,65 @@ class BackendEngine:
                 raise RuntimeError("HIP error: out of memory (injected fault)")
             if self.fault.get("slow_ms"):
                 time.sleep(self.fault["slow_ms"] / 1e3)
+        ts = time.perf_counter_ns()
         while len(self._q) >= self.max_inflight:       # bound the run-ahead (and staging reuse)
             self._reaped.append(self._reap(block=True))  # handed to the next finish()
         t0 = time.perf_counter()
-        toks, pos, slot, samp, sample_reqs, dec_rows, dec_src, n_pre, n_dec = self._build()
+        tb = time.perf_counter_ns()
+        self.host_ns[1] += tb - ts
+        toks, pos, slot, samp, samp_slots, dec_rows, dec_src, tiles, n_pre, n_dec = self._build()
+        self.host_ns[0] += time.perf_counter_ns() - tb
         T = len(toks)
         if T == 0:
             return
         dev = self.device
-        S, D = len(samp), len(dec_rows)
-        buf = np.empty(3 * T + S + 2 * D, dtype=np.int32)
+        S, D, NT = len(samp), len(dec_rows), len(tiles)
+        o_dec = 3 * T + S
+        o_til = o_dec + 2 * D
+        buf = np.empty(o_til + 4 * NT, dtype=np.int32)
         buf[:T] = toks
         buf[T:2 * T] = pos
         buf[2 * T:3 * T] = slot
-        buf[3 * T:3 * T + S] = samp
-        buf[3 * T + S:3 * T + S + D] = dec_rows
-        buf[3 * T + S + D:] = dec_src
+        buf[3 * T:o_dec] = samp
+        buf[o_dec:o_dec + D] = dec_rows
+        buf[o_dec + D:o_til] = dec_src
+        buf[o_til:] = tiles.reshape(-1)
         nbytes = buf.nbytes
         pin = self._pins[self.step_id % 2]
         if pin.numel() < nbytes:
             pin = self._pins[self.step_id % 2] = self._alloc_pin(2 * nbytes)
-        pin[:nbytes].numpy()[:] = buf.view(np.uint8)
+        pin.numpy()[:nbytes] = buf.view(np.uint8)
         d = pin[:nbytes].to(dev, non_blocking=True).view(torch.int32)
         tok_d = d[:T].long()
         if D:
             if self._prev_out is None:
                 raise RuntimeError("decode token without a previous step output")
-            rows = d[3 * T + S:3 * T + S + D].long()
-            src = d[3 * T + S + D:].long()
+            rows = d[o_dec:o_dec + D].long()
+            src = d[o_dec + D:o_til].long()
             tok_d.index_copy_(0, rows, self._prev_out.index_select(0, src).long())
-        out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:3 * T + S].long())
+        til = d[o_til:].view(NT, 4) if self.use_tiles else None
+        out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til)
         self._census(T)
         ev = None
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record()
-        # deterministic bookkeeping: every sampled request gets one token
-        completed, firsts = [], []
-        for i, r in enumerate(sample_reqs):
-            r.generated += 1
-            r.out_idx, r.out_step = i, self.step_id
-            if r.generated == 1:
-                firsts.append(r)
-            if r.generated >= r.gen_tokens:
-                completed.append(r)
-        for r in completed:
-            del self.active[r.slot]
-            self.free.append(r.slot)
+        # deterministic bookkeeping: every sampled slot gets one token
+        ss = samp_slots
+        self.s_gen[ss] += 1
+        self.s_out_idx[ss] = np.arange(len(ss))
+        self.s_out_step[ss] = self.step_id
+        g = self.s_gen[ss]
+        firsts = [self.active[int(x)] for x in ss[g == 1]]
+        done = ss[g >= self.s_gmax[ss]]
+        completed = []
+        for x in done.tolist():
+            r = self.active.pop(x)
+            r.prefilled = int(self.s_plen[x])
+            r.generated = int(self.s_gen[x])
+            completed.append(r)
+            self.free.append(x)
+        self.s_active[done] = False
         self._prev_out = out
         self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out))
         self.step_id += 1

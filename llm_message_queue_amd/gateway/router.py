@@ -164,6 +164,8 @@ class Gateway:
         self._tick_lock = threading.RLock()     # set_healthy from a telemetry thread waits for the tick
         self.unhealthy_peers: set = set()
         self.on_complete = None     # optional callback(msg)
+        self.host_ns = np.zeros(5, dtype=np.int64)   # per-phase host time (host_profile)
+        self._ticks0 = 0
         self._next_req = 1 << 40
 
     # ------------------------------------------------------------------ ingress
@@ -518,18 +520,42 @@ class Gateway:
 
     def _tick(self):
         res = None
+        pc = time.perf_counter_ns
+        ht = self.host_ns
+        t0 = pc()
         if self.engine is not None and self.healthy:
             try:
                 self.engine.launch()
+                t1 = pc()
                 self.ingest()
+                t2 = pc()
                 res = self.finish_backend()
+                t3 = pc()
+                ht[0] += t1 - t0
+                ht[1] += t2 - t1
+                ht[2] += t3 - t2
+                t0 = t3
             except RuntimeError as e:           # HIP error / OOM from the backend
                 self._set_healthy(False, f"backend error: {e}")
         if res is None:
             self.ingest()
+        t4 = pc()
         n = self.dispatch()
+        ht[3] += pc() - t4
+        ht[4] += t4 - t0 if res is None else 0
         self.counters["ticks"] += 1
         return n, res
+
+    def host_profile(self, reset: bool = False) -> Dict[str, float]:
+        """Mean host milliseconds per tick in each phase (launch includes any
+        wait for the GPU when the engine's run-ahead queue is full)."""
+        n = max(1, self.counters["ticks"] - self._ticks0)
+        out = {k: round(float(v) / n / 1e6, 3) for k, v in
+               zip(("launch", "ingest", "finish", "dispatch", "ingest_idle"), self.host_ns)}
+        if reset:
+            self.host_ns[:] = 0
+            self._ticks0 = self.counters["ticks"]
+        return out
 
     def pending(self) -> int:
         return self.qm.total_pending()

@@ -8,8 +8,8 @@ real GPU worker so load signals (in-flight slots, HBM) are live.
 Forward = one continuous-batching step over T tokens (chunked-prefill and
 decode tokens mixed).  GEMMs: ``torch.nn.functional.linear`` (hipBLASLt).
 Everything else: hand-written HIP kernels (``ops.llama_ops.HipOps``):
-residual-add+RMSNorm, RoPE + KV-cache write, unified GQA attention over the
-slot KV cache, SiLU*up.
+residual-add+RMSNorm, RoPE + KV-cache write, segment-tiled MFMA GQA attention
+over the slot KV cache (prefill chunks and decode tokens), SiLU*up.
 """
 from __future__ import annotations
 
@@ -110,9 +110,12 @@ class LlamaStub:
 
     @torch.no_grad()
     def forward(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
-                sample_idx: torch.Tensor) -> torch.Tensor:
+                sample_idx: torch.Tensor, tiles: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One step over T tokens; returns greedy next-token ids for the rows
-        in ``sample_idx`` (the last token of each request's chunk)."""
+        in ``sample_idx`` (the last token of each request's chunk).
+        ``tiles`` (int32 [n, 4], see ``ops.llama_ops.make_tiles``) groups the
+        tokens into per-slot segments for the MFMA attention kernel; without
+        it attention runs per token."""
         cfg, ops = self.cfg, self.ops
         T = tokens.shape[0]
         h = F.embedding(tokens, self.embed)              # [T, d]
@@ -125,8 +128,12 @@ class LlamaStub:
             qkv = F.linear(x, L["wqkv"])
             q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
                             self.kcache[i], self.vcache[i])
-            a = ops.attention(q, self.kcache[i], self.vcache[i], pos, slot, cfg.heads, cfg.kv_heads,
-                              self.scale)
+            if tiles is not None:
+                a = ops.attention_tiles(q, self.kcache[i], self.vcache[i], tiles, cfg.heads, cfg.kv_heads,
+                                        self.scale)
+            else:
+                a = ops.attention(q, self.kcache[i], self.vcache[i], pos, slot, cfg.heads, cfg.kv_heads,
+                                  self.scale)
             ao = F.linear(a, L["wo"])
             x2 = ops.rmsnorm(ao, L["mlp_norm"], cfg.eps, residual=res)
             gu = F.linear(x2, L["w_gu"])

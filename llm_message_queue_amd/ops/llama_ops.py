@@ -81,6 +81,29 @@ class HipOps:
         return o
 
 
+    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None):
+        """Segment-tiled MFMA attention; ``tiles`` int32 [n, 4] on the device =
+        (first token row, n <= 16, slot, first position)."""
+        _check(q, torch.bfloat16, "q")
+        if tiles.dtype != torch.int32 or tiles.dim() != 2 or tiles.shape[1] != 4 or not tiles.is_contiguous():
+            raise ValueError("tiles must be a contiguous int32 [n, 4] tensor")
+        o = out if out is not None else torch.empty_like(q)
+        self.k.attention_tiles(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), tiles.data_ptr(), tiles.shape[0], Hq, Hkv,
+                               kc.shape[2], float(scale), o.data_ptr(), _stream(q))
+        return o
+
+
+def make_tiles(seg_start, seg_len, seg_slot, seg_pos0, tile: int = 16):
+    """Cut segments (runs of consecutive positions of one slot) into
+    attention tiles of <= ``tile`` tokens: int32 [n, 4] numpy array."""
+    out = []
+    for st, n, sl, p0 in zip(seg_start, seg_len, seg_slot, seg_pos0):
+        for a in range(0, n, tile):
+            out.append((st + a, min(tile, n - a), sl, p0 + a))
+    import numpy as _np
+    return _np.asarray(out, dtype=_np.int32).reshape(-1, 4)
+
+
 class RefOps:
     """fp32 PyTorch reference of the same math (bf16 in / bf16 out)."""
 
@@ -145,6 +168,17 @@ class RefOps:
             out.copy_(res)
             return out
         return res
+
+    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None):
+        """Reference: expand tiles to per-token (pos, slot) and reuse ``attention``."""
+        t = tiles.cpu().long()
+        T = q.shape[0]
+        pos = torch.zeros(T, dtype=torch.long)
+        slot = torch.zeros(T, dtype=torch.long)
+        for r0, n, sl, p0 in t.tolist():
+            pos[r0:r0 + n] = torch.arange(p0, p0 + n)
+            slot[r0:r0 + n] = sl
+        return self.attention(q, kc, vc, pos, slot, Hq, Hkv, scale, out=out)
 
 
 def rope_tables(max_pos: int, theta: float = 500000.0, device="cpu"):

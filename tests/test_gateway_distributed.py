@@ -300,3 +300,27 @@ def test_single_rank_fault_requeues_and_recovers():
     assert run_until_done([gw], 10)
     st = gw.qm.get_all_queue_stats()
     assert sum(s.processing_count for s in st.values()) == 0
+
+
+def test_engine_attention_tiles_match_per_token_path():
+    """The engine's segment tiles (decode rows + prefill chunks cut at 16)
+    give the same tokens as per-token attention (reference ops on CPU)."""
+    from llm_message_queue_amd.backend.engine import Request
+    outs = []
+    for use_tiles in (False, True):
+        eng = BackendEngine(MICRO, slots=6, max_ctx=64, token_budget=24, device="cpu", impl="ref", seed=9)
+        eng.use_tiles = use_tiles
+        rng = np.random.default_rng(0)
+        reqs = [Request(i, rng.integers(0, 500, size=int(rng.integers(1, 40))).astype(np.int32), gen_tokens=3)
+                for i in range(10)]
+        done = []
+        pending = list(reqs)
+        for _ in range(200):
+            pending = pending[len(eng.admit(pending)):]
+            done += eng.step().completed
+            if len(done) == 10:
+                break
+        assert len(done) == 10
+        outs.append({r.req_id: (r.generated, r.prefilled) for r in done})
+        outs.append(eng.model.kcache[0].clone())
+    assert outs[0] == outs[2] and torch.equal(outs[1], outs[3])
