@@ -155,16 +155,27 @@ static void attention(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, ui
   check_launch();
 }
 
-// tiles: int32 [n_tiles][4] = {first token row, n (<= 16), slot, first position}
-static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t tiles, int n_tiles, int Hq,
-                            int Hkv, int max_ctx, float scale, uintptr_t out, uintptr_t stream) {
+// tiles: int32 [n_tiles][4] = {first token row, n (<= 16), slot, first position}.
+// The first n_dec tiles are 1-token decode tiles (wave-per-item decode
+// kernel); the rest go to the MFMA segment kernel.  Rows are disjoint.
+static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t tiles, int n_tiles, int n_dec,
+                            int Hq, int Hkv, int max_ctx, float scale, uintptr_t out, uintptr_t stream) {
   require(Hq == 4 * Hkv, "attention_tiles expects a GQA group of exactly 4 heads");
-  if (n_tiles == 0) return;
+  require(0 <= n_dec && n_dec <= n_tiles, "n_dec out of range");
   const float scale_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attention_seg_kernel, dim3(n_tiles * Hkv), dim3(256), 0, S(stream), P<const uint16_t>(q),
-                     P<const uint16_t>(kc), P<const uint16_t>(vc), P<const int32_t>(tiles), Hq, Hkv, max_ctx,
-                     scale_log2, P<uint16_t>(out));
-  check_launch();
+  if (n_dec > 0) {
+    const int items = n_dec * Hkv;
+    hipLaunchKernelGGL(attention_dec_kernel, dim3((items + 3) / 4), dim3(256), 0, S(stream), P<const uint16_t>(q),
+                       P<const uint16_t>(kc), P<const uint16_t>(vc), P<const int32_t>(tiles), items, Hq, Hkv,
+                       max_ctx, scale_log2, P<uint16_t>(out));
+    check_launch();
+  }
+  if (n_tiles > n_dec) {
+    hipLaunchKernelGGL(attention_seg_kernel, dim3((n_tiles - n_dec) * Hkv), dim3(256), 0, S(stream),
+                       P<const uint16_t>(q), P<const uint16_t>(kc), P<const uint16_t>(vc),
+                       P<const int32_t>(tiles) + 4 * n_dec, Hq, Hkv, max_ctx, scale_log2, P<uint16_t>(out));
+    check_launch();
+  }
 }
 
 // ---------------------------------------------------------------------- N9 slot page

@@ -384,6 +384,102 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decode attention (1-token tiles): one WAVE per (token, kv head), the GQA
+// group's 4 query heads handled together by that wave, 4 independent items
+// per 256-thread workgroup (no block barrier).  A decode token attends a
+// short context (tens to hundreds of keys) that no other token of the step
+// shares, so the kernel is latency-bound: no LDS staging of K/V, lane j owns
+// key k0+j and streams its 256-B K row straight from memory for the 4 dot
+// products; P goes through 1 KiB of per-wave LDS; P*V walks the keys with
+// one coalesced 256-B V row per step, each lane accumulating 2 dims x 4
+// heads.  ~40 VGPRs -> full occupancy, so thousands of these waves overlap
+// their memory latency.
+__global__ void __launch_bounds__(256)
+attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                     const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int n_items, int Hq,
+                     int Hkv, int max_ctx, float scale_log2, uint16_t* __restrict__ out) {
+  __shared__ __align__(16) float qs[4][4][128];
+  __shared__ float ps[4][4][64];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int item = blockIdx.x * 4 + wv;
+  if (item >= n_items) return;                 // whole wave; no block barrier below
+  const int tile = item / Hkv;
+  const int g = item % Hkv;
+  const int row = tiles[tile * 4 + 0];
+  const int s = tiles[tile * 4 + 2];
+  const int ctx = tiles[tile * 4 + 3] + 1;
+  const int64_t kvbase = ((int64_t)s * Hkv + g) * max_ctx * 128;
+  {  // q of the 4 heads -> LDS (fp32, pre-scaled by scale*log2e)
+    const int hh = lane >> 4, d0 = (lane & 15) * 8;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(q + ((int64_t)row * Hq + g * 4 + hh) * 128 + d0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qs[wv][hh][d0 + i] = bf(v[i]) * scale_log2;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  float m[4], l[4], a0[4], a1[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) { m[h] = -3.0e38f; l[h] = 0.f; a0[h] = 0.f; a1[h] = 0.f; }
+
+  for (int k0 = 0; k0 < ctx; k0 += 64) {
+    const int key = k0 + lane;
+    const bool live = key < ctx;
+    float sc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+      const uint16_t* kr = kc + kvbase + (int64_t)key * 128;
+#pragma unroll 4
+      for (int ch = 0; ch < 16; ++ch) {
+        const u16x8 kk = *reinterpret_cast<const u16x8*>(kr + ch * 8);
+        float kf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kf[i] = bf(kk[i]);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const float4 qa = *reinterpret_cast<const float4*>(&qs[wv][h][ch * 8]);
+          const float4 qb = *reinterpret_cast<const float4*>(&qs[wv][h][ch * 8 + 4]);
+          sc[h] += qa.x * kf[0] + qa.y * kf[1] + qa.z * kf[2] + qa.w * kf[3] +
+                   qb.x * kf[4] + qb.y * kf[5] + qb.z * kf[6] + qb.w * kf[7];
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const float v = live ? sc[h] : -3.0e38f;
+      const float mn = fmaxf(m[h], wave_max(v));
+      const float p = live ? exp2f(v - mn) : 0.f;
+      const float corr = exp2f(m[h] - mn);
+      l[h] = l[h] * corr + wave_sum(p);
+      a0[h] *= corr;
+      a1[h] *= corr;
+      m[h] = mn;
+      ps[wv][h][lane] = p;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    const int nk = min(64, ctx - k0);
+    const uint16_t* vr = vc + kvbase + (int64_t)k0 * 128 + lane * 2;
+    for (int j = 0; j < nk; ++j) {
+      const uint32_t v2 = *reinterpret_cast<const uint32_t*>(vr + (int64_t)j * 128);
+      const float vlo = bf((uint16_t)(v2 & 0xFFFFu)), vhi = bf((uint16_t)(v2 >> 16));
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const float p = ps[wv][h][j];
+        a0[h] += p * vlo;
+        a1[h] += p * vhi;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();          // ps is rewritten by the next block
+  }
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const float inv = 1.0f / l[h];
+    const uint32_t o = (uint32_t)f32_to_bf16_rne(a0[h] * inv) | ((uint32_t)f32_to_bf16_rne(a1[h] * inv) << 16);
+    *reinterpret_cast<uint32_t*>(out + ((int64_t)row * Hq + g * 4 + h) * 128 + lane * 2) = o;
+  }
+}
+
 // N9: device-side slot census -> host-mapped load page (zero-copy for the
 // router).  page layout (uint32): [0]=seq, [1]=active slots, [2]=free slots,
 // [3]=tokens this step, [4]=step id lo.  Stores are system-scope so a host

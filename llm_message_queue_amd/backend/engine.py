@@ -309,7 +309,7 @@ class BackendEngine:
             src = d[o_dec + D:o_til].long()
             tok_d.index_copy_(0, rows, self._prev_out.index_select(0, src).long())
         til = d[o_til:].view(NT, 4) if self.use_tiles else None
-        out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til)
+        out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til, n_dec=D)
         self._census(T)
         ev = None
         if self.cuda:

@@ -110,12 +110,13 @@ class LlamaStub:
 
     @torch.no_grad()
     def forward(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
-                sample_idx: torch.Tensor, tiles: Optional[torch.Tensor] = None) -> torch.Tensor:
+                sample_idx: torch.Tensor, tiles: Optional[torch.Tensor] = None, n_dec: int = 0) -> torch.Tensor:
         """One step over T tokens; returns greedy next-token ids for the rows
         in ``sample_idx`` (the last token of each request's chunk).
         ``tiles`` (int32 [n, 4], see ``ops.llama_ops.make_tiles``) groups the
-        tokens into per-slot segments for the MFMA attention kernel; without
-        it attention runs per token."""
+        tokens into per-slot segments for the MFMA attention kernel (its first
+        ``n_dec`` rows are 1-token decode tiles); without it attention runs
+        per token."""
         cfg, ops = self.cfg, self.ops
         T = tokens.shape[0]
         h = F.embedding(tokens, self.embed)              # [T, d]
@@ -130,7 +131,7 @@ class LlamaStub:
                             self.kcache[i], self.vcache[i])
             if tiles is not None:
                 a = ops.attention_tiles(q, self.kcache[i], self.vcache[i], tiles, cfg.heads, cfg.kv_heads,
-                                        self.scale)
+                                        self.scale, n_dec=n_dec)
             else:
                 a = ops.attention(q, self.kcache[i], self.vcache[i], pos, slot, cfg.heads, cfg.kv_heads,
                                   self.scale)

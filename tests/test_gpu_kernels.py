@@ -251,6 +251,10 @@ def test_attention_tiles_mfma_vs_ref(ops):
         slot[r0:r0 + n] = sl
     o3 = hip.attention(q, kc, vc, pos.to(DEV), slot.to(DEV), Hq, Hkv, 128 ** -0.5)
     assert (o1.float() - o3.float()).abs().max().item() < 3e-2
+    # decode kernel on the leading 1-token tiles (5 decode tokens, contexts 1..251)
+    o4 = hip.attention_tiles(q, kc, vc, torch.from_numpy(tiles).to(DEV), Hq, Hkv, 128 ** -0.5, n_dec=5)
+    err4 = (o4.float() - o2.float()).abs().max().item()
+    assert err4 < 3e-2, err4
 
 
 def test_tiny_model_forward_hip_vs_ref():
