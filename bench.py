@@ -46,7 +46,7 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--slots", type=int, default=1024)
+    ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--max-ctx", type=int, default=512)
     ap.add_argument("--token-budget", type=int, default=8192)
     ap.add_argument("--gen-tokens", type=int, default=4)

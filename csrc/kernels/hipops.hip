@@ -5,6 +5,8 @@
 // here before every launch so a bad call raises instead of faulting the GPU.
 
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -191,6 +193,24 @@ static py::tuple register_host_page(uintptr_t host_ptr, size_t bytes) {
   return py::make_tuple((uintptr_t)host_ptr, (uintptr_t)dev);
 }
 
+// device address of pinned host memory (torch pin_memory = hipHostMalloc)
+static uintptr_t host_device_ptr(uintptr_t host_ptr) {
+  void* dev = nullptr;
+  HIP_CHECK(hipHostGetDevicePointer(&dev, reinterpret_cast<void*>(host_ptr), 0));
+  return (uintptr_t)dev;
+}
+
+// dst/src: device or host-mapped device addresses; both 16-B aligned
+static void copy_bytes(uintptr_t dst, uintptr_t src, int64_t n, uintptr_t stream) {
+  if (n <= 0) return;
+  require((dst % 16) == 0 && (src % 16) == 0, "copy_bytes needs 16-byte aligned pointers");
+  const int64_t n16 = n / 16;
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>((n16 + 255) / 256, 1), 1024);
+  hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks), dim3(256), 0, S(stream), P<uint8_t>(dst),
+                     P<const uint8_t>(src), n16, n);
+  check_launch();
+}
+
 static void unregister_host_page(uintptr_t host_ptr) {
   HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(host_ptr)));
 }
@@ -236,6 +256,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("attention", &attention);
   m.def("attention_tiles", &attention_tiles);
   m.def("register_host_page", &register_host_page);
+  m.def("host_device_ptr", &host_device_ptr);
+  m.def("copy_bytes", &copy_bytes);
   m.def("unregister_host_page", &unregister_host_page);
   m.def("slot_census", &slot_census);
   m.def("device_info", &device_info);

@@ -480,6 +480,21 @@ attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   }
 }
 
+// Byte copy between device memory and host-mapped pinned memory, run as a
+// kernel on the caller's stream.  Used for the preprocess pipeline's
+// host<->device traffic: the runtime's async H2D path was measured to queue
+// behind the backend's in-flight forward on the other stream (a 60 ms stall
+// per ingest batch); a kernel on the high-priority side stream is not.
+__global__ void __launch_bounds__(256)
+copy_bytes_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t n16, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  if (blockIdx.x == 0)
+    for (int64_t i = n16 * 16 + threadIdx.x; i < n; i += 256) dst[i] = src[i];
+  __threadfence_system();   // host-mapped destination: visible once the stream's event completes
+}
+
 // N9: device-side slot census -> host-mapped load page (zero-copy for the
 // router).  page layout (uint32): [0]=seq, [1]=active slots, [2]=free slots,
 // [3]=tokens this step, [4]=step id lo.  Stores are system-scope so a host

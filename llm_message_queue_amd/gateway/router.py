@@ -165,6 +165,7 @@ class Gateway:
         self.unhealthy_peers: set = set()
         self.on_complete = None     # optional callback(msg)
         self.host_ns = np.zeros(5, dtype=np.int64)   # per-phase host time (host_profile)
+        self.ingest_ns = np.zeros(3, dtype=np.int64)  # [preprocess ns, queue push ns, messages]
         self._ticks0 = 0
         self._next_req = 1 << 40
 
@@ -183,11 +184,16 @@ class Gateway:
             batch, self._inbox = self._inbox, []
         if not batch:
             return []
+        t0 = time.perf_counter_ns()
         self.pre.process_batch(batch, use_gpu=self.use_gpu_pre, prompt_cap=self.prompt_cap)
+        t1 = time.perf_counter_ns()
         for m in batch:
             if not m.queue_name:
                 m.queue_name = priority_name(m.priority)
         errs = self.qm.push_routed(batch)
+        self.ingest_ns[0] += t1 - t0
+        self.ingest_ns[1] += time.perf_counter_ns() - t1
+        self.ingest_ns[2] += len(batch)
         out = []
         for m, e in zip(batch, errs):
             if e is None and self.world > 1:
@@ -552,8 +558,13 @@ class Gateway:
         n = max(1, self.counters["ticks"] - self._ticks0)
         out = {k: round(float(v) / n / 1e6, 3) for k, v in
                zip(("launch", "ingest", "finish", "dispatch", "ingest_idle"), self.host_ns)}
+        nm = max(1, int(self.ingest_ns[2]))
+        out["ingest_msgs_per_tick"] = round(float(self.ingest_ns[2]) / n, 1)
+        out["preprocess_us_per_msg"] = round(float(self.ingest_ns[0]) / nm / 1e3, 2)
+        out["queue_push_us_per_msg"] = round(float(self.ingest_ns[1]) / nm / 1e3, 2)
         if reset:
             self.host_ns[:] = 0
+            self.ingest_ns[:] = 0
             self._ticks0 = self.counters["ticks"]
         return out
 

@@ -179,11 +179,23 @@ class TextPipeline:
         self.L = int(self.cfg.max_tokens)
         self.weights: Optional[ClassifierWeights] = None
         self._packed: Optional[PackedPatterns] = None
-        self._pin = torch.empty(0, dtype=torch.uint8).pin_memory()
         self._dev_bytes = torch.empty(0, dtype=torch.uint8, device=self.device)
-        # own HIP stream: preprocess kernels run concurrently with the
-        # backend forward on the default stream
-        self.stream = torch.cuda.Stream(device=self.device)
+        self._pin = torch.empty(1 << 16, dtype=torch.uint8).pin_memory()
+        self._pin_dev = self.ops.host_device_ptr(self._pin.data_ptr())
+        self._rb = None                                               # pinned readback (host-mapped)
+        self._rb_dev = 0
+        # own HIGH-PRIORITY HIP stream: preprocess kernels run concurrently
+        # with the backend forward on the default stream, and the hardware
+        # scheduler dispatches their workgroups ahead of the forward's pending
+        # GEMM workgroups -- otherwise every preprocess kernel queues behind a
+        # full-chip GEMM and ingest latency grows with the backend's load
+        self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+
+    def _ensure_readback(self, n_int32: int) -> None:
+        if self._rb is None or self._rb.numel() < n_int32:
+            n = max(n_int32, 2 * (self._rb.numel() if self._rb is not None else 0), 1 << 14)
+            self._rb = self.torch.empty(n, dtype=self.torch.int32).pin_memory()
+            self._rb_dev = self.ops.host_device_ptr(self._rb.data_ptr())
 
     def _ensure_weights(self) -> ClassifierWeights:
         if self.weights is None:
@@ -221,6 +233,7 @@ class TextPipeline:
         nb = ob + offsets.nbytes
         if self._pin.numel() < nb:
             self._pin = torch.empty(max(nb, 2 * self._pin.numel()), dtype=torch.uint8).pin_memory()
+            self._pin_dev = self.ops.host_device_ptr(self._pin.data_ptr())
         pin = self._pin
         pnp = pin.numpy()
         pnp[:len(blob)] = np.frombuffer(blob, dtype=np.uint8)
@@ -230,7 +243,11 @@ class TextPipeline:
             self._dev_bytes = torch.empty(max(total, 2 * self._dev_bytes.numel()), dtype=torch.uint8,
                                           device=self.device)
         dev = self._dev_bytes
-        dev[:total].copy_(pin[:total], non_blocking=True)
+        # H2D with a copy kernel reading host-mapped pinned memory: the
+        # runtime's async H2D path was measured to wait for the backend's
+        # queued forward steps on the other stream (~60 ms per batch)
+        self.ops.copy_bytes(dev.data_ptr(), self._pin_dev, total,
+                            torch.cuda.current_stream(self.device).cuda_stream)
         d_off = dev[ob:ob + offsets.nbytes].view(torch.int64)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         L = self.L
@@ -253,13 +270,28 @@ class TextPipeline:
             pred = torch.empty(B, dtype=torch.int32, device=self.device)
             self.ops.classify_head(pooled.data_ptr(), B, w.hidden, w.W2.data_ptr(), w.b2.data_ptr(),
                                    logits.data_ptr(), pred.data_ptr(), stream)
-        ph = None
-        if prompt_cap > 0 and B:
-            ph = hashes[:, :min(prompt_cap, L)].to("cpu", non_blocking=True)
-        stats_h = stats.to("cpu")   # synchronises the stream
-        pred_h = pred.to("cpu").numpy() if pred is not None else None
-        if ph is not None:
-            ph = ph.numpy().view(np.uint32)
+        # Read back with a copy kernel into host-mapped pinned memory, then an
+        # event on THIS stream (see the H2D note above).
+        cap = min(prompt_cap, L) if prompt_cap > 0 and B else 0
+        a16 = lambda n: (n + 3) & ~3                          # int32 count -> 16-B multiple
+        o_pred = a16(B * STAT_COLS)
+        o_ph = o_pred + (a16(B) if pred is not None else 0)
+        need = o_ph + B * cap
+        self._ensure_readback(need)
+        rd = self._rb_dev
+        self.ops.copy_bytes(rd, stats.data_ptr(), 4 * B * STAT_COLS, stream)
+        if pred is not None:
+            self.ops.copy_bytes(rd + 4 * o_pred, pred.data_ptr(), 4 * B, stream)
+        if cap:
+            hc = hashes[:, :cap].contiguous()
+            self.ops.copy_bytes(rd + 4 * o_ph, hc.data_ptr(), 4 * B * cap, stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        ev.synchronize()
+        rbn = self._rb.numpy()
+        stats_h = rbn[:B * STAT_COLS].reshape(B, STAT_COLS).copy()
+        pred_h = rbn[o_pred:o_pred + B].copy() if pred is not None else None
+        ph = rbn[o_ph:o_ph + B * cap].reshape(B, cap).view(np.uint32).copy() if cap else None
         extra = None
         if pk.cpu_patterns:
             extra = np.zeros((B, 8), dtype=np.int64)
@@ -267,5 +299,5 @@ class TextPipeline:
                 for slot, p in pk.cpu_patterns:
                     extra[j, slot] += p.count(c)
         el = (time.perf_counter() - t0) * 1e3
-        return TextResult(stats_h.numpy(), pred_h, el, pred is not None, pk.slot_prio, extra,
+        return TextResult(stats_h, pred_h, el, pred is not None, pk.slot_prio, extra,
                           pooled if keep_device else None, hashes if keep_device else None, L, ph)

@@ -205,6 +205,7 @@ class Preprocessor:
             self.stats["gpu_batches"] += 1
             self.stats["gpu_messages"] += len(work)
             self.stats["last_gpu_ms"] = res.elapsed_ms
+            self.stats["gpu_ms_total"] = self.stats.get("gpu_ms_total", 0.0) + res.elapsed_ms
             for j, i in enumerate(work):
                 m = msgs[i]
                 if res.fallback[j]:
