@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--no-classifier", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--control-plane", default="gloo", choices=["gloo", "nccl"],
+                    help="per-tick load/descriptor exchange: host gloo group or RCCL on a side stream")
     ap.add_argument("--gateway-only-s", type=float, default=3.0,
                     help="seconds of the secondary null-backend gateway measurement (0 = skip)")
     ap.add_argument("--gateway-only-rate", type=float, default=20000.0)
@@ -87,7 +89,7 @@ def main(argv=None) -> int:
         return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    comm = init_from_env()
+    comm = init_from_env(control=a.control_plane)
 
     cfg = default_config()
     cfg.preprocessor.classifier = not a.no_classifier

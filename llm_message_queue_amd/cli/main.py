@@ -58,7 +58,7 @@ def cmd_serve(a, role: str = "serve") -> int:
     ulog.configure(cfg.logging.level, cfg.logging.format, cfg.logging.output)
     rank = int(os.environ.get("RANK", "0"))
     use_gpu = torch.cuda.is_available() and not a.no_gpu
-    comm = init_from_env() if use_gpu else None
+    comm = init_from_env(control=cfg.gpu.control_plane) if use_gpu else None
     engine = page = None
     if use_gpu and role in ("serve", "queue-manager"):
         local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -72,6 +72,12 @@ class SummaryEngine:
             pooled[i] = Hd.mean(0)
         return pooled, toks
 
+    def _link(self, pipe):
+        if getattr(self, "_hostlink", None) is None:
+            from ..ops.hostlink import HostLink
+            self._hostlink = HostLink(self.device, pipe.stream)
+        return self._hostlink
+
     # --------------------------------------------------------------- API
     def summarise(self, groups: Sequence[Tuple[Optional[np.ndarray], Sequence[str]]]
                   ) -> List[Tuple[np.ndarray, List[Tuple[int, int]]]]:
@@ -97,14 +103,13 @@ class SummaryEngine:
             pipe, sm = self._gpu_parts()
             from ..preprocess.oracle import default_patterns
             res = pipe.run(contents, default_patterns(), 0, classify=True, keep_device=True)
+            link = self._link(pipe)
             with torch.cuda.stream(pipe.stream):
-                seg_d = torch.as_tensor(seg, device=self.device)
-                st_d = torch.as_tensor(state, device=self.device)
-                fi_d = torch.as_tensor(first, device=self.device)
+                seg_d, st_d, fi_d, ntok = link.upload([seg, state, first,
+                                                       np.ascontiguousarray(res.stats[:, 5], dtype=np.int32)])
                 sm.project(res.pooled, seg_d, st_d, fi_d)
-                ntok = torch.as_tensor(np.ascontiguousarray(res.stats[:, 5]), device=self.device)
-                hs, cs = sm.salient(res.hashes, ntok, seg_d, k=self.k)
-                new_state = st_d.cpu().numpy()
+                hs, cs = sm.salient(res.hashes, ntok, seg_d, k=self.k, link=link)
+                new_state = link.download([st_d])[0]
             sal = [[(int(h), int(n)) for h, n in zip(hs[c], cs[c]) if n > 0] for c in range(C)]
             return [(new_state[c], sal[c]) for c in range(C)]
         # CPU reference

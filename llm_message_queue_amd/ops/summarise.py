@@ -59,7 +59,10 @@ class Summariser:
         return state
 
     def salient(self, hashes: torch.Tensor, ntok: torch.Tensor, seg_off: torch.Tensor, k: int = 8,
-                stop: Optional[torch.Tensor] = None, ntok_stride: int = 1) -> Tuple[np.ndarray, np.ndarray]:
+                stop: Optional[torch.Tensor] = None, ntok_stride: int = 1, link=None) -> Tuple[np.ndarray, np.ndarray]:
+        """Top-k salient token hashes per segment.  ``link`` (an
+        ``ops.hostlink.HostLink`` on the current stream) reads the result
+        back without waiting for other streams."""
         C = seg_off.numel() - 1
         L = hashes.shape[1]
         stop = self._stop if stop is None else stop
@@ -67,4 +70,7 @@ class Summariser:
         oc = torch.zeros((C, k), dtype=torch.int32, device=self.device)
         self.k.salient_topk(hashes.data_ptr(), L, ntok.data_ptr(), ntok_stride, seg_off.data_ptr(), C,
                             stop.data_ptr(), stop.numel(), k, oh.data_ptr(), oc.data_ptr(), self._s())
+        if link is not None:
+            h, c = link.download([oh, oc])
+            return h.view(np.uint32), c
         return oh.cpu().numpy().view(np.uint32), oc.cpu().numpy()

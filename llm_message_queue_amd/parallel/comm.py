@@ -1,7 +1,8 @@
 """Control-plane communication between GPU backend processes (N10, N11).
 
-One process per GPU, ``torch.distributed`` with the ``nccl`` backend (= RCCL
-on ROCm, over xGMI).  The reference has no inter-service transport at all
+One process per GPU, ``torch.distributed``: the data plane on the ``nccl``
+backend (= RCCL on ROCm, over xGMI), the tiny control messages on a gloo
+group by default (see ``TorchComm`` for why they stay off the GPU streams).  The reference has no inter-service transport at all
 (its three microservices each own a private queue); here
 every scheduler tick does
   * ``all_gather`` of a fixed-size int64 load vector per rank (latency-bound,
@@ -71,25 +72,64 @@ class SoloComm(Comm):
 
 
 class TorchComm(Comm):
-    """torch.distributed process group (nccl=RCCL on GPU tensors, gloo on CPU)."""
+    """torch.distributed: the control plane (load all_gather, descriptor
+    all_to_all, broadcast) on ``group``, the data plane (KV migration
+    send/recv) on ``data_group`` (default: ``group``).
 
-    def __init__(self, device=None, group=None):
+    The control plane must never be ordered behind the backend's forward on
+    the compute stream -- a torch.distributed call on a GPU tensor makes the
+    communicator stream wait for the *current* stream, and a device->host read
+    of the result then waits for every forward step already queued (the 2-deep
+    async engine would be serialised by its own scheduler).  So:
+      * a gloo ``group`` (the default from ``init_from_env``) keeps the tiny
+        control messages on the host: no GPU stream is involved at all;
+      * an nccl ``group`` runs every control collective inside a dedicated
+        high-priority HIP stream and moves bytes with ``HostLink`` copy
+        kernels (host-mapped pinned memory), never through the runtime's
+        async copy path.
+    """
+
+    def __init__(self, device=None, group=None, data_group=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
+        self.data_group = data_group if data_group is not None else group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        backend = dist.get_backend(group)
+        self.backend = dist.get_backend(group)
         if device is None:
-            device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+            device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" \
+                else torch.device("cpu")
         self.device = torch.device(device)
+        self.stream = self.link = None
+        if self.device.type == "cuda":
+            from ..ops.hostlink import HostLink
+            self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+            self.link = HostLink(self.device, self.stream)
+
+    # -- host <-> collective buffers
+    def _put(self, arr):
+        arr = np.ascontiguousarray(arr)
+        if self.link is None:
+            return self.torch.from_numpy(arr.copy())
+        return self.link.upload([arr])[0]
+
+    def _get(self, t) -> np.ndarray:
+        if self.link is None:
+            return t.numpy()
+        return self.link.download([t])[0]
+
+    def _ctx(self):
+        import contextlib
+        return self.torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
     def all_gather_i64(self, vec):
         torch = self.torch
-        v = torch.as_tensor(np.asarray(vec, dtype=np.int64)).to(self.device)
-        out = torch.empty(self.world * v.numel(), dtype=torch.int64, device=self.device)
-        self.dist.all_gather_into_tensor(out, v.reshape(-1), group=self.group)
-        return out.cpu().numpy().reshape(self.world, -1)
+        with self._ctx():
+            v = self._put(np.asarray(vec, dtype=np.int64).reshape(-1))
+            out = torch.empty(self.world * v.numel(), dtype=torch.int64, device=self.device)
+            self.dist.all_gather_into_tensor(out, v, group=self.group)
+            return self._get(out).reshape(self.world, -1)
 
     def all_to_all_rows(self, send, recv_counts, width):
         torch = self.torch
@@ -97,11 +137,12 @@ class TorchComm(Comm):
         flat = np.concatenate([np.asarray(s, dtype=np.int32).reshape(-1) for s in send]) \
             if sum(send_counts) else np.zeros(0, dtype=np.int32)
         total_in = int(sum(recv_counts))
-        inp = torch.as_tensor(flat).to(self.device)
-        out = torch.empty(total_in * width, dtype=torch.int32, device=self.device)
-        self.dist.all_to_all_single(out, inp, output_split_sizes=[c * width for c in recv_counts],
-                                    input_split_sizes=[c * width for c in send_counts], group=self.group)
-        o = out.cpu().numpy().reshape(-1, width) if total_in else np.zeros((0, width), dtype=np.int32)
+        with self._ctx():
+            inp = self._put(flat) if flat.size else torch.empty(0, dtype=torch.int32, device=self.device)
+            out = torch.empty(total_in * width, dtype=torch.int32, device=self.device)
+            self.dist.all_to_all_single(out, inp, output_split_sizes=[c * width for c in recv_counts],
+                                        input_split_sizes=[c * width for c in send_counts], group=self.group)
+            o = self._get(out).reshape(-1, width) if total_in else np.zeros((0, width), dtype=np.int32)
         res, a = [], 0
         for c in recv_counts:
             res.append(o[a:a + c])
@@ -109,19 +150,19 @@ class TorchComm(Comm):
         return res
 
     def broadcast_i64(self, vec, root=0):
-        torch = self.torch
-        v = torch.as_tensor(np.asarray(vec, dtype=np.int64)).to(self.device).clone()
-        self.dist.broadcast(v, src=root, group=self.group)
-        return v.cpu().numpy()
+        with self._ctx():
+            v = self._put(np.asarray(vec, dtype=np.int64).reshape(-1))
+            self.dist.broadcast(v, src=root, group=self.group)
+            return self._get(v)
 
     def send_tensor(self, t, dst):
-        self.dist.send(t, dst=dst, group=self.group)
+        self.dist.send(t, dst=dst, group=self.data_group)
 
     def recv_tensor(self, t, src):
-        self.dist.recv(t, src=src, group=self.group)
+        self.dist.recv(t, src=src, group=self.data_group)
 
     def barrier(self):
-        if self.dist.get_backend(self.group) == "nccl":
+        if self.backend == "nccl":
             self.dist.barrier(group=self.group, device_ids=[self.device.index])
         else:
             self.dist.barrier(group=self.group)
@@ -188,8 +229,14 @@ class FakeComm(Comm):
         self.hub.bar.wait()
 
 
-def init_from_env(backend: Optional[str] = None):
-    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...)."""
+def init_from_env(backend: Optional[str] = None, control: str = "gloo"):
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...).
+
+    The default process group is ``backend`` (nccl = RCCL when a GPU is
+    present): it carries the data plane (KV migration over xGMI).  The
+    control plane uses a ``control`` group: "gloo" (host TCP, default --
+    decoupled from the GPU streams) or "nccl" (RCCL on a high-priority
+    stream, see ``TorchComm``)."""
     import os
     import torch
     import torch.distributed as dist
@@ -205,4 +252,9 @@ def init_from_env(backend: Optional[str] = None):
             torch.cuda.set_device(local)
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend=backend, **kw)
-    return TorchComm()
+    default_backend = dist.get_backend()
+    if control == default_backend or (control == "gloo" and default_backend == "gloo"):
+        return TorchComm()
+    ctrl = dist.new_group(backend=control)
+    return TorchComm(group=ctrl, data_group=dist.group.WORLD,
+                     device=torch.device("cpu") if control == "gloo" else None)

@@ -184,6 +184,7 @@ class GPUConfig:
     hbm_reserve_gb: float = 16.0
     telemetry_period_ms: int = 20
     comm_backend: str = "nccl"        # RCCL on ROCm; "gloo" for CPU tests
+    control_plane: str = "gloo"       # per-tick load/descriptor exchange: gloo (host) or nccl (RCCL)
     rebalance_interval_ms: int = 100
 
 

@@ -333,3 +333,55 @@ def test_slot_census_page():
     r = page.read()
     assert r["active"] == 34 and r["free"] == 66 and r["tokens"] == 77 and r["step"] == 5
     page.close(unlink=True)
+
+
+def test_summary_engine_gpu_matches_cpu_reference():
+    """Conversation summary (N5) end to end: GPU engine (text pipeline + MFMA
+    projection + salient top-k, host transfers through HostLink) vs the CPU
+    reference of the same math."""
+    from llm_message_queue_amd.conversation.summarise import SummaryEngine
+    gpu = SummaryEngine(device=DEV, k=6, alpha=0.7)
+    cpu = SummaryEngine(device="cpu", k=6, alpha=0.7)
+    rng = np.random.default_rng(3)
+    words = ["gpu", "kernel", "latency", "queue", "the", "router", "hbm", "slots", "urgent", "please"]
+    groups = []
+    for c in range(9):
+        prev = None if c % 3 == 0 else rng.standard_normal(256).astype(np.float32)
+        msgs = [" ".join(rng.choice(words, size=int(rng.integers(1, 12)))) for _ in range(1 + c % 4)]
+        groups.append((prev, msgs))
+    a = gpu.summarise(groups)
+    b = cpu.summarise(groups)
+    for (sa, la), (sb, lb) in zip(a, b):
+        assert np.allclose(sa, sb, atol=5e-2, rtol=5e-2)
+        assert [h for h, _ in la] == [h for h, _ in lb] and [n for _, n in la] == [n for _, n in lb]
+
+
+def test_torchcomm_rccl_control_plane_world1():
+    """RCCL control-plane plumbing (high-priority comm stream + HostLink copy
+    kernels) on a 1-rank nccl group -- the multi-rank logic itself is covered
+    on the CPU with FakeComm and gloo."""
+    import socket
+    import torch.distributed as dist
+    from llm_message_queue_amd.parallel.comm import TorchComm
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(DEV))
+    try:
+        c = TorchComm()
+        assert c.backend == "nccl" and c.stream is not None
+        # keep the compute stream busy: control messages must not wait for it
+        x = torch.randn(4096, 4096, device=DEV, dtype=torch.bfloat16)
+        for _ in range(20):
+            x = x @ x * 1e-3
+        g = c.all_gather_i64(np.arange(32, dtype=np.int64))
+        assert g.shape == (1, 32) and (g[0] == np.arange(32)).all()
+        rows = np.arange(3 * 12, dtype=np.int32).reshape(3, 12)
+        got = c.all_to_all_rows([rows], [3], 12)
+        assert np.array_equal(got[0], rows)
+        assert c.broadcast_i64(np.array([7, 9]))[1] == 9
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
