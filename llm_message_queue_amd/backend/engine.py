@@ -73,6 +73,7 @@ class _Inflight:
     firsts: List[Request]
     t0: float
     out: object                   # device tensor of sampled tokens (kept alive for the next gather)
+    t0_ns: int = 0                # monotonic launch time (tracing)
 
 
 class BackendEngine:
@@ -124,6 +125,7 @@ class BackendEngine:
         # n launches (a HIP error / OOM), {"slow_ms": x} stalls every launch,
         # {"drop_heartbeat": True} stops the load-page census
         self.fault: Dict[str, float] = {}
+        self.tracer = None          # utils.tracing.RequestTracer (backend step spans)
         if self.cuda and page is not None and page.dev_ptr is None:
             page.register_device()
         if page is not None:
@@ -262,8 +264,13 @@ class BackendEngine:
         self.free = list(range(self.slots - 1, -1, -1))
         return out
 
-    def launch(self) -> None:
-        """Build the next token batch and enqueue its forward (async)."""
+    def launch(self, wait_cb=None) -> None:
+        """Build the next token batch and enqueue its forward (async).
+
+        If ``max_inflight`` steps are already queued, wait for the oldest;
+        with ``wait_cb`` the wait polls the step's event and calls
+        ``wait_cb()`` in between (the gateway keeps ingesting/dispatching
+        while the GPU computes) instead of blocking."""
         if self.fault:
             if self.fault.get("fail_launch", 0) > 0:
                 self.fault["fail_launch"] -= 1
@@ -274,9 +281,18 @@ class BackendEngine:
                 time.sleep(self.fault["slow_ms"] / 1e3)
         ts = time.perf_counter_ns()
         while len(self._q) >= self.max_inflight:       # bound the run-ahead (and staging reuse)
-            self._reaped.append(self._reap(block=True))  # handed to the next finish()
+            if wait_cb is None:
+                self._reaped.append(self._reap(block=True))  # handed to the next finish()
+                continue
+            f = self._reap(block=False)
+            if f is not None:
+                self._reaped.append(f)
+                continue
+            if not wait_cb():
+                time.sleep(0.0002)
         t0 = time.perf_counter()
         tb = time.perf_counter_ns()
+        t_mono = time.monotonic_ns()
         self.host_ns[1] += tb - ts
         toks, pos, slot, samp, samp_slots, dec_rows, dec_src, tiles, n_pre, n_dec = self._build()
         self.host_ns[0] += time.perf_counter_ns() - tb
@@ -332,7 +348,7 @@ class BackendEngine:
             self.free.append(x)
         self.s_active[done] = False
         self._prev_out = out
-        self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out))
+        self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out, t_mono))
         self.step_id += 1
         self.total_tokens += T
         self.completed_total += len(completed)
@@ -349,6 +365,8 @@ class BackendEngine:
                 return None
         self._q.popleft()
         now = time.monotonic_ns()
+        if self.tracer is not None:
+            self.tracer.step(f.step, f.t0_ns, now, f.T)
         for r in f.firsts:
             r.first_token_ns = now
         for r in f.completed:

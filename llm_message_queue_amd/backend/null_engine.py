@@ -37,7 +37,7 @@ class NullEngine:
         self.active.extend(out)
         return out
 
-    def launch(self) -> None:
+    def launch(self, wait_cb=None) -> None:
         self._launched, self.active = self.active, []
         self.step_id += 1
 

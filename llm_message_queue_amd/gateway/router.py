@@ -164,6 +164,9 @@ class Gateway:
         self._tick_lock = threading.RLock()     # set_healthy from a telemetry thread waits for the tick
         self.unhealthy_peers: set = set()
         self.on_complete = None     # optional callback(msg)
+        self.tracer = None          # optional utils.tracing.RequestTracer
+        self.rec_done = LatencyRecorder(len(self.tiers))   # arrival -> completion (end to end)
+        self._done_buf: List[Tuple[int, int, int]] = []
         self.host_ns = np.zeros(5, dtype=np.int64)   # per-phase host time (host_profile)
         self.ingest_ns = np.zeros(3, dtype=np.int64)  # [preprocess ns, queue push ns, messages]
         self._ticks0 = 0
@@ -484,6 +487,10 @@ class Gateway:
     def _complete(self, m: Message, process_ns: int) -> None:
         m.status = MessageStatus.COMPLETED
         m.completed_at = time.time_ns()
+        if self.tracer is not None:
+            self.tracer.request(m)
+        if m.arrival_ns:
+            self._done_buf.append((m.tier, m.arrival_ns, m.enqueued_at or m.arrival_ns))
         self.qm.complete_message(m.queue_name, m.id, process_ns, m.priority)
         if self.lb is not None and m.endpoint_id:
             self.lb.release_endpoint(m.endpoint_id, process_ns, False)
@@ -516,22 +523,38 @@ class Gateway:
                 self._done_owed[origin].append((handle, tier, r.admitted_ns, r.done_ns, K_DONE))
         return res
 
-    def tick(self):
+    def tick(self, pump=None):
         """One serving tick, pipelined so host work overlaps the forward:
         launch the backend forward (async) -> ingest + GPU preprocess on a
         side stream -> collect the forward (completions free slots) ->
-        dispatch queued requests into free slots for the next forward."""
-        with self._tick_lock:
-            return self._tick()
+        dispatch queued requests into free slots for the next forward.
 
-    def _tick(self):
+        ``pump`` (optional callable) feeds new arrivals; while the launch
+        waits for the GPU (its run-ahead queue is full) the gateway calls it
+        and ingests -- and, on a single rank, dispatches -- so requests are
+        enqueued and admitted while the forward runs instead of at the next
+        tick boundary.  (Multi-rank dispatch is a collective and stays once
+        per tick.)"""
+        with self._tick_lock:
+            return self._tick(pump)
+
+    def _while_waiting(self, pump) -> bool:
+        """Work done while the engine waits for the GPU; True if any."""
+        if pump is not None:
+            pump()
+        did = bool(self.ingest())
+        if self.world == 1:
+            did = self._dispatch_local() > 0 or did
+        return did
+
+    def _tick(self, pump=None):
         res = None
         pc = time.perf_counter_ns
         ht = self.host_ns
         t0 = pc()
         if self.engine is not None and self.healthy:
             try:
-                self.engine.launch()
+                self.engine.launch(wait_cb=lambda: self._while_waiting(pump))
                 t1 = pc()
                 self.ingest()
                 t2 = pc()
@@ -544,13 +567,25 @@ class Gateway:
             except RuntimeError as e:           # HIP error / OOM from the backend
                 self._set_healthy(False, f"backend error: {e}")
         if res is None:
+            if pump is not None:
+                pump()
             self.ingest()
         t4 = pc()
         n = self.dispatch()
         ht[3] += pc() - t4
         ht[4] += t4 - t0 if res is None else 0
         self.counters["ticks"] += 1
+        self.flush_latency()
         return n, res
+
+    def flush_latency(self) -> None:
+        """Move buffered completion timestamps into the e2e histogram."""
+        if self._done_buf:
+            now = time.monotonic_ns()
+            a = np.asarray(self._done_buf, dtype=np.int64)
+            self._done_buf = []
+            tiers = np.clip(a[:, 0], 0, len(self.tiers) - 1)
+            self.rec_done.record(tiers, now - a[:, 1], now - a[:, 2])
 
     def host_profile(self, reset: bool = False) -> Dict[str, float]:
         """Mean host milliseconds per tick in each phase (launch includes any

@@ -324,3 +324,20 @@ def test_engine_attention_tiles_match_per_token_path():
         outs.append({r.req_id: (r.generated, r.prefilled) for r in done})
         outs.append(eng.model.kcache[0].clone())
     assert outs[0] == outs[2] and torch.equal(outs[1], outs[3])
+
+
+def test_request_tracer_chrome_trace(tmp_path):
+    import json
+    from llm_message_queue_amd.utils.tracing import RequestTracer
+    gw = Gateway(cfg(), engine=engine(slots=4), use_gpu_preprocess=False, prompt_cap=8, gen_tokens=2)
+    tr = RequestTracer(sample_every=1)
+    gw.tracer = gw.engine.tracer = tr
+    gw.submit(Workload(seed=2).make(10))
+    assert run_until_done([gw], 10)
+    n = tr.dump(str(tmp_path / "t.json"))
+    ev = json.load(open(tmp_path / "t.json"))["traceEvents"]
+    assert n == len(ev)
+    served = [e for e in ev if e.get("name") == "served"]
+    steps = [e for e in ev if e.get("name", "").startswith("step ")]
+    assert len(served) == 10 and steps and all(e["dur"] >= 0 for e in served + steps)
+    assert {e["tid"] for e in served} <= {1, 2, 3, 4}

@@ -368,7 +368,7 @@ def test_torchcomm_rccl_control_plane_world1():
     port = s.getsockname()[1]
     s.close()
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
-                            device_id=torch.device(DEV))
+                            device_id=torch.device("cuda", 0))
     try:
         c = TorchComm()
         assert c.backend == "nccl" and c.stream is not None
