@@ -50,6 +50,7 @@ def parse(argv=None):
     ap.add_argument("--max-ctx", type=int, default=512)
     ap.add_argument("--token-budget", type=int, default=8192)
     ap.add_argument("--gen-tokens", type=int, default=4)
+    ap.add_argument("--inflight", type=int, default=2, help="forward steps queued ahead on the GPU")
     ap.add_argument("--prompt-cap", type=int, default=32)
     ap.add_argument("--util", type=float, default=0.97)
     ap.add_argument("--tick-ms", type=float, default=0.0, help="minimum serving tick period (0 = dynamic)")
@@ -105,7 +106,7 @@ def main(argv=None) -> int:
     page = SlotPage(f"bench{job}", rank)
     engine = BackendEngine(LlamaConfig.by_name(a.model), slots=a.slots, max_ctx=a.max_ctx,
                            token_budget=a.token_budget, device=dev, impl="hip", seed=1000 + rank,
-                           page=page, gpu_index=rank)
+                           page=page, gpu_index=rank, max_inflight=a.inflight)
     pre = Preprocessor(cfg.preprocessor, use_gpu=True, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = "least_connections"
@@ -252,7 +253,7 @@ def main(argv=None) -> int:
         "config": {"model": f"{a.model}-stub (32L, random bf16)" if a.model == "llama3-8b" else a.model,
                    "global_batch": a.slots * world, "seq_len": a.max_ctx,
                    "parallelism": f"dp{world}", "token_budget": a.token_budget,
-                   "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap,
+                   "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap, "inflight": a.inflight,
                    "classifier": not a.no_classifier},
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),

@@ -103,6 +103,7 @@ class BackendEngine:
         self.s_out_step = np.full(slots, -2, dtype=np.int64)
         self.s_active = np.zeros(slots, dtype=bool)
         self._admit_seq = 0
+        self._mean_plen = 16.0                              # EMA of admitted prompt lengths
         self.page = page
         self.gpu_index = gpu_index
         self.max_inflight = max(1, max_inflight)
@@ -143,6 +144,23 @@ class BackendEngine:
     def inflight(self) -> int:
         return self.slots - len(self.free)
 
+    def admit_capacity(self) -> int:
+        """How many new requests the NEXT step can take: free slots, bounded
+        by the step's prefill headroom (token budget - decode tokens - prompt
+        tokens already admitted but not yet prefilled) over the running mean
+        prompt length.  The dispatcher admits at most this many, so requests
+        that could not start prefilling next step wait in the priority queue
+        (where tier order and aging apply), not in a FIFO inside the engine."""
+        free = len(self.free)
+        if free == 0:
+            return 0
+        act = self.s_active
+        pending = int((self.s_plen[act] - self.s_pref[act]).sum())
+        head = self.token_budget - int(act.sum()) - pending
+        if head <= 0:
+            return 0
+        return min(free, max(1, int(head / max(1.0, self._mean_plen))))
+
     def admit(self, reqs: Sequence[Request]) -> List[Request]:
         now = time.monotonic_ns()
         out = []
@@ -171,6 +189,7 @@ class BackendEngine:
             self.s_seq[s] = self._admit_seq
             self._admit_seq += 1
             self.s_active[s] = True
+            self._mean_plen += 0.01 * (n - self._mean_plen)
             out.append(r)
         return out
 

@@ -25,6 +25,9 @@ class NullEngine:
     def free_slots(self) -> int:
         return self.slots - len(self.active)
 
+    def admit_capacity(self) -> int:
+        return self.free_slots()
+
     def inflight(self) -> int:
         return len(self.active)
 

@@ -252,7 +252,7 @@ class Gateway:
     def _dispatch_local(self) -> int:
         if self.engine is None or not self.healthy:
             return 0
-        free = self.engine.free_slots()
+        free = self.engine.admit_capacity()
         if free <= 0:
             return 0
         msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets())
@@ -288,7 +288,7 @@ class Gateway:
     def _dispatch_global(self) -> int:
         W, me = self.world, self.rank
         depth, age = self._queue_state()
-        free = self.engine.free_slots() if self.engine is not None else 0
+        free = self.engine.admit_capacity() if self.engine is not None else 0
         inflight = self.engine.inflight() if self.engine is not None else 0
         done_for = [len(self._done_owed[r]) for r in range(W)]
         load = planner.make_load(free, inflight, depth, age, healthy=self.engine is not None and self.healthy,

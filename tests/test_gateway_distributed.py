@@ -26,8 +26,9 @@ def cfg():
     return c
 
 
-def engine(slots=8, seed=0):
-    return BackendEngine(MICRO, slots=slots, max_ctx=64, token_budget=64, device="cpu", impl="ref", seed=seed)
+def engine(slots=8, seed=0, token_budget=64):
+    return BackendEngine(MICRO, slots=slots, max_ctx=64, token_budget=token_budget, device="cpu", impl="ref",
+                         seed=seed)
 
 
 def run_until_done(gws, n_expected, max_ticks=400):
@@ -200,8 +201,8 @@ def test_gloo_world2_dispatch():
 # ---------------------------------------------------------------- affinity + KV migration
 def test_affinity_routes_to_home_gpu():
     comms = FakeComm.make(2)
-    gws = [Gateway(cfg(), engine=engine(slots=8, seed=r), comm=comms[r], use_gpu_preprocess=False, prompt_cap=8,
-                   gen_tokens=1) for r in range(2)]
+    gws = [Gateway(cfg(), engine=engine(slots=8, seed=r, token_budget=256), comm=comms[r], use_gpu_preprocess=False,
+                   prompt_cap=8, gen_tokens=1) for r in range(2)]
     msgs = Workload(seed=5).make(6)
     for m in msgs:
         m.priority = 3
@@ -300,6 +301,25 @@ def test_single_rank_fault_requeues_and_recovers():
     assert run_until_done([gw], 10)
     st = gw.qm.get_all_queue_stats()
     assert sum(s.processing_count for s in st.values()) == 0
+
+
+def test_admit_capacity_bounds_prefill_backlog():
+    """The dispatcher may only admit what the next step can start prefilling:
+    requests beyond that wait in the priority queue, not inside the engine."""
+    from llm_message_queue_amd.backend.engine import Request
+    eng = engine(slots=16, token_budget=64)
+    assert eng.admit_capacity() == 4                    # 64 tokens / mean prompt 16
+    eng.admit([Request(i, np.arange(30, dtype=np.int32), gen_tokens=2) for i in range(3)])
+    assert eng.admit_capacity() == 0                    # 3 decode-to-be + 90 pending prefill >= 64
+    eng.step()
+    eng.step()
+    assert 0 < eng.admit_capacity() <= eng.free_slots()
+    gw = Gateway(cfg(), engine=engine(slots=16, token_budget=64), use_gpu_preprocess=False, prompt_cap=30,
+                 gen_tokens=2)
+    gw.submit(Workload(seed=1).make(40))
+    gw.ingest()
+    n = gw.dispatch()
+    assert 0 < n < 16 and gw.pending() == 40 - n       # slots were free, prefill headroom was not
 
 
 def test_engine_attention_tiles_match_per_token_path():
