@@ -127,7 +127,10 @@ def main(argv=None) -> int:
     # token throughput over the second half and convert it to requests/s with
     # the measured tokens per completed request (robust to the prefill/decode
     # waves a saturated start produces).
-    warm = max(a.warmup, 40)
+    # W untimed warm-up ticks (>= 20), then 60 measured saturated ticks; the
+    # tick counts are fixed so every rank issues the same collectives
+    w0 = max(a.warmup, 20)
+    warm = w0 + 60
     t_c0 = None
     tok0 = rt0 = done0 = 0
     for i in range(warm):
@@ -136,7 +139,7 @@ def main(argv=None) -> int:
         if need:
             gw.submit(wl.make(need))
         gw.tick()
-        if i == warm // 3:
+        if i == w0 - 1:
             torch.cuda.synchronize(dev)
             t_c0 = time.perf_counter()
             tok0, rt0, done0 = engine.total_tokens, engine.completed_tokens, engine.completed_total
@@ -144,7 +147,7 @@ def main(argv=None) -> int:
             sat_eng0 = engine.host_ns.copy()
     torch.cuda.synchronize(dev)
     t_c1 = time.perf_counter()
-    n_sat = warm - 1 - warm // 3
+    n_sat = warm - w0
     host_sat = dict(gw.host_profile(), engine_build=round(float(engine.host_ns[0] - sat_eng0[0]) / n_sat / 1e6, 3),
                     engine_sync=round(float(engine.host_ns[1] - sat_eng0[1]) / n_sat / 1e6, 3),
                     tick_ms=round((t_c1 - t_c0) * 1e3 / n_sat, 3),

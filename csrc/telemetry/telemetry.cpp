@@ -46,6 +46,7 @@ using procs_t = amdsmi_status_t (*)(amdsmi_socket_handle, uint32_t*, amdsmi_proc
 using vram_t = amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_vram_usage_t*);
 using act_t = amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_engine_usage_t*);
 using ecc_t = amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_gpu_block_t, amdsmi_error_count_t*);
+using bdf_t = amdsmi_status_t (*)(amdsmi_processor_handle, amdsmi_bdf_t*);
 
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -71,6 +72,7 @@ class Telemetry {
     vram_ = (vram_t)dlsym(lib_, "amdsmi_get_gpu_vram_usage");
     act_ = (act_t)dlsym(lib_, "amdsmi_get_gpu_activity");
     ecc_ = (ecc_t)dlsym(lib_, "amdsmi_get_gpu_ecc_count");
+    bdf_ = (bdf_t)dlsym(lib_, "amdsmi_get_gpu_device_bdf");
     if (!init_ || !sockets_ || !procs_ || !vram_) {
       error_ = "amd-smi symbols missing";
       return;
@@ -95,6 +97,17 @@ class Telemetry {
       for (auto p : ps) gpus_.push_back(p);
     }
     samples_.resize(gpus_.size());
+    // PCI address of each amd-smi processor: the caller maps them to HIP
+    // device indices (amd-smi enumerates every GPU of the node, HIP only the
+    // visible ones, in possibly different order)
+    for (auto p : gpus_) {
+      int64_t key = -1;
+      amdsmi_bdf_t b{};
+      if (bdf_ && bdf_(p, &b) == AMDSMI_STATUS_SUCCESS)
+        key = ((int64_t)b.domain_number << 16) | ((int64_t)b.bus_number << 8) | ((int64_t)b.device_number << 3) |
+              (int64_t)b.function_number;
+      bdfs_.push_back(key);
+    }
     if (gpus_.empty()) error_ = "no GPUs found";
   }
 
@@ -183,6 +196,7 @@ class Telemetry {
       d["umc_pct"] = cp[i].umc_pct;
       d["ecc_uncorrectable"] = cp[i].ecc_uncorrectable;
       d["ts_ns"] = cp[i].ts_ns;
+      d["pci"] = i < bdfs_.size() ? bdfs_[i] : (int64_t)-1;
       for (auto& kv : ov) {
         if (kv.first.first != (int)i) continue;
         if (kv.first.second == "valid") d["valid"] = kv.second != 0.0;
@@ -194,6 +208,7 @@ class Telemetry {
   }
 
   int64_t polls() const { return polls_.load(); }
+  std::vector<int64_t> pci_addresses() const { return bdfs_; }
 
  private:
   void* lib_ = nullptr;
@@ -206,6 +221,8 @@ class Telemetry {
   vram_t vram_ = nullptr;
   act_t act_ = nullptr;
   ecc_t ecc_ = nullptr;
+  bdf_t bdf_ = nullptr;
+  std::vector<int64_t> bdfs_;    // domain<<16 | bus<<8 | device<<3 | function
   std::vector<amdsmi_processor_handle> gpus_;
   std::vector<GpuSample> samples_;
   std::map<std::pair<int, std::string>, double> overrides_;
@@ -231,5 +248,6 @@ PYBIND11_MODULE(_telemetry, m) {
       .def("inject", &Telemetry::inject)
       .def("clear_injections", &Telemetry::clear_injections)
       .def("snapshot", &Telemetry::snapshot, py::arg("synthetic") = 0)
-      .def("polls", &Telemetry::polls);
+      .def("polls", &Telemetry::polls)
+      .def("pci_addresses", [](Telemetry& t) { return t.pci_addresses(); });
 }

@@ -19,18 +19,40 @@ from .. import _native
 from ..utils.logging import get_logger
 
 
+def hip_gpu_map(pci_addresses) -> Dict[int, Optional[int]]:
+    """amd-smi index -> visible HIP device index, matched on PCI domain/bus/
+    device (function ignored).  Unmatched (other containers' GPUs) -> None."""
+    import torch
+    if not torch.cuda.is_available():
+        return {}
+    hip = {}
+    for i in range(torch.cuda.device_count()):
+        p = torch.cuda.get_device_properties(i)
+        hip[(int(p.pci_domain_id) << 16) | (int(p.pci_bus_id) << 8) | (int(p.pci_device_id) << 3)] = i
+    out: Dict[int, Optional[int]] = {}
+    for k, addr in enumerate(pci_addresses):
+        out[k] = hip.get(int(addr) & ~0x7) if addr >= 0 else None
+    if not any(v is not None for v in out.values()):
+        return {}                            # no PCI info: fall back to index order
+    return out
+
+
 class TelemetryService:
     def __init__(self, period_ms: int = 20, pages: Optional[Dict[int, object]] = None, metrics=None,
                  resource_scheduler=None, on_unhealthy: Optional[Callable[[int, str], None]] = None,
                  synthetic: int = 0, gpu_map: Optional[Dict[int, int]] = None):
         self.native = _native.telemetry().Telemetry(int(period_ms))
+        if gpu_map is None and self.native.available():
+            gpu_map = hip_gpu_map(self.native.pci_addresses())
         self.period_s = period_ms / 1e3
         self.pages = pages or {}
         self.metrics = metrics
         self.rs = resource_scheduler
         self.on_unhealthy = on_unhealthy
         self.synthetic = synthetic
-        self.gpu_map = gpu_map or {}
+        # amd-smi index -> HIP device index (by PCI address); GPUs of the node
+        # that this process cannot see map to None and are ignored
+        self.gpu_map = gpu_map if gpu_map is not None else {}
         self.log = get_logger("telemetry")
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
@@ -66,7 +88,11 @@ class TelemetryService:
         snap = self.native.snapshot(self.synthetic)
         self.last = snap
         for s in snap:
-            g = self.gpu_map.get(s["gpu"], s["gpu"])
+            g = self.gpu_map.get(s["gpu"], s["gpu"]) if self.gpu_map else s["gpu"]
+            if g is None:
+                continue
+            if s.get("ts_ns", 1) == 0 and s["valid"] is False and not self.synthetic:
+                continue                    # not polled yet
             page = self.pages.get(g)
             if page is not None:
                 page.set_telemetry(int(s["hbm_used_mb"]), int(s["hbm_total_mb"]), int(s["gfx_pct"]))
