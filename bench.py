@@ -46,9 +46,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--slots", type=int, default=2048)
+    ap.add_argument("--slots", type=int, default=1024)
     ap.add_argument("--max-ctx", type=int, default=512)
-    ap.add_argument("--token-budget", type=int, default=8192)
+    ap.add_argument("--token-budget", type=int, default=4096)
     ap.add_argument("--gen-tokens", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=2, help="forward steps queued ahead on the GPU")
     ap.add_argument("--prompt-cap", type=int, default=32)
@@ -60,6 +60,8 @@ def parse(argv=None):
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace-out", default="", help="Chrome trace of sampled requests + backend steps (timed phase)")
     ap.add_argument("--trace-sample", type=int, default=20, help="trace every Nth completed request")
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="rehearse the multi-rank control flow on CPU (gloo, tiny model); not a measurement")
     ap.add_argument("--control-plane", default="gloo", choices=["gloo", "nccl"],
                     help="per-tick load/descriptor exchange: host gloo group or RCCL on a side stream")
     ap.add_argument("--gateway-only-s", type=float, default=3.0,
@@ -87,12 +89,24 @@ def main(argv=None) -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         print(f"warning: --gpus {a.gpus} != WORLD_SIZE {world}", file=sys.stderr)
-    if not torch.cuda.is_available():
-        print("bench.py needs a GPU (MI355X)", file=sys.stderr)
-        return 2
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    comm = init_from_env(control=a.control_plane)
+    dry = a.cpu_dry_run
+    if dry:
+        # CPU rehearsal of the exact control flow (collectives, tick counts,
+        # reductions) with a tiny model and gloo -- never a measurement
+        dev = torch.device("cpu")
+        comm = init_from_env(backend="gloo", control="gloo")
+        a.model, a.slots, a.max_ctx, a.token_budget, a.prompt_cap = "tiny", 16, 64, 128, 16
+    else:
+        if not torch.cuda.is_available():
+            print("bench.py needs a GPU (MI355X)", file=sys.stderr)
+            return 2
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        comm = init_from_env(control=a.control_plane)
+
+    def dsync():
+        if not dry:
+            torch.cuda.synchronize(dev)
 
     cfg = default_config()
     cfg.preprocessor.classifier = not a.no_classifier
@@ -105,9 +119,9 @@ def main(argv=None) -> int:
     job =os.environ.get("TORCHELASTIC_RUN_ID", str(os.getpid() if world == 1 else "bench"))
     page = SlotPage(f"bench{job}", rank)
     engine = BackendEngine(LlamaConfig.by_name(a.model), slots=a.slots, max_ctx=a.max_ctx,
-                           token_budget=a.token_budget, device=dev, impl="hip", seed=1000 + rank,
+                           token_budget=a.token_budget, device=dev, impl="ref" if dry else "hip", seed=1000 + rank,
                            page=page, gpu_index=rank, max_inflight=a.inflight)
-    pre = Preprocessor(cfg.preprocessor, use_gpu=True, device=str(dev))
+    pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = "least_connections"
     lbcfg.health_check_interval = 0
@@ -115,11 +129,11 @@ def main(argv=None) -> int:
     lb.add_endpoint(Endpoint(id=f"gpu{rank}", type="llm", gpu_index=rank, page=page,
                              max_connections=a.slots))
     gw = Gateway(cfg, preprocessor=pre, engine=engine, comm=comm, load_balancer=lb if world == 1 else None,
-                 use_gpu_preprocess=True, prompt_cap=a.prompt_cap, gen_tokens=a.gen_tokens)
+                 use_gpu_preprocess=not dry, prompt_cap=a.prompt_cap, gen_tokens=a.gen_tokens)
     wl = Workload(seed=a.seed * 1000 + rank)
 
     def sync_all():
-        torch.cuda.synchronize(dev)
+        dsync()
         comm.barrier()
 
     # ---------------------------------------------------------------- warmup + calibration
@@ -140,12 +154,12 @@ def main(argv=None) -> int:
             gw.submit(wl.make(need))
         gw.tick()
         if i == w0 - 1:
-            torch.cuda.synchronize(dev)
+            dsync()
             t_c0 = time.perf_counter()
             tok0, rt0, done0 = engine.total_tokens, engine.completed_tokens, engine.completed_total
             gw.host_profile(reset=True)
             sat_eng0 = engine.host_ns.copy()
-    torch.cuda.synchronize(dev)
+    dsync()
     t_c1 = time.perf_counter()
     n_sat = warm - w0
     host_sat = dict(gw.host_profile(), engine_build=round(float(engine.host_ns[0] - sat_eng0[0]) / n_sat / 1e6, 3),
@@ -252,7 +266,8 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": round(value / BASELINE_RPS, 4),
         "dtype": "bf16",
-        "data": "synthetic (Poisson arrivals, 10/30/40/20 tier mix, random-init weights)",
+        "data": "CPU DRY RUN of the control flow -- not a measurement" if dry else
+                "synthetic (Poisson arrivals, 10/30/40/20 tier mix, random-init weights)",
         "config": {"model": f"{a.model}-stub (32L, random bf16)" if a.model == "llama3-8b" else a.model,
                    "global_batch": a.slots * world, "seq_len": a.max_ctx,
                    "parallelism": f"dp{world}", "token_budget": a.token_budget,
@@ -282,7 +297,7 @@ def main(argv=None) -> int:
         # (GPU preprocess + native queue + dispatcher) against a null backend,
         # Poisson load at --gateway-only-rate per GPU.
         from llm_message_queue_amd.backend.null_engine import NullEngine
-        gw2 = Gateway(cfg, preprocessor=pre, engine=NullEngine(), use_gpu_preprocess=True,
+        gw2 = Gateway(cfg, preprocessor=pre, engine=NullEngine(), use_gpu_preprocess=not dry,
                       prompt_cap=a.prompt_cap, gen_tokens=1)
         arr2 = PoissonArrivals(a.gateway_only_rate, seed=99 + rank)
         sync_all()

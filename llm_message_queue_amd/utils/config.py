@@ -195,7 +195,7 @@ class BackendConfig:
     prompt_tokens: int = 32            # prompt tokens prefilled per request (cap)
     gen_tokens: int = 4                # decode steps per request
     dtype: str = "bf16"
-    token_budget: int = 8192           # max tokens per forward step (prefill chunking)
+    token_budget: int = 4096           # max tokens per forward step (prefill chunking)
 
 
 @dataclass

@@ -1,0 +1,45 @@
+"""bench.py driver contract, rehearsed on CPU: the multi-rank control flow
+(torch.distributed.run, one process per rank, fixed tick counts so every rank
+issues the same collectives, max-over-ranks timing, one JSON line from rank 0)
+with gloo and a tiny model (``--cpu-dry-run``; never a measurement)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, timeout=240):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(args, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_single_rank_dry_run():
+    d = _run([sys.executable, "bench.py", "--cpu-dry-run", "--steps", "4", "--warmup", "2",
+              "--gateway-only-s", "0.3", "--gateway-only-rate", "300"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2 and d["scaling"] == "weak"
+    assert "DRY RUN" in d["data"] and d["value"] > 0 and "gateway_only" in d
+
+
+def test_bench_two_ranks_torchrun_dry_run():
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+              "--cpu-dry-run", "--steps", "5", "--warmup", "2", "--gateway-only-s", "0"])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
