@@ -167,6 +167,7 @@ class Gateway:
         self.tracer = None          # optional utils.tracing.RequestTracer
         self.rec_done = LatencyRecorder(len(self.tiers))   # arrival -> completion (end to end)
         self._done_buf: List[Tuple[int, int, int]] = []
+        self._last_ingest_ns = 0
         self.host_ns = np.zeros(5, dtype=np.int64)   # per-phase host time (host_profile)
         self.ingest_ns = np.zeros(3, dtype=np.int64)  # [preprocess ns, queue push ns, messages]
         self._ticks0 = 0
@@ -538,10 +539,20 @@ class Gateway:
         with self._tick_lock:
             return self._tick(pump)
 
+    WAIT_INGEST_NS = 8_000_000      # min spacing of ingest batches while the GPU is busy
+    WAIT_INGEST_MSGS = 512          # ... unless this many arrived
+
     def _while_waiting(self, pump) -> bool:
-        """Work done while the engine waits for the GPU; True if any."""
+        """Work done while the engine waits for the GPU; True if any.
+        Arrivals are preprocessed in batches (every WAIT_INGEST_NS or
+        WAIT_INGEST_MSGS): each preprocess batch is a fixed chain of small
+        kernels, so tiny batches would cost GPU time the forward needs."""
         if pump is not None:
             pump()
+        now = time.monotonic_ns()
+        if len(self._inbox) < self.WAIT_INGEST_MSGS and now - self._last_ingest_ns < self.WAIT_INGEST_NS:
+            return False
+        self._last_ingest_ns = now
         did = bool(self.ingest())
         if self.world == 1:
             did = self._dispatch_local() > 0 or did

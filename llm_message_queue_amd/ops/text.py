@@ -252,7 +252,8 @@ class TextPipeline:
         stream = torch.cuda.current_stream(self.device).cuda_stream
         L = self.L
         stats = torch.empty((B, STAT_COLS), dtype=torch.int32, device=self.device)
-        hashes = torch.zeros((B, L), dtype=torch.int32, device=self.device)
+        # every reader stops at the message's token count: no zero-fill needed
+        hashes = torch.empty((B, L), dtype=torch.int32, device=self.device)
         self.ops.text_analyze(dev.data_ptr(), d_off.data_ptr(), B, L, pk.table, stats.data_ptr(),
                               hashes.data_ptr(), stream)
         pooled = pred = None
