@@ -159,7 +159,10 @@ class BackendEngine:
         head = self.token_budget - int(act.sum()) - pending
         if head <= 0:
             return 0
-        return min(free, max(1, int(head / max(1.0, self._mean_plen))))
+        # round UP: the last admitted prompt may spill into the following step
+        # (chunked prefill), so a saturated step fills its token budget -- GEMM
+        # cost is quantised in 256-row tiles, the tail rows are nearly free
+        return min(free, max(1, -(-head // max(1, int(round(self._mean_plen))))))
 
     def admit(self, reqs: Sequence[Request]) -> List[Request]:
         now = time.monotonic_ns()
