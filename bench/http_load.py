@@ -1,0 +1,193 @@
+"""HTTP-level load test of the REST API (the reference's doc-only k6 / Go
+load tests, `docs/performance.md:1039-1155`: p99 < 500 ms, error rate < 10%;
+>= 900 RPS of a 1,000 RPS target with 100 workers).
+
+Open-loop Poisson arrivals of ``POST /api/v1/messages`` (4-tier content mix)
+from ``--procs`` client processes, each an aiohttp event loop.  Either starts
+the server itself (``--spawn serve|split``) or targets ``--url``.
+
+    python bench/http_load.py --spawn serve --rate 2000 --duration 10
+    python bench/http_load.py --spawn split --ingress 4 --rate 8000 --duration 10
+    python bench/http_load.py --url http://127.0.0.1:8080 --rate 1000
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import multiprocessing as mp
+import os
+import random
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+BODIES = [
+    {"content": "EMERGENCY: the payment service is down right now", "user_id": "rt"},
+    {"content": "urgent: please review the deploy before noon", "user_id": "hi"},
+    {"content": "can you summarise the meeting notes for the team?", "user_id": "n"},
+    {"content": "background batch job report", "user_id": "lo", "priority": "low"},
+]
+MIX = [0.1, 0.3, 0.4, 0.2]
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+async def _client(urls, rate, duration, seed, out):
+    import aiohttp
+    rng = random.Random(seed)
+    lat, codes = [], {}
+    conn = aiohttp.TCPConnector(limit=0)
+    async with aiohttp.ClientSession(connector=conn) as sess:
+        tasks = []
+
+        async def one(body, url):
+            t0 = time.perf_counter()
+            try:
+                async with sess.post(url + "/api/v1/messages", json=body) as r:
+                    await r.read()
+                    codes[r.status] = codes.get(r.status, 0) + 1
+            except Exception:
+                codes["err"] = codes.get("err", 0) + 1
+            lat.append(time.perf_counter() - t0)
+
+        t_end = time.perf_counter() + duration
+        t_next = time.perf_counter()
+        k = 0
+        while True:
+            now = time.perf_counter()
+            if now >= t_end:
+                break
+            while t_next <= now:
+                body = dict(rng.choices(BODIES, MIX)[0])
+                tasks.append(asyncio.ensure_future(one(body, urls[k % len(urls)])))
+                k += 1
+                t_next += rng.expovariate(rate)
+            await asyncio.sleep(max(0.0, min(t_next - time.perf_counter(), 0.01)))
+        if tasks:
+            await asyncio.wait(tasks, timeout=30)
+    out.put({"sent": k, "codes": codes, "lat": lat})
+
+
+def _client_proc(urls, rate, duration, seed, out):
+    asyncio.run(_client(urls, rate, duration, seed, out))
+
+
+def _wait_up(url, timeout=120.0):
+    import urllib.request
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            with urllib.request.urlopen(url + "/health", timeout=1) as r:
+                if r.status == 200:
+                    return True
+        except Exception:
+            time.sleep(0.2)
+    return False
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--url", default="")
+    ap.add_argument("--spawn", choices=["", "serve", "split", "native"], default="")
+    ap.add_argument("--threads", type=int, default=4, help="native ingress threads")
+    ap.add_argument("--ingress", type=int, default=2, help="api-gateway processes (split)")
+    ap.add_argument("--gpu", action="store_true", help="spawned server uses the GPU")
+    ap.add_argument("--rate", type=float, default=1000.0, help="offered requests/s (total)")
+    ap.add_argument("--duration", type=float, default=10.0)
+    ap.add_argument("--procs", type=int, default=2, help="client processes")
+    a = ap.parse_args()
+    procs, urls = [], []
+    env = dict(os.environ, PYTHONUNBUFFERED="1", LLMQ_LOGGING__LEVEL="warning",
+               LLMQ_QUEUE__WORKER__MAX_CONCURRENT="512", LLMQ_QUEUE__WORKER__MAX_BATCH_SIZE="256",
+               LLMQ_QUEUE__WORKER__PROCESS_INTERVAL="5ms")
+    gpu = [] if a.gpu else ["--no-gpu"]
+    try:
+        if a.spawn == "serve":
+            port = _port()
+            procs.append(subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "serve", "--port",
+                                           str(port), "--host", "127.0.0.1"] + gpu, cwd=ROOT, env=env,
+                                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                          start_new_session=True))
+            urls = [f"http://127.0.0.1:{port}"]
+        elif a.spawn == "split":
+            ring = f"httpload{os.getpid()}"
+            procs.append(subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "queue-manager",
+                                           "--ring", ring, "--port", str(_port())] + gpu, cwd=ROOT, env=env,
+                                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                          start_new_session=True))
+            for _ in range(a.ingress):
+                port = _port()
+                procs.append(subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "api-gateway",
+                                               "--ring", ring, "--port", str(port), "--host", "127.0.0.1",
+                                               "--no-gpu"], cwd=ROOT, env=env, stdout=subprocess.DEVNULL,
+                                              stderr=subprocess.DEVNULL, start_new_session=True))
+                urls.append(f"http://127.0.0.1:{port}")
+        elif a.spawn == "native":
+            ring = f"httpload{os.getpid()}"
+            procs.append(subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "queue-manager",
+                                           "--ring", ring, "--port", str(_port())] + gpu, cwd=ROOT, env=env,
+                                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                          start_new_session=True))
+            port = _port()
+            procs.append(subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "api-gateway",
+                                           "--native", "--ring", ring, "--port", str(port), "--host", "127.0.0.1",
+                                           "--ingress-threads", str(a.threads)], cwd=ROOT, env=env,
+                                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                          start_new_session=True))
+            urls = [f"http://127.0.0.1:{port}"]
+        else:
+            urls = [a.url or "http://127.0.0.1:8080"]
+        for u in urls:
+            if not _wait_up(u):
+                raise SystemExit(f"server {u} did not come up")
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        cs = [ctx.Process(target=_client_proc, args=(urls, a.rate / a.procs, a.duration, 17 + i, q))
+              for i in range(a.procs)]
+        t0 = time.perf_counter()
+        for c in cs:
+            c.start()
+        res = [q.get(timeout=a.duration + 90) for _ in cs]
+        wall = time.perf_counter() - t0
+        for c in cs:
+            c.join(timeout=10)
+        lat = sorted(x for r in res for x in r["lat"])
+        codes = {}
+        for r in res:
+            for k, v in r["codes"].items():
+                codes[str(k)] = codes.get(str(k), 0) + v
+        sent = sum(r["sent"] for r in res)
+        ok = codes.get("202", 0)
+        pct = lambda q_: lat[min(len(lat) - 1, int(q_ * len(lat)))] * 1e3 if lat else 0.0   # noqa: E731
+        print(json.dumps({"mode": a.spawn or "url", "ingress_procs": len(urls), "offered_rps": a.rate,
+                          "sent": sent, "accepted_rps": round(ok / a.duration, 1),
+                          "error_rate": round(1 - ok / max(1, sent), 4), "codes": codes,
+                          "p50_ms": round(pct(0.5), 2), "p99_ms": round(pct(0.99), 2),
+                          "wall_s": round(wall, 1)}))
+    finally:
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,514 @@
+// Native HTTP ingress for the hot path: POST /api/v1/messages.
+//
+// The reference serves every route from one Gin process (api/handlers.go:75-
+// 118) and documents a > 10,000 messages/s target (docs/performance.md:9).
+// A Python ASGI stack tops out at ~1-2k requests/s per process, so the
+// submit route gets a native front end: N epoll threads (SO_REUSEPORT, one
+// listener each), HTTP/1.1 keep-alive + pipelining, a single-pass scan of the
+// JSON body (validation + top-level "id"/"priority"/"user_id" extraction; the
+// body itself is forwarded verbatim), a UUIDv4 when the client gave no id,
+// and a push into the process-shared request ring (shm_ring.h) as a RAW
+// record.  The GPU dispatcher drains the ring in large batches, so
+// preprocessing (text_analyze + MFMA classifier) sees big batches too.
+// Other routes (status, conversations, admin) stay on the Python API server.
+//
+// Response: 202 {"message_id", "priority", "queue_time", "estimated_wait"}
+// where priority is the requested one (0 = to be decided by the
+// preprocessor, which runs asynchronously after the ack); 400 on a malformed
+// body, 503 when the ring is full (back-pressure).
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include <pybind11/pybind11.h>
+
+#include "queue/shm_ring.h"
+
+namespace py = pybind11;
+
+namespace {
+
+constexpr uint32_t TAG_RAW = 3;   // [u64 arrival_mono_ns][36 B uuid][u32 body_len][body]
+
+// ------------------------------------------------------------------ JSON scan
+struct Scan {
+  bool ok = false;
+  std::string id, user_id;
+  int priority = 0;
+};
+
+struct JsonScanner {
+  const char* p;
+  const char* e;
+  int depth = 0;
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  bool str(std::string* out) {
+    if (p >= e || *p != '"') return false;
+    ++p;
+    while (p < e && *p != '"') {
+      if (*p == '\\') {
+        if (p + 1 >= e) return false;
+        if (out) out->push_back(p[1] == 'n' ? '\n' : p[1] == 't' ? '\t' : p[1]);
+        p += (p[1] == 'u') ? 6 : 2;
+        continue;
+      }
+      if ((unsigned char)*p < 0x20) return false;
+      if (out) out->push_back(*p);
+      ++p;
+    }
+    if (p >= e) return false;
+    ++p;
+    return true;
+  }
+  bool num(double* out) {
+    const char* s = p;
+    if (p < e && (*p == '-' || *p == '+')) ++p;
+    bool any = false;
+    while (p < e && ((*p >= '0' && *p <= '9') || *p == '.' || *p == 'e' || *p == 'E' || *p == '-' || *p == '+')) {
+      ++p;
+      any = true;
+    }
+    if (!any) return false;
+    if (out) *out = strtod(std::string(s, p - s).c_str(), nullptr);
+    return true;
+  }
+  bool lit(const char* w) {
+    size_t n = strlen(w);
+    if ((size_t)(e - p) < n || memcmp(p, w, n) != 0) return false;
+    p += n;
+    return true;
+  }
+  bool value() {  // skip any value
+    ws();
+    if (p >= e) return false;
+    if (*p == '"') return str(nullptr);
+    if (*p == '{' || *p == '[') {
+      if (++depth > 64) return false;
+      const char close = *p == '{' ? '}' : ']';
+      const bool obj = *p == '{';
+      ++p;
+      ws();
+      if (p < e && *p == close) {
+        ++p;
+        --depth;
+        return true;
+      }
+      for (;;) {
+        ws();
+        if (obj) {
+          if (!str(nullptr)) return false;
+          ws();
+          if (p >= e || *p != ':') return false;
+          ++p;
+        }
+        if (!value()) return false;
+        ws();
+        if (p < e && *p == ',') {
+          ++p;
+          continue;
+        }
+        if (p < e && *p == close) {
+          ++p;
+          --depth;
+          return true;
+        }
+        return false;
+      }
+    }
+    if (*p == 't') return lit("true");
+    if (*p == 'f') return lit("false");
+    if (*p == 'n') return lit("null");
+    return num(nullptr);
+  }
+};
+
+int priority_from_string(const std::string& s) {
+  std::string l;
+  for (char c : s) l.push_back((char)tolower((unsigned char)c));
+  if (l == "realtime" || l == "1") return 1;
+  if (l == "high" || l == "urgent" || l == "2") return 2;
+  if (l == "normal" || l == "3") return 3;
+  if (l == "low" || l == "4") return 4;
+  return -1;
+}
+
+Scan scan_message(const char* b, size_t n) {
+  Scan r;
+  JsonScanner js{b, b + n};
+  js.ws();
+  if (js.p >= js.e || *js.p != '{') return r;
+  ++js.p;
+  js.ws();
+  if (js.p < js.e && *js.p == '}') {
+    ++js.p;
+    r.ok = true;
+    return r;
+  }
+  for (;;) {
+    js.ws();
+    std::string key;
+    if (!js.str(&key)) return r;
+    js.ws();
+    if (js.p >= js.e || *js.p != ':') return r;
+    ++js.p;
+    js.ws();
+    if (key == "id" || key == "user_id") {
+      std::string v;
+      if (js.p < js.e && *js.p == '"') {
+        if (!js.str(&v)) return r;
+        (key == "id" ? r.id : r.user_id) = v;
+      } else if (!js.value()) {
+        return r;
+      }
+    } else if (key == "priority") {
+      if (js.p < js.e && *js.p == '"') {
+        std::string v;
+        if (!js.str(&v)) return r;
+        r.priority = v.empty() ? 0 : priority_from_string(v);
+        if (r.priority < 0) return r;                 // unknown priority name -> 400
+      } else if (js.p < js.e && *js.p == 'n') {
+        if (!js.lit("null")) return r;
+      } else {
+        double d = 0;
+        if (!js.num(&d)) return r;
+        r.priority = (int)d;
+        if (r.priority < 0 || r.priority > 4) return r;
+      }
+    } else if (!js.value()) {
+      return r;
+    }
+    js.ws();
+    if (js.p < js.e && *js.p == ',') {
+      ++js.p;
+      continue;
+    }
+    if (js.p < js.e && *js.p == '}') {
+      ++js.p;
+      js.ws();
+      r.ok = js.p == js.e;
+      return r;
+    }
+    return r;
+  }
+}
+
+// ------------------------------------------------------------------ HTTP
+struct Conn {
+  std::string in, out;
+  size_t out_off = 0;
+  bool close_after = false;
+};
+
+int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+std::string rfc3339_now() {
+  auto now = std::chrono::system_clock::now();
+  auto ns = std::chrono::duration_cast<std::chrono::nanoseconds>(now.time_since_epoch()).count();
+  time_t s = (time_t)(ns / 1000000000);
+  struct tm tmv;
+  gmtime_r(&s, &tmv);
+  char buf[64];
+  size_t k = strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%S", &tmv);
+  snprintf(buf + k, sizeof buf - k, ".%09lldZ", (long long)(ns % 1000000000));
+  return buf;
+}
+
+class HttpIngress {
+ public:
+  HttpIngress(int port, const std::string& ring, int threads, const std::string& host)
+      : port_(port), host_(host), ring_(ring, 1 << 26, "open"), nthreads_(threads > 0 ? threads : 4) {}
+  ~HttpIngress() { stop(); }
+
+  int start() {
+    if (running_.exchange(true)) return port_;
+    for (int i = 0; i < nthreads_; ++i) {
+      int fd = listen_socket();
+      if (fd < 0) {
+        stop();
+        throw std::runtime_error("ingress: cannot listen on port " + std::to_string(port_) + ": " + strerror(errno));
+      }
+      if (port_ == 0) {  // ephemeral: reuse the port the first listener got
+        sockaddr_in a{};
+        socklen_t al = sizeof a;
+        getsockname(fd, (sockaddr*)&a, &al);
+        port_ = ntohs(a.sin_port);
+      }
+      lfds_.push_back(fd);
+      th_.emplace_back([this, fd, i] { loop(fd, i); });
+    }
+    return port_;
+  }
+
+  void stop() {
+    if (!running_.exchange(false)) return;
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
+    th_.clear();
+    for (int fd : lfds_) ::close(fd);
+    lfds_.clear();
+  }
+
+  py::dict stats() const {
+    py::dict d;
+    d["accepted"] = accepted_.load();
+    d["rejected_full"] = rejected_full_.load();
+    d["bad_request"] = bad_.load();
+    d["requests"] = requests_.load();
+    d["connections"] = conns_.load();
+    d["port"] = port_;
+    return d;
+  }
+
+ private:
+  int listen_socket() {
+    int fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+    if (fd < 0) return -1;
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(port_);
+    inet_pton(AF_INET, host_.c_str(), &a.sin_addr);
+    if (bind(fd, (sockaddr*)&a, sizeof a) < 0 || listen(fd, 1024) < 0) {
+      ::close(fd);
+      return -1;
+    }
+    return fd;
+  }
+
+  void loop(int lfd, int tid) {
+    int ep = epoll_create1(0);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = lfd;
+    epoll_ctl(ep, EPOLL_CTL_ADD, lfd, &ev);
+    std::unordered_map<int, Conn> conns;
+    std::mt19937_64 rng((uint64_t)mono_ns() ^ ((uint64_t)tid << 40) ^ (uint64_t)(uintptr_t)this);
+    std::vector<epoll_event> evs(256);
+    char buf[65536];
+    while (running_.load()) {
+      int n = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
+      for (int k = 0; k < n; ++k) {
+        int fd = evs[k].data.fd;
+        if (fd == lfd) {
+          for (;;) {
+            int c = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK);
+            if (c < 0) break;
+            int one = 1;
+            setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+            epoll_event ce{};
+            ce.events = EPOLLIN | EPOLLRDHUP;
+            ce.data.fd = c;
+            epoll_ctl(ep, EPOLL_CTL_ADD, c, &ce);
+            conns[c];
+            conns_++;
+          }
+          continue;
+        }
+        auto it = conns.find(fd);
+        if (it == conns.end()) continue;
+        Conn& cn = it->second;
+        bool dead = (evs[k].events & (EPOLLERR | EPOLLHUP)) != 0;
+        if (evs[k].events & EPOLLIN) {
+          for (;;) {
+            ssize_t r = ::read(fd, buf, sizeof buf);
+            if (r > 0) {
+              cn.in.append(buf, (size_t)r);
+              if (cn.in.size() > (8u << 20)) dead = true;
+              continue;
+            }
+            if (r == 0) dead = true;
+            break;
+          }
+          if (!dead) process(cn, rng);
+        }
+        if (!dead && !cn.out.empty()) dead = !flush(fd, cn, ep);
+        if (dead || (cn.close_after && cn.out.empty())) {
+          epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
+          ::close(fd);
+          conns.erase(it);
+          conns_--;
+        }
+      }
+    }
+    for (auto& kv : conns) ::close(kv.first);
+    ::close(ep);
+  }
+
+  bool flush(int fd, Conn& cn, int ep) {
+    while (cn.out_off < cn.out.size()) {
+      ssize_t w = ::write(fd, cn.out.data() + cn.out_off, cn.out.size() - cn.out_off);
+      if (w > 0) {
+        cn.out_off += (size_t)w;
+        continue;
+      }
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        epoll_event ce{};
+        ce.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
+        ce.data.fd = fd;
+        epoll_ctl(ep, EPOLL_CTL_MOD, fd, &ce);
+        return true;
+      }
+      return false;
+    }
+    cn.out.clear();
+    cn.out_off = 0;
+    return true;
+  }
+
+  static void respond(Conn& cn, int code, const char* reason, const std::string& body, bool keep) {
+    char hdr[256];
+    int n = snprintf(hdr, sizeof hdr,
+                     "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n%s\r\n", code,
+                     reason, body.size(), keep ? "" : "Connection: close\r\n");
+    cn.out.append(hdr, (size_t)n);
+    cn.out.append(body);
+    if (!keep) cn.close_after = true;
+  }
+
+  static std::string uuid4(std::mt19937_64& rng) {
+    uint64_t a = rng(), b = rng();
+    a = (a & 0xFFFFFFFFFFFF0FFFull) | 0x0000000000004000ull;
+    b = (b & 0x3FFFFFFFFFFFFFFFull) | 0x8000000000000000ull;
+    char s[40];
+    snprintf(s, sizeof s, "%08x-%04x-%04x-%04x-%012llx", (unsigned)(a >> 32), (unsigned)((a >> 16) & 0xFFFF),
+             (unsigned)(a & 0xFFFF), (unsigned)(b >> 48), (unsigned long long)(b & 0xFFFFFFFFFFFFull));
+    return s;
+  }
+
+  void process(Conn& cn, std::mt19937_64& rng) {
+    size_t pos = 0;
+    while (!cn.close_after) {
+      size_t he = cn.in.find("\r\n\r\n", pos);
+      if (he == std::string::npos) break;
+      const char* h = cn.in.data() + pos;
+      size_t hl = he - pos;
+      // request line
+      const char* sp1 = (const char*)memchr(h, ' ', hl);
+      if (!sp1) {
+        respond(cn, 400, "Bad Request", "{\"error\":\"bad request line\"}", false);
+        break;
+      }
+      const char* sp2 = (const char*)memchr(sp1 + 1, ' ', hl - (sp1 + 1 - h));
+      if (!sp2) {
+        respond(cn, 400, "Bad Request", "{\"error\":\"bad request line\"}", false);
+        break;
+      }
+      std::string method(h, sp1 - h), path(sp1 + 1, sp2 - sp1 - 1);
+      bool http10 = std::string(sp2 + 1, std::min<size_t>(8, hl - (sp2 + 1 - h))) == "HTTP/1.0";
+      size_t clen = 0;
+      bool keep = !http10;
+      // headers (case-insensitive names)
+      const char* line = (const char*)memchr(h, '\n', hl);
+      while (line && line < h + hl) {
+        ++line;
+        const char* eol = (const char*)memchr(line, '\n', h + hl - line);
+        const char* le = eol ? eol : h + hl;
+        const char* colon = (const char*)memchr(line, ':', le - line);
+        if (colon) {
+          std::string name(line, colon - line);
+          for (auto& c : name) c = (char)tolower((unsigned char)c);
+          const char* v = colon + 1;
+          while (v < le && (*v == ' ' || *v == '\t')) ++v;
+          std::string val(v, le - v);
+          while (!val.empty() && (val.back() == '\r' || val.back() == ' ')) val.pop_back();
+          if (name == "content-length") clen = (size_t)strtoull(val.c_str(), nullptr, 10);
+          else if (name == "connection") {
+            for (auto& c : val) c = (char)tolower((unsigned char)c);
+            if (val == "close") keep = false;
+            else if (val == "keep-alive") keep = true;
+          }
+        }
+        line = eol;
+      }
+      if (cn.in.size() < he + 4 + clen) break;  // body not complete yet
+      const char* body = cn.in.data() + he + 4;
+      requests_++;
+      if (method == "POST" && (path == "/api/v1/messages" || path == "/api/v1/messages/")) {
+        Scan s = scan_message(body, clen);
+        if (!s.ok) {
+          bad_++;
+          respond(cn, 400, "Bad Request", "{\"error\":\"Invalid message format\"}", keep);
+        } else {
+          std::string id = s.id.empty() ? uuid4(rng) : s.id;
+          std::string rec(8 + 36 + 4 + clen, '\0');
+          const int64_t t = mono_ns();
+          memcpy(&rec[0], &t, 8);
+          memcpy(&rec[8], id.data(), std::min<size_t>(36, id.size()));
+          const uint32_t bl = (uint32_t)clen;
+          memcpy(&rec[44], &bl, 4);
+          memcpy(&rec[48], body, clen);
+          if (id.size() > 36 || !ring_.push(rec, TAG_RAW)) {
+            if (id.size() > 36) {
+              bad_++;
+              respond(cn, 400, "Bad Request", "{\"error\":\"id longer than 36 bytes\"}", keep);
+            } else {
+              rejected_full_++;
+              respond(cn, 503, "Service Unavailable", "{\"error\":\"Failed to queue message: queue full\"}", keep);
+            }
+          } else {
+            accepted_++;
+            std::string out = "{\"message_id\":\"" + id + "\",\"priority\":" + std::to_string(s.priority) +
+                              ",\"queue_time\":\"" + rfc3339_now() + "\",\"estimated_wait\":0}";
+            respond(cn, 202, "Accepted", out, keep);
+          }
+        }
+      } else if (method == "GET" && path == "/health") {
+        respond(cn, 200, "OK", "{\"status\":\"ok\",\"version\":\"1.0.0\",\"time\":\"" + rfc3339_now() + "\"}", keep);
+      } else {
+        respond(cn, 404, "Not Found", "{\"error\":\"route served by the API server\"}", keep);
+      }
+      pos = he + 4 + clen;
+    }
+    if (pos) cn.in.erase(0, pos);
+  }
+
+  int port_;
+  std::string host_;
+  llmq::ShmRing ring_;
+  int nthreads_;
+  std::atomic<bool> running_{false};
+  std::vector<std::thread> th_;
+  std::vector<int> lfds_;
+  std::atomic<int64_t> accepted_{0}, rejected_full_{0}, bad_{0}, requests_{0}, conns_{0};
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_ingress, m) {
+  m.doc() = "native HTTP ingress for POST /api/v1/messages -> shared request ring";
+  m.attr("TAG_RAW") = TAG_RAW;
+  py::class_<HttpIngress>(m, "HttpIngress")
+      .def(py::init<int, const std::string&, int, const std::string&>(), py::arg("port"), py::arg("ring"),
+           py::arg("threads") = 4, py::arg("host") = "0.0.0.0")
+      .def("start", &HttpIngress::start)
+      .def("stop", &HttpIngress::stop, py::call_guard<py::gil_scoped_release>())
+      .def("stats", &HttpIngress::stats);
+  m.def("scan_message", [](py::bytes b) {
+    std::string s = b;
+    Scan r = scan_message(s.data(), s.size());
+    return py::make_tuple(r.ok, r.id, r.priority, r.user_id);
+  });
+}

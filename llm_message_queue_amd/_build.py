@@ -50,6 +50,13 @@ def _targets() -> Dict[str, dict]:
             flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
             libs=["-lrt"],
         ),
+        "_ingress": dict(
+            compiler="g++",
+            sources=[os.path.join(CSRC, "ingress", "http_ingress.cpp")],
+            deps=[os.path.join(CSRC, "queue", "shm_ring.h")],
+            flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
+            libs=["-lrt"],
+        ),
         "_hipops": dict(
             compiler=os.path.join(ROCM, "bin", "hipcc"),
             sources=[os.path.join(k, "hipops.hip")],

@@ -65,3 +65,7 @@ def telemetry():
 
 def shmring():
     return load("_shmring", autobuild=True)
+
+
+def ingress():
+    return load("_ingress", autobuild=True)

@@ -18,6 +18,7 @@ Behaviour notes vs the reference:
 """
 from __future__ import annotations
 
+import asyncio
 import dataclasses
 import json
 import time
@@ -90,12 +91,14 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         m.created_at = m.updated_at = now
         return m
 
-    def _enqueue(m: Message) -> Optional[JSONResponse]:
+    async def _enqueue(m: Message) -> Optional[JSONResponse]:
         if G.cfg.queue.enable_metrics:
             m.metadata["analysis"] = json.dumps(G.preprocessor.analyze_message_content(m.content),
                                                 separators=(",", ":"))
         try:
-            err = G.submit(m)
+            # await the micro-batch (GPU preprocess + queue push) without
+            # blocking the event loop: concurrent requests share one batch
+            err = await asyncio.wait_for(asyncio.wrap_future(G.submit_future(m)), timeout=30.0)
         except Exception as e:
             return _err(500, f"Failed to queue message: {e}")
         if err is not None:
@@ -108,7 +111,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             m = _bind_message(await _json(request))
         except (ValueError, PriorityParseError, TypeError) as e:
             return _err(400, f"Invalid message format: {e}")
-        bad = _enqueue(m)
+        bad = await _enqueue(m)
         if bad is not None:
             return bad
         if m.conversation_id:
@@ -226,7 +229,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             G.state.add_message(cid, m)
         except ConversationNotFound:
             return _err(500, "Failed to add message to conversation")
-        bad = _enqueue(m)
+        bad = await _enqueue(m)
         if bad is not None:
             return bad
         return JSONResponse({"message_id": m.id, "conversation_id": cid, "priority": int(m.priority),

@@ -43,6 +43,26 @@ def _build_engine(cfg, model: str, device):
                          token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank), page
 
 
+def cmd_native_ingress(a) -> int:
+    """``api-gateway --native``: the C++ HTTP ingress for POST /api/v1/messages
+    feeding the shared request ring (no Python request handling at all)."""
+    from ..gateway.native_ingress import NativeIngress
+    cfg = _load_cfg(a.config)
+    port = a.port or cfg.server.port
+    ing = NativeIngress(port, a.ring or cfg.server.shared_ring, a.ingress_threads, a.host or cfg.server.host)
+    port = ing.start()
+    print(json.dumps({"event": "listening", "host": a.host or cfg.server.host, "port": port, "role": "native-ingress",
+                      "ring": ing.ring, "threads": a.ingress_threads}), flush=True)
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, lambda *_: stop.set())
+    while not stop.is_set():
+        stop.wait(0.5)
+    print(json.dumps({"event": "stopped", **ing.stats()}), flush=True)
+    ing.stop()
+    return 0
+
+
 def cmd_serve(a, role: str = "serve") -> int:
     import torch
     from ..balancer.load_balancer import Endpoint
@@ -183,6 +203,8 @@ def main(argv=None) -> int:
         p.add_argument("--no-gpu", action="store_true")
         p.add_argument("--ring", default="", help="shared request ring name (api-gateway/queue-manager)")
         p.add_argument("--no-ring", action="store_true", help="api-gateway/queue-manager without the shared ring")
+        p.add_argument("--native", action="store_true", help="api-gateway: C++ HTTP ingress for POST /messages")
+        p.add_argument("--ingress-threads", type=int, default=4)
     p = sub.add_parser("scheduler")
     p.add_argument("--config", default=None)
     p.add_argument("--gateway", default="http://127.0.0.1:8080")
@@ -194,7 +216,7 @@ def main(argv=None) -> int:
     if a.cmd in ("serve", "server"):
         return cmd_serve(a, "serve")
     if a.cmd == "api-gateway":
-        return cmd_serve(a, "api-gateway")
+        return cmd_native_ingress(a) if a.native else cmd_serve(a, "api-gateway")
     if a.cmd == "queue-manager":
         return cmd_serve(a, "queue-manager")
     if a.cmd == "scheduler":

@@ -200,9 +200,15 @@ class GatewayApp:
 
     def submit(self, msg: Message, timeout_s: float = 30.0) -> Optional[QueueError]:
         """Preprocess (micro-batched on the GPU) and enqueue one message."""
+        return self.submit_future(msg).result(timeout=timeout_s)
+
+    def submit_future(self, msg: Message):
+        """Non-blocking ``submit``: a concurrent Future of the queue error
+        (None on success).  HTTP handlers await it instead of blocking the
+        event loop for the micro-batch window."""
         if not msg.arrival_ns:
             msg.arrival_ns = time.monotonic_ns()
-        return self.batcher.submit(msg).result(timeout=timeout_s)
+        return self.batcher.submit(msg)
 
     def estimated_wait_ns(self, msg: Message) -> int:
         """Requests ahead of this one / observed dispatch rate (reference:
@@ -265,17 +271,35 @@ class GatewayApp:
 
     # ------------------------------------------------------------------ shared rings
     def _ring_loop(self) -> None:
-        """Dispatcher: drain the request ring into the local queue."""
+        """Dispatcher: drain the request ring into the local queue.  Records
+        from a Python ingress are already preprocessed; RAW records from the
+        native HTTP ingress are preprocessed here in one batch per drain."""
+        from .shm_bridge import TAG_RAW, decode_message, decode_raw
         while not self._stop.is_set():
-            msgs = self.ring.get_messages(self.cfg.preprocessor.max_batch, timeout_ms=100)
-            if not msgs:
+            recs = self.ring.get_records(self.cfg.preprocessor.max_batch, timeout_ms=100)
+            if not recs:
                 continue
-            for m in msgs:
+            now = time.time_ns()
+            ready, raw, bad = [], [], []
+            for tag, b in recs:
+                if tag == TAG_RAW:
+                    try:
+                        m = decode_raw(b)
+                    except Exception:
+                        continue                  # the ingress validated the JSON; drop garbage
+                    m.created_at = m.updated_at = now
+                    raw.append(m)
+                else:
+                    ready.append(decode_message(b))
+            if raw:
+                self.preprocessor.process_batch(raw, use_gpu=self.preprocessor.gpu_enabled(),
+                                                prompt_cap=self.gateway.prompt_cap)
+                ready.extend(raw)
+            for m in ready:
                 if not m.queue_name:
                     m.queue_name = priority_name(m.priority)
-            errs = self.standard.push_routed(msgs)
-            bad = []
-            for m, e in zip(msgs, errs):
+            errs = self.standard.push_routed(ready)
+            for m, e in zip(ready, errs):
                 if e is None:
                     self.messages.put(m)
                 else:

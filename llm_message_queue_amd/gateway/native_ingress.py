@@ -1,0 +1,27 @@
+"""Native HTTP ingress (``csrc/ingress/http_ingress.cpp``) for the hot route
+``POST /api/v1/messages``: C++ epoll threads accept, validate and ack
+requests and push the raw bodies into the shared request ring that the GPU
+dispatcher (``cli queue-manager``) drains and preprocesses in batches.
+Other routes stay on the Python API server (``cli serve`` / ``api-gateway``).
+"""
+from __future__ import annotations
+
+from .. import _native
+
+
+class NativeIngress:
+    def __init__(self, port: int = 8080, ring: str = "default", threads: int = 4, host: str = "0.0.0.0"):
+        self.ring = ring
+        self._k = _native.ingress().HttpIngress(int(port), f"llmq-{ring}-req", int(threads), host)
+        self.port = int(port)
+
+    def start(self) -> int:
+        """Start listening; returns the bound port (useful with port 0)."""
+        self.port = self._k.start()
+        return self.port
+
+    def stop(self) -> None:
+        self._k.stop()
+
+    def stats(self) -> dict:
+        return dict(self._k.stats())

@@ -24,8 +24,9 @@ import numpy as np
 from .. import _native
 from ..models.message import Message
 
-TAG_MESSAGE = 1
-TAG_EVENT = 2
+TAG_MESSAGE = 1          # preprocessed Message (msgpack), from a Python ingress
+TAG_EVENT = 2            # status event back to the ingress
+TAG_RAW = 3              # raw JSON body from the native HTTP ingress (not yet preprocessed)
 
 _FIELDS = ("id", "conversation_id", "user_id", "content", "priority", "status", "queue_name",
            "retry_count", "max_retries", "timeout", "created_at", "updated_at", "scheduled_at",
@@ -48,6 +49,20 @@ def decode_message(b: bytes) -> Message:
         m.metadata = {}
     p = rec[len(_FIELDS)]
     m.prompt_ids = None if p is None else np.frombuffer(p, dtype=np.uint32).copy()
+    return m
+
+
+def decode_raw(b: bytes) -> Message:
+    """TAG_RAW record of the native ingress: [u64 arrival monotonic ns][36 B
+    id][u32 body length][JSON body].  Raises ValueError on a bad body."""
+    import json
+    arrival = int.from_bytes(b[0:8], "little", signed=True)
+    mid = b[8:44].rstrip(b"\x00").decode()
+    n = int.from_bytes(b[44:48], "little")
+    body = json.loads(b[48:48 + n])
+    m = Message.from_dict(body)
+    m.id = mid
+    m.arrival_ns = arrival
     return m
 
 
@@ -82,6 +97,10 @@ class RingPair:
     # dispatcher side
     def get_messages(self, max_n: int = 4096, timeout_ms: int = 0) -> List[Message]:
         return [decode_message(b) for _, b in self.requests.pop(max_n, timeout_ms)]
+
+    def get_records(self, max_n: int = 4096, timeout_ms: int = 0):
+        """[(tag, payload)]: TAG_MESSAGE records and TAG_RAW records."""
+        return self.requests.pop(max_n, timeout_ms)
 
     def put_events(self, msgs: Iterable[Message], error: str = "") -> int:
         recs = [encode_event(m, error) for m in msgs]

@@ -1,0 +1,99 @@
+"""Native C++ HTTP ingress -> shared request ring -> dispatcher (preprocess,
+queue, CPU workers) end to end, plus the ingress's HTTP/JSON edge cases."""
+import json
+import os
+import socket
+import time
+import urllib.request
+
+import pytest
+
+from llm_message_queue_amd import _native
+from llm_message_queue_amd.gateway.native_ingress import NativeIngress
+from llm_message_queue_amd.gateway.shm_bridge import RingPair
+
+
+def _post(port, body, raw=False):
+    data = body if raw else json.dumps(body).encode()
+    req = urllib.request.Request(f"http://127.0.0.1:{port}/api/v1/messages", data=data, method="POST",
+                                 headers={"Content-Type": "application/json"})
+    try:
+        with urllib.request.urlopen(req, timeout=5) as r:
+            return r.status, json.loads(r.read())
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read())
+
+
+def test_json_scanner():
+    scan = _native.ingress().scan_message
+    assert scan(b'{"content":"hi","priority":"urgent","id":"abc"}') == (True, "abc", 2, "")
+    assert scan(b'{"content":"a\\"b","metadata":{"x":[1,{"y":null}]},"priority":4,"user_id":"u"}')[0:3:2] == (True, 4)
+    assert scan(b'{}') == (True, "", 0, "")
+    for bad in (b'', b'[1]', b'{"content":}', b'{"priority":"bogus"}', b'{"a":1,}', b'{"a":1} x', b'{"priority":9}'):
+        assert not scan(bad)[0], bad
+
+
+@pytest.fixture
+def stack():
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    from llm_message_queue_amd.utils.config import default_config
+    cfg = default_config()
+    cfg.queue.worker.process_interval = 5_000_000
+    name = f"pyt-native-{os.getpid()}"
+    ring = RingPair(name, 1 << 20, "create")
+    disp = GatewayApp(cfg, use_gpu=False, simulate_ms=(1, 1, 1, 1), role="dispatcher", ring=ring)
+    ing = NativeIngress(0, name, threads=2, host="127.0.0.1")
+    port = ing.start()
+    yield disp, ing, port
+    ing.stop()
+    disp.stop()
+    ring.close(unlink=True)
+
+
+def test_native_ingress_end_to_end(stack):
+    disp, ing, port = stack
+    ids = []
+    for i in range(30):
+        body = {"content": ("EMERGENCY now " if i % 5 == 0 else "hello ") + str(i), "user_id": f"u{i}"}
+        if i % 7 == 0:
+            body["priority"] = "low"
+        code, r = _post(port, body)
+        assert code == 202 and len(r["message_id"]) == 36, r
+        ids.append(r["message_id"])
+    code, r = _post(port, {"content": "mine", "id": "client-id-1"})
+    assert code == 202 and r["message_id"] == "client-id-1"
+    ids.append("client-id-1")
+    t0 = time.time()
+    while time.time() - t0 < 10 and not all((disp.messages.get(i) and disp.messages.get(i).status == "completed")
+                                            for i in ids):
+        time.sleep(0.02)
+    got = [disp.messages.get(i) for i in ids]
+    assert all(g is not None and g.status == "completed" for g in got)
+    assert got[5].priority == 1 and got[5].metadata.get("analyzed")        # preprocessed in the dispatcher
+    assert got[7].priority == 4 and got[0].arrival_ns > 0
+    assert ing.stats()["accepted"] == 31
+
+
+def test_native_ingress_http_edges(stack):
+    _, ing, port = stack
+    assert _post(port, b'{"content": "x",', raw=True)[0] == 400
+    with urllib.request.urlopen(f"http://127.0.0.1:{port}/health", timeout=5) as r:
+        assert r.status == 200 and json.loads(r.read())["status"] == "ok"
+    try:
+        urllib.request.urlopen(f"http://127.0.0.1:{port}/api/v1/queues/stats", timeout=5)
+        assert False
+    except urllib.error.HTTPError as e:
+        assert e.code == 404
+    # keep-alive + pipelining: two requests in one write, two responses in order
+    b1 = json.dumps({"content": "one"}).encode()
+    b2 = json.dumps({"content": "two", "priority": 2}).encode()
+    req = b"".join(b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n%s" % (len(b), b)
+                   for b in (b1, b2))
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(req)
+    data = b""
+    t0 = time.time()
+    while data.count(b"HTTP/1.1 202") < 2 and time.time() - t0 < 5:
+        data += s.recv(65536)
+    s.close()
+    assert data.count(b"HTTP/1.1 202") == 2 and b'"priority":2' in data
