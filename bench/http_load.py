@@ -109,6 +109,7 @@ def main() -> None:
     ap.add_argument("--procs", type=int, default=2, help="client processes")
     a = ap.parse_args()
     procs, urls = [], []
+    api_url = ""
     env = dict(os.environ, PYTHONUNBUFFERED="1", LLMQ_LOGGING__LEVEL="warning",
                LLMQ_QUEUE__WORKER__MAX_CONCURRENT="512", LLMQ_QUEUE__WORKER__MAX_BATCH_SIZE="256",
                LLMQ_QUEUE__WORKER__PROCESS_INTERVAL="5ms")
@@ -136,8 +137,11 @@ def main() -> None:
                 urls.append(f"http://127.0.0.1:{port}")
         elif a.spawn == "native":
             ring = f"httpload{os.getpid()}"
+            api_port = _port()
+            api_url = f"http://127.0.0.1:{api_port}"
             procs.append(subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "queue-manager",
-                                           "--ring", ring, "--port", str(_port())] + gpu, cwd=ROOT, env=env,
+                                           "--ring", ring, "--port", str(api_port), "--host", "127.0.0.1"] + gpu,
+                                          cwd=ROOT, env=env,
                                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                           start_new_session=True))
             port = _port()
@@ -149,8 +153,8 @@ def main() -> None:
             urls = [f"http://127.0.0.1:{port}"]
         else:
             urls = [a.url or "http://127.0.0.1:8080"]
-        for u in urls:
-            if not _wait_up(u):
+        for u in urls + ([api_url] if api_url else []):
+            if not _wait_up(u, timeout=300):
                 raise SystemExit(f"server {u} did not come up")
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
@@ -169,13 +173,20 @@ def main() -> None:
             for k, v in r["codes"].items():
                 codes[str(k)] = codes.get(str(k), 0) + v
         sent = sum(r["sent"] for r in res)
+        dispatcher = None
+        if api_url:                              # what the GPU/CPU dispatcher behind the ring did
+            import urllib.request
+            time.sleep(2.0)
+            with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as r:
+                st = json.loads(r.read())
+            dispatcher = {"dispatch": st.get("dispatch"), "latency": st.get("latency"), "rings": st.get("rings")}
         ok = codes.get("202", 0)
         pct = lambda q_: lat[min(len(lat) - 1, int(q_ * len(lat)))] * 1e3 if lat else 0.0   # noqa: E731
         print(json.dumps({"mode": a.spawn or "url", "ingress_procs": len(urls), "offered_rps": a.rate,
                           "sent": sent, "accepted_rps": round(ok / a.duration, 1),
                           "error_rate": round(1 - ok / max(1, sent), 4), "codes": codes,
                           "p50_ms": round(pct(0.5), 2), "p99_ms": round(pct(0.99), 2),
-                          "wall_s": round(wall, 1)}))
+                          "wall_s": round(wall, 1), "dispatcher": dispatcher}))
     finally:
         for p in procs:
             try:

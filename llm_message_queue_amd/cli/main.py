@@ -103,7 +103,9 @@ def cmd_serve(a, role: str = "serve") -> int:
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
-    if rank == 0 and role in ("serve", "api-gateway"):
+    if rank == 0 and role in ("serve", "api-gateway", "queue-manager"):
+        # queue-manager serves the full API too: with a native ingress in
+        # front, status / conversation / admin routes live with the dispatcher
         import uvicorn
         from ..api.server import create_app
         app = create_app(gapp)
