@@ -106,7 +106,10 @@ def main() -> None:
     ap.add_argument("--gpu", action="store_true", help="spawned server uses the GPU")
     ap.add_argument("--rate", type=float, default=1000.0, help="offered requests/s (total)")
     ap.add_argument("--duration", type=float, default=10.0)
-    ap.add_argument("--procs", type=int, default=2, help="client processes")
+    ap.add_argument("--procs", type=int, default=2, help="client processes (python client) / threads (native)")
+    ap.add_argument("--client", choices=["python", "native"], default="python",
+                    help="native = csrc/tools/http_bench.cpp (open-loop, keep-alive, no coordinated omission)")
+    ap.add_argument("--conns", type=int, default=16, help="native client: connections per thread")
     a = ap.parse_args()
     procs, urls = [], []
     api_url = ""
@@ -156,6 +159,24 @@ def main() -> None:
         for u in urls + ([api_url] if api_url else []):
             if not _wait_up(u, timeout=300):
                 raise SystemExit(f"server {u} did not come up")
+        if a.client == "native":
+            exe = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"llmq_http_bench_{os.getpid()}")
+            subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", os.path.join(ROOT, "csrc", "tools", "http_bench.cpp"),
+                            "-o", exe], check=True)
+            host, port = urls[0].split("//")[1].split(":")
+            r = subprocess.run([exe, host, port, str(a.rate), str(a.duration), str(a.procs), str(a.conns)],
+                               capture_output=True, text=True, timeout=a.duration + 60)
+            os.unlink(exe)
+            out = json.loads(r.stdout.strip().splitlines()[-1])
+            if api_url:
+                import urllib.request
+                time.sleep(2.0)
+                with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
+                    st = json.loads(rr.read())
+                out["dispatcher"] = {"dispatch": st.get("dispatch"), "latency": st.get("latency")}
+            out["mode"] = a.spawn or "url"
+            print(json.dumps(out))
+            return
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         cs = [ctx.Process(target=_client_proc, args=(urls, a.rate / a.procs, a.duration, 17 + i, q))
