@@ -73,7 +73,7 @@ static void embed_pool(uintptr_t hashes, int L, uintptr_t row_off, int B, int ro
   require(H % EP_NCHUNK == 0, "hidden dim must be a multiple of 256");
   require(B >= 0 && rows_upper >= 0, "bad sizes");
   if (B == 0 || rows_upper == 0) return;
-  const size_t smem = EP_TM * EP_D * 2 + EP_TM * EP_NCHUNK * 4 + 2 * EP_TM * 4 + 16;
+  const size_t smem = EP_TM * EP_D * 2 + EP_TM * EP_HS_STRIDE * 4 + 2 * EP_TM * 4 + 16;
   if (!g_embed_attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)embed_pool_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
