@@ -276,6 +276,24 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         return {"queues": tiers, "total_pending": G.standard.total_pending(), "latency": lat,
                 "dead_letter": G.factory.dead_letter_queue.size(), "delayed": G.factory.delayed_queue.size()}
 
+    @app.get("/api/v1/metrics")
+    def metrics_json():
+        """JSON metrics summary (doc-only in the reference, docs/api.md:647-698:
+        requests/s, average response time, error rate, queue lengths)."""
+        c = G.gateway.counters
+        done = G.gateway.rec_done.summary()
+        failed = sum(G.standard.get_queue_stats(n).failed_count for n in G.gateway.tiers)
+        completed = sum(G.standard.get_queue_stats(n).completed_count for n in G.gateway.tiers)
+        return {"requests_total": G.messages_seen() + c["submitted"], "dispatched_total": c["dispatched"],
+                "completed_total": completed, "failed_total": failed,
+                "requests_per_second": round(G._dispatch_rate(), 2),
+                "error_rate": round(failed / max(1, completed + failed), 6),
+                "latency": {"dispatch": G.gateway.rec.summary(), "end_to_end": done},
+                "queue_lengths": {n: G.standard.size(n) for n in G.gateway.tiers},
+                "dead_letter": G.factory.dead_letter_queue.size(), "delayed": G.factory.delayed_queue.size(),
+                "gpu": {"healthy": G.gateway.healthy, "reason": G.gateway.health_reason,
+                        "inflight_slots": G.engine.inflight() if G.engine is not None else 0}}
+
     # ------------------------------------------------------------------ resources
     @app.post("/api/v1/resources")
     async def register_resource(request: Request):

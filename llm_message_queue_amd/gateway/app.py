@@ -90,6 +90,7 @@ class GatewayApp:
         self._ring_thread: Optional[threading.Thread] = None
         self._snap_thread: Optional[threading.Thread] = None
         self.telemetry = None
+        self._accepted = 0
         self.cfg = cfg
         self.log = get_logger("app")
         self.metrics: QueueMetrics = default_metrics()
@@ -195,6 +196,7 @@ class GatewayApp:
         for m, e in zip(msgs, errs):
             if e is None:
                 self.messages.put(m)
+                self._accepted += 1
         self._wake.set()
         return errs
 
@@ -209,6 +211,10 @@ class GatewayApp:
         if not msg.arrival_ns:
             msg.arrival_ns = time.monotonic_ns()
         return self.batcher.submit(msg)
+
+    def messages_seen(self) -> int:
+        """Messages accepted through this app's ingress (micro-batcher)."""
+        return self._accepted
 
     def estimated_wait_ns(self, msg: Message) -> int:
         """Requests ahead of this one / observed dispatch rate (reference:
@@ -302,6 +308,7 @@ class GatewayApp:
             for m, e in zip(ready, errs):
                 if e is None:
                     self.messages.put(m)
+                    self._accepted += 1
                 else:
                     m.status = MessageStatus.FAILED
                     bad.append(m)

@@ -159,3 +159,14 @@ def test_cors(client):
 def test_config_endpoint_redacts(client):
     d = client.get("/api/v1/config").json()
     assert d["database"]["postgres"]["password"] == "***" and d["queue"]["levels"][0]["name"] == "realtime"
+
+
+def test_json_metrics_summary(client):
+    for i in range(3):
+        assert client.post("/api/v1/messages", json={"content": f"metrics json {i}"}).status_code == 202
+    r = client.get("/api/v1/metrics")
+    assert r.status_code == 200
+    d = r.json()
+    assert d["requests_total"] >= 3 and "requests_per_second" in d and 0.0 <= d["error_rate"] <= 1.0
+    assert set(d["queue_lengths"]) == {"realtime", "high", "normal", "low"}
+    assert "dispatch" in d["latency"] and "end_to_end" in d["latency"]
