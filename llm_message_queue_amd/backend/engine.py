@@ -50,6 +50,9 @@ class Request:
     meta: object = None
     out_idx: int = -1             # row of the previous step's output holding my last token
     out_step: int = -1
+    conv: int = -1                # conversation key: its KV stays resident in the slot between turns
+    reused: int = 0               # context tokens served from the resident KV (not re-prefilled)
+    history: Optional[np.ndarray] = None   # earlier dialog tokens, prefilled only if not resident
 
 
 @dataclass
@@ -92,6 +95,17 @@ class BackendEngine:
         self.impl = impl
         self.active: Dict[int, Request] = {}            # slot -> request
         self.free: List[int] = list(range(slots - 1, -1, -1))
+        # Conversation KV residency (BASELINE config 4): when a request of a
+        # conversation completes, its slot keeps the KV of the dialog so far
+        # (prompt + generated tokens except the last) and parks in an LRU;
+        # the conversation's next turn is admitted into that slot and only
+        # prefills its new tokens.  Parked slots count as free: they are
+        # evicted (LRU) when no truly free slot is left.
+        self.conv_lru: "collections.OrderedDict[int, int]" = collections.OrderedDict()
+        self.s_conv = np.full(slots, -1, dtype=np.int64)
+        self.s_cached = np.zeros(slots, dtype=np.int64)
+        self.kv_reused_tokens = 0
+        self.kv_evictions = 0
         # per-slot host state (the batch builder is vectorised over these)
         self.s_prompt = np.zeros((slots, max_ctx), dtype=np.int32)
         self.s_plen = np.zeros(slots, dtype=np.int64)
@@ -139,10 +153,23 @@ class BackendEngine:
 
     # ------------------------------------------------------------------ admission
     def free_slots(self) -> int:
-        return len(self.free)
+        return len(self.free) + len(self.conv_lru)
 
     def inflight(self) -> int:
-        return self.slots - len(self.free)
+        return self.slots - self.free_slots()
+
+    def _take_slot(self) -> int:
+        if self.free:
+            return self.free.pop()
+        conv, s = self.conv_lru.popitem(last=False)          # evict the least recently used context
+        self.s_conv[s] = -1
+        self.kv_evictions += 1
+        return s
+
+    def resident_context(self, conv: int) -> int:
+        """Tokens of conversation ``conv`` resident in this engine's KV (0 if none)."""
+        s = self.conv_lru.get(conv)
+        return int(self.s_cached[s]) if s is not None else 0
 
     def admit_capacity(self) -> int:
         """How many new requests the NEXT step can take: free slots, bounded
@@ -151,7 +178,7 @@ class BackendEngine:
         prompt length.  The dispatcher admits at most this many, so requests
         that could not start prefilling next step wait in the priority queue
         (where tier order and aging apply), not in a FIFO inside the engine."""
-        free = len(self.free)
+        free = len(self.free) + len(self.conv_lru)
         if free == 0:
             return 0
         act = self.s_active
@@ -169,7 +196,7 @@ class BackendEngine:
         out = []
         cap = self.max_ctx - 1
         for r in reqs:
-            if not self.free:
+            if not self.free and not self.conv_lru:
                 break
             if r.gen_tokens < 1:
                 r.gen_tokens = 1
@@ -177,21 +204,38 @@ class BackendEngine:
             r.prompt = np.asarray(r.prompt[:plen], dtype=np.int64) % self.cfg.vocab
             if len(r.prompt) == 0:
                 r.prompt = np.zeros(1, dtype=np.int64)
-            s = r.slot = self.free.pop()
+            base = 0
+            s = self.conv_lru.pop(r.conv, None) if r.conv >= 0 else None
+            if s is not None:
+                base = int(self.s_cached[s])
+                if base + len(r.prompt) + r.gen_tokens > cap + 1:
+                    base = 0                                  # context window full: restart the dialog KV
+            else:
+                s = self._take_slot()
+            if base == 0 and r.history is not None and len(r.history):
+                # not resident here: replay the dialog (most recent tokens that fit)
+                room = cap + 1 - r.gen_tokens - len(r.prompt)
+                if room > 0:
+                    h = np.asarray(r.history[-room:], dtype=np.int64) % self.cfg.vocab
+                    r.prompt = np.concatenate([h, r.prompt])
+            r.slot = s
+            r.reused = base
             r.prefilled = 0
             r.generated = 0
             r.out_idx = r.out_step = -1
             r.admitted_ns = now
             self.active[s] = r
             n = len(r.prompt)
-            self.s_prompt[s, :n] = r.prompt
-            self.s_plen[s] = n
-            self.s_pref[s] = 0
+            self.s_prompt[s, base:base + n] = r.prompt
+            self.s_plen[s] = base + n
+            self.s_pref[s] = base
             self.s_gen[s] = 0
             self.s_gmax[s] = r.gen_tokens
             self.s_seq[s] = self._admit_seq
             self._admit_seq += 1
             self.s_active[s] = True
+            self.s_conv[s] = r.conv
+            self.kv_reused_tokens += base
             self._mean_plen += 0.01 * (n - self._mean_plen)
             out.append(r)
         return out
@@ -283,6 +327,8 @@ class BackendEngine:
         self._prev_out = None
         self.active.clear()
         self.s_active[:] = False
+        self.conv_lru.clear()
+        self.s_conv[:] = -1
         self.free = list(range(self.slots - 1, -1, -1))
         return out
 
@@ -364,10 +410,20 @@ class BackendEngine:
         completed = []
         for x in done.tolist():
             r = self.active.pop(x)
-            r.prefilled = int(self.s_plen[x])
+            r.prefilled = int(self.s_plen[x]) - r.reused
             r.generated = int(self.s_gen[x])
             completed.append(r)
-            self.free.append(x)
+            if r.conv >= 0:
+                # park the dialog KV: every position but the last sampled token
+                self.s_cached[x] = self.s_plen[x] + self.s_gen[x] - 1
+                old = self.conv_lru.pop(r.conv, None)
+                if old is not None and old != x:           # a stale copy elsewhere: free it
+                    self.s_conv[old] = -1
+                    self.free.append(old)
+                self.conv_lru[r.conv] = x
+            else:
+                self.s_conv[x] = -1
+                self.free.append(x)
         self.s_active[done] = False
         self._prev_out = out
         self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out, t_mono))

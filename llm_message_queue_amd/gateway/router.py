@@ -97,7 +97,15 @@ class LatencyRecorder:
 
 # --------------------------------------------------------------------------- descriptors
 K_DISPATCH, K_DONE, K_FAIL = 1, 2, 3     # K_FAIL: an evacuating backend hands a request back
-DESC_HDR = 12
+DESC_HDR = 14       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, -, conv lo/hi]
+
+
+def conv_key(conversation_id: str) -> int:
+    """63-bit key of a conversation id (KV residency / affinity)."""
+    if not conversation_id:
+        return -1
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(conversation_id.encode(), digest_size=8).digest(), "little") >> 1
 
 
 def _split64(a: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
@@ -166,6 +174,14 @@ class Gateway:
         self.on_complete = None     # optional callback(msg)
         self.tracer = None          # optional utils.tracing.RequestTracer
         self.rec_done = LatencyRecorder(len(self.tiers))   # arrival -> completion (end to end)
+        # conversation KV residency: turns of a dialog go to the GPU that holds
+        # its KV (conv_home) and prefill only their new tokens there
+        import collections
+        self.kv_residency = True
+        self.conv_home: "collections.OrderedDict[str, int]" = collections.OrderedDict()
+        self.conv_hist: "collections.OrderedDict[str, np.ndarray]" = collections.OrderedDict()
+        self.max_dialogs = 200_000
+        self.history_cap = int(getattr(cfg.backend, "max_ctx", 512))
         self._done_buf: List[Tuple[int, int, int]] = []
         self._last_ingest_ns = 0
         self.host_ns = np.zeros(5, dtype=np.int64)   # per-phase host time (host_profile)
@@ -235,7 +251,31 @@ class Gateway:
         prompt = m.prompt_ids if m.prompt_ids is not None else np.zeros(1, dtype=np.uint32)
         p = np.asarray(prompt, dtype=np.uint32).astype(np.int64).astype(np.int32) \
             if len(prompt) else np.zeros(1, dtype=np.int32)
-        return Request(req_id=m.handle, prompt=p, gen_tokens=self.gen_tokens, tier=tier, meta=m)
+        ck = conv_key(m.conversation_id) if self.kv_residency else -1
+        hist = self.conv_hist.get(m.conversation_id) if m.conversation_id else None
+        return Request(req_id=m.handle, prompt=p, gen_tokens=self.gen_tokens, tier=tier, meta=m, conv=ck,
+                       history=hist)
+
+    def _remember_dialog(self, m: Message, gpu: int) -> None:
+        """Completion of a conversation turn: its home GPU (KV residency) and
+        the dialog tokens a non-resident replay needs (prompt + generated;
+        generated ids stay on the device, placeholders stand in for them --
+        the cost, not the values, is what a replay pays)."""
+        cid = m.conversation_id
+        if not cid:
+            return
+        self.conv_home[cid] = gpu
+        self.conv_home.move_to_end(cid)
+        p = np.asarray(m.prompt_ids if m.prompt_ids is not None else [], dtype=np.uint32).astype(np.int32)
+        h = self.conv_hist.get(cid)
+        add = np.concatenate([p, np.zeros(max(0, self.gen_tokens - 1), dtype=np.int32)])
+        h = add if h is None else np.concatenate([h, add])[-self.history_cap:]
+        self.conv_hist[cid] = h
+        self.conv_hist.move_to_end(cid)
+        while len(self.conv_home) > self.max_dialogs:
+            self.conv_home.popitem(last=False)
+        while len(self.conv_hist) > self.max_dialogs:
+            self.conv_hist.popitem(last=False)
 
     def _record(self, tiers, arrival, enq, now):
         tiers = np.asarray(tiers, dtype=np.int64)
@@ -396,6 +436,10 @@ class Gateway:
         h = m.metadata.get("home_gpu") if m.metadata else None
         if h is None and self.state_manager is not None and m.conversation_id:
             h = self.state_manager.home_gpu(m.conversation_id)
+            if h is not None and h < 0:
+                h = None
+        if h is None and m.conversation_id:
+            h = self.conv_home.get(m.conversation_id)
         h = -1 if h is None else int(h)
         if effective and (h in self.unhealthy_peers or (h == self.rank and not self.healthy)):
             return -1
@@ -411,6 +455,8 @@ class Gateway:
         row[9] = self.gen_tokens
         p = np.asarray(m.prompt_ids if m.prompt_ids is not None else [], dtype=np.uint32)[:cap]
         row[10] = len(p)
+        ck = conv_key(m.conversation_id) if self.kv_residency else -1
+        row[12], row[13] = _split64(np.array([ck]))[0][0], _split64(np.array([ck]))[1][0]
         row[DESC_HDR:DESC_HDR + len(p)] = p.view(np.int32)
 
     def _foreign_request(self, row: np.ndarray, cap: int) -> Request:
@@ -419,9 +465,10 @@ class Gateway:
         enq = int(_join64(row[7:8], row[8:9])[0])
         origin, tier, gen, plen = int(row[3]), int(row[4]), int(row[9]), int(row[10])
         prompt = row[DESC_HDR:DESC_HDR + max(1, plen)].copy()
+        ck = int(_join64(row[12:13], row[13:14])[0])
         self._next_req += 1
         return Request(req_id=self._next_req, prompt=prompt, gen_tokens=gen, tier=tier,
-                       meta=(origin, handle, tier, arrival, enq))
+                       meta=(origin, handle, tier, arrival, enq), conv=ck)
 
     def _remote_fail(self, row: np.ndarray) -> None:
         """The backend my request was sent to evacuated it: queue it again."""
@@ -482,6 +529,7 @@ class Gateway:
         self.inflight_by_tier[m.tier] -= 1
         adm = int(_join64(row[5:6], row[6:7])[0])
         done = int(_join64(row[7:8], row[8:9])[0])
+        self._remember_dialog(m, int(row[3]))
         self._complete(m, done - adm)
 
     # ------------------------------------------------------------------ backend step
@@ -518,6 +566,7 @@ class Gateway:
                 self.local.pop(m.handle, None)
                 if 0 <= r.tier < len(self.inflight_by_tier):
                     self.inflight_by_tier[r.tier] -= 1
+                self._remember_dialog(m, self.rank)
                 self._complete(m, r.done_ns - r.admitted_ns)
             else:
                 origin, handle, tier = self.foreign.pop(r.req_id)

@@ -361,3 +361,72 @@ def test_request_tracer_chrome_trace(tmp_path):
     steps = [e for e in ev if e.get("name", "").startswith("step ")]
     assert len(served) == 10 and steps and all(e["dur"] >= 0 for e in served + steps)
     assert {e["tid"] for e in served} <= {1, 2, 3, 4}
+
+
+# ---------------------------------------------------------------- conversation KV residency
+def test_conversation_kv_resident_between_turns_matches_full_prefill():
+    """Turn 2 of a dialog admitted into the slot that kept turn 1's KV must
+    produce exactly the KV a fresh prefill of the whole dialog produces
+    (gen_tokens=1: the cached context is exactly the turn-1 prompt)."""
+    from llm_message_queue_amd.backend.engine import Request
+    p1 = np.arange(5, 17, dtype=np.int32)
+    p2 = np.arange(100, 109, dtype=np.int32)
+    a = engine(slots=4, token_budget=64)
+    a.admit([Request(1, p1, gen_tokens=1, conv=77)])
+    a.drain()
+    assert a.resident_context(77) == len(p1) and a.free_slots() == 4      # parked slot counts as free
+    (r2,) = a.admit([Request(2, p2, gen_tokens=1, conv=77)])
+    assert r2.reused == len(p1)
+    a.drain()
+    assert a.kv_reused_tokens == len(p1) and r2.prefilled == len(p2)
+    b = engine(slots=4, token_budget=64)
+    (rb,) = b.admit([Request(3, np.concatenate([p1, p2]), gen_tokens=1)])
+    b.drain()
+    n = len(p1) + len(p2)
+    for L in range(MICRO.layers):
+        assert torch.allclose(a.model.kcache[L][r2.slot, :, :n].float(), b.model.kcache[L][rb.slot, :, :n].float(),
+                              atol=2e-2)
+        assert torch.allclose(a.model.vcache[L][r2.slot, :, :n].float(), b.model.vcache[L][rb.slot, :, :n].float(),
+                              atol=2e-2)
+
+
+def test_conversation_slots_evicted_lru_when_full():
+    from llm_message_queue_amd.backend.engine import Request
+    e = engine(slots=2, token_budget=64)
+    for c in (1, 2):
+        e.admit([Request(c, np.arange(4, dtype=np.int32), gen_tokens=2, conv=c)])
+    e.drain()
+    assert e.resident_context(1) == 5 and e.resident_context(2) == 5
+    e.admit([Request(3, np.arange(4, dtype=np.int32), gen_tokens=2, conv=3)])   # evicts conv 1 (LRU)
+    e.drain()
+    assert e.resident_context(1) == 0 and e.resident_context(2) == 5 and e.kv_evictions == 1
+    # a context that would overflow max_ctx restarts from scratch
+    (r,) = e.admit([Request(4, np.arange(60, dtype=np.int32), gen_tokens=2, conv=2)])
+    assert r.reused == 0
+
+
+@pytest.mark.parametrize("residency", [True, False])
+def test_gateway_dialog_turns_reuse_or_replay(residency):
+    """Turn 2 of a conversation: with KV residency only its new tokens are
+    prefilled (the dialog KV is reused); without it the dialog is replayed."""
+    gw = Gateway(cfg(), engine=engine(slots=8, token_budget=256), use_gpu_preprocess=False, prompt_cap=8,
+                 gen_tokens=3)
+    gw.kv_residency = residency
+    t1 = Workload(seed=9).make(4)
+    for i, m in enumerate(t1):
+        m.conversation_id = f"dlg-{i}"
+    gw.submit(t1)
+    assert run_until_done([gw], 4)
+    tok1 = gw.engine.total_tokens
+    t2 = Workload(seed=10).make(4)
+    for i, m in enumerate(t2):
+        m.conversation_id = f"dlg-{i}"
+    gw.submit(t2)
+    assert run_until_done([gw], 8)
+    tok2 = gw.engine.total_tokens - tok1
+    new_prefill = sum(len(m.prompt_ids) for m in t2) + 4 * (3 - 1)      # prompts + decode steps
+    if residency:
+        assert gw.engine.kv_reused_tokens > 0 and tok2 == new_prefill
+        assert all(gw.conv_home[f"dlg-{i}"] == 0 for i in range(4))
+    else:
+        assert gw.engine.kv_reused_tokens == 0 and tok2 > new_prefill    # dialog replayed
