@@ -184,14 +184,17 @@ def main(argv=None) -> int:
     rate = a.rate if a.rate > 0 else a.util * capacity
     # drain the calibration backlog (untimed)
     gw.drop_pending()
-    for _ in range(64):
-        gw.tick()
-        if engine.inflight() == 0:
-            break
-    busy = comm.all_gather_i64(np.array([engine.inflight()], dtype=np.int64))
+
+    def busy_local():
+        # the stop decision must be GLOBAL: every tick is a collective, so all
+        # ranks have to run the same number of them
+        return (engine.inflight() + len(gw.remote_out) + sum(len(v) for v in gw._done_owed.values())
+                + gw.pending())
+
+    busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
     while busy.max() > 0:
         gw.tick()
-        busy = comm.all_gather_i64(np.array([engine.inflight()], dtype=np.int64))
+        busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
     gw.rec.reset()
     gw.flush_latency()
     gw.rec_done.reset()

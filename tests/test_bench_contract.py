@@ -38,8 +38,8 @@ def test_bench_single_rank_dry_run():
     assert "DRY RUN" in d["data"] and d["value"] > 0 and "gateway_only" in d
 
 
-def test_bench_two_ranks_torchrun_dry_run():
-    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+def test_bench_four_ranks_torchrun_dry_run():
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "4",
               "--cpu-dry-run", "--steps", "5", "--warmup", "2", "--gateway-only-s", "0"])
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["value"] > 0
