@@ -334,10 +334,16 @@ class GatewayApp:
     # ------------------------------------------------------------------ dispatch
     def _serve_loop(self) -> None:
         gw = self.gateway
-        while not self._stop.is_set():
+        while True:
+            if self._stop.is_set():
+                gw.request_stop()
+            if gw.peers_stopping:
+                break
             gw.tick()
             self._dispatch_times.append((time.monotonic(), gw.counters["dispatched"]))
-            if self.engine.inflight() == 0 and gw.pending() == 0:
+            idle = (gw.cluster_idle if gw.world > 1 else
+                    self.engine.inflight() == 0 and gw.pending() == 0)
+            if idle:                      # (multi-rank: only when every rank is idle)
                 self._wake.wait(0.01)
                 self._wake.clear()
 

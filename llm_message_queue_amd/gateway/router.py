@@ -169,6 +169,12 @@ class Gateway:
         # conversations homed on it are re-homed wherever they land next
         self.healthy = True
         self.health_reason = ""
+        # coordinated shutdown: a stopping rank flags it in its load vector and
+        # every rank leaves its serve loop after the same tick (each tick is a
+        # collective, so ranks must stop together)
+        self.stopping = False
+        self.peers_stopping = False
+        self.cluster_idle = False     # every rank idle at the last load exchange
         self._tick_lock = threading.RLock()     # set_healthy from a telemetry thread waits for the tick
         self.unhealthy_peers: set = set()
         self.on_complete = None     # optional callback(msg)
@@ -333,8 +339,13 @@ class Gateway:
         inflight = self.engine.inflight() if self.engine is not None else 0
         done_for = [len(self._done_owed[r]) for r in range(W)]
         load = planner.make_load(free, inflight, depth, age, healthy=self.engine is not None and self.healthy,
-                                 done_for=done_for, pinned=[int(x) for x in self.pinned])
+                                 done_for=done_for, pinned=[int(x) for x in self.pinned], stopping=self.stopping)
         loads = self.comm.all_gather_i64(load)
+        if loads[:, planner.L_STOP].any():
+            self.peers_stopping = True
+        self.cluster_idle = not (loads[:, planner.L_INFLIGHT].any()
+                                 or loads[:, planner.L_DEPTH:planner.L_DEPTH + planner.NTIERS].any()
+                                 or loads[:, planner.L_DONE:planner.L_DONE + W].any())
         self.unhealthy_peers = {i for i in range(W) if loads[i, planner.L_HEALTHY] == 0}
         quota = planner.plan_dispatch(loads, [a // 1000 for a in self.aging_ns])
         # pop exactly my per-tier grant
@@ -662,6 +673,11 @@ class Gateway:
             self.ingest_ns[:] = 0
             self._ticks0 = self.counters["ticks"]
         return out
+
+    def request_stop(self) -> None:
+        self.stopping = True
+        if self.world == 1:
+            self.peers_stopping = True
 
     def pending(self) -> int:
         return self.qm.total_pending()

@@ -30,18 +30,20 @@ L_FREE, L_INFLIGHT = 0, 1
 L_DEPTH = 2          # 4 tiers: 2..5
 L_AGE_US = 6         # 4 tiers: 6..9 (oldest head wait, microseconds)
 L_HBM_USED, L_HBM_TOTAL, L_HEALTHY, L_EPOCH = 10, 11, 12, 13
+L_STOP = 14          # the rank is shutting down: every rank leaves after this same tick
 L_DONE = 16
 NTIERS = 4
 
 
 def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[int], hbm_used_mib: int = 0,
               hbm_total_mib: int = 0, healthy: bool = True, epoch: int = 0,
-              done_for: Sequence[int] = (), pinned: Sequence[int] = ()) -> np.ndarray:
+              done_for: Sequence[int] = (), pinned: Sequence[int] = (), stopping: bool = False) -> np.ndarray:
     v = np.zeros(LOAD_WIDTH, dtype=np.int64)
     v[L_FREE], v[L_INFLIGHT] = free, inflight
     v[L_DEPTH:L_DEPTH + NTIERS] = list(depth)[:NTIERS]
     v[L_AGE_US:L_AGE_US + NTIERS] = list(age_us)[:NTIERS]
     v[L_HBM_USED], v[L_HBM_TOTAL], v[L_HEALTHY], v[L_EPOCH] = hbm_used_mib, hbm_total_mib, int(healthy), epoch
+    v[L_STOP] = int(stopping)
     for r, n in enumerate(done_for):
         v[L_DONE + r] = n
     for j, n in enumerate(pinned):

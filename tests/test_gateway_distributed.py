@@ -430,3 +430,25 @@ def test_gateway_dialog_turns_reuse_or_replay(residency):
         assert all(gw.conv_home[f"dlg-{i}"] == 0 for i in range(4))
     else:
         assert gw.engine.kv_reused_tokens == 0 and tok2 > new_prefill    # dialog replayed
+
+
+def test_coordinated_stop_across_ranks():
+    """One rank stopping makes every rank leave after the same tick (ticks are
+    collectives; a rank-local exit would strand the others)."""
+    comms = FakeComm.make(3)
+    gws = [Gateway(cfg(), engine=engine(slots=4, seed=r), comm=comms[r], use_gpu_preprocess=False, prompt_cap=8,
+                   gen_tokens=2) for r in range(3)]
+    ticks = [0, 0, 0]
+
+    def loop(r):
+        while not gws[r].peers_stopping:
+            if r == 1 and ticks[r] == 5:
+                gws[r].request_stop()
+            gws[r].tick()
+            ticks[r] += 1
+
+    ths = [threading.Thread(target=loop, args=(r,)) for r in range(3)]
+    [t.start() for t in ths]
+    [t.join(timeout=30) for t in ths]
+    assert not any(t.is_alive() for t in ths)
+    assert ticks[0] == ticks[1] == ticks[2] == 6
