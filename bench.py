@@ -36,7 +36,8 @@ import time
 import numpy as np
 
 BASELINE_RPS = 10000.0          # "sustain > 10,000 req/s" (reference docs target)
-P99_TARGET_MS = 500.0           # BASELINE.md operating point
+P99_TARGET_MS = 500.0           # BASELINE.md operating point (all tiers)
+REALTIME_P99_TARGET_MS = 100.0  # BASELINE.md operating point (realtime tier)
 METRIC = "requests/sec + p99 enqueue->dispatch latency, 4-tier mix at 1/2/4/8 backends"
 
 
@@ -82,7 +83,7 @@ def main(argv=None) -> int:
     from llm_message_queue_amd.gateway.router import Gateway, LatencyRecorder
     from llm_message_queue_amd.gateway.workload import PoissonArrivals, Workload
     from llm_message_queue_amd.models.llama_stub import LlamaConfig
-    from llm_message_queue_amd.parallel.comm import init_from_env
+    from llm_message_queue_amd.parallel.comm import init_from_env, local_device_index
     from llm_message_queue_amd.preprocess.preprocessor import Preprocessor
     from llm_message_queue_amd.utils.config import default_config
 
@@ -102,6 +103,7 @@ def main(argv=None) -> int:
         if not torch.cuda.is_available():
             print("bench.py needs a GPU (MI355X)", file=sys.stderr)
             return 2
+        local = local_device_index()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         comm = init_from_env(control=a.control_plane)
@@ -295,7 +297,13 @@ def main(argv=None) -> int:
         "p99_by_tier_ms": [round(x, 3) for x in lat["p99_by_tier_ms"]],
         "requests_by_tier": lat["count_by_tier"],
         "p99_target_ms": P99_TARGET_MS,
-        "p99_target_met": bool(lat_done["p99_ms"] <= P99_TARGET_MS),
+        # BASELINE.md operating point: p99 enqueue->dispatch <= 500 ms over
+        # all tiers and <= 100 ms for the realtime tier (judged on the
+        # stricter arrival->dispatch clock, which adds ingest + preprocess)
+        "p99_target_met": bool(lat["p99_ms"] <= P99_TARGET_MS
+                               and lat["p99_by_tier_ms"][0] <= REALTIME_P99_TARGET_MS),
+        # stricter still: arrival -> last generated token of the 8B backend
+        "p99_e2e_target_met": bool(lat_done["p99_ms"] <= P99_TARGET_MS),
         "offered_rate_per_gpu": round(rate, 2),
         "calibrated_capacity_per_gpu": round(capacity, 2),
         "backend_tokens_per_s": round(tokens / elapsed, 1) if elapsed > 0 else 0.0,

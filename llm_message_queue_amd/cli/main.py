@@ -67,7 +67,7 @@ def cmd_serve(a, role: str = "serve") -> int:
     import torch
     from ..balancer.load_balancer import Endpoint
     from ..gateway.app import GatewayApp
-    from ..parallel.comm import init_from_env
+    from ..parallel.comm import init_from_env, local_device_index
     from ..utils import logging as ulog
 
     cfg = _load_cfg(a.config)
@@ -81,7 +81,7 @@ def cmd_serve(a, role: str = "serve") -> int:
     comm = init_from_env(control=cfg.gpu.control_plane) if use_gpu else None
     engine = page = None
     if use_gpu and role in ("serve", "queue-manager"):
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = local_device_index()
         torch.cuda.set_device(local)
         engine, page = _build_engine(cfg, a.model, torch.device("cuda", local))
     ring, app_role = None, "serve"

@@ -229,6 +229,26 @@ class FakeComm(Comm):
         self.hub.bar.wait()
 
 
+def local_device_index() -> int:
+    """HIP device of this rank: ``LOCAL_RANK`` on a node with one GPU per rank
+    (the production layout).  When more ranks than GPUs share the node
+    (rehearsing a multi-rank job on a 1-GPU box) ranks wrap round the devices;
+    ``init_from_env`` then keeps RCCL out of it (RCCL refuses two ranks on one
+    device) and runs every group on gloo."""
+    import os
+    import torch
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    return local % n if n > 0 else local
+
+
+def gpus_oversubscribed() -> bool:
+    import os
+    import torch
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    return 0 < n < int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+
+
 def init_from_env(backend: Optional[str] = None, control: str = "gloo"):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...).
 
@@ -246,9 +266,14 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo"):
     if not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl" and gpus_oversubscribed():
+            import sys
+            print("comm: more ranks than GPUs on this node -- RCCL needs one device per rank, "
+                  "using gloo for every group (rehearsal layout, not a measurement of xGMI)", file=sys.stderr)
+            backend = control = "gloo"
         kw = {}
         if backend == "nccl":
-            local = int(os.environ.get("LOCAL_RANK", "0"))
+            local = local_device_index()
             torch.cuda.set_device(local)
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend=backend, **kw)
