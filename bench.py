@@ -55,7 +55,7 @@ def parse(argv=None):
     ap.add_argument("--aging-ms", default="50,100,150,200",
                     help="per-tier aging deadlines (realtime,high,normal,low), ms")
     ap.add_argument("--prompt-cap", type=int, default=32)
-    ap.add_argument("--util", type=float, default=0.97)
+    ap.add_argument("--util", type=float, default=0.95)
     ap.add_argument("--tick-ms", type=float, default=0.0, help="minimum serving tick period (0 = dynamic)")
     ap.add_argument("--rate", type=float, default=0.0, help="per-GPU offered req/s (0 = calibrate)")
     ap.add_argument("--no-classifier", action="store_true")
