@@ -15,7 +15,11 @@
 // Response: 202 {"message_id", "priority", "queue_time", "estimated_wait"}
 // where priority is the requested one (0 = to be decided by the
 // preprocessor, which runs asynchronously after the ack); 400 on a malformed
-// body, 503 when the ring is full (back-pressure).
+// body, 503 when the ring is full (back-pressure).  With a Guard attached
+// (guard.h) every request is authenticated (API key / JWT), authorised
+// (RBAC) and rate-limited (global / per IP / per user) inline: 401 / 403 /
+// 429 + Retry-After.  ``envelope`` wraps bodies in the documented
+// {"code","message","data","timestamp"} format (docs/api.md:12-20).
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -27,6 +31,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <ctime>
@@ -37,7 +42,9 @@
 #include <vector>
 
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
+#include "ingress/guard.h"
 #include "queue/shm_ring.h"
 
 namespace py = pybind11;
@@ -212,7 +219,7 @@ Scan scan_message(const char* b, size_t n) {
 
 // ------------------------------------------------------------------ HTTP
 struct Conn {
-  std::string in, out;
+  std::string in, out, ip;
   size_t out_off = 0;
   bool close_after = false;
 };
@@ -277,8 +284,14 @@ class HttpIngress {
     d["requests"] = requests_.load();
     d["connections"] = conns_.load();
     d["port"] = port_;
+    d["unauthorized"] = unauth_.load();
+    d["forbidden"] = forbidden_.load();
+    d["rate_limited"] = limited_.load();
     return d;
   }
+
+  void set_guard(std::shared_ptr<llmq::Guard> g) { guard_ = std::move(g); }
+  void set_envelope(bool on) { envelope_ = on; }
 
  private:
   int listen_socket() {
@@ -314,7 +327,9 @@ class HttpIngress {
         int fd = evs[k].data.fd;
         if (fd == lfd) {
           for (;;) {
-            int c = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK);
+            sockaddr_in pa{};
+            socklen_t pl = sizeof pa;
+            int c = accept4(lfd, (sockaddr*)&pa, &pl, SOCK_NONBLOCK);
             if (c < 0) break;
             int one = 1;
             setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
@@ -322,7 +337,9 @@ class HttpIngress {
             ce.events = EPOLLIN | EPOLLRDHUP;
             ce.data.fd = c;
             epoll_ctl(ep, EPOLL_CTL_ADD, c, &ce);
-            conns[c];
+            char ipb[INET_ADDRSTRLEN] = {0};
+            inet_ntop(AF_INET, &pa.sin_addr, ipb, sizeof ipb);
+            conns[c].ip = ipb;
             conns_++;
           }
           continue;
@@ -378,14 +395,55 @@ class HttpIngress {
     return true;
   }
 
-  static void respond(Conn& cn, int code, const char* reason, const std::string& body, bool keep) {
+  void respond(Conn& cn, int code, const char* reason, const std::string& raw, bool keep,
+               const std::string& extra_hdr = "") {
+    std::string body;
+    if (envelope_) {
+      // error bodies are {"error": "..."}: lift the text into "message"
+      const bool err = code >= 400;
+      std::string msg = "success";
+      if (err) {
+        const size_t a = raw.find(":\"");
+        const size_t b = raw.rfind('"');
+        msg = (a != std::string::npos && b > a + 2) ? raw.substr(a + 2, b - a - 2) : reason;
+      }
+      body = "{\"code\":" + std::to_string(code) + ",\"message\":\"" + msg + "\"," +
+             (err ? "\"error\":\"" + msg + "\"" : "\"data\":" + raw) + ",\"timestamp\":\"" + rfc3339_now() + "\"}";
+    }
+    const std::string& b = envelope_ ? body : raw;
     char hdr[256];
     int n = snprintf(hdr, sizeof hdr,
-                     "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n%s\r\n", code,
-                     reason, body.size(), keep ? "" : "Connection: close\r\n");
+                     "HTTP/1.1 %d %s\r\nContent-Type: application/json\r\nContent-Length: %zu\r\n%s", code,
+                     reason, b.size(), keep ? "" : "Connection: close\r\n");
     cn.out.append(hdr, (size_t)n);
-    cn.out.append(body);
+    cn.out.append(extra_hdr);
+    cn.out.append("\r\n");
+    cn.out.append(b);
     if (!keep) cn.close_after = true;
+  }
+
+  // 401 / 403 / 429 for a guard verdict; returns true when the request may proceed
+  bool admit(Conn& cn, const std::string& method, const std::string& path, const std::string& key,
+             const std::string& auth, const std::string& user, bool keep) {
+    if (!guard_) return true;
+    llmq::GuardResult g = guard_->check(method, path, cn.ip, key, auth, user);
+    if (g.code == llmq::G_OK) return true;
+    std::string why;
+    for (char c : g.reason) why.push_back(c == '"' || c == '\\' ? '\'' : c);
+    if (g.code == llmq::G_UNAUTHORIZED) {
+      unauth_++;
+      respond(cn, 401, "Unauthorized", "{\"error\":\"" + why + "\"}", keep,
+              "WWW-Authenticate: " + std::string(guard_->key_header() == "authorization" ? "Bearer" : "Bearer, ApiKey") + "\r\n");
+    } else if (g.code == llmq::G_FORBIDDEN) {
+      forbidden_++;
+      respond(cn, 403, "Forbidden", "{\"error\":\"" + why + "\"}", keep);
+    } else {
+      limited_++;
+      const int ra = std::max(1, (int)std::ceil(g.retry_after_s));
+      respond(cn, 429, "Too Many Requests", "{\"error\":\"" + why + "\"}", keep,
+              "Retry-After: " + std::to_string(ra) + "\r\n");
+    }
+    return false;
   }
 
   static std::string uuid4(std::mt19937_64& rng) {
@@ -420,6 +478,7 @@ class HttpIngress {
       bool http10 = std::string(sp2 + 1, std::min<size_t>(8, hl - (sp2 + 1 - h))) == "HTTP/1.0";
       size_t clen = 0;
       bool keep = !http10;
+      std::string api_key, authz;
       // headers (case-insensitive names)
       const char* line = (const char*)memchr(h, '\n', hl);
       while (line && line < h + hl) {
@@ -435,6 +494,8 @@ class HttpIngress {
           std::string val(v, le - v);
           while (!val.empty() && (val.back() == '\r' || val.back() == ' ')) val.pop_back();
           if (name == "content-length") clen = (size_t)strtoull(val.c_str(), nullptr, 10);
+          else if (name == "authorization") authz = val;
+          else if (guard_ && name == guard_->key_header()) api_key = val;
           else if (name == "connection") {
             for (auto& c : val) c = (char)tolower((unsigned char)c);
             if (val == "close") keep = false;
@@ -448,7 +509,9 @@ class HttpIngress {
       requests_++;
       if (method == "POST" && (path == "/api/v1/messages" || path == "/api/v1/messages/")) {
         Scan s = scan_message(body, clen);
-        if (!s.ok) {
+        if (!admit(cn, method, path, api_key, authz, s.ok ? s.user_id : std::string(), keep)) {
+          // rejected by the guard (401 / 403 / 429)
+        } else if (!s.ok) {
           bad_++;
           respond(cn, 400, "Bad Request", "{\"error\":\"Invalid message format\"}", keep);
         } else {
@@ -493,6 +556,9 @@ class HttpIngress {
   std::vector<std::thread> th_;
   std::vector<int> lfds_;
   std::atomic<int64_t> accepted_{0}, rejected_full_{0}, bad_{0}, requests_{0}, conns_{0};
+  std::atomic<int64_t> unauth_{0}, forbidden_{0}, limited_{0};
+  std::shared_ptr<llmq::Guard> guard_;
+  bool envelope_ = false;
 };
 
 }  // namespace
@@ -505,7 +571,46 @@ PYBIND11_MODULE(_ingress, m) {
            py::arg("threads") = 4, py::arg("host") = "0.0.0.0")
       .def("start", &HttpIngress::start)
       .def("stop", &HttpIngress::stop, py::call_guard<py::gil_scoped_release>())
-      .def("stats", &HttpIngress::stats);
+      .def("stats", &HttpIngress::stats)
+      .def("set_guard", &HttpIngress::set_guard)
+      .def("set_envelope", &HttpIngress::set_envelope);
+  py::class_<llmq::Guard, std::shared_ptr<llmq::Guard>>(m, "Guard")
+      .def(py::init<std::string, std::string, std::vector<std::string>, std::string, std::string, int64_t, bool,
+                    std::unordered_map<std::string, std::vector<std::string>>, std::string, double, double, double,
+                    double, double, double, double>(),
+           py::arg("method") = "none", py::arg("api_key_header") = "X-API-Key",
+           py::arg("api_keys") = std::vector<std::string>{}, py::arg("jwt_secret") = "", py::arg("jwt_issuer") = "",
+           py::arg("jwt_leeway_s") = 0, py::arg("rbac") = false,
+           py::arg("roles") = std::unordered_map<std::string, std::vector<std::string>>{},
+           py::arg("default_role") = "user", py::arg("global_rps") = 0.0, py::arg("global_burst") = 0.0,
+           py::arg("ip_rps") = 0.0, py::arg("ip_burst") = 0.0, py::arg("user_rps") = 0.0, py::arg("user_burst") = 0.0,
+           py::arg("idle_s") = 60.0)
+      .def("check",
+           [](llmq::Guard& g, const std::string& method, const std::string& path, const std::string& ip,
+              const std::string& api_key, const std::string& authorization, const std::string& user,
+              int64_t now_ns, int64_t wall_s) {
+             llmq::GuardResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = g.check(method, path, ip, api_key, authorization, user, now_ns, wall_s);
+             }
+             return py::make_tuple(r.code, r.subject, r.role, r.reason, r.retry_after_s);
+           },
+           py::arg("method"), py::arg("path"), py::arg("ip") = "", py::arg("api_key") = "",
+           py::arg("authorization") = "", py::arg("user") = "", py::arg("now_ns") = 0, py::arg("wall_s") = 0)
+      .def("allow_user",
+           [](llmq::Guard& g, const std::string& user) {
+             double ra = 0;
+             bool ok = g.allow_user(user, &ra);
+             return py::make_tuple(ok, ra);
+           })
+      .def("sign_jwt", &llmq::Guard::sign_jwt)
+      .def("role_allows", &llmq::Guard::role_allows)
+      .def_property_readonly("key_header", &llmq::Guard::key_header)
+      .def_property_readonly("auth_enabled", &llmq::Guard::auth_enabled)
+      .def_property_readonly("active", &llmq::Guard::any)
+      .def("tracked_keys", &llmq::Guard::tracked_keys)
+      .def_static("permission_for", &llmq::Guard::permission_for);
   m.def("scan_message", [](py::bytes b) {
     std::string s = b;
     Scan r = scan_message(s.data(), s.size());

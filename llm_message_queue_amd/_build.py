@@ -53,9 +53,9 @@ def _targets() -> Dict[str, dict]:
         "_ingress": dict(
             compiler="g++",
             sources=[os.path.join(CSRC, "ingress", "http_ingress.cpp")],
-            deps=[os.path.join(CSRC, "queue", "shm_ring.h")],
+            deps=[os.path.join(CSRC, "queue", "shm_ring.h"), os.path.join(CSRC, "ingress", "guard.h")],
             flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
-            libs=["-lrt"],
+            libs=["-lrt", "-lcrypto"],
         ),
         "_hipops": dict(
             compiler=os.path.join(ROCM, "bin", "hipcc"),

@@ -14,13 +14,19 @@ Behaviour notes vs the reference:
   * ``setUserPriority`` accepts ``realtime`` (D18);
   * ``estimated_wait`` comes from live queue depth / dispatch rate;
   * CORS: echo an allowed Origin (or any, with "*"), allow credentials,
-    OPTIONS -> 204 (`:121-148`).
+    OPTIONS -> 204 (`:121-148`);
+  * doc-only features of the reference, off by default: API-key / JWT
+    authentication, RBAC and token-bucket rate limits (``api/security.py``,
+    401 / 403 / 429 + Retry-After), and the ``{"code","message","data",
+    "timestamp"}`` response envelope (`docs/api.md:12-20`,
+    ``server.response_envelope``).
 """
 from __future__ import annotations
 
 import asyncio
 import dataclasses
 import json
+import math
 import time
 import uuid
 from typing import Any, Dict, List, Optional
@@ -36,6 +42,7 @@ from ..preprocess import oracle
 from ..queue.core import QueueError
 from ..scheduler.resource_scheduler import Resource, ResourceError
 from ..utils.metrics import CONTENT_TYPE_LATEST
+from .security import guard_from_config, redact_config
 
 VERSION = "1.0.0"
 
@@ -56,6 +63,58 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
     app = FastAPI(title="llm_message_queue_amd", version=VERSION)
     origins = allowed_origins if allowed_origins is not None else ["*"]
     G = gw_app
+
+    # ------------------------------------------------------------------ guard
+    # authentication / RBAC / rate limits (api/security.py; native checks).
+    # Middleware order, outermost first: CORS -> envelope -> guard -> route.
+    guard = guard_from_config(G.cfg)
+    app.state.guard = guard
+    if guard is not None:
+        @app.middleware("http")
+        async def guard_mw(request: Request, call_next):
+            if request.method == "OPTIONS":
+                return await call_next(request)
+            path = request.url.path
+            user = request.headers.get("x-user-id", "") or request.query_params.get("user_id", "")
+            if not user and request.method == "POST" and path.rstrip("/") == "/api/v1/messages":
+                try:  # per-user limits key on the body's user_id (cached for the route)
+                    body = json.loads(await request.body() or b"{}")
+                    user = str(body.get("user_id", "") or "") if isinstance(body, dict) else ""
+                except ValueError:
+                    user = ""
+            code, subject, role, reason, retry = guard.check(
+                request.method, path, request.client.host if request.client else "",
+                request.headers.get(guard.key_header, ""), request.headers.get("authorization", ""), user)
+            if code == 401:
+                return JSONResponse({"error": reason}, status_code=401, headers={"WWW-Authenticate": "Bearer"})
+            if code in (403, 429):
+                hdrs = {"Retry-After": str(max(1, math.ceil(retry)))} if code == 429 else None
+                return JSONResponse({"error": reason}, status_code=code, headers=hdrs)
+            request.state.subject, request.state.role = subject, role
+            return await call_next(request)
+
+    # ------------------------------------------------------------------ envelope
+    if G.cfg.server.response_envelope:
+        @app.middleware("http")
+        async def envelope(request: Request, call_next):
+            resp = await call_next(request)
+            if not resp.headers.get("content-type", "").startswith("application/json"):
+                return resp
+            raw = b"".join([chunk async for chunk in resp.body_iterator])
+            try:
+                payload = json.loads(raw) if raw else None
+            except ValueError:
+                return Response(raw, status_code=resp.status_code, headers=dict(resp.headers))
+            code = resp.status_code
+            env: Dict[str, Any] = {"code": code}
+            if code >= 400:
+                msg = payload.get("error", "") if isinstance(payload, dict) else ""
+                env.update(message=msg or "error", error=msg or "error")
+            else:
+                env.update(message="success", data=payload)
+            env["timestamp"] = format_time(time.time_ns())
+            hdrs = {k: v for k, v in resp.headers.items() if k.lower() not in ("content-length", "content-type")}
+            return JSONResponse(env, status_code=code, headers=hdrs)
 
     # ------------------------------------------------------------------ CORS
     @app.middleware("http")
@@ -449,9 +508,6 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
 
     @app.get("/api/v1/config")
     def get_config():
-        d = dataclasses.asdict(G.cfg)
-        d["database"]["postgres"]["password"] = "***"
-        d["database"]["redis"]["password"] = "***"
-        return d
+        return redact_config(dataclasses.asdict(G.cfg))
 
     return app

@@ -49,7 +49,8 @@ def cmd_native_ingress(a) -> int:
     from ..gateway.native_ingress import NativeIngress
     cfg = _load_cfg(a.config)
     port = a.port or cfg.server.port
-    ing = NativeIngress(port, a.ring or cfg.server.shared_ring, a.ingress_threads, a.host or cfg.server.host)
+    ing = NativeIngress(port, a.ring or cfg.server.shared_ring, a.ingress_threads, a.host or cfg.server.host,
+                        cfg=cfg)
     port = ing.start()
     print(json.dumps({"event": "listening", "host": a.host or cfg.server.host, "port": port, "role": "native-ingress",
                       "ring": ing.ring, "threads": a.ingress_threads}), flush=True)
@@ -193,6 +194,20 @@ def cmd_validate(a) -> int:
     return 0
 
 
+def cmd_token(a) -> int:
+    """Issue an HS256 JWT with the configured secret/issuer (jwt authentication)."""
+    from ..api.security import issue_token
+    cfg = _load_cfg(a.config)
+    jwt = cfg.security.authentication.jwt
+    secret = a.secret or jwt.secret
+    if not secret:
+        print(json.dumps({"error": "no jwt secret (security.authentication.jwt.secret or --secret)"}))
+        return 1
+    ttl = int(a.ttl_hours * 3600) if a.ttl_hours > 0 else int(jwt.expiration) * 3600
+    print(issue_token(secret, a.subject, a.role, ttl_s=ttl, issuer=jwt.issuer))
+    return 0
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="llmq")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -213,6 +228,12 @@ def main(argv=None) -> int:
     p.add_argument("--iterations", type=int, default=0)
     p = sub.add_parser("validate-config")
     p.add_argument("--config", default=None)
+    p = sub.add_parser("token", help="issue a JWT for security.authentication.method=jwt")
+    p.add_argument("--config", default=None)
+    p.add_argument("--subject", required=True)
+    p.add_argument("--role", default="")
+    p.add_argument("--secret", default="", help="override the configured secret")
+    p.add_argument("--ttl-hours", type=float, default=0.0, help="default: jwt.expiration")
     sub.add_parser("bench", add_help=False)
     a, rest = ap.parse_known_args(argv)
     if a.cmd in ("serve", "server"):
@@ -225,6 +246,8 @@ def main(argv=None) -> int:
         return cmd_scheduler(a)
     if a.cmd == "validate-config":
         return cmd_validate(a)
+    if a.cmd == "token":
+        return cmd_token(a)
     if a.cmd == "bench":
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         sys.path.insert(0, root)

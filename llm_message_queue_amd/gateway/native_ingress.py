@@ -10,10 +10,20 @@ from .. import _native
 
 
 class NativeIngress:
-    def __init__(self, port: int = 8080, ring: str = "default", threads: int = 4, host: str = "0.0.0.0"):
+    def __init__(self, port: int = 8080, ring: str = "default", threads: int = 4, host: str = "0.0.0.0",
+                 cfg=None):
+        """``cfg`` (optional): attach the config's guard (authentication, RBAC,
+        rate limits -- ``api/security.py``) and response envelope."""
         self.ring = ring
         self._k = _native.ingress().HttpIngress(int(port), f"llmq-{ring}-req", int(threads), host)
         self.port = int(port)
+        self.guard = None
+        if cfg is not None:
+            from ..api.security import guard_from_config
+            self.guard = guard_from_config(cfg)
+            if self.guard is not None:
+                self._k.set_guard(self.guard)
+            self._k.set_envelope(bool(cfg.server.response_envelope))
 
     def start(self) -> int:
         """Start listening; returns the bound port (useful with port 0)."""

@@ -38,6 +38,9 @@ class ServerConfig:
     # shared-memory request ring the two modes exchange messages through
     shared_ring: str = "default"
     shared_ring_bytes: int = 64 << 20
+    # wrap JSON bodies in {"code","message","data","timestamp"} (docs/api.md:12-20);
+    # off by default: the reference's handlers return bare objects
+    response_envelope: bool = False
 
 
 @dataclass
@@ -139,6 +142,23 @@ class SchedulerConfig:
 
 
 @dataclass
+class RateLimitRule:
+    requests_per_second: float = 0.0   # 0 = unlimited
+    burst_size: int = 0                # 0 = max(1, requests_per_second)
+    window_size: int = 60              # idle seconds before a per-key bucket is dropped
+
+
+@dataclass
+class RateLimitConfig:
+    """``loadbalancer.rate_limiting`` (docs/configuration.md:503-537; doc-only
+    in the reference).  Token buckets, enforced by the native guard."""
+    enabled: bool = False
+    global_: RateLimitRule = field(default_factory=RateLimitRule)
+    per_ip: RateLimitRule = field(default_factory=RateLimitRule)
+    per_user: RateLimitRule = field(default_factory=RateLimitRule)
+
+
+@dataclass
 class LoadBalancerConfig:
     algorithm: str = "weighted_round_robin"
     health_check_interval: int = 30 * S
@@ -146,6 +166,7 @@ class LoadBalancerConfig:
     enable_session_affinity: bool = True
     session_timeout: int = 0           # 0 = never expires (reference behaviour)
     healthy_threshold: int = 2
+    rate_limiting: RateLimitConfig = field(default_factory=RateLimitConfig)
 
 
 @dataclass
@@ -210,6 +231,50 @@ class ConversationConfig:
 
 
 @dataclass
+class JWTConfig:
+    secret: str = ""
+    expiration: int = 24               # hours (tokens issued by `cli token`)
+    algorithm: str = "HS256"           # the only accepted algorithm
+    issuer: str = "llm-message-queue"
+    leeway: int = 0                    # seconds of clock skew tolerated on exp/nbf
+
+
+@dataclass
+class APIKeyConfig:
+    header_name: str = "X-API-Key"
+    # "key", "key:user" or "key:user:role"
+    valid_keys: List[str] = field(default_factory=list)
+
+
+@dataclass
+class AuthenticationConfig:
+    method: str = "none"               # none | api_key | jwt
+    jwt: JWTConfig = field(default_factory=JWTConfig)
+    api_key: APIKeyConfig = field(default_factory=APIKeyConfig)
+
+
+def _default_roles() -> Dict[str, List[str]]:
+    return {"admin": ["*"],
+            "user": ["message:read", "message:write", "conversation:read", "conversation:write", "queue:read"],
+            "readonly": ["message:read", "conversation:read", "queue:read"]}
+
+
+@dataclass
+class AuthorizationConfig:
+    enabled: bool = False
+    policy: str = "rbac"
+    roles: Dict[str, List[str]] = field(default_factory=_default_roles)
+    default_role: str = "user"
+
+
+@dataclass
+class SecurityConfig:
+    """``security`` (docs/configuration.md:732-805; doc-only in the reference)."""
+    authentication: AuthenticationConfig = field(default_factory=AuthenticationConfig)
+    authorization: AuthorizationConfig = field(default_factory=AuthorizationConfig)
+
+
+@dataclass
 class Config:
     server: ServerConfig = field(default_factory=ServerConfig)
     database: DatabaseConfig = field(default_factory=DatabaseConfig)
@@ -222,6 +287,7 @@ class Config:
     gpu: GPUConfig = field(default_factory=GPUConfig)
     backend: BackendConfig = field(default_factory=BackendConfig)
     conversation: ConversationConfig = field(default_factory=ConversationConfig)
+    security: SecurityConfig = field(default_factory=SecurityConfig)
 
     def to_dict(self) -> Dict[str, Any]:
         return dataclasses.asdict(self)
@@ -234,6 +300,12 @@ _DURATION_FIELDS = {
     "health_check_interval", "session_timeout", "heartbeat_timeout", "autoscale_cooldown",
     "max_idle_time",
 }
+
+
+# YAML keys that are Python keywords
+_KEY_ALIASES = {"global": "global_"}
+# list fields holding strings (the rest are int lists, e.g. gpu.devices)
+_STR_LIST_FIELDS = {"valid_keys"}
 
 
 class ConfigError(ValueError):
@@ -273,6 +345,7 @@ def _merge(obj: Any, data: Dict[str, Any], path: str = "") -> None:
     fields = {f.name: f for f in dataclasses.fields(obj)}
     for key, value in data.items():
         k = str(key).lower()
+        k = _KEY_ALIASES.get(k, k)
         if k not in fields:
             continue  # unknown keys are ignored, as viper does
         cur = getattr(obj, k)
@@ -286,14 +359,28 @@ def _merge(obj: Any, data: Dict[str, Any], path: str = "") -> None:
                 _merge(q, lv, f"{full}[{i}]")
                 levels.append(q)
             setattr(obj, k, levels)
+        elif k == "roles":
+            # role -> [permissions] or role -> {permissions: [...]} (the docs' form)
+            if not isinstance(value, dict):
+                raise ConfigError(f"{full}: expected a mapping")
+            roles = {}
+            for role, perms in value.items():
+                if isinstance(perms, dict):
+                    perms = perms.get("permissions", [])
+                if isinstance(perms, str):
+                    perms = [p.strip() for p in perms.split(",") if p.strip()]
+                roles[str(role)] = [str(p) for p in (perms or [])]
+            setattr(obj, k, roles)
         elif isinstance(cur, dict):
             if not isinstance(value, dict):
                 raise ConfigError(f"{full}: expected a mapping")
             setattr(obj, k, {str(a): int(b) for a, b in value.items()})
         elif isinstance(cur, list):
             if isinstance(value, str):
-                value = [int(x) for x in value.split(",") if x.strip()]
-            setattr(obj, k, list(value or []))
+                value = [x.strip() for x in value.split(",") if x.strip()]
+                if k not in _STR_LIST_FIELDS:
+                    value = [int(x) for x in value]
+            setattr(obj, k, [str(x) for x in value] if k in _STR_LIST_FIELDS else list(value or []))
         else:
             setattr(obj, k, _coerce(k, cur, value, fields[k].type))
 
@@ -335,6 +422,26 @@ def validate(cfg: Config) -> Config:
         seen.add(lv.priority)
     if cfg.gpu.slots_per_gpu <= 0:
         raise ConfigError("gpu.slots_per_gpu must be > 0")
+    auth = cfg.security.authentication
+    if auth.method not in ("none", "api_key", "jwt"):
+        raise ConfigError("security.authentication.method must be none, api_key or jwt")
+    if auth.method == "jwt":
+        if not auth.jwt.secret:
+            raise ConfigError("security.authentication.jwt.secret must be set for jwt authentication")
+        if auth.jwt.algorithm.upper() != "HS256":
+            raise ConfigError("security.authentication.jwt.algorithm: only HS256 is supported")
+    if auth.method == "api_key" and not auth.api_key.valid_keys:
+        raise ConfigError("security.authentication.api_key.valid_keys must list at least one key")
+    az = cfg.security.authorization
+    if az.enabled:
+        if az.policy != "rbac":
+            raise ConfigError("security.authorization.policy: only rbac is supported")
+        if az.default_role not in az.roles:
+            raise ConfigError(f"security.authorization.default_role {az.default_role!r} is not a defined role")
+    for name in ("global_", "per_ip", "per_user"):
+        r = getattr(cfg.loadbalancer.rate_limiting, name)
+        if r.requests_per_second < 0 or r.burst_size < 0:
+            raise ConfigError(f"loadbalancer.rate_limiting.{name.rstrip('_')}: values must be >= 0")
     return cfg
 
 

@@ -28,7 +28,7 @@ def test_native_runtime_under_sanitizer(san, tmp_path):
     exe = str(tmp_path / "stress")
     src = os.path.join(ROOT, "csrc", "tests", "stress_native.cpp")
     cmd = [cxx, "-std=c++17", "-O1", "-g", f"-fsanitize={san}", "-fno-omit-frame-pointer",
-           f"-I{os.path.join(ROOT, 'csrc')}", src, "-o", exe, "-lrt", "-pthread"]
+           f"-I{os.path.join(ROOT, 'csrc')}", src, "-o", exe, "-lrt", "-lcrypto", "-pthread"]
     if "undefined" in san:
         cmd.insert(5, "-fno-sanitize-recover=undefined")
     b = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
