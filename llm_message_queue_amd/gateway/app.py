@@ -116,7 +116,7 @@ class GatewayApp:
         self.gateway = Gateway(cfg, preprocessor=self.preprocessor, engine=engine, comm=comm,
                                load_balancer=self.lb if engine is not None else None, metrics=self.metrics,
                                state_manager=self.state, use_gpu_preprocess=self.preprocessor.gpu_enabled(),
-                               queue_manager=self.standard)
+                               queue_manager=self.standard, dead_letter=self.factory.dead_letter_queue)
         self.gateway.on_complete = self._on_complete
         self.batcher = MicroBatcher(self._flush, cfg.preprocessor.batch_window_us, cfg.preprocessor.max_batch)
         self._stop = threading.Event()

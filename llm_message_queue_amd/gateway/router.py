@@ -122,7 +122,7 @@ class Gateway:
                  comm: Optional[Comm] = None, load_balancer=None, metrics=None, state_manager=None,
                  use_gpu_preprocess: Optional[bool] = None, prompt_cap: Optional[int] = None,
                  gen_tokens: Optional[int] = None, name: str = "gateway",
-                 queue_manager: Optional[QueueManager] = None):
+                 queue_manager: Optional[QueueManager] = None, dead_letter=None):
         from ..preprocess.preprocessor import Preprocessor
         self.cfg = cfg
         self.log = get_logger("gateway")
@@ -162,7 +162,11 @@ class Gateway:
         self._done_owed: Dict[int, List[Tuple[int, int, int, int]]] = {r: [] for r in range(self.world)}
         self.rec = LatencyRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
-                         "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0}
+                         "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0}
+        # overload shedding (expire_queued) -> dead-letter queue
+        self.shed_expired = bool(getattr(q, "shed_expired", True))
+        self.dead_letter = dead_letter
+        self.on_expire = None       # optional callback(msg)
         # failure detection: a backend error (HIP error / OOM), the telemetry
         # poller (ECC, amd-smi gone) or an operator marks this GPU unhealthy;
         # it then takes no new work, its in-flight requests are re-routed and
@@ -292,9 +296,61 @@ class Gateway:
 
     # ------------------------------------------------------------------ dispatch
     def dispatch(self) -> int:
+        if self.shed_expired:
+            self.expire_queued()
         if self.world == 1:
             return self._dispatch_local()
         return self._dispatch_global()
+
+    def expire_queued(self, now: Optional[int] = None) -> int:
+        """Overload shedding: pop every tier head whose deadline (arrival +
+        ``timeout``) has passed and move it to the dead-letter queue (status
+        ``timeout``).  Tiers are FIFO, so the expired requests of a tier are
+        its head run; the cost when nothing expired is one peek per tier.
+        Runs before the load exchange, so multi-rank plans only see live
+        requests."""
+        now = time.monotonic_ns() if now is None else now
+        out: List[Message] = []
+        for name in self.tiers:
+            while True:
+                try:
+                    m = self.qm.peek_message(name)
+                except QueueError:
+                    break
+                if not self._expired(m, now):
+                    break
+                try:
+                    m = self.qm.pop_message(name)
+                except QueueError:
+                    break
+                h = self._home(m)
+                if 0 <= h < self.world and self.pinned[h] > 0:
+                    self.pinned[h] -= 1
+                out.append(m)
+        self._shed(out)
+        return len(out)
+
+    @staticmethod
+    def _expired(m: Message, now: int) -> bool:
+        t0 = m.arrival_ns or m.enqueued_at
+        return bool(m.timeout > 0 and t0 and now - t0 > m.timeout)
+
+    def _shed(self, out: List[Message]) -> None:
+        """Popped, expired requests -> status timeout + dead-letter queue."""
+        for m in out:
+            m.status = MessageStatus.TIMEOUT
+            self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
+        if out:
+            self.counters["expired"] += len(out)
+            if self.dead_letter is not None:
+                by_q: Dict[str, List[Message]] = {}
+                for m in out:
+                    by_q.setdefault(m.queue_name, []).append(m)
+                for q, ms in by_q.items():
+                    self.dead_letter.push_many(ms, "deadline exceeded before dispatch", q)
+            if self.on_expire is not None:
+                for m in out:
+                    self.on_expire(m)
 
     def _dispatch_local(self) -> int:
         if self.engine is None or not self.healthy:
@@ -305,6 +361,15 @@ class Gateway:
         msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets())
         if not msgs:
             return 0
+        if self.shed_expired:     # expired requests behind a live tier head
+            now = time.monotonic_ns()
+            dead = [i for i, m in enumerate(msgs) if self._expired(m, now)]
+            if dead:
+                self._shed([msgs[i] for i in dead])
+                keep = np.ones(len(msgs), dtype=bool)
+                keep[dead] = False
+                msgs = [m for m, k in zip(msgs, keep) if k]
+                tier_idx = np.asarray(tier_idx)[keep]
         reqs = []
         for m, t in zip(msgs, tier_idx):
             t = int(t)

@@ -15,7 +15,7 @@ import queue as _pyqueue
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional
+from typing import Callable, List, Optional, Sequence
 
 from ..models.message import Message, format_time
 from ..utils.logging import get_logger
@@ -75,6 +75,30 @@ class DeadLetterQueue:
                 ch.put_nowait(item)
             except _pyqueue.Full:
                 self.dropped_notifications += 1
+
+    def push_many(self, messages: Sequence[Message], fail_reason: str, source_queue: str) -> int:
+        """Bulk ``push`` (one log line; overload shedding moves thousands at
+        once).  Items beyond ``max_size`` are dropped; returns how many were
+        kept."""
+        now = time.time_ns()
+        with self._lock:
+            room = len(messages) if self.max_size <= 0 else max(0, self.max_size - len(self._items))
+            items = [DeadLetterItem(m, str(fail_reason), now, source_queue, m.retry_count) for m in messages[:room]]
+            self._items.extend(items)
+            handlers = list(self._handlers)
+            chans = list(self._notify)
+        if items:
+            self.logger.warning("Messages moved to dead letter queue", count=len(items), reason=str(fail_reason),
+                                source=source_queue, dropped=len(messages) - len(items))
+        for item in items:
+            for h in handlers:
+                threading.Thread(target=self._run_handler, args=(h, item), daemon=True).start()
+            for ch in chans:
+                try:
+                    ch.put_nowait(item)
+                except _pyqueue.Full:
+                    self.dropped_notifications += 1
+        return len(items)
 
     def restore(self, item: DeadLetterItem) -> None:
         """Re-insert an item from a snapshot (no handlers/notifications fire)."""

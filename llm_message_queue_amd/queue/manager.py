@@ -211,11 +211,12 @@ class QueueManager:
             self.metrics.process_time.labels(self.name, queue_name, p).observe(processing_time_ns / 1e9)
 
     def fail_message(self, queue_name: str, message_id: str, err: Optional[BaseException] = None,
-                     priority: Optional[int] = None) -> None:
+                     priority: Optional[int] = None, quiet: bool = False) -> None:
         if queue_name not in self._queues:
             return
         self.mlq.fail_message(queue_name)
-        self.logger.warning("Failed message", queue=queue_name, message_id=message_id, error=str(err))
+        if not quiet:   # bulk callers (overload shedding) log once themselves
+            self.logger.warning("Failed message", queue=queue_name, message_id=message_id, error=str(err))
         if self.metrics:
             p = priority_name(priority) if priority is not None else "unknown"
             self.metrics.processing.labels(self.name, queue_name, p).dec()

@@ -123,6 +123,10 @@ class QueueConfig:
     # delayed and dead-lettered messages; replayed on start.  "" disables.
     snapshot_path: str = ""
     snapshot_interval: int = 0         # ns; 0 = only at shutdown
+    # overload shedding: a request still queued when its ``timeout`` (the
+    # reference's per-message processing deadline, 30 s default) has elapsed
+    # since arrival goes to the dead-letter queue instead of a GPU slot
+    shed_expired: bool = True
 
 
 @dataclass

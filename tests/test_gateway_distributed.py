@@ -452,3 +452,62 @@ def test_coordinated_stop_across_ranks():
     [t.join(timeout=30) for t in ths]
     assert not any(t.is_alive() for t in ths)
     assert ticks[0] == ticks[1] == ticks[2] == 6
+
+
+# ---------------------------------------------------------------- overload shedding
+def test_expired_requests_go_to_dead_letter_not_gpu():
+    """A request still queued past its deadline (arrival + timeout) is shed
+    to the DLQ with status ``timeout``; live ones are served (BASELINE
+    config 5: dead-letter under sustained overload)."""
+    from llm_message_queue_amd.queue.dead_letter import DeadLetterQueue
+    import time
+    dlq = DeadLetterQueue()
+    gw = Gateway(cfg(), engine=engine(slots=4), use_gpu_preprocess=False, prompt_cap=8, gen_tokens=2,
+                 dead_letter=dlq)
+    msgs = Workload(seed=5).make(30)
+    now = time.monotonic_ns()
+    for i, m in enumerate(msgs):
+        if i % 3 == 0:                       # 10 requests arrived 2 s ago with a 1 s deadline
+            m.arrival_ns = now - 2_000_000_000
+            m.timeout = 1_000_000_000
+    stale = [m for i, m in enumerate(msgs) if i % 3 == 0]
+    # the stale ones queued first (tier heads), then the live ones
+    gw.submit(stale)
+    gw.ingest()
+    gw.submit([m for i, m in enumerate(msgs) if i % 3])
+    gw.ingest()
+    gw.dispatch()
+    assert gw.counters["expired"] == 10 and dlq.size() == 10
+    assert all(m.status == "timeout" and not m.dispatched_at for m in stale)
+    assert {it.message.id for it in dlq.get_all()} == {m.id for m in stale}
+    assert all(it.fail_reason == "deadline exceeded before dispatch" for it in dlq.get_all())
+    assert run_until_done([gw], 20)
+    assert gw.counters["completed"] == 20 and gw.pending() == 0
+    # shedding off: everything is served
+    c = cfg()
+    c.queue.shed_expired = False
+    gw2 = Gateway(c, engine=engine(slots=4), use_gpu_preprocess=False, prompt_cap=8, gen_tokens=2)
+    ms = Workload(seed=6).make(6)
+    for m in ms:
+        m.arrival_ns, m.timeout = now - 2_000_000_000, 1_000_000_000
+    gw2.submit(ms)
+    assert run_until_done([gw2], 6) and gw2.counters["expired"] == 0
+
+
+def test_expired_requests_behind_a_live_head_are_shed_at_pop():
+    from llm_message_queue_amd.queue.dead_letter import DeadLetterQueue
+    import time
+    dlq = DeadLetterQueue()
+    gw = Gateway(cfg(), engine=engine(slots=8, token_budget=256), use_gpu_preprocess=False, prompt_cap=8,
+                 gen_tokens=2, dead_letter=dlq)
+    msgs = Workload(seed=7).make(8)
+    for m in msgs:                           # one tier (no priority keywords)
+        m.content, m.priority, m.queue_name = "plain request text", 3, "normal"
+    now = time.monotonic_ns()
+    for m in msgs[1::2]:                     # interleaved: live head, stale, live, stale ...
+        m.arrival_ns, m.timeout = now - 5_000_000_000, 1_000_000_000
+    gw.submit(msgs)
+    gw.ingest()
+    gw.dispatch()
+    assert gw.counters["expired"] == 4 and gw.counters["dispatched"] == 4 and dlq.size() == 4
+    assert all(m.status == "timeout" for m in msgs[1::2])
