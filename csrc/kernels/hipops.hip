@@ -136,24 +136,24 @@ static void silu_mul(uintptr_t gu, uintptr_t out, int T, int F, uintptr_t stream
 }
 
 static void rope_kv(uintptr_t qkv, uintptr_t pos, uintptr_t slot, uintptr_t cos_t, uintptr_t sin_t, int T,
-                    int Hq, int Hkv, int max_ctx, uintptr_t q_out, uintptr_t kc, uintptr_t vc,
+                    int Hq, int Hkv, int max_ctx, int n_slots, uintptr_t q_out, uintptr_t kc, uintptr_t vc,
                     uintptr_t stream) {
   require(Hq % 4 == 0 && Hkv >= 1, "bad head counts");
   if (T == 0) return;
   hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, S(stream), P<const uint16_t>(qkv),
                      P<const int32_t>(pos), P<const int32_t>(slot), P<const float>(cos_t),
-                     P<const float>(sin_t), Hq, Hkv, max_ctx, P<uint16_t>(q_out), P<uint16_t>(kc),
+                     P<const float>(sin_t), Hq, Hkv, max_ctx, n_slots, P<uint16_t>(q_out), P<uint16_t>(kc),
                      P<uint16_t>(vc));
   check_launch();
 }
 
 static void attention(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, uintptr_t slot, int T, int Hq,
-                      int Hkv, int max_ctx, float scale, uintptr_t out, uintptr_t stream) {
+                      int Hkv, int max_ctx, int n_slots, float scale, uintptr_t out, uintptr_t stream) {
   require(Hq % Hkv == 0 && Hq / Hkv <= 4, "attention expects a GQA group of <= 4 heads");
   if (T == 0) return;
   hipLaunchKernelGGL(attention_kernel, dim3(T * Hkv), dim3(256), 0, S(stream), P<const uint16_t>(q),
                      P<const uint16_t>(kc), P<const uint16_t>(vc), P<const int32_t>(pos),
-                     P<const int32_t>(slot), Hq, Hkv, max_ctx, scale, P<uint16_t>(out));
+                     P<const int32_t>(slot), Hq, Hkv, max_ctx, n_slots, scale, P<uint16_t>(out));
   check_launch();
 }
 
@@ -161,7 +161,8 @@ static void attention(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, ui
 // The first n_dec tiles are 1-token decode tiles (wave-per-item decode
 // kernel); the rest go to the MFMA segment kernel.  Rows are disjoint.
 static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t tiles, int n_tiles, int n_dec,
-                            int Hq, int Hkv, int max_ctx, float scale, uintptr_t out, uintptr_t stream) {
+                            int Hq, int Hkv, int max_ctx, int n_slots, int T, float scale, uintptr_t out,
+                            uintptr_t stream) {
   require(Hq == 4 * Hkv, "attention_tiles expects a GQA group of exactly 4 heads");
   require(0 <= n_dec && n_dec <= n_tiles, "n_dec out of range");
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -169,13 +170,14 @@ static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t t
     const int items = n_dec * Hkv;
     hipLaunchKernelGGL(attention_dec_kernel, dim3((items + 3) / 4), dim3(256), 0, S(stream), P<const uint16_t>(q),
                        P<const uint16_t>(kc), P<const uint16_t>(vc), P<const int32_t>(tiles), items, Hq, Hkv,
-                       max_ctx, scale_log2, P<uint16_t>(out));
+                       max_ctx, n_slots, T, scale_log2, P<uint16_t>(out));
     check_launch();
   }
   if (n_tiles > n_dec) {
     hipLaunchKernelGGL(attention_seg_kernel, dim3((n_tiles - n_dec) * Hkv), dim3(256), 0, S(stream),
                        P<const uint16_t>(q), P<const uint16_t>(kc), P<const uint16_t>(vc),
-                       P<const int32_t>(tiles) + 4 * n_dec, Hq, Hkv, max_ctx, scale_log2, P<uint16_t>(out));
+                       P<const int32_t>(tiles) + 4 * n_dec, Hq, Hkv, max_ctx, n_slots, T, scale_log2,
+                       P<uint16_t>(out));
     check_launch();
   }
 }

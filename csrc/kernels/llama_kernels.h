@@ -114,7 +114,7 @@ silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out, int
 __global__ void __launch_bounds__(256)
 rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos,
                const int32_t* __restrict__ slot, const float* __restrict__ cos_t,
-               const float* __restrict__ sin_t, int Hq, int Hkv, int max_ctx,
+               const float* __restrict__ sin_t, int Hq, int Hkv, int max_ctx, int n_slots,
                uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc) {
   const int t = blockIdx.x;
   const int tid = threadIdx.x;
@@ -122,6 +122,9 @@ rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos
   const int hg = tid >> 6;           // 4 head groups
   const int p = pos[t];
   const int s = slot[t];
+  // a corrupt descriptor must not become a wild KV-cache write (GPU fault):
+  // out-of-range (slot, pos) rows are dropped
+  if ((unsigned)s >= (unsigned)n_slots || (unsigned)p >= (unsigned)max_ctx) return;
   const float c = cos_t[(int64_t)p * 64 + i];
   const float sn = sin_t[(int64_t)p * 64 + i];
   const int64_t row = (int64_t)t * (Hq + 2 * Hkv) * 128;
@@ -150,7 +153,7 @@ constexpr int AT_ROW = 136;  // 128 bf16 + 8 pad (272 B rows)
 __global__ void __launch_bounds__(256)
 attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                  const uint16_t* __restrict__ vc, const int32_t* __restrict__ pos,
-                 const int32_t* __restrict__ slot, int Hq, int Hkv, int max_ctx, float scale,
+                 const int32_t* __restrict__ slot, int Hq, int Hkv, int max_ctx, int n_slots, float scale,
                  uint16_t* __restrict__ out) {
   __shared__ __align__(16) uint16_t Ks[AT_KEYS * AT_ROW];
   __shared__ __align__(16) uint16_t Vs[AT_KEYS * AT_ROW];
@@ -165,6 +168,7 @@ attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc
   const int h = g * group + wv;
   const int ctx = pos[t] + 1;
   const int s = slot[t];
+  if ((unsigned)s >= (unsigned)n_slots || ctx < 1 || ctx > max_ctx) return;   // whole block: no barrier skipped
   const int64_t kvbase = ((int64_t)s * Hkv + g) * max_ctx * 128;
 
   if (wv < group) {
@@ -255,7 +259,7 @@ constexpr int SA_PROW = 72;   // P row : 64 keys + 8 pad
 __global__ void __launch_bounds__(256)
 attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                      const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int Hq, int Hkv,
-                     int max_ctx, float scale_log2, uint16_t* __restrict__ out) {
+                     int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
   __shared__ __align__(16) uint16_t Ks[SA_KEYS * 128];
   __shared__ __align__(16) uint16_t Vt[128 * SA_VROW];
   __shared__ __align__(16) uint16_t Ps[4][16 * SA_PROW];
@@ -269,6 +273,10 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   const int n = tiles[tile * 4 + 1];
   const int s = tiles[tile * 4 + 2];
   const int pos0 = tiles[tile * 4 + 3];
+  // block-uniform descriptor check (before any barrier): a corrupt tile is skipped, never dereferenced
+  if ((unsigned)s >= (unsigned)n_slots || n < 1 || n > 16 || pos0 < 0 || pos0 + n > max_ctx || tok0 < 0 ||
+      tok0 + n > T)
+    return;
   const int h = g * 4 + wv;
   const int ctx = pos0 + n;
   const int64_t kvbase = ((int64_t)s * Hkv + g) * max_ctx * 128;
@@ -398,7 +406,7 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
 __global__ void __launch_bounds__(256)
 attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                      const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int n_items, int Hq,
-                     int Hkv, int max_ctx, float scale_log2, uint16_t* __restrict__ out) {
+                     int Hkv, int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
   __shared__ __align__(16) float qs[4][4][128];
   __shared__ float ps[4][4][64];
   const int lane = threadIdx.x & 63;
@@ -410,6 +418,7 @@ attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   const int row = tiles[tile * 4 + 0];
   const int s = tiles[tile * 4 + 2];
   const int ctx = tiles[tile * 4 + 3] + 1;
+  if ((unsigned)s >= (unsigned)n_slots || ctx < 1 || ctx > max_ctx || (unsigned)row >= (unsigned)T) return;
   const int64_t kvbase = ((int64_t)s * Hkv + g) * max_ctx * 128;
   {  // q of the 4 heads -> LDS (fp32, pre-scaled by scale*log2e)
     const int hh = lane >> 4, d0 = (lane & 15) * 8;

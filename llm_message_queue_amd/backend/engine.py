@@ -127,6 +127,7 @@ class BackendEngine:
         self.completed_tokens = 0
         self._q: Deque[_Inflight] = collections.deque()
         self._reaped: List[_Inflight] = []               # reaped by launch(), not yet returned
+        self._fence: List[object] = []                   # events of steps dropped by abort_all
         self.host_ns = np.zeros(2, dtype=np.int64)       # [batch build, wait for GPU] host time
         self._prev_out = None                            # device int32 [n_samples] of the last launched step
         # double-buffered pinned staging (a buffer is reused only after the
@@ -322,6 +323,11 @@ class BackendEngine:
         so it is safe after a device error; reap first if the GPU is fine."""
         out = [r for f in list(self._q) + self._reaped for r in f.completed]
         out += list(self.active.values())
+        # steps still queued on the GPU keep reading their pinned staging
+        # buffers (the async H2D copy may not have run yet): the next launch
+        # must not refill a buffer before they finish, so their events stay
+        # as a fence (waited in launch; a dead device raises there instead)
+        self._fence.extend(f.event for f in self._q if f.event is not None)
         self._q.clear()
         self._reaped = []
         self._prev_out = None
@@ -348,6 +354,10 @@ class BackendEngine:
             if self.fault.get("slow_ms"):
                 time.sleep(self.fault["slow_ms"] / 1e3)
         ts = time.perf_counter_ns()
+        if self._fence:                                # steps dropped by abort_all still in flight
+            for ev in self._fence:
+                ev.synchronize()
+            self._fence = []
         while len(self._q) >= self.max_inflight:       # bound the run-ahead (and staging reuse)
             if wait_cb is None:
                 self._reaped.append(self._reap(block=True))  # handed to the next finish()

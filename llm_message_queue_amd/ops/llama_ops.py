@@ -68,7 +68,7 @@ class HipOps:
             raise ValueError("kv cache shape mismatch")
         q = q_out if q_out is not None else torch.empty((T, Hq * 128), dtype=qkv.dtype, device=qkv.device)
         self.k.rope_kv(qkv.data_ptr(), pos.data_ptr(), slot.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), T,
-                       Hq, Hkv, max_ctx, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), _stream(qkv))
+                       Hq, Hkv, max_ctx, S, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), _stream(qkv))
         return q
 
     def attention(self, q, kc, vc, pos, slot, Hq, Hkv, scale, out=None):
@@ -77,7 +77,7 @@ class HipOps:
         max_ctx = kc.shape[2]
         o = out if out is not None else torch.empty_like(q)
         self.k.attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), pos.data_ptr(), slot.data_ptr(), T, Hq, Hkv,
-                         max_ctx, float(scale), o.data_ptr(), _stream(q))
+                         max_ctx, kc.shape[0], float(scale), o.data_ptr(), _stream(q))
         return o
 
 
@@ -91,7 +91,8 @@ class HipOps:
             raise ValueError("tiles must be a contiguous int32 [n, 4] tensor")
         o = out if out is not None else torch.empty_like(q)
         self.k.attention_tiles(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), tiles.data_ptr(), tiles.shape[0],
-                               int(n_dec), Hq, Hkv, kc.shape[2], float(scale), o.data_ptr(), _stream(q))
+                               int(n_dec), Hq, Hkv, kc.shape[2], kc.shape[0], q.shape[0], float(scale),
+                               o.data_ptr(), _stream(q))
         return o
 
 
