@@ -13,6 +13,9 @@ gateway must show under overload:
     tiers first and keep serving realtime;
   * latency of the SERVED requests (arrival -> dispatch, arrival -> last
     token) per tier: bounded by the deadline, not by the backlog;
+  * ordering: each run compares FIFO within a tier (the reference's order)
+    with adaptive LIFO (``queue.adaptive_lifo``: an overloaded tier serves
+    its newest request, the stale head is shed at its deadline);
   * failures: ``--fault-every N`` injects a backend launch failure every N
     ticks; the evacuated in-flight requests are re-queued (and shed to the
     DLQ like any other request if their deadline passes).
@@ -44,6 +47,9 @@ def main() -> None:
     ap.add_argument("--deadline-ms", type=float, default=1000.0, help="per-request timeout (queue deadline)")
     ap.add_argument("--queue-max", type=int, default=10000, help="per-tier queue bound (QUEUE_FULL beyond)")
     ap.add_argument("--fault-every", type=int, default=0, help="inject a backend launch fault every N ticks")
+    ap.add_argument("--policies", default="fifo,adaptive_lifo", help="comma list: fifo, adaptive_lifo")
+    ap.add_argument("--lifo-after-ms", type=float, default=0.0,
+                    help="adaptive LIFO threshold (0 = each tier's aging deadline)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--cpu", action="store_true", help="control-flow check on CPU (tiny model); not a measurement")
     a = ap.parse_args()
@@ -95,65 +101,85 @@ def main() -> None:
         gw.tick()
     rate = a.overload * cap
 
-    # ---- overload phase
-    served_tier = np.zeros(ntier, dtype=np.int64)
-    expired_tier = np.zeros(ntier, dtype=np.int64)
-    gw.on_complete = lambda m: served_tier.__setitem__(m.tier, served_tier[m.tier] + 1)
-    gw.on_expire = lambda m: expired_tier.__setitem__(gw.tier_of_queue.get(m.queue_name, ntier - 1),
-                                                      expired_tier[gw.tier_of_queue.get(m.queue_name, ntier - 1)] + 1)
-    gw.rec.reset()
-    gw.rec_done.reset()
-    c0 = dict(gw.counters)
+    # ---- overload phases: FIFO within a tier (the reference's order), then adaptive LIFO
     deadline_ns = int(a.deadline_ms * 1e6)
-    arrivals = PoissonArrivals(rate, seed=3)
-    faults = 0
-    gc.collect()
-    gc.freeze()
-    gc.disable()
-    start = time.monotonic()
-    arrivals.reset(start)
+    lifo = [int(a.lifo_after_ms * 1e6) if a.lifo_after_ms > 0 else int(lv.max_wait_time)
+            for lv in sorted(cfg.queue.levels, key=lambda lv: lv.priority)]
 
-    def pump():
-        due = arrivals.due(time.monotonic())
-        if due:
-            msgs = wl.make(len(due))
-            for m, ts in zip(msgs, due):
-                m.arrival_ns = int(ts * 1e9)
-                m.timeout = deadline_ns
-            gw.submit(msgs)
+    def phase(policy: str, seed: int) -> dict:
+        gw.lifo_ns = lifo if policy == "adaptive_lifo" else None
+        served_tier = np.zeros(ntier, dtype=np.int64)
+        expired_tier = np.zeros(ntier, dtype=np.int64)
+        gw.on_complete = lambda m: served_tier.__setitem__(m.tier, served_tier[m.tier] + 1)
 
-    ticks = 0
-    while time.monotonic() - start < a.seconds:
-        pump()
-        if a.fault_every and ticks and ticks % a.fault_every == 0:
-            engine.inject(fail_launch=1)
-            faults += 1
-        gw.tick(pump=pump)
-        if not gw.healthy:          # an injected fault evacuated the backend: bring it back
-            gw.set_healthy(True)
-        ticks += 1
-    elapsed = time.monotonic() - start
-    gc.enable()
-    c1 = gw.counters
-    lat = gw.rec.summary()
-    gw.flush_latency()
-    done = gw.rec_done.summary()
+        def on_expire(m):
+            t = gw.tier_of_queue.get(m.queue_name, ntier - 1)
+            expired_tier[t] += 1
+        gw.on_expire = on_expire
+        gw.rec.reset()
+        gw.rec_done.reset()
+        c0 = dict(gw.counters)
+        d0 = dlq.size()
+        arrivals = PoissonArrivals(rate, seed=seed)
+        faults = 0
+        gc.collect()
+        gc.freeze()
+        gc.disable()
+        start = time.monotonic()
+        arrivals.reset(start)
+
+        def pump():
+            due = arrivals.due(time.monotonic())
+            if due:
+                msgs = wl.make(len(due))
+                for m, ts in zip(msgs, due):
+                    m.arrival_ns = int(ts * 1e9)
+                    m.timeout = deadline_ns
+                gw.submit(msgs)
+
+        ticks = 0
+        while time.monotonic() - start < a.seconds:
+            pump()
+            if a.fault_every and ticks and ticks % a.fault_every == 0:
+                engine.inject(fail_launch=1)
+                faults += 1
+            gw.tick(pump=pump)
+            if not gw.healthy:          # an injected fault evacuated the backend: bring it back
+                gw.set_healthy(True)
+            ticks += 1
+        elapsed = time.monotonic() - start
+        gc.enable()
+        c1 = gw.counters
+        lat = gw.rec.summary()
+        gw.flush_latency()
+        done = gw.rec_done.summary()
+        res = {
+            "policy": policy, "seconds": round(elapsed, 2),
+            "goodput_rps": round((c1["completed"] - c0["completed"]) / elapsed, 1),
+            "dispatched_rps": round((c1["dispatched"] - c0["dispatched"]) / elapsed, 1),
+            "submitted": c1["submitted"] - c0["submitted"],
+            "rejected_queue_full": c1["rejected"] - c0["rejected"],
+            "expired_to_dlq": c1["expired"] - c0["expired"], "dlq_added": dlq.size() - d0,
+            "served_by_tier": served_tier.tolist(), "expired_by_tier": expired_tier.tolist(),
+            "served_p50_arrival_to_dispatch_ms": round(lat["p50_ms"], 1),
+            "served_p99_arrival_to_dispatch_ms_by_tier": [round(x, 1) for x in lat["p99_by_tier_ms"]],
+            "served_p99_e2e_ms_by_tier": [round(x, 1) for x in done["p99_by_tier_ms"]],
+            "served_p50_e2e_ms": round(done["p50_ms"], 1),
+            "faults_injected": faults, "evacuated": c1["evacuated"] - c0["evacuated"],
+        }
+        # drain between phases (untimed): drop the backlog, finish in-flight work
+        gw.drop_pending()
+        while engine.inflight() or gw.pending():
+            gw.tick()
+        return res
+
+    phases = [phase(p, 3 + i) for i, p in enumerate(a.policies.split(","))]
     out = {
         "bench": "sustained overload" + (" (CPU control-flow check, not a measurement)" if a.cpu else ""),
         "model": a.model, "slots": a.slots,
         "calibrated_capacity_rps": round(cap, 1), "offered_rps": round(rate, 1), "overload": a.overload,
-        "deadline_ms": a.deadline_ms, "queue_max_per_tier": a.queue_max, "seconds": round(elapsed, 2),
-        "goodput_rps": round((c1["completed"] - c0["completed"]) / elapsed, 1),
-        "dispatched_rps": round((c1["dispatched"] - c0["dispatched"]) / elapsed, 1),
-        "submitted": c1["submitted"] - c0["submitted"],
-        "rejected_queue_full": c1["rejected"] - c0["rejected"],
-        "expired_to_dlq": c1["expired"] - c0["expired"], "dlq_size": dlq.size(),
-        "served_by_tier": served_tier.tolist(), "expired_by_tier": expired_tier.tolist(),
-        "served_p99_arrival_to_dispatch_ms_by_tier": [round(x, 1) for x in lat["p99_by_tier_ms"]],
-        "served_p99_e2e_ms_by_tier": [round(x, 1) for x in done["p99_by_tier_ms"]],
-        "served_p50_e2e_ms": round(done["p50_ms"], 1),
-        "faults_injected": faults, "evacuated": c1["evacuated"] - c0["evacuated"],
-        "still_queued": gw.pending(),
+        "deadline_ms": a.deadline_ms, "queue_max_per_tier": a.queue_max, "lifo_after_ns": lifo,
+        "phases": phases,
     }
     line = json.dumps(out)
     print(line, flush=True)

@@ -115,6 +115,24 @@ class NamedQueue {
     return false;
   }
 
+  // newest item of the most urgent non-empty bucket (adaptive LIFO)
+  bool pop_tail_locked(Item* out, int64_t now) {
+    for (auto& b : buckets_) {
+      if (!b.ring.empty()) {
+        *out = b.ring.back();
+        b.ring.pop_back();
+        size_--;
+        st_.pending--;
+        st_.processing++;
+        st_.popped++;
+        st_.total_wait_ns += now - out->enq_ns;
+        st_.last_update_ns = now;
+        return true;
+      }
+    }
+    return false;
+  }
+
   // remove a specific handle (admin DELETE /queues/:type/:id)
   bool remove_locked(int64_t handle, int64_t now) {
     for (auto& b : buckets_) {
@@ -252,11 +270,19 @@ class MultiLevelQueue {
   // Dispatcher batch pop: strict priority over `tiers` (ordered most urgent
   // first) with aging and per-tier budgets (<0 = unlimited).  Appends to
   // (hs, ti, enq): handle, tier index, enqueue time.
+  //
+  // Adaptive LIFO (`lifo_ns`, optional, per tier, 0 = off): while a tier's
+  // head has waited longer than lifo_ns[i] the tier is overloaded, and its
+  // NEWEST request is served instead of the oldest -- served requests keep a
+  // short queue wait and the stale head runs into its deadline and is shed
+  // (the gateway's expiry), instead of every request waiting nearly the
+  // whole deadline under FIFO.  FIFO resumes once the head is younger.
   void pop_tiers(const std::vector<std::string>& tiers, int64_t count, const std::vector<int64_t>& aging_ns,
                  std::vector<int64_t> budget, std::vector<int64_t>& hs, std::vector<int32_t>& ti,
-                 std::vector<int64_t>& enq) {
+                 std::vector<int64_t>& enq, const std::vector<int64_t>& lifo_ns = {}) {
     const size_t T = tiers.size();
-    if (aging_ns.size() != T || budget.size() != T) throw std::invalid_argument("tier arg mismatch");
+    if (aging_ns.size() != T || budget.size() != T || (!lifo_ns.empty() && lifo_ns.size() != T))
+      throw std::invalid_argument("tier arg mismatch");
     std::vector<std::shared_ptr<NamedQueue>> qs(T);
     for (size_t i = 0; i < T; ++i) qs[i] = get(tiers[i]);
     {
@@ -282,7 +308,11 @@ class MultiLevelQueue {
         }
         if (pick < 0) break;
         Item it;
-        qs[pick]->pop_locked(&it, now);
+        const Item* h = qs[pick]->head_locked();
+        if (!lifo_ns.empty() && lifo_ns[pick] > 0 && now - h->enq_ns > lifo_ns[pick])
+          qs[pick]->pop_tail_locked(&it, now);
+        else
+          qs[pick]->pop_locked(&it, now);
         hs.push_back(it.handle);
         enq.push_back(it.enq_ns);
         ti.push_back(pick);

@@ -148,6 +148,9 @@ class Gateway:
         self.tier_prio = [lv.priority for lv in levels]
         self.tier_of_queue = {n: i for i, n in enumerate(self.tiers)}
         self.aging_ns = [lv.max_wait_time if q.enable_aging else 0 for lv in levels]
+        la = int(getattr(q, "lifo_after", 0))
+        self.lifo_ns = ([la if la > 0 else int(lv.max_wait_time) for lv in levels]
+                        if getattr(q, "adaptive_lifo", False) else None)
         self.max_conc = [lv.max_concurrent for lv in levels]
         for n in self.tiers:                          # D1: the level queues exist
             self.qm.create_queue(n)
@@ -358,7 +361,7 @@ class Gateway:
         free = self.engine.admit_capacity()
         if free <= 0:
             return 0
-        msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets())
+        msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets(), self.lifo_ns)
         if not msgs:
             return 0
         if self.shed_expired:     # expired requests behind a live tier head
@@ -417,7 +420,7 @@ class Gateway:
         mine = quota[me]                              # [W, 4]
         per_tier = mine.sum(axis=0)
         msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, int(per_tier.sum()), [0] * len(self.tiers),
-                                                [int(x) for x in per_tier])
+                                                [int(x) for x in per_tier], self.lifo_ns)
         by_tier: Dict[int, List[Message]] = {t: [] for t in range(len(self.tiers))}
         for m, t in zip(msgs, tier_idx):
             m.tier = int(t)

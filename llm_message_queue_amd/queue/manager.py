@@ -186,8 +186,8 @@ class QueueManager:
         return msgs
 
     def pop_tiers(self, tiers: Sequence[str], count: int, aging_ns: Sequence[int],
-                  budget: Sequence[int]):
-        msgs, tier_idx, enq = self.mlq.pop_tiers(tiers, count, aging_ns, budget)
+                  budget: Sequence[int], lifo_ns: Optional[Sequence[int]] = None):
+        msgs, tier_idx, enq = self.mlq.pop_tiers(tiers, count, aging_ns, budget, lifo_ns)
         if self.metrics and msgs:
             for m in msgs:
                 p = priority_name(m.priority)

@@ -127,6 +127,12 @@ class QueueConfig:
     # reference's per-message processing deadline, 30 s default) has elapsed
     # since arrival goes to the dead-letter queue instead of a GPU slot
     shed_expired: bool = True
+    # adaptive LIFO under overload: while a tier's head has waited longer than
+    # ``lifo_after`` (0 = that tier's max_wait_time) serve the newest request
+    # of the tier; FIFO otherwise.  Pairs with shed_expired (the stale head
+    # is shed at its deadline).  Off = the reference's FIFO-within-priority.
+    adaptive_lifo: bool = False
+    lifo_after: int = 0
 
 
 @dataclass
@@ -302,7 +308,7 @@ _DURATION_FIELDS = {
     "max_wait_time", "monitor_interval", "cleanup_interval", "max_retention_period",
     "process_interval", "initial_backoff", "max_backoff", "check_interval", "timeout",
     "health_check_interval", "session_timeout", "heartbeat_timeout", "autoscale_cooldown",
-    "max_idle_time",
+    "max_idle_time", "lifo_after",
 }
 
 

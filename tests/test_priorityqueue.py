@@ -119,6 +119,27 @@ def test_pop_tiers_strict_priority_aging_and_budgets():
     assert [m.content for m in msgs] == ["l2"]
 
 
+def test_pop_tiers_adaptive_lifo():
+    """While a tier's head is older than its LIFO threshold, the newest
+    request is served (overload); FIFO otherwise."""
+    q = mlq4()
+    for i in range(4):
+        q.push("normal", new_message("c", "u", f"n{i}", 3))
+    time.sleep(0.01)
+    # head younger than 1 s: FIFO
+    msgs, _, _ = q.pop_tiers(LEVELS, 1, [0] * 4, [-1] * 4, [0, 0, 1_000_000_000, 0])
+    assert msgs[0].content == "n0"
+    # head older than 1 ms: newest first; other tiers unaffected
+    q.push("high", new_message("c", "u", "h0", 2))
+    q.push("high", new_message("c", "u", "h1", 2))
+    msgs, tiers, _ = q.pop_tiers(LEVELS, 4, [0] * 4, [-1] * 4, [0, 0, 1_000_000, 0])
+    assert [m.content for m in msgs] == ["h0", "h1", "n3", "n2"] and list(tiers) == [1, 1, 2, 2]
+    st = q.get_stats("normal")
+    assert st.pending_count == 1 and st.processing_count == 3
+    with pytest.raises(Exception):
+        q.pop_tiers(LEVELS, 1, [0] * 4, [-1] * 4, [0, 0])          # per-tier lengths must match
+
+
 def test_concurrent_push_pop_no_loss():
     q = MultiLevelQueue(0)
     for n in LEVELS:
