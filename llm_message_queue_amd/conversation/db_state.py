@@ -7,10 +7,14 @@ ids are ``conv_<unixnano>`` (`:271-273`).  ``add_message`` inserts the
 message, bumps ``message_count`` and appends completed contents to
 ``context`` (`:116-138`).
 
-Here the relational store is stdlib ``sqlite3`` (GORM/Postgres is not in this
-image) and the optional Redis level is the RESP client (``resp.RespClient``).
-The reference's two Redis client majors (go-redis v8 + v9, D25) collapse into
-one client.
+The relational store is Postgres (as in the reference, spoken over the wire
+protocol by ``pgwire.PgConnection`` -- no driver package in this image) or
+stdlib ``sqlite3`` for single-node deployments and tests; the statements
+are written once, in the dialect both accept (``?`` placeholders converted
+to ``$n`` for Postgres, ``INSERT ... ON CONFLICT (id) DO UPDATE`` upserts,
+BIGINT nanosecond timestamps).  The optional Redis level is the RESP client
+(``resp.RespClient``).  The reference's two Redis client majors (go-redis
+v8 + v9, D25) collapse into one client.
 """
 from __future__ import annotations
 
@@ -26,9 +30,46 @@ _CONV_COLS = ("id", "user_id", "title", "context", "status", "state", "priority"
               "last_activity", "last_active_time", "created_at", "updated_at", "completed_at", "metadata")
 
 
-class DBStateManager:
-    def __init__(self, path: str = ":memory:", redis=None, redis_ttl_s: int = 24 * 3600):
+class _SQLiteDB:
+    def __init__(self, path: str):
         self.db = sqlite3.connect(path, check_same_thread=False)
+
+    def execute(self, sql: str, params=()) -> list:
+        cur = self.db.execute(sql, tuple(params))
+        rows = cur.fetchall()
+        self.db.commit()
+        return rows
+
+    def close(self) -> None:
+        self.db.close()
+
+
+class _PostgresDB:
+    def __init__(self, conn):
+        self.conn = conn
+
+    def execute(self, sql: str, params=()) -> list:
+        from .pgwire import qmark_to_dollar
+        return self.conn.execute(qmark_to_dollar(sql), tuple(params)).rows
+
+    def close(self) -> None:
+        self.conn.close()
+
+
+_MSG_UPSERT = ("INSERT INTO messages VALUES (?,?,?,?,?) ON CONFLICT (id) DO UPDATE SET "
+               "conversation_id = excluded.conversation_id, user_id = excluded.user_id, "
+               "created_at = excluded.created_at, doc = excluded.doc")
+
+
+class DBStateManager:
+    def __init__(self, path: str = ":memory:", redis=None, redis_ttl_s: int = 24 * 3600, pg=None):
+        """``pg``: a ``pgwire.PgConnection`` (or DSN string) -> Postgres;
+        otherwise SQLite at ``path``."""
+        if pg is not None:
+            from .pgwire import PgConnection
+            self.db = _PostgresDB(PgConnection.from_dsn(pg) if isinstance(pg, str) else pg)
+        else:
+            self.db = _SQLiteDB(path)
         self.redis = redis
         self.redis_ttl_s = redis_ttl_s
         self._lock = threading.RLock()
@@ -36,14 +77,21 @@ class DBStateManager:
         self._last_id = 0
         with self._lock:
             self.db.execute("CREATE TABLE IF NOT EXISTS conversations (id TEXT PRIMARY KEY, user_id TEXT, "
-                            "title TEXT, context TEXT, status TEXT, state TEXT, priority INTEGER, "
-                            "message_count INTEGER, last_activity INTEGER, last_active_time INTEGER, "
-                            "created_at INTEGER, updated_at INTEGER, completed_at INTEGER, metadata TEXT)")
+                            "title TEXT, context TEXT, status TEXT, state TEXT, priority BIGINT, "
+                            "message_count BIGINT, last_activity BIGINT, last_active_time BIGINT, "
+                            "created_at BIGINT, updated_at BIGINT, completed_at BIGINT, metadata TEXT)")
             self.db.execute("CREATE TABLE IF NOT EXISTS messages (id TEXT PRIMARY KEY, conversation_id TEXT, "
-                            "user_id TEXT, created_at INTEGER, doc TEXT)")
+                            "user_id TEXT, created_at BIGINT, doc TEXT)")
             self.db.execute("CREATE INDEX IF NOT EXISTS msg_conv ON messages(conversation_id)")
             self.db.execute("CREATE INDEX IF NOT EXISTS conv_user ON conversations(user_id)")
-            self.db.commit()
+
+    @classmethod
+    def from_config(cls, cfg, redis=None) -> "DBStateManager":
+        """``database.backend``: postgres -> the configured server; else SQLite."""
+        if (cfg.database.backend or "").lower() == "postgres":
+            from .persistence import postgres_dsn
+            return cls(pg=postgres_dsn(cfg), redis=redis)
+        return cls(cfg.database.sqlite_path, redis=redis)
 
     # ------------------------------------------------------------------ helpers
     def _gen_id(self) -> str:
@@ -94,7 +142,6 @@ class DBStateManager:
             self.db.execute(f"INSERT INTO conversations VALUES ({','.join('?' * len(_CONV_COLS))})",
                             (conv.id, user_id, title, "", "active", "", int(priority), 0, now, now, now, now, 0,
                              "{}"))
-            self.db.commit()
         self._cache_put(conv)
         return conv
 
@@ -114,8 +161,9 @@ class DBStateManager:
                     self._cache[c.id] = c
                 return c
         with self._lock:
-            row = self.db.execute(f"SELECT {','.join(_CONV_COLS)} FROM conversations WHERE id = ?",
-                                  (conversation_id,)).fetchone()
+            rows = self.db.execute(f"SELECT {','.join(_CONV_COLS)} FROM conversations WHERE id = ?",
+                                   (conversation_id,))
+        row = rows[0] if rows else None
         if row is None:
             raise ConversationNotFound(conversation_id)
         c = self._row_to_conv(row)
@@ -129,17 +177,15 @@ class DBStateManager:
             with self._lock:
                 self.db.execute(f"UPDATE conversations SET {', '.join(c + ' = ?' for c in cols)} WHERE id = ?",
                                 (*vals, conversation_id))
-                self.db.commit()
         self._invalidate(conversation_id)
 
     def add_message(self, conversation_id: str, message: Message) -> None:
         conv = self.get_conversation(conversation_id)
         message.conversation_id = conversation_id
         with self._lock:
-            self.db.execute("INSERT OR REPLACE INTO messages VALUES (?,?,?,?,?)",
+            self.db.execute(_MSG_UPSERT,
                             (message.id, conversation_id, message.user_id, message.created_at or time.time_ns(),
                              json.dumps(message.to_dict())))
-            self.db.commit()
         now = time.time_ns()
         upd = {"message_count": conv.message_count + 1, "last_activity": now, "updated_at": now}
         if message.status == MessageStatus.COMPLETED:
@@ -149,13 +195,13 @@ class DBStateManager:
     def get_conversation_messages(self, conversation_id: str, limit: int = 100) -> List[Message]:
         with self._lock:
             rows = self.db.execute("SELECT doc FROM messages WHERE conversation_id = ? ORDER BY created_at DESC "
-                                   "LIMIT ?", (conversation_id, int(limit))).fetchall()
+                                   "LIMIT ?", (conversation_id, int(limit)))
         return [Message.from_dict(json.loads(r[0])) for r in rows]
 
     def get_user_conversations(self, user_id: str, limit: int = 100) -> List[Conversation]:
         with self._lock:
             rows = self.db.execute(f"SELECT {','.join(_CONV_COLS)} FROM conversations WHERE user_id = ? "
-                                   "ORDER BY last_activity DESC LIMIT ?", (user_id, int(limit))).fetchall()
+                                   "ORDER BY last_activity DESC LIMIT ?", (user_id, int(limit)))
         return [self._row_to_conv(r) for r in rows]
 
     def archive_conversation(self, conversation_id: str) -> None:
@@ -164,13 +210,12 @@ class DBStateManager:
     def delete_conversation(self, conversation_id: str) -> None:
         with self._lock:
             self.db.execute("DELETE FROM conversations WHERE id = ?", (conversation_id,))
-            self.db.commit()
         self._invalidate(conversation_id)
 
     def get_active_conversations(self, limit: int = 100) -> List[Conversation]:
         with self._lock:
             rows = self.db.execute(f"SELECT {','.join(_CONV_COLS)} FROM conversations WHERE status = 'active' "
-                                   "ORDER BY last_activity DESC LIMIT ?", (int(limit),)).fetchall()
+                                   "ORDER BY last_activity DESC LIMIT ?", (int(limit),))
         return [self._row_to_conv(r) for r in rows]
 
     def update_conversation_priority(self, conversation_id: str, priority: int) -> None:
@@ -181,15 +226,14 @@ class DBStateManager:
 
     def update_message(self, message: Message) -> None:
         with self._lock:
-            self.db.execute("INSERT OR REPLACE INTO messages VALUES (?,?,?,?,?)",
+            self.db.execute(_MSG_UPSERT,
                             (message.id, message.conversation_id, message.user_id,
                              message.created_at or time.time_ns(), json.dumps(message.to_dict())))
-            self.db.commit()
 
     def get_message(self, message_id: str) -> Optional[Message]:
         with self._lock:
-            row = self.db.execute("SELECT doc FROM messages WHERE id = ?", (message_id,)).fetchone()
-        return None if row is None else Message.from_dict(json.loads(row[0]))
+            rows = self.db.execute("SELECT doc FROM messages WHERE id = ?", (message_id,))
+        return Message.from_dict(json.loads(rows[0][0])) if rows else None
 
     def close(self) -> None:
         with self._lock:

@@ -171,52 +171,50 @@ class RedisPersistenceStore(PersistenceStore):
 
 
 class PostgresPersistenceStore(PersistenceStore):
-    """Requires ``psycopg2`` (absent from this image)."""
+    """``PostgresPersistenceStore`` (`persistence.go:162-320`): one row per
+    conversation with the reference's ``ConversationModel`` columns
+    (`:168-177`), upserted on save.  Speaks the wire protocol itself
+    (``pgwire.PgConnection``; no driver package in this image)."""
 
-    def __init__(self, dsn: str):
-        try:
-            import psycopg2  # noqa: F401
-        except ImportError as e:
-            raise RuntimeError("PostgresPersistenceStore needs psycopg2, which is not installed; "
-                               "use the sqlite or redis backend") from e
-        import psycopg2
-        self._conn = psycopg2.connect(dsn)
-        self._lock = threading.Lock()
-        with self._lock, self._conn.cursor() as cur:
-            cur.execute("CREATE TABLE IF NOT EXISTS conversations (id TEXT PRIMARY KEY, user_id TEXT, "
-                        "created_at TIMESTAMPTZ, last_active_time TIMESTAMPTZ, completed_at TIMESTAMPTZ, "
-                        "state TEXT, messages JSONB, metadata JSONB, doc BYTEA)")
-            self._conn.commit()
+    def __init__(self, dsn_or_conn):
+        from .pgwire import PgConnection
+        self._conn = PgConnection.from_dsn(dsn_or_conn) if isinstance(dsn_or_conn, str) else dsn_or_conn
+        self._conn.simple("CREATE TABLE IF NOT EXISTS conversation_models (id TEXT PRIMARY KEY, user_id TEXT, "
+                          "created_at BIGINT, last_active_time BIGINT, completed_at BIGINT, state TEXT, "
+                          "messages TEXT, metadata TEXT, doc TEXT);"
+                          "CREATE INDEX IF NOT EXISTS conversation_models_user ON conversation_models (user_id)")
 
-    def save_conversation(self, conv):  # pragma: no cover - needs a server
-        doc = _dump(conv)
+    def save_conversation(self, conv):
+        doc = _dump(conv).decode()
         d = json.loads(doc)
-        with self._lock, self._conn.cursor() as cur:
-            cur.execute("INSERT INTO conversations VALUES (%s,%s,%s,%s,%s,%s,%s,%s,%s) ON CONFLICT (id) DO UPDATE "
-                        "SET last_active_time=EXCLUDED.last_active_time, completed_at=EXCLUDED.completed_at, "
-                        "state=EXCLUDED.state, messages=EXCLUDED.messages, metadata=EXCLUDED.metadata, doc=EXCLUDED.doc",
-                        (conv.id, conv.user_id, d["created_at"], d["last_active_time"],
-                         d["completed_at"] if conv.completed_at else None, conv.state,
-                         json.dumps(d["messages"]), json.dumps(conv.metadata), doc))
-            self._conn.commit()
+        self._conn.execute(
+            "INSERT INTO conversation_models VALUES ($1,$2,$3,$4,$5,$6,$7,$8,$9) ON CONFLICT (id) DO UPDATE "
+            "SET last_active_time = excluded.last_active_time, completed_at = excluded.completed_at, "
+            "state = excluded.state, messages = excluded.messages, metadata = excluded.metadata, doc = excluded.doc",
+            (conv.id, conv.user_id, int(conv.created_at or 0), int(conv.last_active_time or 0),
+             int(conv.completed_at) if conv.completed_at else None, conv.state,
+             json.dumps(d.get("messages", [])), json.dumps(conv.metadata), doc))
 
-    def load_conversation(self, conversation_id):  # pragma: no cover
-        with self._lock, self._conn.cursor() as cur:
-            cur.execute("SELECT doc FROM conversations WHERE id = %s", (conversation_id,))
-            row = cur.fetchone()
+    def load_conversation(self, conversation_id):
+        row = self._conn.execute("SELECT doc FROM conversation_models WHERE id = $1", (conversation_id,)).fetchone()
         if row is None:
             raise ConversationNotFound(conversation_id)
-        return _load(bytes(row[0]))
+        return _load(row[0].encode())
 
-    def list_user_conversations(self, user_id):  # pragma: no cover
-        with self._lock, self._conn.cursor() as cur:
-            cur.execute("SELECT id FROM conversations WHERE user_id = %s ORDER BY id", (user_id,))
-            return [r[0] for r in cur.fetchall()]
+    def list_user_conversations(self, user_id):
+        rows = self._conn.execute("SELECT id FROM conversation_models WHERE user_id = $1 ORDER BY id", (user_id,))
+        return [r[0] for r in rows.rows]
 
-    def delete_conversation(self, conversation_id):  # pragma: no cover
-        with self._lock, self._conn.cursor() as cur:
-            cur.execute("DELETE FROM conversations WHERE id = %s", (conversation_id,))
-            self._conn.commit()
+    def delete_conversation(self, conversation_id):
+        self._conn.execute("DELETE FROM conversation_models WHERE id = $1", (conversation_id,))
+
+    def close(self):
+        self._conn.close()
+
+
+def postgres_dsn(cfg) -> str:
+    p = cfg.database.postgres
+    return f"host={p.host} port={p.port} user={p.user} password={p.password} dbname={p.dbname} sslmode={p.sslmode}"
 
 
 def make_store(cfg) -> Optional[PersistenceStore]:
@@ -234,7 +232,5 @@ def make_store(cfg) -> Optional[PersistenceStore]:
         return RedisPersistenceStore(RespClient(r.addr, r.password, r.db), "conversation:",
                                      cfg.queue.max_retention_period)
     if b == "postgres":
-        p = cfg.database.postgres
-        return PostgresPersistenceStore(
-            f"host={p.host} port={p.port} user={p.user} password={p.password} dbname={p.dbname} sslmode={p.sslmode}")
+        return PostgresPersistenceStore(postgres_dsn(cfg))
     raise ValueError(f"unknown persistence backend {b!r}")

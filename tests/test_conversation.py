@@ -9,6 +9,7 @@ import pytest
 from llm_message_queue_amd.conversation.db_state import DBStateManager
 from llm_message_queue_amd.conversation.persistence import (MemoryPersistenceStore, PostgresPersistenceStore,
                                                             RedisPersistenceStore, SQLitePersistenceStore)
+from llm_message_queue_amd.conversation.pgwire import MiniPostgres, PgConnection, PgError, qmark_to_dollar
 from llm_message_queue_amd.conversation.resp import MiniRedis, RespClient
 from llm_message_queue_amd.conversation.state_manager import DAY_NS, StateManager
 from llm_message_queue_amd.conversation.summarise import SummaryEngine
@@ -78,13 +79,16 @@ def test_cleanup_rules():
     assert s.find_conversation(fresh.id) is fresh
 
 
-@pytest.mark.parametrize("kind", ["memory", "sqlite", "redis"])
+@pytest.mark.parametrize("kind", ["memory", "sqlite", "redis", "postgres"])
 def test_persistence_roundtrip(kind, tmp_path):
     srv = None
     if kind == "memory":
         store = MemoryPersistenceStore()
     elif kind == "sqlite":
         store = SQLitePersistenceStore(str(tmp_path / "s.db"))
+    elif kind == "postgres":
+        srv = MiniPostgres(password="pw")
+        store = PostgresPersistenceStore(f"host=127.0.0.1 port={srv.port} user=postgres password=pw dbname=llm_queue")
     else:
         srv = MiniRedis()
         store = RedisPersistenceStore(RespClient(srv.addr), "conversation:", 3600 * 1_000_000_000)
@@ -96,6 +100,9 @@ def test_persistence_roundtrip(kind, tmp_path):
         got = store.load_conversation("c1")
         assert got.user_id == "u1" and got.messages[0].content == "hello" and got.summary_vec == [0.5] * 4
         assert store.list_user_conversations("u1") == ["c1"]
+        c.messages.append(new_message("c1", "u1", "again", 3))
+        store.save_conversation(c)                  # upsert
+        assert len(store.load_conversation("c1").messages) == 2
         store.delete_conversation("c1")
         assert store.list_user_conversations("u1") == []
         with pytest.raises(ConversationNotFound):
@@ -105,13 +112,36 @@ def test_persistence_roundtrip(kind, tmp_path):
             srv.close()
 
 
-def test_postgres_store_gated():
+@pytest.mark.parametrize("auth", ["scram", "md5", "password", "trust"])
+def test_pgwire_auth_params_and_errors(auth):
+    """The wire-protocol client against the in-process protocol-v3 server:
+    every auth method, typed parameters (never spliced into SQL), NULLs,
+    errors with SQLSTATE, and the connection staying usable after one."""
+    srv = MiniPostgres(password="s3cret", auth=auth)
     try:
-        import psycopg2  # noqa: F401
-        pytest.skip("psycopg2 present")
-    except ImportError:
-        with pytest.raises(RuntimeError):
-            PostgresPersistenceStore("host=localhost")
+        if auth == "trust":
+            PgConnection("127.0.0.1", srv.port, "postgres", "anything", "db").close()
+        else:
+            with pytest.raises(PgError) as ei:
+                PgConnection("127.0.0.1", srv.port, "postgres", "wrong", "db")
+            assert ei.value.sqlstate == "28P01"
+        pg = PgConnection("127.0.0.1", srv.port, "postgres", "s3cret", "db")
+        pg.simple("CREATE TABLE t (id TEXT PRIMARY KEY, n BIGINT, x DOUBLE PRECISION, note TEXT)")
+        evil = "a'); DROP TABLE t; --"
+        assert pg.execute("INSERT INTO t VALUES ($1, $2, $3, $4)", ("k1", 2 ** 40, 0.5, evil)).rowcount == 1
+        pg.execute("INSERT INTO t VALUES ($1, $2, $3, $4)", ("k2", None, None, None))
+        rows = pg.execute("SELECT id, n, x, note FROM t ORDER BY id").rows
+        assert rows == [("k1", 2 ** 40, 0.5, evil), ("k2", None, None, None)]
+        with pytest.raises(PgError) as e2:
+            pg.execute("INSERT INTO t VALUES ($1, $2, $3, $4)", ("k1", 1, 1.0, ""))
+        assert e2.value.sqlstate == "23505"                      # unique violation
+        with pytest.raises(PgError):
+            pg.execute("SELEC nonsense")
+        assert pg.execute("SELECT count(*) FROM t").rows == [(2,)] and pg.txn_status == "I"
+        assert qmark_to_dollar("a = ? AND b = '?' AND c = ?") == "a = $1 AND b = '?' AND c = $2"
+        pg.close()
+    finally:
+        srv.close()
 
 
 def test_async_write_behind_and_reload():
@@ -149,10 +179,16 @@ def test_summarise_on_evict_cpu_reference():
     assert s.pending_evictions() == 0
 
 
-def test_db_state_manager_with_redis_cache():
+@pytest.mark.parametrize("sql", ["sqlite", "postgres"])
+def test_db_state_manager_with_redis_cache(sql):
     srv = MiniRedis()
+    pgs = MiniPostgres(password="pw") if sql == "postgres" else None
     try:
-        db = DBStateManager(":memory:", redis=RespClient(srv.addr))
+        if pgs is not None:
+            db = DBStateManager(pg=f"host=127.0.0.1 port={pgs.port} user=postgres password=pw dbname=q",
+                                redis=RespClient(srv.addr))
+        else:
+            db = DBStateManager(":memory:", redis=RespClient(srv.addr))
         c = db.create_conversation("u1", "title", 2)
         assert c.id.startswith("conv_") and c.status == "active"
         m = new_message(c.id, "u1", "first answer", 3)
@@ -175,8 +211,12 @@ def test_db_state_manager_with_redis_cache():
         db.delete_conversation(c.id)
         with pytest.raises(ConversationNotFound):
             db.get_conversation(c.id)
+        if pgs is not None:
+            assert pgs.statements > 10                 # really went over the wire
     finally:
         srv.close()
+        if pgs is not None:
+            pgs.close()
 
 
 def test_resp_client_ttl_and_sets():
