@@ -90,3 +90,69 @@ def test_telemetry_snapshot_or_unavailable(served):
         mine = [s for s in snap if (tel.gpu_map.get(s["gpu"], s["gpu"]) if tel.gpu_map else s["gpu"]) == 0]
         assert mine and mine[0]["valid"] and mine[0]["hbm_total_mb"] > 100_000, (snap, tel.gpu_map)
         assert served.app_.gateway.healthy              # telemetry of other GPUs never evacuates ours
+
+
+def test_backend_fault_evacuation_with_steps_in_flight():
+    """Launch faults while 2 steps are queued on the GPU: the evacuated
+    requests are re-queued and completed, and the steps dropped by the
+    evacuation finish before their pinned staging buffers are refilled
+    (regression: refilling them under an in-flight H2D fed the kernels
+    mismatched descriptors)."""
+    from llm_message_queue_amd.backend.engine import BackendEngine
+    from llm_message_queue_amd.gateway.router import Gateway
+    from llm_message_queue_amd.gateway.workload import Workload
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.utils.config import default_config
+
+    cfg = default_config()
+    cfg.queue.enable_metrics = False
+    eng = BackendEngine(LlamaConfig.tiny(), slots=32, max_ctx=64, token_budget=256, device="cuda:0", impl="hip",
+                        max_inflight=2)
+    gw = Gateway(cfg, engine=eng, use_gpu_preprocess=True, prompt_cap=16, gen_tokens=3)
+    gw.submit(Workload(seed=3).make(200))
+    faults = 0
+    for i in range(400):
+        if i % 7 == 3 and faults < 10:
+            eng.inject(fail_launch=1)
+            faults += 1
+        gw.tick()
+        if not gw.healthy:
+            gw.set_healthy(True)
+        if gw.counters["completed"] >= 200:
+            break
+    torch.cuda.synchronize()
+    assert faults == 10 and gw.counters["evacuated"] > 0
+    assert gw.counters["completed"] >= 200, gw.counters
+
+
+def test_overload_expiry_and_adaptive_lifo_on_gpu():
+    """Requests past their deadline are shed to the DLQ, never dispatched;
+    with adaptive LIFO the newest requests of an overloaded tier go first."""
+    from llm_message_queue_amd.backend.engine import BackendEngine
+    from llm_message_queue_amd.gateway.router import Gateway
+    from llm_message_queue_amd.gateway.workload import Workload
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.queue.dead_letter import DeadLetterQueue
+    from llm_message_queue_amd.utils.config import default_config
+
+    cfg = default_config()
+    cfg.queue.enable_metrics = False
+    cfg.queue.adaptive_lifo = True
+    cfg.queue.lifo_after = 1_000_000                      # 1 ms
+    dlq = DeadLetterQueue()
+    eng = BackendEngine(LlamaConfig.tiny(), slots=8, max_ctx=64, token_budget=128, device="cuda:0", impl="hip")
+    gw = Gateway(cfg, engine=eng, use_gpu_preprocess=True, prompt_cap=16, gen_tokens=2, dead_letter=dlq)
+    msgs = Workload(seed=4).make(64)
+    now = time.monotonic_ns()
+    for i, m in enumerate(msgs):
+        m.timeout = 200_000_000 if i < 16 else 30_000_000_000
+        m.arrival_ns = now - (500_000_000 if i < 16 else 0)
+    gw.submit(msgs)
+    for _ in range(200):
+        gw.tick()
+        if gw.counters["completed"] + gw.counters["expired"] >= 64:
+            break
+    torch.cuda.synchronize()
+    assert gw.counters["expired"] == 16 and dlq.size() == 16
+    assert all(m.status == "timeout" and not m.dispatched_at for m in msgs[:16])
+    assert gw.counters["completed"] == 48
