@@ -82,7 +82,7 @@ class _Inflight:
 class BackendEngine:
     def __init__(self, model_cfg: LlamaConfig, slots: int = 256, max_ctx: int = 512,
                  token_budget: int = 2048, device="cuda", impl: str = "hip", seed: int = 0,
-                 page=None, gpu_index: int = 0, max_inflight: int = 2):
+                 page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True):
         self.cfg = model_cfg
         self.slots = slots
         self.max_ctx = max_ctx
@@ -91,7 +91,8 @@ class BackendEngine:
         self.token_budget = max(token_budget, slots)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
-        self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed)
+        self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed,
+                               residual_in_gemm=residual_in_gemm)
         self.impl = impl
         self.active: Dict[int, Request] = {}            # slot -> request
         self.free: List[int] = list(range(slots - 1, -1, -1))

@@ -7,8 +7,9 @@ real GPU worker so load signals (in-flight slots, HBM) are live.
 
 Forward = one continuous-batching step over T tokens (chunked-prefill and
 decode tokens mixed).  GEMMs: ``torch.nn.functional.linear`` (hipBLASLt).
-Everything else: hand-written HIP kernels (``ops.llama_ops.HipOps``):
-residual-add+RMSNorm, RoPE + KV-cache write, segment-tiled MFMA GQA attention
+The o / down projections accumulate into the residual stream in the GEMM
+epilogue (beta = 1).  Everything else: hand-written HIP kernels
+(``ops.llama_ops.HipOps``): RMSNorm (optionally fused with the residual add), RoPE + KV-cache write, segment-tiled MFMA GQA attention
 over the slot KV cache (prefill chunks and decode tokens), SiLU*up.
 """
 from __future__ import annotations
@@ -62,7 +63,7 @@ class LlamaConfig:
 
 class LlamaStub:
     def __init__(self, cfg: LlamaConfig, slots: int, max_ctx: int, device="cuda", impl: str = "hip",
-                 seed: int = 0, dtype=torch.bfloat16):
+                 seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -71,6 +72,12 @@ class LlamaStub:
         self.impl = impl
         self.slots = slots
         self.max_ctx = max_ctx
+        # o / down projections accumulate straight into the residual stream
+        # (hipBLASLt beta = 1: res += a @ W^T, one rounding); the following
+        # RMSNorm then only reads res -- half its HBM traffic
+        # (profiles/r1_gemm_experiments.md).  False: F.linear + fused
+        # residual-add RMSNorm.
+        self.residual_in_gemm = residual_in_gemm
         g = torch.Generator(device=self.device).manual_seed(seed)
         std = 0.02
 
@@ -117,15 +124,26 @@ class LlamaStub:
         tokens into per-slot segments for the MFMA attention kernel (its first
         ``n_dec`` rows are 1-token decode tiles); without it attention runs
         per token."""
+        xf = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec)
+        sel = xf.index_select(0, sample_idx)
+        logits = F.linear(sel, self.lm_head)
+        return torch.argmax(logits, dim=-1).to(torch.int32)
+
+    @torch.no_grad()
+    def hidden(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
+               tiles: Optional[torch.Tensor] = None, n_dec: int = 0) -> torch.Tensor:
+        """The 32-layer trunk: final-normed hidden states [T, d] (writes the
+        step's K/V into the cache)."""
         cfg, ops = self.cfg, self.ops
-        T = tokens.shape[0]
         h = F.embedding(tokens, self.embed)              # [T, d]
         res = h.clone()
         x = ops.rmsnorm(h, self.layers[0]["attn_norm"], cfg.eps)
         out = None
+        fused = self.residual_in_gemm
         for i, L in enumerate(self.layers):
             if i > 0:
-                x = ops.rmsnorm(out, L["attn_norm"], cfg.eps, residual=res)
+                x = ops.rmsnorm(res, L["attn_norm"], cfg.eps) if fused else \
+                    ops.rmsnorm(out, L["attn_norm"], cfg.eps, residual=res)
             qkv = F.linear(x, L["wqkv"])
             q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
                             self.kcache[i], self.vcache[i])
@@ -135,12 +153,16 @@ class LlamaStub:
             else:
                 a = ops.attention(q, self.kcache[i], self.vcache[i], pos, slot, cfg.heads, cfg.kv_heads,
                                   self.scale)
-            ao = F.linear(a, L["wo"])
-            x2 = ops.rmsnorm(ao, L["mlp_norm"], cfg.eps, residual=res)
+            if fused:
+                res.addmm_(a, L["wo"].t())
+                x2 = ops.rmsnorm(res, L["mlp_norm"], cfg.eps)
+            else:
+                x2 = ops.rmsnorm(F.linear(a, L["wo"]), L["mlp_norm"], cfg.eps, residual=res)
             gu = F.linear(x2, L["w_gu"])
             act = ops.silu_mul(gu)
-            out = F.linear(act, L["w_down"])
-        xf = ops.rmsnorm(out, self.final_norm, cfg.eps, residual=res)
-        sel = xf.index_select(0, sample_idx)
-        logits = F.linear(sel, self.lm_head)
-        return torch.argmax(logits, dim=-1).to(torch.int32)
+            if fused:
+                res.addmm_(act, L["w_down"].t())
+            else:
+                out = F.linear(act, L["w_down"])
+        return ops.rmsnorm(res, self.final_norm, cfg.eps) if fused else \
+            ops.rmsnorm(out, self.final_norm, cfg.eps, residual=res)

@@ -511,3 +511,19 @@ def test_expired_requests_behind_a_live_head_are_shed_at_pop():
     gw.dispatch()
     assert gw.counters["expired"] == 4 and gw.counters["dispatched"] == 4 and dlq.size() == 4
     assert all(m.status == "timeout" for m in msgs[1::2])
+
+
+def test_residual_in_gemm_matches_fused_norm_path():
+    """o/down accumulating into the residual stream (addmm, beta = 1) gives
+    the same trunk output as F.linear + residual-add RMSNorm (bf16 rounding
+    differs by one step)."""
+    from llm_message_queue_amd.models.llama_stub import LlamaStub
+    cfg = LlamaConfig(vocab=512, dim=2048, layers=2, heads=16, kv_heads=4, ffn=512)
+    a = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, residual_in_gemm=True)
+    b = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, residual_in_gemm=False)
+    tok = torch.randint(0, cfg.vocab, (12,), generator=torch.Generator().manual_seed(0))
+    pos = torch.tensor(list(range(6)) * 2, dtype=torch.int32)
+    slot = torch.tensor([0] * 6 + [1] * 6, dtype=torch.int32)
+    ha, hb = a.hidden(tok, pos, slot).float(), b.hidden(tok, pos, slot).float()
+    assert torch.allclose(ha, hb, atol=5e-2, rtol=5e-2), (ha - hb).abs().max()
+    assert torch.allclose(a.kcache[1], b.kcache[1], atol=5e-2, rtol=5e-2)

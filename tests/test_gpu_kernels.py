@@ -273,6 +273,14 @@ def test_tiny_model_forward_hip_vs_ref():
     assert a.shape == (2,) and (a == c).float().mean().item() >= 0.5
     # greedy tokens may differ on near-ties; hidden-state agreement is checked per op above
     assert (a == b).float().mean().item() >= 0.5
+    # trunk: HIP kernels + residual-in-GEMM vs PyTorch fp32-accumulating reference ops
+    # without it (fresh caches so both see the same context)
+    m3 = LlamaStub(cfg, slots=4, max_ctx=64, device=DEV, impl="hip", seed=3, residual_in_gemm=True)
+    m4 = LlamaStub(cfg, slots=4, max_ctx=64, device=DEV, impl="ref", seed=3, residual_in_gemm=False)
+    h3 = m3.hidden(tok, pos, slot, tiles=tiles).float()
+    h4 = m4.hidden(tok, pos, slot).float()
+    err = ((h3 - h4).abs().max() / h4.abs().max()).item()
+    assert err < 5e-2, err
 
 
 # ----------------------------------------------------------------------------- summarise
