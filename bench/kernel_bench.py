@@ -80,8 +80,17 @@ def main() -> None:
         tiles = torch.from_numpy(make_tiles(starts, lens, slots, pos0)).to(dev)
         q = torch.randn(T, Hq * 128, device=dev).to(torch.bfloat16)
         o = torch.empty_like(q)
-        ms = timeit(lambda: ops.attention_tiles(q, kc, vc, tiles, Hq, Hkv, 128 ** -0.5, out=o, n_dec=768), a.reps)
-        rec("attention_tiles_step", ms, tokens=T, decode=768)
+        for sk in (32, 64):
+            ms = timeit(lambda: ops.attention_tiles(q, kc, vc, tiles, Hq, Hkv, 128 ** -0.5, out=o, n_dec=768,
+                                                    seg_keys=sk), a.reps)
+            rec(f"attention_tiles_step_seg{sk}", ms, tokens=T, decode=768)
+            seg = tiles[768:].contiguous()
+            ms = timeit(lambda: ops.attention_tiles(q, kc, vc, seg, Hq, Hkv, 128 ** -0.5, out=o, n_dec=0,
+                                                    seg_keys=sk), a.reps)
+            rec(f"attention_seg_only_keys{sk}", ms, tiles=int(seg.shape[0]))
+        dec = tiles[:768].contiguous()
+        ms = timeit(lambda: ops.attention_tiles(q, kc, vc, dec, Hq, Hkv, 128 ** -0.5, out=o, n_dec=768), a.reps)
+        rec("attention_dec_only", ms, tokens=768)
         pos = torch.tensor(sum([list(range(p, p + n)) for p, n in zip(pos0, lens)], []), dtype=torch.int32,
                            device=dev)
         slot = torch.tensor(sum([[s] * n for s, n in zip(slots, lens)], []), dtype=torch.int32, device=dev)

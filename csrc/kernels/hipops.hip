@@ -162,7 +162,8 @@ static void attention(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, ui
 // kernel); the rest go to the MFMA segment kernel.  Rows are disjoint.
 static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t tiles, int n_tiles, int n_dec,
                             int Hq, int Hkv, int max_ctx, int n_slots, int T, float scale, uintptr_t out,
-                            uintptr_t stream) {
+                            uintptr_t stream, int seg_keys) {
+  require(seg_keys == 32 || seg_keys == 64, "seg_keys must be 32 or 64");
   require(Hq == 4 * Hkv, "attention_tiles expects a GQA group of exactly 4 heads");
   require(0 <= n_dec && n_dec <= n_tiles, "n_dec out of range");
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -174,7 +175,8 @@ static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t t
     check_launch();
   }
   if (n_tiles > n_dec) {
-    hipLaunchKernelGGL(attention_seg_kernel, dim3((n_tiles - n_dec) * Hkv), dim3(256), 0, S(stream),
+    auto kern = seg_keys == 32 ? attention_seg_kernel<32> : attention_seg_kernel<64>;
+    hipLaunchKernelGGL(kern, dim3((n_tiles - n_dec) * Hkv), dim3(256), 0, S(stream),
                        P<const uint16_t>(q), P<const uint16_t>(kc), P<const uint16_t>(vc),
                        P<const int32_t>(tiles) + 4 * n_dec, Hq, Hkv, max_ctx, n_slots, T, scale_log2,
                        P<uint16_t>(out));

@@ -252,14 +252,23 @@ attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc
 //               V is staged TRANSPOSED (Vt[dim][key], 2 keys packed per
 //               dword write) so B fragments are 16-B reads; 8 dim tiles x
 //               2 k-steps per 64 keys, O in 32 accumulator VGPRs.
-constexpr int SA_KEYS = 64;
-constexpr int SA_VROW = 72;   // Vt row: 64 keys + 8 pad (144 B)
-constexpr int SA_PROW = 72;   // P row : 64 keys + 8 pad
-
+//
+// KEYS (32 or 64) is the key block per iteration.  Serving prompts are short
+// (<= 32 tokens), so the 32-key block does no masked MFMA work on them and
+// halves the LDS and score registers: more workgroups resident per CU, and
+// this latency-bound kernel runs in fewer rounds.  Long dialog contexts loop
+// over more blocks.
+template <int KEYS>
 __global__ void __launch_bounds__(256)
 attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                      const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int Hq, int Hkv,
                      int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
+  static_assert(KEYS == 32 || KEYS == 64, "key block");
+  constexpr int SA_KEYS = KEYS;
+  constexpr int SA_VROW = KEYS + 8;   // Vt row: KEYS keys + 8 pad
+  constexpr int SA_PROW = KEYS + 8;   // P row
+  constexpr int NJ = KEYS / 16;       // 16-key score tiles per block
+  constexpr int NKS = KEYS / 32;      // 32-key PV k-steps per block
   __shared__ __align__(16) uint16_t Ks[SA_KEYS * 128];
   __shared__ __align__(16) uint16_t Vt[128 * SA_VROW];
   __shared__ __align__(16) uint16_t Ps[4][16 * SA_PROW];
@@ -297,9 +306,9 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
 
   for (int k0 = 0; k0 < ctx; k0 += SA_KEYS) {
     __syncthreads();
-    // K: 64 keys x 16 chunks, row-coalesced, chunk-swizzled
+    // K: KEYS keys x 16 chunks, row-coalesced, chunk-swizzled
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < KEYS / 16; ++r) {
       const int c = tid + r * 256;
       const int key = c >> 4, ch = c & 15;
       uint4 kv = make_uint4(0u, 0u, 0u, 0u);
@@ -308,9 +317,9 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
     }
     // V^T: item = (key pair kp, chunk ch); two keys per dword store
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < KEYS / 32; ++r) {
       const int c = tid + r * 256;
-      const int kp = c & 31, ch = c >> 5;
+      const int kp = c % (KEYS / 2), ch = c / (KEYS / 2);
       const int ka = k0 + 2 * kp;
       uint4 va = make_uint4(0u, 0u, 0u, 0u), vb = make_uint4(0u, 0u, 0u, 0u);
       if (ka < ctx) va = *reinterpret_cast<const uint4*>(vc + kvbase + (int64_t)ka * 128 + ch * 8);
@@ -324,9 +333,9 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
     __syncthreads();
 
     // ---- S = Q K^T (C layout: sc[j][k] = S[row 4fq+k][key k0 + 16j + fr])
-    f32x4 sc[4];
+    f32x4 sc[NJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       sc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -341,7 +350,7 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
       const int lim = (row < n) ? pos0 + row : -1;       // causal: key <= position
       float mx = -3.0e38f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int key = k0 + j * 16 + fr;
         const float v = (key <= lim) ? sc[j][k] * scale_log2 : -3.0e38f;
         sc[j][k] = v;
@@ -353,7 +362,7 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
       const float corr = exp2f(mrow[k] - mn);
       float sum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int key = k0 + j * 16 + fr;
         const float p = (key <= lim) ? exp2f(sc[j][k] - mn) : 0.f;
         sum += p;
@@ -370,7 +379,7 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
     __builtin_amdgcn_wave_barrier();
     // ---- O += P V
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < NKS; ++ks) {
       const bf16x8 pf = *reinterpret_cast<const bf16x8*>(P + fr * SA_PROW + ks * 32 + fq * 8);
 #pragma unroll
       for (int nt = 0; nt < 8; ++nt) {
@@ -469,7 +478,8 @@ attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
     __builtin_amdgcn_wave_barrier();
     const int nk = min(64, ctx - k0);
     const uint16_t* vr = vc + kvbase + (int64_t)k0 * 128 + lane * 2;
-    for (int j = 0; j < nk; ++j) {
+#pragma unroll 8
+    for (int j = 0; j < nk; ++j) {   // unrolled: 8 independent V-row loads in flight per wave
       const uint32_t v2 = *reinterpret_cast<const uint32_t*>(vr + (int64_t)j * 128);
       const float vlo = bf((uint16_t)(v2 & 0xFFFFu)), vhi = bf((uint16_t)(v2 >> 16));
 #pragma unroll

@@ -172,7 +172,7 @@ class RefOps:
             return out
         return res
 
-    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None, n_dec: int = 0):
+    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None, n_dec: int = 0, seg_keys: int = 32):
         """Reference: expand tiles to per-token (pos, slot) and reuse ``attention``."""
         t = tiles.cpu().long()
         T = q.shape[0]

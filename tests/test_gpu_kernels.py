@@ -243,6 +243,10 @@ def test_attention_tiles_mfma_vs_ref(ops):
     o2 = ref.attention_tiles(q, kc, vc, torch.from_numpy(tiles), Hq, Hkv, 128 ** -0.5)
     err = (o1.float() - o2.float()).abs().max().item()
     assert err < 3e-2, err
+    # the 64-key block variant (contexts crossing 32- and 64-key blocks)
+    o1b = hip.attention_tiles(q, kc, vc, torch.from_numpy(tiles).to(DEV), Hq, Hkv, 128 ** -0.5, seg_keys=64)
+    err = (o1b.float() - o2.float()).abs().max().item()
+    assert err < 3e-2, err
     # per-token kernel agrees too (same rows)
     pos = torch.zeros(T, dtype=torch.int32)
     slot = torch.zeros(T, dtype=torch.int32)
