@@ -81,18 +81,19 @@ class HipOps:
         return o
 
 
-    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None, n_dec: int = 0):
+    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None, n_dec: int = 0, seg_keys: int = 32):
         """Tiled attention; ``tiles`` int32 [n, 4] on the device = (first
         token row, n <= 16, slot, first position).  The first ``n_dec`` tiles
         must be 1-token (decode) tiles: they run on the wave-per-item decode
-        kernel, the rest on the MFMA segment kernel."""
+        kernel, the rest on the MFMA segment kernel (``seg_keys`` keys per
+        block: 32 or 64)."""
         _check(q, torch.bfloat16, "q")
         if tiles.dtype != torch.int32 or tiles.dim() != 2 or tiles.shape[1] != 4 or not tiles.is_contiguous():
             raise ValueError("tiles must be a contiguous int32 [n, 4] tensor")
         o = out if out is not None else torch.empty_like(q)
         self.k.attention_tiles(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), tiles.data_ptr(), tiles.shape[0],
                                int(n_dec), Hq, Hkv, kc.shape[2], kc.shape[0], q.shape[0], float(scale),
-                               o.data_ptr(), _stream(q))
+                               o.data_ptr(), _stream(q), int(seg_keys))
         return o
 
 
