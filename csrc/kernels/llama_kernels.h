@@ -259,7 +259,7 @@ attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc
 // this latency-bound kernel runs in fewer rounds.  Long dialog contexts loop
 // over more blocks.
 template <int KEYS>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, KEYS == 32 ? 4 : 3)
 attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                      const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int Hq, int Hkv,
                      int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
