@@ -406,17 +406,24 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
 // group's 4 query heads handled together by that wave, 4 independent items
 // per 256-thread workgroup (no block barrier).  A decode token attends a
 // short context (tens to hundreds of keys) that no other token of the step
-// shares, so the kernel is latency-bound: no LDS staging of K/V, lane j owns
-// key k0+j and streams its 256-B K row straight from memory for the 4 dot
-// products; P goes through 1 KiB of per-wave LDS; P*V walks the keys with
-// one coalesced 256-B V row per step, each lane accumulating 2 dims x 4
-// heads.  ~40 VGPRs -> full occupancy, so thousands of these waves overlap
-// their memory latency.
+// shares, so the kernel is latency-bound and is laid out to shorten the
+// dependent chain per wave:
+//   * scores: 8 keys per pass, 8 lanes per key, each lane 16 dims of the K
+//     row (two 16-B loads; the 8 lanes of a key read its 256-B row) against
+//     the 4 heads' q slices held in registers as bf16 pairs,
+//     v_dot2c_f32_bf16 (fp32 accumulate); the 8 partial dots are combined
+//     with 3 xor-shuffles.  A 26-key context is 4 passes of 2 loads + 32 dot2
+//     per lane (a lane-per-key layout idles 60% of the lanes on it);
+//   * online softmax over the 64-key block with lane = key (wave max/sum);
+//   * P.V: the two half-waves take even / odd keys, each lane 4 dims (one
+//     8-B load per key; a half-wave reads a 256-B V row), so the serial key
+//     loop is half as long; the halves are summed with one xor-32 shuffle.
+// LDS: 1 KiB of scores/probabilities per wave.
 __global__ void __launch_bounds__(256)
 attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                      const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int n_items, int Hq,
                      int Hkv, int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
-  __shared__ __align__(16) float qs[4][4][128];
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   __shared__ float ps[4][4][64];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -429,73 +436,101 @@ attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   const int ctx = tiles[tile * 4 + 3] + 1;
   if ((unsigned)s >= (unsigned)n_slots || ctx < 1 || ctx > max_ctx || (unsigned)row >= (unsigned)T) return;
   const int64_t kvbase = ((int64_t)s * Hkv + g) * max_ctx * 128;
-  {  // q of the 4 heads -> LDS (fp32, pre-scaled by scale*log2e)
-    const int hh = lane >> 4, d0 = (lane & 15) * 8;
-    const u16x8 v = *reinterpret_cast<const u16x8*>(q + ((int64_t)row * Hq + g * 4 + hh) * 128 + d0);
+  const int part = lane & 7, ksub = lane >> 3;         // score layout: 8 keys x 8 dim-parts of 16
+  uint32_t qv[4][8];                                   // q of head h, dims [part*16, +16), bf16 pairs
 #pragma unroll
-    for (int i = 0; i < 8; ++i) qs[wv][hh][d0 + i] = bf(v[i]) * scale_log2;
+  for (int h = 0; h < 4; ++h) {
+    const uint4* src = reinterpret_cast<const uint4*>(q + ((int64_t)row * Hq + g * 4 + h) * 128 + part * 16);
+    const uint4 a = src[0], b = src[1];
+    qv[h][0] = a.x; qv[h][1] = a.y; qv[h][2] = a.z; qv[h][3] = a.w;
+    qv[h][4] = b.x; qv[h][5] = b.y; qv[h][6] = b.z; qv[h][7] = b.w;
   }
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_wave_barrier();
-  float m[4], l[4], a0[4], a1[4];
+  float m[4], l[4], acc[4][4];
 #pragma unroll
-  for (int h = 0; h < 4; ++h) { m[h] = -3.0e38f; l[h] = 0.f; a0[h] = 0.f; a1[h] = 0.f; }
-
+  for (int h = 0; h < 4; ++h) {
+    m[h] = -3.0e38f;
+    l[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[h][i] = 0.f;
+  }
+  const int kh = lane >> 5, dp = lane & 31;            // P.V layout: key parity x 4-dim slices
   for (int k0 = 0; k0 < ctx; k0 += 64) {
-    const int key = k0 + lane;
-    const bool live = key < ctx;
-    float sc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (live) {
-      const uint16_t* kr = kc + kvbase + (int64_t)key * 128;
-#pragma unroll 4
-      for (int ch = 0; ch < 16; ++ch) {
-        const u16x8 kk = *reinterpret_cast<const u16x8*>(kr + ch * 8);
-        float kf[8];
+    const int nk = min(64, ctx - k0);
+    // ---- scores of keys k0 .. k0+nk-1 (pre-scaled by scale*log2e) -> ps
+    for (int kb = 0; kb < nk; kb += 8) {
+      const int key = kb + ksub;
+      float d[4] = {0.f, 0.f, 0.f, 0.f};
+      if (key < nk) {
+        const uint4* kr = reinterpret_cast<const uint4*>(kc + kvbase + (int64_t)(k0 + key) * 128 + part * 16);
+        const uint4 a = kr[0], b = kr[1];
+        const uint32_t kw[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) kf[i] = bf(kk[i]);
+        for (int h = 0; h < 4; ++h)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const float4 qa = *reinterpret_cast<const float4*>(&qs[wv][h][ch * 8]);
-          const float4 qb = *reinterpret_cast<const float4*>(&qs[wv][h][ch * 8 + 4]);
-          sc[h] += qa.x * kf[0] + qa.y * kf[1] + qa.z * kf[2] + qa.w * kf[3] +
-                   qb.x * kf[4] + qb.y * kf[5] + qb.z * kf[6] + qb.w * kf[7];
-        }
+          for (int i = 0; i < 8; ++i)
+            d[h] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qv[h][i]),
+                                                   __builtin_bit_cast(bf16x2_t, kw[i]), d[h], false);
+      }
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        d[h] += __shfl_xor(d[h], 1, 64);
+        d[h] += __shfl_xor(d[h], 2, 64);
+        d[h] += __shfl_xor(d[h], 4, 64);
+      }
+      if (part == 0 && key < nk) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) ps[wv][h][key] = d[h] * scale_log2;
       }
     }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    // ---- online softmax over the block, lane = key
+    const bool live = lane < nk;
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      const float v = live ? sc[h] : -3.0e38f;
+      const float v = live ? ps[wv][h][lane] : -3.0e38f;
       const float mn = fmaxf(m[h], wave_max(v));
       const float p = live ? exp2f(v - mn) : 0.f;
       const float corr = exp2f(m[h] - mn);
       l[h] = l[h] * corr + wave_sum(p);
-      a0[h] *= corr;
-      a1[h] *= corr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[h][i] *= corr;
       m[h] = mn;
       ps[wv][h][lane] = p;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
-    const int nk = min(64, ctx - k0);
-    const uint16_t* vr = vc + kvbase + (int64_t)k0 * 128 + lane * 2;
-#pragma unroll 8
-    for (int j = 0; j < nk; ++j) {   // unrolled: 8 independent V-row loads in flight per wave
-      const uint32_t v2 = *reinterpret_cast<const uint32_t*>(vr + (int64_t)j * 128);
-      const float vlo = bf((uint16_t)(v2 & 0xFFFFu)), vhi = bf((uint16_t)(v2 >> 16));
+    // ---- O += P V (half-wave kh takes keys of parity kh)
+    const uint16_t* vr = vc + kvbase + (int64_t)k0 * 128 + dp * 4;
+#pragma unroll 4
+    for (int j = kh; j < nk; j += 2) {
+      const uint2 v2 = *reinterpret_cast<const uint2*>(vr + (int64_t)j * 128);
+      const float v0 = bf((uint16_t)(v2.x & 0xFFFFu)), v1 = bf((uint16_t)(v2.x >> 16));
+      const float v2f = bf((uint16_t)(v2.y & 0xFFFFu)), v3 = bf((uint16_t)(v2.y >> 16));
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
         const float p = ps[wv][h][j];
-        a0[h] += p * vlo;
-        a1[h] += p * vhi;
+        acc[h][0] += p * v0;
+        acc[h][1] += p * v1;
+        acc[h][2] += p * v2f;
+        acc[h][3] += p * v3;
       }
     }
     __builtin_amdgcn_wave_barrier();          // ps is rewritten by the next block
   }
 #pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    const float inv = 1.0f / l[h];
-    const uint32_t o = (uint32_t)f32_to_bf16_rne(a0[h] * inv) | ((uint32_t)f32_to_bf16_rne(a1[h] * inv) << 16);
-    *reinterpret_cast<uint32_t*>(out + ((int64_t)row * Hq + g * 4 + h) * 128 + lane * 2) = o;
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[h][i] += __shfl_xor(acc[h][i], 32, 64);
+  if (kh == 0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const float inv = 1.0f / l[h];
+      uint2 o;
+      o.x = (uint32_t)f32_to_bf16_rne(acc[h][0] * inv) | ((uint32_t)f32_to_bf16_rne(acc[h][1] * inv) << 16);
+      o.y = (uint32_t)f32_to_bf16_rne(acc[h][2] * inv) | ((uint32_t)f32_to_bf16_rne(acc[h][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(out + ((int64_t)row * Hq + g * 4 + h) * 128 + dp * 4) = o;
+    }
   }
 }
 
