@@ -88,6 +88,20 @@ def main() -> None:
             ms = timeit(lambda: ops.attention_tiles(q, kc, vc, seg, Hq, Hkv, 128 ** -0.5, out=o, n_dec=0,
                                                     seg_keys=sk), a.reps)
             rec(f"attention_seg_only_keys{sk}", ms, tiles=int(seg.shape[0]))
+        # long dialog contexts: 256 chunks of 4..32 new tokens at positions 100..460
+        starts2, lens2, slots2, pos2 = [], [], [], []
+        row2 = 0
+        for i in range(256):
+            n = int(rng.integers(4, 33))
+            starts2.append(row2); lens2.append(n); slots2.append(i); pos2.append(int(rng.integers(100, 460)))
+            row2 += n
+        tiles2 = torch.from_numpy(make_tiles(starts2, lens2, slots2, pos2)).to(dev)
+        q2 = torch.randn(row2, Hq * 128, device=dev).to(torch.bfloat16)
+        o2 = torch.empty_like(q2)
+        for sk in (32, 64):
+            ms = timeit(lambda: ops.attention_tiles(q2, kc, vc, tiles2, Hq, Hkv, 128 ** -0.5, out=o2, n_dec=0,
+                                                    seg_keys=sk), a.reps)
+            rec(f"attention_seg_long_ctx_keys{sk}", ms, tiles=int(tiles2.shape[0]), tokens=row2)
         dec = tiles[:768].contiguous()
         ms = timeit(lambda: ops.attention_tiles(q, kc, vc, dec, Hq, Hkv, 128 ** -0.5, out=o, n_dec=768), a.reps)
         rec("attention_dec_only", ms, tokens=768)
