@@ -269,9 +269,14 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   constexpr int SA_PROW = KEYS + 8;   // P row
   constexpr int NJ = KEYS / 16;       // 16-key score tiles per block
   constexpr int NKS = KEYS / 32;      // 32-key PV k-steps per block
-  __shared__ __align__(16) uint16_t Ks[SA_KEYS * 128];
-  __shared__ __align__(16) uint16_t Vt[128 * SA_VROW];
-  __shared__ __align__(16) uint16_t Ps[4][16 * SA_PROW];
+  // one LDS array: K tile | V^T tile | per-wave P tiles; after the key loop
+  // the same bytes stage the output tiles for 16-B global stores
+  constexpr int SA_OROW = 136;                        // O staging row: 128 dims + 8 pad
+  constexpr int SA_LDS = SA_KEYS * 128 + 128 * SA_VROW + 4 * 16 * SA_PROW;
+  static_assert(SA_LDS >= 4 * 16 * SA_OROW, "output staging must fit");
+  __shared__ __align__(16) uint16_t smem[SA_LDS];
+  uint16_t* Ks = smem;
+  uint16_t* Vt = smem + SA_KEYS * 128;
   const int tile = blockIdx.x / Hkv;
   const int g = blockIdx.x % Hkv;
   const int tid = threadIdx.x;
@@ -302,7 +307,7 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   for (int nt = 0; nt < 8; ++nt) o[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float mrow[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
   float lrow[4] = {0.f, 0.f, 0.f, 0.f};
-  uint16_t* P = Ps[wv];
+  uint16_t* P = smem + SA_KEYS * 128 + 128 * SA_VROW + wv * 16 * SA_PROW;
 
   for (int k0 = 0; k0 < ctx; k0 += SA_KEYS) {
     __syncthreads();
@@ -388,16 +393,27 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
       }
     }
   }
-  // ---- epilogue: o[nt][k] = O[row 4fq+k][dim 16nt + fr]
+  // ---- epilogue: o[nt][k] = O[row 4fq+k][dim 16nt + fr] -> LDS (row-major,
+  // 272-B rows: the 4 row-quads of a store land 16 banks apart) -> 16-B
+  // global stores of whole row chunks (4 per lane instead of 32 2-byte ones)
+  __syncthreads();                                    // every wave is done with K / V^T / P
+  uint16_t* Os = smem + wv * 16 * SA_OROW;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int row = 4 * fq + k;
-    if (row < n) {
-      const float inv = 1.0f / lrow[k];
-      uint16_t* dst = out + ((int64_t)(tok0 + row) * Hq + h) * 128;
+    const float inv = row < n ? 1.0f / lrow[k] : 0.f;
 #pragma unroll
-      for (int nt = 0; nt < 8; ++nt) dst[nt * 16 + fr] = f32_to_bf16_rne(o[nt][k] * inv);
-    }
+    for (int nt = 0; nt < 8; ++nt) Os[row * SA_OROW + nt * 16 + fr] = f32_to_bf16_rne(o[nt][k] * inv);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);                 // this wave's O stores landed (lgkmcnt 0)
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = lane + 64 * r;                      // 16 rows x 16 chunks of 8 dims
+    const int row = c >> 4, ch = c & 15;
+    if (row < n)
+      *reinterpret_cast<uint4*>(out + ((int64_t)(tok0 + row) * Hq + h) * 128 + ch * 8) =
+          *reinterpret_cast<const uint4*>(Os + row * SA_OROW + ch * 8);
   }
 }
 
