@@ -35,16 +35,35 @@ from ..utils.logging import get_logger
 DAY_NS = 24 * 3600 * 1_000_000_000
 
 
+def message_tokens(m: Message) -> int:
+    """Tokens a message adds to a context window: the preprocessor's
+    ``word_count`` (GPU tokenizer, Go ``strings.Fields`` semantics) when it
+    ran, else a whitespace split."""
+    wc = m.metadata.get("word_count") if m.metadata else None
+    if wc is not None:
+        try:
+            return int(wc)
+        except (TypeError, ValueError):
+            pass
+    return len(m.content.split())
+
+
 class StateManager:
     def __init__(self, *, conversation_ttl: int = DAY_NS, cleanup_interval: int = 60 * 1_000_000_000,
                  max_conversations: int = 1000, max_context_length: int = 4096,
                  max_idle_time: int = 30 * 60 * 1_000_000_000, persistence=None,
                  async_persistence: bool = True, summary_engine=None, summarise_on_evict: bool = True,
-                 logger=None):
+                 logger=None, max_context_tokens: int = 0):
         self.conversation_ttl = conversation_ttl
         self.cleanup_interval = cleanup_interval
         self.max_conversations = max_conversations
         self.max_context_length = max_context_length
+        # token-aware window (SURVEY.md §5 long-context plan): besides the
+        # reference's message-count cap, keep the window's token total (the
+        # preprocessor's word_count, i.e. the GPU tokenizer's count) under
+        # this budget by evicting the oldest messages (summarised, N5).  0 = off
+        self.max_context_tokens = int(max_context_tokens)
+        self._ctx_tokens: Dict[str, int] = {}
         self.max_idle_time = max_idle_time
         self.persistence = persistence
         self.async_persistence = async_persistence and persistence is not None
@@ -67,7 +86,8 @@ class StateManager:
         return cls(conversation_ttl=cfg.queue.max_retention_period, cleanup_interval=cfg.queue.cleanup_interval,
                    max_conversations=c.max_conversations, max_context_length=c.max_context_length,
                    max_idle_time=c.max_idle_time, persistence=persistence, summary_engine=summary_engine,
-                   summarise_on_evict=c.summarise_on_evict, **kw)
+                   summarise_on_evict=c.summarise_on_evict,
+                   max_context_tokens=getattr(c, "max_context_tokens", 0), **kw)
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> None:
@@ -202,13 +222,37 @@ class StateManager:
             conv.last_active_time = now
             conv.last_activity = now
             conv.updated_at = now
+            excess = 0
             if self.max_context_length > 0 and len(conv.messages) > self.max_context_length:
                 excess = len(conv.messages) - self.max_context_length
+            if self.max_context_tokens > 0:
+                # running total, cached per conversation OBJECT (a conversation
+                # dropped by cleanup and re-created under the same id recounts)
+                cached = self._ctx_tokens.get(conversation_id)
+                tot = cached[1] if cached is not None and cached[0] is conv else None
+                if tot is None:
+                    tot = sum(message_tokens(m) for m in conv.messages[:-1])
+                tot += message_tokens(message)
+                tot -= sum(message_tokens(m) for m in conv.messages[:excess])
+                # evict oldest while over budget (the newest message always stays)
+                while tot > self.max_context_tokens and excess < len(conv.messages) - 1:
+                    tot -= message_tokens(conv.messages[excess])
+                    excess += 1
+                self._ctx_tokens[conversation_id] = (conv, tot)
+            if excess:
                 evicted = conv.messages[:excess]
                 conv.messages = conv.messages[excess:]
                 if self.summarise_on_evict:
                     self._evicted.setdefault(conversation_id, []).extend(m.content for m in evicted)
         self._persist(conv)
+
+    def context_tokens(self, conversation_id: str) -> int:
+        """Token total of the conversation's current window."""
+        with self._lock:
+            conv = self._convs.get(conversation_id)
+            if conv is None:
+                raise ConversationNotFound(conversation_id)
+            return sum(message_tokens(m) for m in conv.messages)
 
     def update_conversation_state(self, conversation_id: str, state: str) -> None:
         with self._lock:
@@ -242,6 +286,7 @@ class StateManager:
             if ids is not None:
                 self._users[conv.user_id] = [i for i in ids if i != conversation_id]
             self._evicted.pop(conversation_id, None)
+            self._ctx_tokens.pop(conversation_id, None)
         with self._dirty_cv:
             self._dirty.pop(conversation_id, None)
         if self.persistence is not None:

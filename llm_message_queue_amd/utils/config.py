@@ -233,6 +233,7 @@ class BackendConfig:
 class ConversationConfig:
     max_conversations: int = 1000      # per user (cmd/server/main.go:75)
     max_context_length: int = 4096     # messages (cmd/server/main.go:76)
+    max_context_tokens: int = 0        # token budget of the window (0 = off); oldest evicted + summarised
     max_idle_time: int = 30 * 60 * S
     summarise_on_evict: bool = True
     summary_dim: int = 256

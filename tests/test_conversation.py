@@ -30,6 +30,31 @@ def test_get_or_create_and_find():
     assert s.find_conversation("nope") is None
 
 
+def test_token_budget_window():
+    """Token-aware context window: the oldest messages leave once the
+    window's token total (preprocessor word_count, else whitespace split)
+    exceeds max_context_tokens; evicted text is queued for summarising;
+    the newest message always stays."""
+    s = sm(max_context_tokens=10)
+    s.get_conversation("c", "u")
+    for i in range(4):
+        s.add_message("c", new_message("c", "u", f"w{i} a b c", 3))       # 4 tokens each
+    assert [m.content.split()[0] for m in s.get_conversation_context("c")] == ["w2", "w3"]
+    assert s.context_tokens("c") == 8 and s.pending_evictions() == 2      # w0, w1 await summarising
+    big = new_message("c", "u", "x", 3)
+    big.metadata["word_count"] = 50                                        # GPU tokenizer count wins
+    s.add_message("c", big)
+    assert [m.content for m in s.get_conversation_context("c")] == ["x"] and s.context_tokens("c") == 50
+    s.add_message("c", new_message("c", "u", "y z", 3))
+    assert [m.content for m in s.get_conversation_context("c")] == ["y z"]
+    # both caps: the message-count cap applies first
+    s2 = sm(max_context_length=2, max_context_tokens=100)
+    s2.get_conversation("d", "u")
+    for i in range(3):
+        s2.add_message("d", new_message("d", "u", f"m{i}", 3))
+    assert [m.content for m in s2.get_conversation_context("d")] == ["m1", "m2"] and s2.context_tokens("d") == 2
+
+
 def test_add_message_truncates_and_queues_evictions():
     s = sm(max_context_length=3)
     s.get_conversation("c", "u")
