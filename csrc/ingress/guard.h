@@ -313,7 +313,7 @@ class Guard {
 
   // Permission a route needs ("" = public).
   static std::string permission_for(const std::string& method, const std::string& path) {
-    if (path == "/health" || path == "/metrics") return "";
+    if (path == "/health" || path == "/api/v1/health" || path == "/metrics") return "";
     const bool read = method == "GET" || method == "HEAD";
     auto starts = [&](const char* p) { return path.compare(0, strlen(p), p) == 0; };
     if (starts("/api/v1/admin") || starts("/api/v1/config")) return "admin:write";
@@ -346,7 +346,8 @@ class Guard {
     if (wall_s == 0) wall_s = (int64_t)time(nullptr);
     const std::string perm = permission_for(method, path);
     r.role = default_role_;
-    if (!perm.empty()) {
+    if (perm.empty()) return r;          // /health, /metrics: public and never throttled (probes, scrapes)
+    {
       if (method_ == "api_key") {
         const KeyInfo* ki = match_key(api_key);
         if (!ki) return fail(r, G_UNAUTHORIZED, "missing or invalid API key");

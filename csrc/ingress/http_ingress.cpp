@@ -538,7 +538,7 @@ class HttpIngress {
             respond(cn, 202, "Accepted", out, keep);
           }
         }
-      } else if (method == "GET" && path == "/health") {
+      } else if (method == "GET" && (path == "/health" || path == "/api/v1/health")) {
         respond(cn, 200, "OK", "{\"status\":\"ok\",\"version\":\"1.0.0\",\"time\":\"" + rfc3339_now() + "\"}", keep);
       } else {
         respond(cn, 404, "Not Found", "{\"error\":\"route served by the API server\"}", keep);

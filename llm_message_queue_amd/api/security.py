@@ -35,6 +35,7 @@ def guard_from_config(cfg) -> Optional[Any]:
                      user_rps=rl.per_user.requests_per_second, user_burst=float(rl.per_user.burst_size))
     if auth.method == "none" and not az.enabled and not any(v > 0 for k, v in rates.items() if k.endswith("rps")):
         return None
+    # /health and /metrics stay public and unthrottled (Guard.permission_for == "")
     g = _native.ingress().Guard(
         method=auth.method, api_key_header=auth.api_key.header_name, api_keys=list(auth.api_key.valid_keys),
         jwt_secret=auth.jwt.secret, jwt_issuer=auth.jwt.issuer, jwt_leeway_s=int(auth.jwt.leeway),

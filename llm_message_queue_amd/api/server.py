@@ -47,6 +47,46 @@ from .security import guard_from_config, redact_config
 VERSION = "1.0.0"
 
 
+def business_error_code(status: int, path: str, msg: str) -> Optional[int]:
+    """The documented business / system error codes (`docs/api.md:745-771`
+    of the reference: 1001-1010, 2001-2008) for an error response; reported
+    as ``error_code`` in the envelope format."""
+    m = (msg or "").lower()
+    if status == 429:
+        return 1009                                   # request rate too high
+    if status == 408 or "timeout" in m or "deadline" in m:
+        return 1010                                   # message processing timed out
+    if status == 404:
+        if "/conversations" in path:
+            return 1005                               # conversation does not exist
+        if "/messages" in path:
+            return 1004                               # message does not exist
+        return None
+    if "full" in m:
+        return 1007                                   # queue full
+    if status == 400:
+        if "priority" in m:
+            return 1003                               # invalid priority
+        if "user_id" in m:
+            return 1006                               # invalid user id
+        if "too long" in m:
+            return 1002                               # content too long
+        if "content" in m or "empty" in m or "eof" in m:
+            return 1001                               # content empty
+        return None
+    if status == 503:
+        return 2003                                   # queue service unavailable
+    if status >= 500:
+        if "redis" in m:
+            return 2002
+        if "database" in m or "postgres" in m or "sqlite" in m:
+            return 2001
+        if "queue" in m:
+            return 2003
+        return None
+    return None
+
+
 def _err(code: int, msg: str) -> JSONResponse:
     return JSONResponse({"error": msg}, status_code=code)
 
@@ -110,6 +150,9 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             if code >= 400:
                 msg = payload.get("error", "") if isinstance(payload, dict) else ""
                 env.update(message=msg or "error", error=msg or "error")
+                biz = business_error_code(code, request.url.path, msg)
+                if biz:
+                    env["error_code"] = biz
             else:
                 env.update(message="success", data=payload)
             env["timestamp"] = format_time(time.time_ns())
@@ -134,6 +177,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
 
     # ------------------------------------------------------------------ health / metrics
     @app.get("/health")
+    @app.get("/api/v1/health")            # the path the reference's API docs use (docs/api.md:796)
     def health():
         return {"status": "ok", "version": VERSION, "time": format_time(time.time_ns())}
 

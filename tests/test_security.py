@@ -180,8 +180,12 @@ def test_api_server_response_envelope():
             b = bad.json()
             assert bad.status_code == 400 and b["code"] == 400 and "Invalid message format" in b["error"]
             assert "data" not in b
+            bp = c.post("/api/v1/messages", json={"content": "x", "priority": "bogus"}).json()
+            assert bp["code"] == 400 and bp["error_code"] == 1003          # documented business codes
             nf = c.get("/api/v1/conversations/does-not-exist").json()
-            assert nf["code"] == 404
+            assert nf["code"] == 404 and nf["error_code"] == 1005
+            assert c.get("/api/v1/messages/nope").json()["error_code"] == 1004
+            assert c.get("/api/v1/health").json()["data"]["status"] == "ok"
             assert c.get("/metrics").text.startswith("#") or "llm_queue" in c.get("/metrics").text
     finally:
         gw.stop()
