@@ -119,9 +119,11 @@ static void salient_topk(uintptr_t hashes, int L, uintptr_t ntok, int stride, ui
 // ---------------------------------------------------------------------- llama stub
 static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T, int D, float eps,
                     uintptr_t stream) {
-  require(D % 2048 == 0 && D <= 8192, "rmsnorm expects D % 2048 == 0 and D <= 8192");
+  require(D % 2048 == 0 && D >= 2048 && D <= 8192, "rmsnorm expects D in {2048, 4096, 6144, 8192}");
   if (T == 0) return;
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3(T), dim3(256), 0, S(stream), P<const uint16_t>(x),
+  auto kern = D == 2048 ? rmsnorm_kernel<1> : D == 4096 ? rmsnorm_kernel<2> : D == 6144 ? rmsnorm_kernel<3>
+                                                                            : rmsnorm_kernel<4>;
+  hipLaunchKernelGGL(kern, dim3(T), dim3(256), 0, S(stream), P<const uint16_t>(x),
                      res ? P<uint16_t>(res) : nullptr, P<const uint16_t>(w), P<uint16_t>(y), D, eps);
   check_launch();
 }

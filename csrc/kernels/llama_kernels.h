@@ -40,17 +40,21 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // y = rmsnorm(x (+ residual)) * w.  If `res` is non-null: res <- x + res (the
-// new residual stream) and the norm is taken of that sum.  D % 2048 == 0
-// (one 256-thread block per row, 8 bf16 per thread per pass).
+// new residual stream) and the norm is taken of that sum.  D = NPASS * 2048
+// (one 256-thread block per row, 8 bf16 per thread per pass); NPASS is a
+// template parameter so every pass's 16-B loads are issued before the first
+// is consumed (D = 4096 for the 8B model: 2 loads in flight per thread).
+template <int NPASS>
 __global__ void __launch_bounds__(256)
 rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
                uint16_t* __restrict__ y, int D, float eps) {
   const int row = blockIdx.x;
   const int tid = threadIdx.x;
-  const int npass = D / 2048;
-  float v[4][8];
+  constexpr int npass = NPASS;
+  float v[NPASS][8];
   float ss = 0.f;
-  for (int p = 0; p < npass && p < 4; ++p) {
+#pragma unroll
+  for (int p = 0; p < npass; ++p) {
     const int col = p * 2048 + tid * 8;
     const u16x8 xv = *reinterpret_cast<const u16x8*>(x + (int64_t)row * D + col);
     u16x8 rv;
@@ -78,7 +82,8 @@ rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ res, const
   __syncthreads();
   const float tot = red[0] + red[1] + red[2] + red[3];
   const float inv = rsqrtf(tot / (float)D + eps);
-  for (int p = 0; p < npass && p < 4; ++p) {
+#pragma unroll
+  for (int p = 0; p < npass; ++p) {
     const int col = p * 2048 + tid * 8;
     const u16x8 wv = *reinterpret_cast<const u16x8*>(w + col);
     u16x8 o;
@@ -110,7 +115,9 @@ silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out, int
 
 // RoPE (rotate-half, Llama-3) on q and k of the fused qkv projection, then
 // write k/v into this layer's cache at (slot, pos).  One block per token;
-// thread i handles rotary pair i (0..63) of heads tid/64, tid/64+4, ...
+// thread t takes rotary pairs 4j..4j+3 (j = t & 15) of head slot t >> 4, so a
+// head is 16 threads x 8-B accesses (two coalesced 128-B halves: dims i and
+// i + 64) and a block covers 16 heads per pass.
 __global__ void __launch_bounds__(256)
 rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos,
                const int32_t* __restrict__ slot, const float* __restrict__ cos_t,
@@ -118,32 +125,50 @@ rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos
                uint16_t* __restrict__ q_out, uint16_t* __restrict__ kc, uint16_t* __restrict__ vc) {
   const int t = blockIdx.x;
   const int tid = threadIdx.x;
-  const int i = tid & 63;            // rotary pair index (dims i and i + 64)
-  const int hg = tid >> 6;           // 4 head groups
+  const int j = tid & 15;            // pairs 4j .. 4j+3
+  const int hs = tid >> 4;           // head slot 0..15
   const int p = pos[t];
   const int s = slot[t];
   // a corrupt descriptor must not become a wild KV-cache write (GPU fault):
   // out-of-range (slot, pos) rows are dropped
   if ((unsigned)s >= (unsigned)n_slots || (unsigned)p >= (unsigned)max_ctx) return;
-  const float c = cos_t[(int64_t)p * 64 + i];
-  const float sn = sin_t[(int64_t)p * 64 + i];
+  const float4 c = *reinterpret_cast<const float4*>(cos_t + (int64_t)p * 64 + 4 * j);
+  const float4 sn = *reinterpret_cast<const float4*>(sin_t + (int64_t)p * 64 + 4 * j);
+  const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
   const int64_t row = (int64_t)t * (Hq + 2 * Hkv) * 128;
-  for (int h = hg; h < Hq; h += 4) {
-    const float x0 = bf(qkv[row + h * 128 + i]);
-    const float x1 = bf(qkv[row + h * 128 + i + 64]);
-    q_out[(int64_t)t * Hq * 128 + h * 128 + i] = f32_to_bf16_rne(x0 * c - x1 * sn);
-    q_out[(int64_t)t * Hq * 128 + h * 128 + i + 64] = f32_to_bf16_rne(x1 * c + x0 * sn);
+  auto rot = [&](uint2 lo, uint2 hi, uint2* olo, uint2* ohi) {
+    const uint16_t* a = reinterpret_cast<const uint16_t*>(&lo);
+    const uint16_t* b = reinterpret_cast<const uint16_t*>(&hi);
+    uint16_t* oa = reinterpret_cast<uint16_t*>(olo);
+    uint16_t* ob = reinterpret_cast<uint16_t*>(ohi);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x0 = bf(a[k]), x1 = bf(b[k]);
+      oa[k] = f32_to_bf16_rne(x0 * cc[k] - x1 * ss[k]);
+      ob[k] = f32_to_bf16_rne(x1 * cc[k] + x0 * ss[k]);
+    }
+  };
+  for (int h = hs; h < Hq; h += 16) {
+    const uint2 lo = *reinterpret_cast<const uint2*>(qkv + row + h * 128 + 4 * j);
+    const uint2 hi = *reinterpret_cast<const uint2*>(qkv + row + h * 128 + 64 + 4 * j);
+    uint2 olo, ohi;
+    rot(lo, hi, &olo, &ohi);
+    uint16_t* dst = q_out + (int64_t)t * Hq * 128 + h * 128;
+    *reinterpret_cast<uint2*>(dst + 4 * j) = olo;
+    *reinterpret_cast<uint2*>(dst + 64 + 4 * j) = ohi;
   }
-  for (int h = hg; h < Hkv; h += 4) {
+  for (int h = hs; h < Hkv; h += 16) {
     const int64_t kb = row + (int64_t)(Hq + h) * 128;
     const int64_t vb = row + (int64_t)(Hq + Hkv + h) * 128;
-    const float x0 = bf(qkv[kb + i]);
-    const float x1 = bf(qkv[kb + i + 64]);
+    const uint2 lo = *reinterpret_cast<const uint2*>(qkv + kb + 4 * j);
+    const uint2 hi = *reinterpret_cast<const uint2*>(qkv + kb + 64 + 4 * j);
+    uint2 olo, ohi;
+    rot(lo, hi, &olo, &ohi);
     const int64_t dst = (((int64_t)s * Hkv + h) * max_ctx + p) * 128;
-    kc[dst + i] = f32_to_bf16_rne(x0 * c - x1 * sn);
-    kc[dst + i + 64] = f32_to_bf16_rne(x1 * c + x0 * sn);
-    vc[dst + i] = qkv[vb + i];
-    vc[dst + i + 64] = qkv[vb + i + 64];
+    *reinterpret_cast<uint2*>(kc + dst + 4 * j) = olo;
+    *reinterpret_cast<uint2*>(kc + dst + 64 + 4 * j) = ohi;
+    *reinterpret_cast<uint2*>(vc + dst + 4 * j) = *reinterpret_cast<const uint2*>(qkv + vb + 4 * j);
+    *reinterpret_cast<uint2*>(vc + dst + 64 + 4 * j) = *reinterpret_cast<const uint2*>(qkv + vb + 64 + 4 * j);
   }
 }
 
