@@ -185,7 +185,10 @@ def main(argv=None) -> int:
     tok_per_req = max(1.0, (engine.completed_tokens - rt0) / done)
     cap_local = tok_rate / tok_per_req
     caps = comm.all_gather_i64(np.array([int(cap_local * 1000)], dtype=np.int64))[:, 0] / 1000.0
-    capacity = float(np.min(caps))
+    # job capacity per GPU = mean over ranks: the dispatch planner moves a
+    # slower rank's excess to GPUs with free slots, so the job (not its
+    # slowest member) is what the offered load is sized against
+    capacity = float(np.mean(caps))
     rate = a.rate if a.rate > 0 else a.util * capacity
     # drain the calibration backlog (untimed)
     gw.drop_pending()
