@@ -345,6 +345,8 @@ class Gateway:
             self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
         if out:
             self.counters["expired"] += len(out)
+            if self.metrics is not None:
+                self.metrics.requests_rejected.labels("deadline_exceeded").inc(len(out))
             if self.dead_letter is not None:
                 by_q: Dict[str, List[Message]] = {}
                 for m in out:
