@@ -14,7 +14,9 @@
 //
 // Tiling (gfx950): one 256-thread workgroup (4 waves) per 64-row tile.
 //   * the 64 x 256 bf16 A tile (32 KiB) is gathered ONCE into LDS with 16-byte
-//     loads; its 16-byte chunks are XOR-swizzled (chunk ^ (row & 15)) so the
+//     register-staged loads (for row gathers from a ~32 MiB table an LDS-DMA
+//     global_load_lds with per-lane source rows reads at the same rate, per
+//     the MI355X microarchitecture measurements, so the simpler form stays); its 16-byte chunks are XOR-swizzled (chunk ^ (row & 15)) so the
 //     v_mfma_f32_16x16x32_bf16 A-fragment reads (16 rows x one chunk per lane
 //     group) are bank-conflict free for every ds_read_b128 lane group;
 //   * the tile stays resident while the 4 waves sweep H in 256-column chunks

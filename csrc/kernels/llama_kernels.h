@@ -278,6 +278,11 @@ attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc
 //               dword write) so B fragments are 16-B reads; 8 dim tiles x
 //               2 k-steps per 64 keys, O in 32 accumulator VGPRs.
 //
+// XCD mapping: blockIdx = tile * Hkv + g and workgroups are dealt round-robin
+// to the 8 XCDs, so with Hkv = 8 every tile's kv head g runs on XCD g: the
+// tiles of one prefill chunk (which re-read each other's K/V rows) share that
+// XCD's L2 by construction, with no remap needed.
+//
 // KEYS (32 or 64) is the key block per iteration.  Serving prompts are short
 // (<= 32 tokens), so the 32-key block does no masked MFMA work on them and
 // halves the LDS and score registers: more workgroups resident per CU, and
