@@ -52,6 +52,8 @@ namespace py = pybind11;
 namespace {
 
 constexpr uint32_t TAG_RAW = 3;   // [u64 arrival_mono_ns][36 B uuid][u32 body_len][body]
+constexpr size_t kMaxBody = 4u << 20;   // POST body cap (413 beyond; the read buffer caps at 8 MiB)
+constexpr size_t kMaxHeader = 64u << 10; // request line + headers cap (431 beyond)
 
 // ------------------------------------------------------------------ JSON scan
 struct Scan {
@@ -460,7 +462,11 @@ class HttpIngress {
     size_t pos = 0;
     while (!cn.close_after) {
       size_t he = cn.in.find("\r\n\r\n", pos);
-      if (he == std::string::npos) break;
+      if (he == std::string::npos) {
+        if (cn.in.size() - pos > kMaxHeader)
+          respond(cn, 431, "Request Header Fields Too Large", "{\"error\":\"header too large\"}", false);
+        break;
+      }
       const char* h = cn.in.data() + pos;
       size_t hl = he - pos;
       // request line
@@ -477,7 +483,7 @@ class HttpIngress {
       std::string method(h, sp1 - h), path(sp1 + 1, sp2 - sp1 - 1);
       bool http10 = std::string(sp2 + 1, std::min<size_t>(8, hl - (sp2 + 1 - h))) == "HTTP/1.0";
       size_t clen = 0;
-      bool keep = !http10;
+      bool keep = !http10, bad_len = false, chunked = false;
       std::string api_key, authz;
       // headers (case-insensitive names)
       const char* line = (const char*)memchr(h, '\n', hl);
@@ -493,7 +499,13 @@ class HttpIngress {
           while (v < le && (*v == ' ' || *v == '\t')) ++v;
           std::string val(v, le - v);
           while (!val.empty() && (val.back() == '\r' || val.back() == ' ')) val.pop_back();
-          if (name == "content-length") clen = (size_t)strtoull(val.c_str(), nullptr, 10);
+          if (name == "content-length") {
+            // digits only, bounded before any arithmetic on it (an unchecked
+            // 2^64-1 would wrap the body-complete test below)
+            bad_len = val.empty() || val.size() > 12 ||
+                      val.find_first_not_of("0123456789") != std::string::npos;
+            clen = bad_len ? 0 : (size_t)strtoull(val.c_str(), nullptr, 10);
+          } else if (name == "transfer-encoding") chunked = true;
           else if (name == "authorization") authz = val;
           else if (guard_ && name == guard_->key_header()) api_key = val;
           else if (name == "connection") {
@@ -503,6 +515,16 @@ class HttpIngress {
           }
         }
         line = eol;
+      }
+      if (bad_len || chunked || clen > kMaxBody) {
+        bad_++;
+        if (clen > kMaxBody)
+          respond(cn, 413, "Payload Too Large", "{\"error\":\"body exceeds 4 MiB\"}", false);
+        else if (chunked)
+          respond(cn, 501, "Not Implemented", "{\"error\":\"chunked transfer encoding not supported\"}", false);
+        else
+          respond(cn, 400, "Bad Request", "{\"error\":\"bad Content-Length\"}", false);
+        break;
       }
       if (cn.in.size() < he + 4 + clen) break;  // body not complete yet
       const char* body = cn.in.data() + he + 4;

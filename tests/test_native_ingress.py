@@ -97,3 +97,49 @@ def test_native_ingress_http_edges(stack):
         data += s.recv(65536)
     s.close()
     assert data.count(b"HTTP/1.1 202") == 2 and b'"priority":2' in data
+
+
+def _raw(port, payload, timeout=3.0):
+    s = socket.create_connection(("127.0.0.1", port))
+    s.settimeout(timeout)
+    try:
+        s.sendall(payload)
+        data = b""
+        while True:
+            try:
+                chunk = s.recv(65536)
+            except (socket.timeout, ConnectionResetError):
+                break
+            if not chunk:
+                break
+            data += chunk
+            if b"\r\n\r\n" in data:
+                break
+        return data
+    finally:
+        s.close()
+
+
+def test_native_ingress_hostile_framing(stack):
+    """Untrusted framing: absurd / non-numeric Content-Length, chunked bodies,
+    oversized headers and random bytes get a clean error (or a close) and the
+    server keeps serving."""
+    _, ing, port = stack
+    post = b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\n"
+    assert b" 400 " in _raw(port, post + b"Content-Length: 18446744073709551615\r\n\r\n{}")
+    assert b" 400 " in _raw(port, post + b"Content-Length: -5\r\n\r\n{}")
+    assert b" 400 " in _raw(port, post + b"Content-Length: 12abc\r\n\r\n{}")
+    assert b" 413 " in _raw(port, post + b"Content-Length: 999999999\r\n\r\n{}")
+    assert b" 501 " in _raw(port, post + b"Transfer-Encoding: chunked\r\n\r\n2\r\n{}\r\n0\r\n\r\n")
+    assert b" 431 " in _raw(port, post + b"X-Pad: " + b"a" * (70 << 10))
+    import random
+    rnd = random.Random(3)
+    for _ in range(40):
+        junk = bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(1, 400)))
+        if rnd.random() < 0.5:
+            junk = post + junk + b"\r\n\r\n"
+        _raw(port, junk, timeout=0.3)
+    with urllib.request.urlopen(f"http://127.0.0.1:{port}/health", timeout=5) as r:
+        assert r.status == 200
+    code, r = _post(port, {"content": "still alive"})
+    assert code == 202
