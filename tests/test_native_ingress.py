@@ -143,3 +143,33 @@ def test_native_ingress_hostile_framing(stack):
         assert r.status == 200
     code, r = _post(port, {"content": "still alive"})
     assert code == 202
+
+
+def test_json_scanner_properties():
+    """The native scanner on arbitrary bytes never faults, and accepts every
+    well-formed JSON object whose reserved fields are absent."""
+    from hypothesis import given, settings, strategies as st
+    scan = _native.ingress().scan_message
+    leaf = st.none() | st.booleans() | st.integers(-10**12, 10**12) | st.floats(allow_nan=False, allow_infinity=False) \
+        | st.text(max_size=20)
+    val = st.recursive(leaf, lambda c: st.lists(c, max_size=4) | st.dictionaries(st.text(max_size=8), c, max_size=4),
+                       max_leaves=12)
+    reserved = {"id", "priority", "user_id", "content"}
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.binary(max_size=200))
+    def arbitrary(b):
+        r = scan(b)
+        assert isinstance(r, tuple) and r[0] in (True, False)
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.dictionaries(st.text(max_size=8).filter(lambda k: k not in reserved), val, max_size=5), st.booleans())
+    def wellformed(d, ascii_only):
+        doc = json.dumps(d, ensure_ascii=ascii_only).encode()
+        assert scan(doc)[0], d
+        # every strict prefix of an object is malformed and must be refused
+        for k in range(0, len(doc), max(1, len(doc) // 7)):
+            assert not scan(doc[:k])[0], doc[:k]
+
+    arbitrary()
+    wellformed()
