@@ -74,6 +74,8 @@ def cmd_serve(a, role: str = "serve") -> int:
     cfg = _load_cfg(a.config)
     if a.port:
         cfg.server.port = a.port
+    if getattr(a, "grpc_port", 0):
+        cfg.server.grpc_port = a.grpc_port
     if a.host:
         cfg.server.host = a.host
     ulog.configure(cfg.logging.level, cfg.logging.format, cfg.logging.output)
@@ -115,8 +117,16 @@ def cmd_serve(a, role: str = "serve") -> int:
         t.start()
         print(json.dumps({"event": "listening", "host": cfg.server.host, "port": cfg.server.port,
                           "gpu": use_gpu, "role": role}), flush=True)
+        grpc_srv = None
+        if cfg.server.grpc_port:
+            from ..api.grpc_server import GrpcServer
+            grpc_srv = GrpcServer(gapp, cfg.server.grpc_port, cfg.server.host, cfg.server.grpc_max_workers)
+            print(json.dumps({"event": "listening", "host": cfg.server.host, "port": grpc_srv.start(),
+                              "protocol": "grpc", "service": "llmq.v1.MessageQueue"}), flush=True)
         while not stop.is_set() and t.is_alive():
             stop.wait(0.5)
+        if grpc_srv is not None:
+            grpc_srv.stop()
         server.should_exit = True
         t.join(timeout=5)
     else:
@@ -216,6 +226,7 @@ def main(argv=None) -> int:
         p.add_argument("--config", default=None, help="config dir or file (default: ./configs)")
         p.add_argument("--host", default="")
         p.add_argument("--port", type=int, default=0)
+        p.add_argument("--grpc-port", type=int, default=0, help="also serve llmq.v1.MessageQueue over gRPC")
         p.add_argument("--model", default="llama3-8b")
         p.add_argument("--no-gpu", action="store_true")
         p.add_argument("--ring", default="", help="shared request ring name (api-gateway/queue-manager)")

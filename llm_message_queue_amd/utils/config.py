@@ -41,6 +41,9 @@ class ServerConfig:
     # wrap JSON bodies in {"code","message","data","timestamp"} (docs/api.md:12-20);
     # off by default: the reference's handlers return bare objects
     response_envelope: bool = False
+    # gRPC front-end (api/grpc_server.py, service llmq.v1.MessageQueue); 0 = off
+    grpc_port: int = 0
+    grpc_max_workers: int = 32
 
 
 @dataclass

@@ -1,0 +1,113 @@
+"""gRPC front-end (api/grpc_server.py): unary + streaming submission, watch
+until completion, stats/health, the guard on call metadata, and the
+checked-in proto schema kept in sync with the runtime descriptors."""
+import os
+import time
+
+import grpc
+import pytest
+
+from llm_message_queue_amd.api.grpc_server import GrpcClient, GrpcServer, pb, proto_source
+from llm_message_queue_amd.api.security import issue_token
+from llm_message_queue_amd.gateway.app import GatewayApp
+from llm_message_queue_amd.utils.config import default_config
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SECRET = "grpc-test-secret"
+
+
+def _stack(cfg=None):
+    cfg = cfg or default_config()
+    cfg.queue.worker.process_interval = 5_000_000
+    cfg.preprocessor.batch_window_us = 200
+    gw = GatewayApp(cfg, use_gpu=False, simulate_ms=(1, 1, 1, 1))
+    srv = GrpcServer(gw, 0, "127.0.0.1", max_workers=8)
+    port = srv.start()
+    return gw, srv, port
+
+
+def test_proto_file_matches_runtime_schema():
+    with open(os.path.join(ROOT, "proto", "llmq.proto")) as f:
+        assert f.read() == proto_source(), "regenerate proto/llmq.proto from grpc_server.proto_source()"
+    # wire round trip of the map + repeated fields
+    r = pb["SubmitRequest"](content="x", priority=2, metadata={"k": "v"})
+    assert pb["SubmitRequest"].FromString(r.SerializeToString()).metadata["k"] == "v"
+
+
+def test_grpc_submit_watch_stream_and_stats():
+    gw, srv, port = _stack()
+    cli = GrpcClient(f"127.0.0.1:{port}", gzip=True)
+    try:
+        assert cli.health().status == "ok"
+        r = cli.submit("EMERGENCY: server down", user_id="u1", metadata={"team": "ops"})
+        assert r.code == 202 and len(r.message_id) == 36 and r.priority == 1     # preprocessed -> realtime
+        states = [m.status for m in cli.watch(r.message_id, timeout_ms=10_000)]
+        assert states[-1] == "completed", states
+        info = cli.get_message(r.message_id)
+        assert info.user_id == "u1" and '"team":"ops"' in info.metadata_json
+        r2 = cli.submit("routine", id="client-7", priority_name="low")
+        assert r2.message_id == "client-7" and r2.priority == 4
+        # bidirectional stream: replies in request order, bad items reported inline
+        reqs = [pb["SubmitRequest"](content=f"m{i}", user_id=f"s{i}") for i in range(50)]
+        reqs.insert(10, pb["SubmitRequest"](content="bad", priority_name="bogus"))
+        replies = list(cli.submit_stream(reqs, timeout=30))
+        assert len(replies) == 51
+        assert replies[10].code == 400 and "priority" in replies[10].error
+        ok = [x for x in replies if x.code == 202]
+        assert len(ok) == 50 and len({x.message_id for x in ok}) == 50
+        t0 = time.time()
+        while time.time() - t0 < 10 and not all(
+                (gw.messages.get(x.message_id) and gw.messages.get(x.message_id).status == "completed") for x in ok):
+            time.sleep(0.02)
+        assert all(gw.messages.get(x.message_id).status == "completed" for x in ok)
+        batch = cli.submit_batch([pb["SubmitRequest"](content=f"b{i}", priority=1 + i % 4) for i in range(40)])
+        assert [x.priority for x in batch] == [1 + i % 4 for i in range(40)] and all(x.code == 202 for x in batch)
+        st = cli.queue_stats()
+        assert [t.name for t in st.tiers] == ["realtime", "high", "normal", "low"]
+        assert sum(t.completed for t in st.tiers) >= 52
+        with pytest.raises(grpc.RpcError) as e:
+            cli.get_message("nope")
+        assert e.value.code() == grpc.StatusCode.NOT_FOUND
+        with pytest.raises(grpc.RpcError) as e:
+            cli.submit("x", priority=9)
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    finally:
+        cli.close()
+        srv.stop()
+        gw.stop()
+
+
+def test_grpc_guard_on_metadata():
+    cfg = default_config()
+    cfg.security.authentication.method = "jwt"
+    cfg.security.authentication.jwt.secret = SECRET
+    cfg.security.authorization.enabled = True
+    cfg.loadbalancer.rate_limiting.enabled = True
+    cfg.loadbalancer.rate_limiting.per_user.requests_per_second = 0.001
+    cfg.loadbalancer.rate_limiting.per_user.burst_size = 2
+    gw, srv, port = _stack(cfg)
+    target = f"127.0.0.1:{port}"
+    anon = GrpcClient(target)
+    user = GrpcClient(target, token=issue_token(SECRET, "alice"))
+    ro = GrpcClient(target, token=issue_token(SECRET, "rita", "readonly"))
+    try:
+        assert anon.health().status == "ok"                      # public
+        with pytest.raises(grpc.RpcError) as e:
+            anon.submit("hi")
+        assert e.value.code() == grpc.StatusCode.UNAUTHENTICATED
+        with pytest.raises(grpc.RpcError) as e:
+            ro.submit("hi")
+        assert e.value.code() == grpc.StatusCode.PERMISSION_DENIED
+        assert len(ro.queue_stats().tiers) == 4                  # queue:read is allowed
+        assert user.submit("a").code == 202
+        assert user.submit("b").code == 202
+        with pytest.raises(grpc.RpcError) as e:
+            user.submit("c")                                     # per-user burst 2 spent
+        assert e.value.code() == grpc.StatusCode.RESOURCE_EXHAUSTED
+        md = dict(e.value.trailing_metadata() or ())
+        assert int(md["retry-after"]) >= 1
+    finally:
+        for c in (anon, user, ro):
+            c.close()
+        srv.stop()
+        gw.stop()
