@@ -263,19 +263,33 @@ class _Service:
         pending: "_queue.Queue" = _queue.Queue(maxsize=4096)
         END = object()
 
+        def put(item) -> bool:
+            # bounded queue: a client that stops reading replies must not pin
+            # this thread forever once the call is gone
+            while context.is_active():
+                try:
+                    pending.put(item, timeout=0.5)
+                    return True
+                except _queue.Full:
+                    continue
+            return False
+
         def reader():
             try:
                 for req in request_iterator:
-                    for item in self._submit_many((req,)):
-                        pending.put(item)
+                    if not all(put(item) for item in self._submit_many((req,))):
+                        return
             except grpc.RpcError:
                 pass
             finally:
-                pending.put(END)
+                put(END)
 
         threading.Thread(target=reader, daemon=True, name="grpc-submit-reader").start()
-        while True:
-            item = pending.get()
+        while context.is_active():
+            try:
+                item = pending.get(timeout=0.5)
+            except _queue.Empty:
+                continue
             if item is END:
                 return
             yield self._collect(item)

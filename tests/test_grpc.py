@@ -111,3 +111,31 @@ def test_grpc_guard_on_metadata():
             c.close()
         srv.stop()
         gw.stop()
+
+
+def test_grpc_stream_cancel_releases_server_threads():
+    """A client that abandons a SubmitStream mid-way must not pin server
+    handler threads (the pool has 8 workers; 12 abandoned streams in a row
+    would exhaust it if any leaked)."""
+    import threading
+    gw, srv, port = _stack()
+    cli = GrpcClient(f"127.0.0.1:{port}")
+    try:
+        for k in range(12):
+            gate = threading.Event()
+
+            def reqs():
+                for i in range(5):
+                    yield pb["SubmitRequest"](content=f"c{k}-{i}")
+                gate.wait(5)                      # keep the request side open
+
+            call = cli.submit_stream(reqs())
+            assert next(call).code == 202
+            call.cancel()
+            gate.set()
+        assert cli.health(timeout=5).status == "ok"
+        assert cli.submit("after", timeout=10).code == 202
+    finally:
+        cli.close()
+        srv.stop()
+        gw.stop()
