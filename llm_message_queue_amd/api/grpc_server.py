@@ -312,10 +312,13 @@ class _Service:
 
     def WatchMessage(self, req, context):
         """One ``MessageInfo`` per observed status change; ends at a terminal
-        status, at ``timeout_ms`` (default 60 s) or when the client leaves."""
+        status, at ``timeout_ms`` (default 60 s) or when the client leaves.
+        Each open watch holds one handler thread (``server.grpc_max_workers``
+        bounds concurrent watches plus in-flight calls)."""
         self._admit(context, "WatchMessage")
         deadline = time.monotonic() + (req.timeout_ms / 1e3 if req.timeout_ms > 0 else 60.0)
         last = None
+        nap = 0.002                                   # poll backoff 2 -> 50 ms, reset on change
         while context.is_active() and time.monotonic() < deadline:
             m = self.G.messages.get(req.message_id)
             if m is None:
@@ -324,10 +327,12 @@ class _Service:
                 return
             if m.status != last:
                 last = m.status
+                nap = 0.002
                 yield self._info(m)
                 if last in TERMINAL:
                     return
-            time.sleep(0.005)
+            time.sleep(nap)
+            nap = min(0.05, nap * 2)
 
     def QueueStats(self, req, context):
         self._admit(context, "QueueStats")
