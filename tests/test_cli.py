@@ -35,10 +35,10 @@ def test_validate_config():
 
 
 def test_serve_monolith_and_scheduler():
-    port = _port()
+    port, gport = _port(), _port()
     env = dict(os.environ, LLMQ_LOGGING__LEVEL="warning", LLMQ_QUEUE__WORKER__PROCESS_INTERVAL="5ms")
     srv = subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "serve", "--no-gpu", "--port",
-                            str(port), "--host", "127.0.0.1"], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                            str(port), "--host", "127.0.0.1", "--grpc-port", str(gport)], cwd=ROOT, env=env, stdout=subprocess.PIPE,
                            stderr=subprocess.DEVNULL, text=True, start_new_session=True)
     base = f"http://127.0.0.1:{port}"
     try:
@@ -60,6 +60,21 @@ def test_serve_monolith_and_scheduler():
             time.sleep(0.05)
         m = _get(base + f"/api/v1/messages/{mid}")
         assert m["status"] == "completed" and m["priority"] == 1
+        # the same gateway over gRPC (--grpc-port)
+        from llm_message_queue_amd.api.grpc_server import GrpcClient
+        g = GrpcClient(f"127.0.0.1:{gport}")
+        t0 = time.time()
+        while True:
+            try:
+                assert g.get_message(mid, timeout=2).status == "completed"
+                break
+            except Exception:
+                if time.time() - t0 > 30:
+                    raise
+                time.sleep(0.2)
+        r = g.submit("hello over grpc", user_id="cli")
+        assert [x.status for x in g.watch(r.message_id, timeout_ms=10_000)][-1] == "completed"
+        g.close()
         # the autoscaler binary against the live gateway: one scheduling round
         sch = subprocess.run([sys.executable, "-m", "llm_message_queue_amd.cli", "scheduler", "--gateway", base,
                               "--iterations", "1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
