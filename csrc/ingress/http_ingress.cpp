@@ -224,6 +224,7 @@ struct Conn {
   std::string in, out, ip;
   size_t out_off = 0;
   bool close_after = false;
+  bool continued = false;   // "100 Continue" already sent for the pending request
 };
 
 int64_t mono_ns() {
@@ -349,7 +350,7 @@ class HttpIngress {
         auto it = conns.find(fd);
         if (it == conns.end()) continue;
         Conn& cn = it->second;
-        bool dead = (evs[k].events & (EPOLLERR | EPOLLHUP)) != 0;
+        bool dead = (evs[k].events & (EPOLLERR | EPOLLHUP)) != 0, eof = false;
         if (evs[k].events & EPOLLIN) {
           for (;;) {
             ssize_t r = ::read(fd, buf, sizeof buf);
@@ -358,10 +359,11 @@ class HttpIngress {
               if (cn.in.size() > (8u << 20)) dead = true;
               continue;
             }
-            if (r == 0) dead = true;
+            if (r == 0) eof = true;   // peer half-closed: answer what it sent, then close
             break;
           }
           if (!dead) process(cn, rng);
+          if (eof) cn.close_after = true;
         }
         if (!dead && !cn.out.empty()) dead = !flush(fd, cn, ep);
         if (dead || (cn.close_after && cn.out.empty())) {
@@ -483,7 +485,7 @@ class HttpIngress {
       std::string method(h, sp1 - h), path(sp1 + 1, sp2 - sp1 - 1);
       bool http10 = std::string(sp2 + 1, std::min<size_t>(8, hl - (sp2 + 1 - h))) == "HTTP/1.0";
       size_t clen = 0;
-      bool keep = !http10, bad_len = false, chunked = false;
+      bool keep = !http10, bad_len = false, chunked = false, expect100 = false;
       std::string api_key, authz;
       // headers (case-insensitive names)
       const char* line = (const char*)memchr(h, '\n', hl);
@@ -506,6 +508,10 @@ class HttpIngress {
                       val.find_first_not_of("0123456789") != std::string::npos;
             clen = bad_len ? 0 : (size_t)strtoull(val.c_str(), nullptr, 10);
           } else if (name == "transfer-encoding") chunked = true;
+          else if (name == "expect") {
+            for (auto& c : val) c = (char)tolower((unsigned char)c);
+            expect100 = val == "100-continue";
+          }
           else if (name == "authorization") authz = val;
           else if (guard_ && name == guard_->key_header()) api_key = val;
           else if (name == "connection") {
@@ -526,7 +532,15 @@ class HttpIngress {
           respond(cn, 400, "Bad Request", "{\"error\":\"bad Content-Length\"}", false);
         break;
       }
-      if (cn.in.size() < he + 4 + clen) break;  // body not complete yet
+      if (cn.in.size() < he + 4 + clen) {  // body not complete yet
+        // curl and friends hold a large body back until told to send it
+        if (expect100 && !cn.continued) {
+          cn.out.append("HTTP/1.1 100 Continue\r\n\r\n");
+          cn.continued = true;
+        }
+        break;
+      }
+      cn.continued = false;
       const char* body = cn.in.data() + he + 4;
       requests_++;
       if (method == "POST" && (path == "/api/v1/messages" || path == "/api/v1/messages/")) {

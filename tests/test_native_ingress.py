@@ -173,3 +173,33 @@ def test_json_scanner_properties():
 
     arbitrary()
     wellformed()
+
+
+def test_native_ingress_expect_continue_and_half_close(stack):
+    _, ing, port = stack
+    body = json.dumps({"content": "x" * 2000}).encode()
+    s = socket.create_connection(("127.0.0.1", port))
+    s.settimeout(5)
+    s.sendall(b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nExpect: 100-continue\r\n"
+              b"Content-Length: %d\r\n\r\n" % len(body))
+    assert s.recv(4096).startswith(b"HTTP/1.1 100 Continue\r\n\r\n")
+    s.sendall(body)
+    data = b""
+    while b"\r\n\r\n" not in data:
+        data += s.recv(65536)
+    assert data.startswith(b"HTTP/1.1 202")
+    s.close()
+    # a client that half-closes after its request still gets the answer
+    s = socket.create_connection(("127.0.0.1", port))
+    s.settimeout(5)
+    b2 = json.dumps({"content": "bye"}).encode()
+    s.sendall(b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n%s" % (len(b2), b2))
+    s.shutdown(socket.SHUT_WR)
+    data = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    assert data.startswith(b"HTTP/1.1 202")
