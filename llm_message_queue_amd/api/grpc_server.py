@@ -351,14 +351,50 @@ class _Service:
         return pb["HealthReply"](status="ok", version=VERSION, time=format_time(time.time_ns()))
 
 
+def _counted(fn, rpc: str, streaming: bool, metrics):
+    """Count each call in ``llm_grpc_requests_total{method, code}``."""
+    if metrics is None or not hasattr(metrics, "grpc_requests"):
+        return fn
+
+    def code_of(context, exc) -> str:
+        c = context.code() if hasattr(context, "code") else None
+        if c is None:
+            return "OK" if exc is None else "UNKNOWN"
+        return c.name
+
+    if streaming:
+        def gen(req, context):
+            exc = None
+            try:
+                yield from fn(req, context)
+            except BaseException as e:        # abort() / cancel / GeneratorExit
+                exc = e
+                raise
+            finally:
+                metrics.grpc_requests.labels(rpc, code_of(context, exc)).inc()
+        return gen
+
+    def unary(req, context):
+        exc = None
+        try:
+            return fn(req, context)
+        except BaseException as e:
+            exc = e
+            raise
+        finally:
+            metrics.grpc_requests.labels(rpc, code_of(context, exc)).inc()
+    return unary
+
+
 def _handler(svc: _Service) -> grpc.GenericRpcHandler:
     table = {}
+    metrics = getattr(svc.G, "metrics", None)
     for rpc, (req, resp, cs, ss, _) in RPCS.items():
         make = {(False, False): grpc.unary_unary_rpc_method_handler,
                 (False, True): grpc.unary_stream_rpc_method_handler,
                 (True, True): grpc.stream_stream_rpc_method_handler,
                 (True, False): grpc.stream_unary_rpc_method_handler}[(cs, ss)]
-        table[rpc] = make(getattr(svc, rpc), request_deserializer=pb[req].FromString,
+        table[rpc] = make(_counted(getattr(svc, rpc), rpc, ss, metrics), request_deserializer=pb[req].FromString,
                           response_serializer=pb[resp].SerializeToString)
     return grpc.method_handlers_generic_handler(f"{PACKAGE}.{SERVICE}", table)
 

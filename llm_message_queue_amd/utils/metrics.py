@@ -93,6 +93,8 @@ class QueueMetrics:
         self.requests_rejected = Counter("llm_queue_requests_rejected_total",
                                          "Requests rejected at admission", ["reason"],
                                          registry=r)
+        self.grpc_requests = Counter("llm_grpc_requests_total", "gRPC calls by method and final status",
+                                     ["method", "code"], registry=r)
 
     def render(self) -> bytes:
         if not HAVE_PROM or self.registry is None:

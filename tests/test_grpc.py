@@ -71,6 +71,10 @@ def test_grpc_submit_watch_stream_and_stats():
         with pytest.raises(grpc.RpcError) as e:
             cli.submit("x", priority=9)
         assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        prom = gw.metrics.render().decode()
+        assert 'llm_grpc_requests_total{code="OK",method="Submit"}' in prom
+        assert 'llm_grpc_requests_total{code="NOT_FOUND",method="GetMessage"}' in prom
+        assert 'llm_grpc_requests_total{code="INVALID_ARGUMENT",method="Submit"}' in prom
     finally:
         cli.close()
         srv.stop()
