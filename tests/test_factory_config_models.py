@@ -124,3 +124,22 @@ def test_conversation_roundtrip():
     c.evicted_count = 3
     c2 = Conversation.from_dict(json.loads(json.dumps(c.to_dict())))
     assert c2.id == "c1" and len(c2.messages) == 1 and c2.summary_tokens == [1, 2] and c2.evicted_count == 3
+
+
+def test_grafana_dashboard_queries_only_exported_series():
+    """Every series the shipped Grafana dashboard queries is one the gateway
+    registers (deployments/grafana/dashboards/llmq.json vs utils/metrics.py)."""
+    import json as _json
+    import os as _os
+    import re as _re
+    from llm_message_queue_amd.utils.metrics import QueueMetrics
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    dash = _json.load(open(_os.path.join(root, "deployments", "grafana", "dashboards", "llmq.json")))
+    exprs = [t["expr"] for p in dash["panels"] for t in p.get("targets", [])]
+    used = {re_m for e in exprs for re_m in _re.findall(r"\b(llm_[a-z0-9_]+)", e)}
+    names = set()
+    suffix = {"counter": ("_total",), "histogram": ("_bucket", "_sum", "_count"), "gauge": ("",)}
+    for fam in QueueMetrics().registry.collect():
+        names.update(fam.name + x for x in suffix.get(fam.type, ("",)))
+    missing = sorted(u for u in used if u not in names)
+    assert used and not missing, missing
