@@ -287,8 +287,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         if user_id:
             convs = G.state.get_user_conversations(user_id)
         else:
-            with G.state._lock:
-                convs = list(G.state._convs.values())
+            convs = G.state.all_conversations()
         if state:
             convs = [c for c in convs if c.state == state]
         return {"conversations": [c.to_dict(False) for c in convs[offset:offset + limit]], "total": len(convs)}

@@ -265,6 +265,12 @@ class StateManager:
                 conv.completed_at = time.time_ns()
         self._persist(conv)
 
+    def all_conversations(self) -> List[Conversation]:
+        """Snapshot of every in-memory conversation (``GET /conversations``
+        without a user filter)."""
+        with self._lock:
+            return list(self._convs.values())
+
     def get_user_conversations(self, user_id: str) -> List[Conversation]:
         with self._lock:
             ids = list(self._users.get(user_id, []))
