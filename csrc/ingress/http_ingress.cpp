@@ -290,6 +290,7 @@ class HttpIngress {
     d["unauthorized"] = unauth_.load();
     d["forbidden"] = forbidden_.load();
     d["rate_limited"] = limited_.load();
+    d["refused_no_fd"] = refused_fd_.load();
     return d;
   }
 
@@ -307,7 +308,7 @@ class HttpIngress {
     a.sin_family = AF_INET;
     a.sin_port = htons(port_);
     inet_pton(AF_INET, host_.c_str(), &a.sin_addr);
-    if (bind(fd, (sockaddr*)&a, sizeof a) < 0 || listen(fd, 1024) < 0) {
+    if (bind(fd, (sockaddr*)&a, sizeof a) < 0 || listen(fd, SOMAXCONN) < 0) {
       ::close(fd);
       return -1;
     }
@@ -324,6 +325,9 @@ class HttpIngress {
     std::mt19937_64 rng((uint64_t)mono_ns() ^ ((uint64_t)tid << 40) ^ (uint64_t)(uintptr_t)this);
     std::vector<epoll_event> evs(256);
     char buf[65536];
+    // out of descriptors: accept + close with this spare so the pending
+    // connection is refused instead of the level-triggered listener spinning
+    int spare = ::open("/dev/null", O_RDONLY | O_CLOEXEC);
     while (running_.load()) {
       int n = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
       for (int k = 0; k < n; ++k) {
@@ -333,7 +337,19 @@ class HttpIngress {
             sockaddr_in pa{};
             socklen_t pl = sizeof pa;
             int c = accept4(lfd, (sockaddr*)&pa, &pl, SOCK_NONBLOCK);
-            if (c < 0) break;
+            if (c < 0) {
+              if ((errno == EMFILE || errno == ENFILE) && spare >= 0) {
+                ::close(spare);
+                // (accept reports EMFILE before it looks at the backlog)
+                int d = accept4(lfd, nullptr, nullptr, 0);
+                if (d >= 0) ::close(d);
+                spare = ::open("/dev/null", O_RDONLY | O_CLOEXEC);
+                if (d < 0) break;                    // backlog drained
+                refused_fd_++;
+                continue;
+              }
+              break;
+            }
             int one = 1;
             setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
             epoll_event ce{};
@@ -375,6 +391,7 @@ class HttpIngress {
       }
     }
     for (auto& kv : conns) ::close(kv.first);
+    if (spare >= 0) ::close(spare);
     ::close(ep);
   }
 
@@ -592,7 +609,7 @@ class HttpIngress {
   std::vector<std::thread> th_;
   std::vector<int> lfds_;
   std::atomic<int64_t> accepted_{0}, rejected_full_{0}, bad_{0}, requests_{0}, conns_{0};
-  std::atomic<int64_t> unauth_{0}, forbidden_{0}, limited_{0};
+  std::atomic<int64_t> unauth_{0}, forbidden_{0}, limited_{0}, refused_fd_{0};
   std::shared_ptr<llmq::Guard> guard_;
   bool envelope_ = false;
 };

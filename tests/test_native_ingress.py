@@ -203,3 +203,106 @@ def test_native_ingress_expect_continue_and_half_close(stack):
         data += chunk
     s.close()
     assert data.startswith(b"HTTP/1.1 202")
+
+
+def test_native_ingress_1500_concurrent_keepalive_connections(stack):
+    """The reference's "> 1,000 concurrent connections" target
+    (docs/performance.md:11): 1500 open keep-alive connections, two requests
+    each, every one answered 202 on its own connection."""
+    import selectors
+    _, ing, port = stack
+    N = 1500
+    body = json.dumps({"content": "conn test"}).encode()
+    req = b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body)
+    socks = []
+    try:
+        for _ in range(N):
+            s = socket.create_connection(("127.0.0.1", port), timeout=10)
+            socks.append(s)
+        for rnd in range(2):
+            for s in socks:
+                s.sendall(req)
+            sel = selectors.DefaultSelector()
+            got = {}
+            for s in socks:
+                s.setblocking(False)
+                sel.register(s, selectors.EVENT_READ)
+                got[s] = b""
+            done = 0
+            t0 = time.time()
+            while done < N and time.time() - t0 < 30:
+                for key, _ in sel.select(timeout=1):
+                    s = key.fileobj
+                    got[s] += s.recv(4096)
+                    if b"\r\n\r\n" in got[s] and got[s].count(b"}") >= 1:
+                        sel.unregister(s)
+                        done += 1
+            sel.close()
+            assert done == N, (rnd, done)
+            assert all(g.startswith(b"HTTP/1.1 202") for g in got.values())
+            for s in socks:
+                s.setblocking(True)
+        assert ing.stats()["accepted"] >= 2 * N
+    finally:
+        for s in socks:
+            s.close()
+
+
+_FD_CHILD = r'''
+import os, resource, sys, json, time
+sys.path.insert(0, sys.argv[1])
+from llm_message_queue_amd.gateway.native_ingress import NativeIngress
+from llm_message_queue_amd.gateway.shm_bridge import RingPair
+name = f"pyt-fd-{os.getpid()}"
+ring = RingPair(name, 1 << 20, "create")
+ing = NativeIngress(0, name, threads=1, host="127.0.0.1")
+port = ing.start()
+soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+used = len(os.listdir("/proc/self/fd"))
+resource.setrlimit(resource.RLIMIT_NOFILE, (used + 40, hard))
+print(port, flush=True)
+sys.stdin.readline()
+t0 = time.process_time()
+time.sleep(1.0)
+cpu = time.process_time() - t0
+print(json.dumps({"refused": ing.stats()["refused_no_fd"], "cpu_s": cpu}), flush=True)
+sys.stdin.readline()
+ing.stop()
+ring.close(unlink=True)
+'''
+
+
+def test_native_ingress_survives_descriptor_exhaustion():
+    """Past RLIMIT_NOFILE the ingress refuses new connections (instead of its
+    level-triggered listener spinning) and serves again once fds free up."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([sys.executable, "-c", _FD_CHILD, root], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                         text=True)
+    try:
+        port = int(p.stdout.readline())
+        socks = []
+        for _ in range(80):
+            try:
+                socks.append(socket.create_connection(("127.0.0.1", port), timeout=2))
+            except OSError:
+                pass
+        time.sleep(0.3)
+        p.stdin.write("\n")
+        p.stdin.flush()
+        st = json.loads(p.stdout.readline())
+        assert st["refused"] > 0
+        assert st["cpu_s"] < 0.5, st                   # no accept spin while exhausted
+        for s in socks:
+            s.close()
+        time.sleep(0.3)
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/health", timeout=5) as r:
+            assert r.status == 200
+    finally:
+        try:
+            p.stdin.write("\n")
+            p.stdin.flush()
+        except OSError:
+            pass
+        p.wait(timeout=20)
