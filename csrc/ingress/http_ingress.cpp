@@ -225,6 +225,7 @@ struct Conn {
   size_t out_off = 0;
   bool close_after = false;
   bool continued = false;   // "100 Continue" already sent for the pending request
+  int64_t last_ns = 0;      // last byte received (idle / slow-client reaping)
 };
 
 int64_t mono_ns() {
@@ -291,11 +292,13 @@ class HttpIngress {
     d["forbidden"] = forbidden_.load();
     d["rate_limited"] = limited_.load();
     d["refused_no_fd"] = refused_fd_.load();
+    d["idle_closed"] = idle_closed_.load();
     return d;
   }
 
   void set_guard(std::shared_ptr<llmq::Guard> g) { guard_ = std::move(g); }
   void set_envelope(bool on) { envelope_ = on; }
+  void set_idle_timeout(double seconds) { idle_ns_.store(seconds > 0 ? (int64_t)(seconds * 1e9) : 0); }
 
  private:
   int listen_socket() {
@@ -328,8 +331,27 @@ class HttpIngress {
     // out of descriptors: accept + close with this spare so the pending
     // connection is refused instead of the level-triggered listener spinning
     int spare = ::open("/dev/null", O_RDONLY | O_CLOEXEC);
+    int64_t next_sweep = mono_ns() + 1'000'000'000;
     while (running_.load()) {
       int n = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
+      const int64_t idle = idle_ns_.load(std::memory_order_relaxed);
+      if (idle > 0 && mono_ns() >= next_sweep) {
+        // reap connections silent for longer than the idle timeout: idle
+        // keep-alives and slow / stalled senders (slowloris) alike
+        const int64_t now = mono_ns();
+        next_sweep = now + std::min<int64_t>(idle / 4 + 1, 1'000'000'000);
+        for (auto it = conns.begin(); it != conns.end();) {
+          if (now - it->second.last_ns > idle && it->second.out_off >= it->second.out.size()) {
+            epoll_ctl(ep, EPOLL_CTL_DEL, it->first, nullptr);
+            ::close(it->first);
+            it = conns.erase(it);
+            conns_--;
+            idle_closed_++;
+          } else {
+            ++it;
+          }
+        }
+      }
       for (int k = 0; k < n; ++k) {
         int fd = evs[k].data.fd;
         if (fd == lfd) {
@@ -359,6 +381,7 @@ class HttpIngress {
             char ipb[INET_ADDRSTRLEN] = {0};
             inet_ntop(AF_INET, &pa.sin_addr, ipb, sizeof ipb);
             conns[c].ip = ipb;
+            conns[c].last_ns = mono_ns();
             conns_++;
           }
           continue;
@@ -371,6 +394,7 @@ class HttpIngress {
           for (;;) {
             ssize_t r = ::read(fd, buf, sizeof buf);
             if (r > 0) {
+              cn.last_ns = mono_ns();
               cn.in.append(buf, (size_t)r);
               if (cn.in.size() > (8u << 20)) dead = true;
               continue;
@@ -609,7 +633,8 @@ class HttpIngress {
   std::vector<std::thread> th_;
   std::vector<int> lfds_;
   std::atomic<int64_t> accepted_{0}, rejected_full_{0}, bad_{0}, requests_{0}, conns_{0};
-  std::atomic<int64_t> unauth_{0}, forbidden_{0}, limited_{0}, refused_fd_{0};
+  std::atomic<int64_t> unauth_{0}, forbidden_{0}, limited_{0}, refused_fd_{0}, idle_closed_{0};
+  std::atomic<int64_t> idle_ns_{60'000'000'000};   // 60 s; 0 = never reap
   std::shared_ptr<llmq::Guard> guard_;
   bool envelope_ = false;
 };
@@ -626,7 +651,8 @@ PYBIND11_MODULE(_ingress, m) {
       .def("stop", &HttpIngress::stop, py::call_guard<py::gil_scoped_release>())
       .def("stats", &HttpIngress::stats)
       .def("set_guard", &HttpIngress::set_guard)
-      .def("set_envelope", &HttpIngress::set_envelope);
+      .def("set_envelope", &HttpIngress::set_envelope)
+      .def("set_idle_timeout", &HttpIngress::set_idle_timeout, py::arg("seconds"));
   py::class_<llmq::Guard, std::shared_ptr<llmq::Guard>>(m, "Guard")
       .def(py::init<std::string, std::string, std::vector<std::string>, std::string, std::string, int64_t, bool,
                     std::unordered_map<std::string, std::vector<std::string>>, std::string, double, double, double,

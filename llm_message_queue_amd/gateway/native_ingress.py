@@ -24,6 +24,12 @@ class NativeIngress:
             if self.guard is not None:
                 self._k.set_guard(self.guard)
             self._k.set_envelope(bool(cfg.server.response_envelope))
+            self.set_idle_timeout(getattr(cfg.server, "idle_timeout", 60_000_000_000) / 1e9)
+
+    def set_idle_timeout(self, seconds: float) -> None:
+        """Close connections silent for longer than this (idle keep-alives and
+        stalled / slowloris senders); 0 = never.  Default 60 s."""
+        self._k.set_idle_timeout(float(seconds))
 
     def start(self) -> int:
         """Start listening; returns the bound port (useful with port 0)."""

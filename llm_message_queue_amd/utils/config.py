@@ -44,6 +44,9 @@ class ServerConfig:
     # gRPC front-end (api/grpc_server.py, service llmq.v1.MessageQueue); 0 = off
     grpc_port: int = 0
     grpc_max_workers: int = 32
+    # native ingress: close connections silent this long (idle keep-alive,
+    # slowloris); 0 = never
+    idle_timeout: int = 60_000_000_000
 
 
 @dataclass
@@ -312,7 +315,7 @@ _DURATION_FIELDS = {
     "max_wait_time", "monitor_interval", "cleanup_interval", "max_retention_period",
     "process_interval", "initial_backoff", "max_backoff", "check_interval", "timeout",
     "health_check_interval", "session_timeout", "heartbeat_timeout", "autoscale_cooldown",
-    "max_idle_time", "lifo_after",
+    "max_idle_time", "lifo_after", "idle_timeout",
 }
 
 

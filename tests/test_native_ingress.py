@@ -306,3 +306,25 @@ def test_native_ingress_survives_descriptor_exhaustion():
         except OSError:
             pass
         p.wait(timeout=20)
+
+
+def test_native_ingress_reaps_idle_and_stalled_connections(stack):
+    _, ing, port = stack
+    ing.set_idle_timeout(0.4)
+    idle = socket.create_connection(("127.0.0.1", port), timeout=5)
+    stalled = socket.create_connection(("127.0.0.1", port), timeout=5)
+    stalled.sendall(b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nContent-Le")   # slowloris
+    busy = socket.create_connection(("127.0.0.1", port), timeout=5)
+    body = json.dumps({"content": "k"}).encode()
+    req = b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body)
+    t0 = time.time()
+    while time.time() - t0 < 1.5:                 # keeps talking: must survive
+        busy.sendall(req)
+        assert busy.recv(4096).startswith(b"HTTP/1.1 202")
+        time.sleep(0.1)
+    assert idle.recv(10) == b"" and stalled.recv(10) == b""          # closed by the server
+    busy.sendall(req)
+    assert busy.recv(4096).startswith(b"HTTP/1.1 202")
+    assert ing.stats()["idle_closed"] >= 2
+    for s in (idle, stalled, busy):
+        s.close()
