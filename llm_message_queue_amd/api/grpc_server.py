@@ -404,9 +404,17 @@ class GrpcServer:
     returns the bound port)."""
 
     def __init__(self, gw_app, port: int = 0, host: str = "0.0.0.0", max_workers: int = 32,
-                 gzip: bool = True):
+                 gzip: bool = True, tls_cert: str = "", tls_key: str = ""):
+        """``tls_cert`` / ``tls_key``: PEM files -> TLS on the port
+        (``server.grpc_tls_cert`` / ``server.grpc_tls_key``); empty = plaintext."""
         self.G = gw_app
         self.host, self.port = host, port
+        self.creds = None
+        if tls_cert or tls_key:
+            if not (tls_cert and tls_key):
+                raise ValueError("gRPC TLS needs both a certificate and a key")
+            with open(tls_key, "rb") as k, open(tls_cert, "rb") as c:
+                self.creds = grpc.ssl_server_credentials([(k.read(), c.read())])
         self._server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers,
                                                               thread_name_prefix="grpc"),
                                    options=server_options(),
@@ -414,7 +422,9 @@ class GrpcServer:
         self._server.add_generic_rpc_handlers((_handler(_Service(gw_app, guard_from_config(gw_app.cfg))),))
 
     def start(self) -> int:
-        self.port = self._server.add_insecure_port(f"{self.host}:{self.port}")
+        addr = f"{self.host}:{self.port}"
+        self.port = (self._server.add_secure_port(addr, self.creds) if self.creds is not None
+                     else self._server.add_insecure_port(addr))
         self._server.start()
         return self.port
 
@@ -426,9 +436,17 @@ class GrpcClient:
     """Thin client for ``llmq.v1.MessageQueue`` (no generated stubs needed)."""
 
     def __init__(self, target: str, token: str = "", api_key: str = "", api_key_header: str = "x-api-key",
-                 gzip: bool = False):
-        self.channel = grpc.insecure_channel(target, options=[("grpc.max_receive_message_length", 4 << 20)],
-                                             compression=grpc.Compression.Gzip if gzip else None)
+                 gzip: bool = False, root_cert: str = ""):
+        """``root_cert``: PEM file of the CA (or the self-signed server
+        certificate) -> TLS channel; empty = plaintext."""
+        opts = [("grpc.max_receive_message_length", 4 << 20)]
+        comp = grpc.Compression.Gzip if gzip else None
+        if root_cert:
+            with open(root_cert, "rb") as f:
+                cred = grpc.ssl_channel_credentials(root_certificates=f.read())
+            self.channel = grpc.secure_channel(target, cred, options=opts, compression=comp)
+        else:
+            self.channel = grpc.insecure_channel(target, options=opts, compression=comp)
         md = []
         if token:
             md.append(("authorization", f"Bearer {token}"))

@@ -120,7 +120,8 @@ def cmd_serve(a, role: str = "serve") -> int:
         grpc_srv = None
         if cfg.server.grpc_port:
             from ..api.grpc_server import GrpcServer
-            grpc_srv = GrpcServer(gapp, cfg.server.grpc_port, cfg.server.host, cfg.server.grpc_max_workers)
+            grpc_srv = GrpcServer(gapp, cfg.server.grpc_port, cfg.server.host, cfg.server.grpc_max_workers,
+                                  tls_cert=cfg.server.grpc_tls_cert, tls_key=cfg.server.grpc_tls_key)
             print(json.dumps({"event": "listening", "host": cfg.server.host, "port": grpc_srv.start(),
                               "protocol": "grpc", "service": "llmq.v1.MessageQueue"}), flush=True)
         while not stop.is_set() and t.is_alive():

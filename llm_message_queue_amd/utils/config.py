@@ -44,6 +44,8 @@ class ServerConfig:
     # gRPC front-end (api/grpc_server.py, service llmq.v1.MessageQueue); 0 = off
     grpc_port: int = 0
     grpc_max_workers: int = 32
+    grpc_tls_cert: str = ""     # PEM paths; both set -> TLS on the gRPC port
+    grpc_tls_key: str = ""
     # native ingress: close connections silent this long (idle keep-alive,
     # slowloris); 0 = never
     idle_timeout: int = 60_000_000_000

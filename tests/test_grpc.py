@@ -143,3 +143,33 @@ def test_grpc_stream_cancel_releases_server_threads():
         cli.close()
         srv.stop()
         gw.stop()
+
+
+def test_grpc_tls(tmp_path):
+    import shutil
+    import subprocess
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI not available")
+    key, crt = tmp_path / "k.pem", tmp_path / "c.pem"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
+                    "-days", "1", "-subj", "/CN=localhost", "-addext", "subjectAltName=DNS:localhost"],
+                   check=True, capture_output=True)
+    cfg = default_config()
+    cfg.queue.worker.process_interval = 5_000_000
+    gw = GatewayApp(cfg, use_gpu=False, simulate_ms=(1, 1, 1, 1))
+    srv = GrpcServer(gw, 0, "127.0.0.1", max_workers=4, tls_cert=str(crt), tls_key=str(key))
+    port = srv.start()
+    sec = GrpcClient(f"localhost:{port}", root_cert=str(crt))
+    plain = GrpcClient(f"127.0.0.1:{port}")
+    try:
+        assert sec.submit("over tls").code == 202
+        with pytest.raises(grpc.RpcError) as e:
+            plain.health(timeout=3)                       # plaintext client cannot talk to a TLS port
+        assert e.value.code() in (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED)
+    finally:
+        sec.close()
+        plain.close()
+        srv.stop()
+        gw.stop()
+    with pytest.raises(ValueError):
+        GrpcServer(gw, 0, tls_cert=str(crt))
