@@ -29,7 +29,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run_mode(gw, engine, wl, convs, turns, residency, think_s, timeout_s, tag):
-    import numpy as np
     import torch
     gw.kv_residency = residency
     gw.conv_home.clear()

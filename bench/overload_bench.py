@@ -57,7 +57,7 @@ def main() -> None:
     import torch
 
     from llm_message_queue_amd.backend.engine import BackendEngine
-    from llm_message_queue_amd.gateway.router import Gateway, LatencyRecorder
+    from llm_message_queue_amd.gateway.router import Gateway
     from llm_message_queue_amd.gateway.workload import PoissonArrivals, Workload
     from llm_message_queue_amd.models.llama_stub import LlamaConfig
     from llm_message_queue_amd.preprocess.preprocessor import Preprocessor

@@ -35,10 +35,9 @@ from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, Response
 
 from ..balancer.load_balancer import Endpoint, LoadBalancerError
-from ..models.message import (ConversationNotFound, ConversationState, Message, MessageStatus,
+from ..models.message import (ConversationNotFound, Message, MessageStatus,
                               PriorityParseError, format_time, level_priority_from_name, parse_priority,
                               priority_name)
-from ..preprocess import oracle
 from ..queue.core import QueueError
 from ..scheduler.resource_scheduler import Resource, ResourceError
 from ..utils.metrics import CONTENT_TYPE_LATEST

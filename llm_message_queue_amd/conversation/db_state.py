@@ -24,7 +24,7 @@ import threading
 import time
 from typing import Any, Dict, List, Optional
 
-from ..models.message import Conversation, ConversationNotFound, Message, MessageStatus, format_time, parse_time
+from ..models.message import Conversation, ConversationNotFound, Message, MessageStatus
 
 _CONV_COLS = ("id", "user_id", "title", "context", "status", "state", "priority", "message_count",
               "last_activity", "last_active_time", "created_at", "updated_at", "completed_at", "metadata")

@@ -18,7 +18,7 @@ import sqlite3
 import threading
 from typing import Dict, List, Optional
 
-from ..models.message import Conversation, ConversationNotFound, format_time, parse_time
+from ..models.message import Conversation, ConversationNotFound
 
 
 class PersistenceStore:

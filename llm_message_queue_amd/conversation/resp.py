@@ -11,7 +11,7 @@ import socket
 import socketserver
 import threading
 import time
-from typing import Dict, List, Optional, Set, Tuple, Union
+from typing import Dict, List, Optional, Set, Union
 
 Reply = Union[None, int, bytes, str, list, Exception]
 

@@ -9,7 +9,7 @@ plain PyTorch fp32 with identically seeded weights.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 

@@ -16,7 +16,7 @@ from the moment the ingress process received the request.
 """
 from __future__ import annotations
 
-from typing import Iterable, List, Optional, Sequence, Tuple
+from typing import Iterable, List, Sequence
 
 import msgpack
 import numpy as np

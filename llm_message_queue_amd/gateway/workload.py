@@ -13,7 +13,6 @@ keyword patterns as a substring.
 """
 from __future__ import annotations
 
-import uuid
 from typing import List, Optional, Tuple
 
 import numpy as np

@@ -17,7 +17,7 @@ poll, `cmd/queue-manager/main.go:112-124`, plus the anti-starvation it lacks):
 """
 from __future__ import annotations
 
-from typing import List, Sequence
+from typing import Sequence
 
 import numpy as np
 

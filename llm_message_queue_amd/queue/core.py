@@ -7,9 +7,8 @@ carries integer handles only.  Message objects live in ``self._store``.
 """
 from __future__ import annotations
 
-import threading
 import time
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 

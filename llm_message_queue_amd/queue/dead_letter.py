@@ -14,7 +14,7 @@ from __future__ import annotations
 import queue as _pyqueue
 import threading
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
 
 from ..models.message import Message, format_time

@@ -24,7 +24,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 from ..models.message import Message, QueueStats, priority_name, now_ns
 from ..utils.logging import get_logger
 from ..utils.metrics import QueueMetrics, default_metrics
-from .core import MultiLevelQueue, QueueEmpty, QueueError, QueueNotFound
+from .core import MultiLevelQueue, QueueError, QueueNotFound
 
 
 @dataclass
