@@ -156,9 +156,10 @@ class _Service:
         self.guard = guard
 
     # ------------------------------------------------------------------ guard
-    def _admit(self, context, rpc: str, user: str = "") -> None:
+    def _check(self, context, rpc: str, user: str = ""):
+        """Guard verdict for one call / one item: (code, reason, retry_after)."""
         if self.guard is None or rpc == "Health":
-            return
+            return 0, "", 0.0
         md = {k.lower(): v for k, v in context.invocation_metadata()}
         method, path = RPCS[rpc][4]
         peer = context.peer() or ""                       # "ipv4:1.2.3.4:port" / "ipv6:[::1]:port"
@@ -166,6 +167,10 @@ class _Service:
         code, _, _, reason, retry = self.guard.check(method, path.replace("{id}", "x"), ip,
                                                      md.get(self.guard.key_header.lower(), ""),
                                                      md.get("authorization", ""), user or md.get("x-user-id", ""))
+        return code, reason, retry
+
+    def _admit(self, context, rpc: str, user: str = "") -> None:
+        code, reason, retry = self._check(context, rpc, user)
         if code == 401:
             context.abort(grpc.StatusCode.UNAUTHENTICATED, reason)
         if code == 403:
@@ -220,15 +225,17 @@ class _Service:
             context.abort(grpc.StatusCode.UNAVAILABLE, r.error)
         return r
 
-    def _submit_many(self, reqs):
-        """Bind + submit every item first (one micro-batch), then collect."""
+    def _submit_many(self, reqs, context):
+        """Bind + submit every item first (one micro-batch), then collect.
+        Every item is its own request to the guard (global / IP / user
+        buckets are charged per message, so batching does not bypass them);
+        a rejected item gets its status in ``code`` / ``error``."""
         staged = []
         for req in reqs:
-            if self.guard is not None and self.guard.active and req.user_id:
-                ok, _ = self.guard.allow_user(req.user_id)
-                if not ok:
-                    staged.append((None, req.id, 429, "user rate limit exceeded"))
-                    continue
+            code, reason, _ = self._check(context, "Submit", req.user_id)
+            if code:
+                staged.append((None, req.id, code, reason))
+                continue
             try:
                 m = self._bind(req)
             except (ValueError, PriorityParseError, TypeError) as e:
@@ -250,10 +257,14 @@ class _Service:
     def SubmitBatch(self, req, context):
         """Many submissions per RPC: per-message gRPC costs (HTTP/2 frames,
         completion-queue round trips) are paid once per batch."""
-        self._admit(context, "SubmitBatch")
         if len(req.items) > 10_000:
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, "at most 10000 items per batch")
-        return pb["SubmitBatchReply"](items=[self._collect(x) for x in self._submit_many(req.items)])
+        staged = self._submit_many(req.items, context)
+        if staged and all(x[0] is None and x[2] in (401, 403) for x in staged):
+            # bad credentials for the whole call: fail it as a unary call would
+            code, why = staged[0][2], staged[0][3]
+            context.abort(grpc.StatusCode.UNAUTHENTICATED if code == 401 else grpc.StatusCode.PERMISSION_DENIED, why)
+        return pb["SubmitBatchReply"](items=[self._collect(x) for x in staged])
 
     def SubmitStream(self, request_iterator, context):
         """Replies in request order.  A reader thread submits as requests arrive
@@ -277,7 +288,7 @@ class _Service:
         def reader():
             try:
                 for req in request_iterator:
-                    if not all(put(item) for item in self._submit_many((req,))):
+                    if not all(put(item) for item in self._submit_many((req,), context)):
                         return
             except grpc.RpcError:
                 pass

@@ -173,3 +173,27 @@ def test_grpc_tls(tmp_path):
         gw.stop()
     with pytest.raises(ValueError):
         GrpcServer(gw, 0, tls_cert=str(crt))
+
+
+def test_grpc_batch_items_charge_rate_limits_individually():
+    """A batch cannot bypass the global bucket: each item takes a token."""
+    cfg = default_config()
+    cfg.security.authentication.method = "jwt"
+    cfg.security.authentication.jwt.secret = SECRET
+    cfg.loadbalancer.rate_limiting.enabled = True
+    cfg.loadbalancer.rate_limiting.global_.requests_per_second = 0.001
+    cfg.loadbalancer.rate_limiting.global_.burst_size = 5
+    gw, srv, port = _stack(cfg)
+    good = GrpcClient(f"127.0.0.1:{port}", token=issue_token(SECRET, "bob"))
+    bad = GrpcClient(f"127.0.0.1:{port}", token="not-a-token")
+    try:
+        out = good.submit_batch([pb["SubmitRequest"](content=f"x{i}") for i in range(10)])
+        assert [x.code for x in out].count(202) == 5 and [x.code for x in out].count(429) == 5
+        with pytest.raises(grpc.RpcError) as e:
+            bad.submit_batch([pb["SubmitRequest"](content="y")])
+        assert e.value.code() == grpc.StatusCode.UNAUTHENTICATED
+    finally:
+        good.close()
+        bad.close()
+        srv.stop()
+        gw.stop()
