@@ -44,6 +44,7 @@ from ..utils.metrics import CONTENT_TYPE_LATEST
 from .security import guard_from_config, redact_config
 
 VERSION = "1.0.0"
+MAX_BODY = 4 << 20
 
 
 def business_error_code(status: int, path: str, msg: str) -> Optional[int]:
@@ -157,6 +158,22 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             env["timestamp"] = format_time(time.time_ns())
             hdrs = {k: v for k, v in resp.headers.items() if k.lower() not in ("content-length", "content-type")}
             return JSONResponse(env, status_code=code, headers=hdrs)
+
+    # ------------------------------------------------------------------ body cap
+    # same 4 MiB cap as the native ingress: a declared oversize body is
+    # refused before it is read (413), not buffered into memory
+    @app.middleware("http")
+    async def body_cap(request: Request, call_next):
+        cl = request.headers.get("content-length")
+        if cl is not None:
+            if not cl.isdigit():
+                return JSONResponse({"error": "bad Content-Length"}, status_code=400)
+            if int(cl) > MAX_BODY:
+                return JSONResponse({"error": "body exceeds 4 MiB"}, status_code=413)
+        elif request.headers.get("transfer-encoding", "").lower() == "chunked":
+            if len(await request.body()) > MAX_BODY:     # cached: the route reads it again
+                return JSONResponse({"error": "body exceeds 4 MiB"}, status_code=413)
+        return await call_next(request)
 
     # ------------------------------------------------------------------ CORS
     @app.middleware("http")

@@ -68,6 +68,11 @@ def test_bad_bodies(client):
     assert client.post("/api/v1/messages", json={"content": "x", "priority": "soonish"}).status_code == 400
     assert client.post("/api/v1/conversations", json={}).status_code == 400
     assert client.get("/api/v1/messages/nope").status_code == 404
+    # 4 MiB body cap (same as the native ingress): declared or chunked
+    big = b'{"content":"' + b"x" * (4 << 20) + b'"}'
+    assert client.post("/api/v1/messages", content=big).status_code == 413
+    assert client.post("/api/v1/messages", content=iter([big[:1 << 20], big[1 << 20:]])).status_code == 413
+    assert client.post("/api/v1/messages", content=iter([b'{"content":', b'"chunked ok"}'])).status_code == 202
 
 
 def test_conversation_flow(client):
