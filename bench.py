@@ -61,6 +61,8 @@ def parse(argv=None):
     ap.add_argument("--no-classifier", action="store_true")
     ap.add_argument("--no-residual-gemm", action="store_true",
                     help="o/down as F.linear + fused residual-add RMSNorm (default: residual in the GEMM epilogue)")
+    ap.add_argument("--split-qkv", action="store_true",
+                    help="q and kv as two GEMMs into one buffer (bench/qkv_split.py; default: one fused QKV GEMM)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--trace-out", default="", help="Chrome trace of sampled requests + backend steps (timed phase)")
@@ -134,7 +136,7 @@ def main(argv=None) -> int:
     engine = BackendEngine(LlamaConfig.by_name(a.model), slots=a.slots, max_ctx=a.max_ctx,
                            token_budget=a.token_budget, device=dev, impl="ref" if dry else "hip", seed=1000 + rank,
                            page=page, gpu_index=rank, max_inflight=a.inflight,
-                           residual_in_gemm=not a.no_residual_gemm)
+                           residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = "least_connections"
@@ -293,7 +295,8 @@ def main(argv=None) -> int:
                    "parallelism": f"dp{world}", "token_budget": a.token_budget,
                    "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap, "inflight": a.inflight,
                    "aging_ms": a.aging_ms, "util": a.util,
-                   "classifier": not a.no_classifier, "residual_in_gemm": not a.no_residual_gemm},
+                   "classifier": not a.no_classifier, "residual_in_gemm": not a.no_residual_gemm,
+                   "split_qkv": a.split_qkv},
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),
         "p99_enqueue_to_dispatch_ms": round(lat["p99_enq_ms"], 3),

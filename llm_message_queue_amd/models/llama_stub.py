@@ -63,7 +63,7 @@ class LlamaConfig:
 
 class LlamaStub:
     def __init__(self, cfg: LlamaConfig, slots: int, max_ctx: int, device="cuda", impl: str = "hip",
-                 seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True):
+                 seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -78,6 +78,14 @@ class LlamaStub:
         # (profiles/r1_gemm_experiments.md).  False: F.linear + fused
         # residual-add RMSNorm.
         self.residual_in_gemm = residual_in_gemm
+        # QKV as two GEMMs (q: d x d, kv: 2*kv_heads*hd x d) written into
+        # column slices of one qkv buffer: the fused 6144-wide GEMM at
+        # T = 4096 is 384 256x256 tiles = 1.5 rounds over 256 CUs; the split
+        # pair measured ~15% faster in isolation (bench/qkv_split.py) and cut
+        # in-model GEMM time 4.3%, but the serving step did not get shorter
+        # (profiles/r1_gemm_experiments.md), so it is off by default.  The
+        # weight stays one tensor; its row slices are contiguous views.
+        self.split_qkv = split_qkv
         g = torch.Generator(device=self.device).manual_seed(seed)
         std = 0.02
 
@@ -144,7 +152,13 @@ class LlamaStub:
             if i > 0:
                 x = ops.rmsnorm(res, L["attn_norm"], cfg.eps) if fused else \
                     ops.rmsnorm(out, L["attn_norm"], cfg.eps, residual=res)
-            qkv = F.linear(x, L["wqkv"])
+            if self.split_qkv:
+                nq = cfg.heads * cfg.head_dim
+                qkv = torch.empty((x.shape[0], L["wqkv"].shape[0]), dtype=x.dtype, device=x.device)
+                torch.mm(x, L["wqkv"][:nq].t(), out=qkv[:, :nq])
+                torch.mm(x, L["wqkv"][nq:].t(), out=qkv[:, nq:])
+            else:
+                qkv = F.linear(x, L["wqkv"])
             q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
                             self.kcache[i], self.vcache[i])
             if tiles is not None:

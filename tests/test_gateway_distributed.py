@@ -527,3 +527,18 @@ def test_residual_in_gemm_matches_fused_norm_path():
     ha, hb = a.hidden(tok, pos, slot).float(), b.hidden(tok, pos, slot).float()
     assert torch.allclose(ha, hb, atol=5e-2, rtol=5e-2), (ha - hb).abs().max()
     assert torch.allclose(a.kcache[1], b.kcache[1], atol=5e-2, rtol=5e-2)
+
+
+def test_split_qkv_matches_fused_qkv_gemm():
+    """q and kv GEMMs written into column slices of one buffer == the fused
+    QKV GEMM (same weight tensor, row-slice views): bitwise equal trunk."""
+    from llm_message_queue_amd.models.llama_stub import LlamaStub
+    cfg = LlamaConfig(vocab=512, dim=2048, layers=2, heads=16, kv_heads=4, ffn=512)
+    a = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, split_qkv=True)
+    b = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, split_qkv=False)
+    tok = torch.randint(0, cfg.vocab, (12,), generator=torch.Generator().manual_seed(0))
+    pos = torch.tensor(list(range(6)) * 2, dtype=torch.int32)
+    slot = torch.tensor([0] * 6 + [1] * 6, dtype=torch.int32)
+    ha, hb = a.hidden(tok, pos, slot).float(), b.hidden(tok, pos, slot).float()
+    assert torch.allclose(ha, hb, atol=1e-2, rtol=1e-2), (ha - hb).abs().max()
+    assert torch.allclose(a.kcache[1].float(), b.kcache[1].float(), atol=1e-2, rtol=1e-2)
