@@ -56,6 +56,9 @@ def parse(argv=None):
                     help="per-tier aging deadlines (realtime,high,normal,low), ms")
     ap.add_argument("--prompt-cap", type=int, default=32)
     ap.add_argument("--util", type=float, default=0.95)
+    ap.add_argument("--steady-ticks", type=int, default=-1,
+                    help="untimed serving ticks at the offered rate before the timed window, so it starts in "
+                         "steady state (-1 = max(60, 4 x --warmup))")
     ap.add_argument("--tick-ms", type=float, default=0.0, help="minimum serving tick period (0 = dynamic)")
     ap.add_argument("--rate", type=float, default=0.0, help="per-GPU offered req/s (0 = calibrate)")
     ap.add_argument("--no-classifier", action="store_true")
@@ -147,6 +150,10 @@ def main(argv=None) -> int:
     gw = Gateway(cfg, preprocessor=pre, engine=engine, comm=comm, load_balancer=lb if world == 1 else None,
                  use_gpu_preprocess=not dry, prompt_cap=a.prompt_cap, gen_tokens=a.gen_tokens)
     wl = Workload(seed=a.seed * 1000 + rank)
+    # one throw-away forward per cold-start shape (small T / small lm_head
+    # M): their one-time GEMM kernel selection must not land on live
+    # requests when the gateway goes idle -> busy (engine.warm_shapes)
+    warmed = engine.warm_shapes()
 
     def sync_all():
         dsync()
@@ -209,29 +216,9 @@ def main(argv=None) -> int:
     gw.flush_latency()
     gw.rec_done.reset()
     arrivals = PoissonArrivals(rate, seed=a.seed * 1000 + rank)
-
-    # ---------------------------------------------------------------- timed
-    # A serving process keeps long-lived state (queues, slots, stores); a
-    # full cyclic-GC pass over it is a multi-ms stall that lands on whatever
-    # requests are waiting.  Freeze the warm heap and collect between runs.
-    gc.collect()
-    gc.freeze()
-    gc.disable()
-    gw.host_profile(reset=True)
-    eng_host0 = engine.host_ns.copy()
-    tracer = None
-    if a.trace_out:
-        from llm_message_queue_amd.utils.tracing import RequestTracer
-        tracer = RequestTracer(sample_every=a.trace_sample)
-        gw.tracer = engine.tracer = tracer
-    d0 = gw.counters["dispatched"]
-    tok0 = engine.total_tokens
-    sync_all()
-    t0 = time.perf_counter()
-    mono0 = time.monotonic()
-    arrivals.reset(mono0)
     tick_s = a.tick_ms / 1e3
-    next_tick = mono0
+    clock = {"next_tick": 0.0}
+
     def pump():
         due = arrivals.due(time.monotonic())
         if due:
@@ -240,20 +227,63 @@ def main(argv=None) -> int:
                 m.arrival_ns = int(ts * 1e9)
             gw.submit(msgs)
 
-    for _ in range(a.steps):
+    def serve_tick():
         # Dynamic batching: ticks run back-to-back while there is work (a
         # busy forward is the batching window); while a launch waits for the
         # GPU the gateway keeps pulling arrivals through ``pump`` (ingest +
         # dispatch into free slots).  An idle gateway sleeps until the next
         # arrival.  --tick-ms > 0 adds a minimum tick period.
         now = time.monotonic()
-        if tick_s > 0 and now < next_tick:
-            time.sleep(next_tick - now)
+        if tick_s > 0 and now < clock["next_tick"]:
+            time.sleep(clock["next_tick"] - now)
         elif engine.inflight() == 0 and gw.pending() == 0 and arrivals.t_next > now:
             time.sleep(min(arrivals.t_next - now, 0.05))
-        next_tick = max(next_tick + tick_s, time.monotonic())
+        clock["next_tick"] = max(clock["next_tick"] + tick_s, time.monotonic())
         pump()
         gw.tick(pump=pump)
+
+    # A serving process keeps long-lived state (queues, slots, stores); a
+    # full cyclic-GC pass over it is a multi-ms stall that lands on whatever
+    # requests are waiting.  Freeze the warm heap and collect between runs.
+    gc.collect()
+    gc.freeze()
+    gc.disable()
+
+    # ---------------------------------------------------------------- steady state (untimed)
+    # Serve the offered Poisson load for a fixed number of ticks (the same on
+    # every rank: each tick is a collective) so the timed window starts with
+    # the queues, batch slots and prefill/decode mix of a running system, not
+    # from the empty one the calibration drain leaves.  The arrival clock
+    # keeps running into the timed window.
+    steady = a.steady_ticks if a.steady_ticks >= 0 else max(60, 4 * a.warmup)
+    sync_all()
+    mono0 = time.monotonic()
+    arrivals.reset(mono0)
+    clock["next_tick"] = mono0
+    for _ in range(steady):
+        serve_tick()
+    gw.flush_latency()
+    gw.rec.reset()
+    gw.rec_done.reset()
+
+    # ---------------------------------------------------------------- timed
+    gw.host_profile(reset=True)
+    eng_host0 = engine.host_ns.copy()
+    tracer = None
+    if a.trace_out:
+        from llm_message_queue_amd.utils.tracing import RequestTracer
+        tracer = RequestTracer(sample_every=a.trace_sample)
+        gw.tracer = engine.tracer = tracer
+    # the window edge's device synchronise must not stall live arrivals: let
+    # the queued forwards finish while still ingesting/admitting, so the
+    # synchronise itself finds an idle GPU
+    gw.quiesce(pump)
+    d0 = gw.counters["dispatched"]
+    tok0 = engine.total_tokens
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        serve_tick()
     sync_all()
     t1 = time.perf_counter()
     gc.enable()
@@ -314,6 +344,8 @@ def main(argv=None) -> int:
         # stricter still: arrival -> last generated token of the 8B backend
         "p99_e2e_target_met": bool(lat_done["p99_ms"] <= P99_TARGET_MS),
         "offered_rate_per_gpu": round(rate, 2),
+        "steady_ticks": steady,
+        "warm_shapes": warmed,
         "calibrated_capacity_per_gpu": round(capacity, 2),
         "backend_tokens_per_s": round(tokens / elapsed, 1) if elapsed > 0 else 0.0,
         "dispatched": dispatched,

@@ -120,6 +120,12 @@ class BackendEngine:
         self.s_active = np.zeros(slots, dtype=bool)
         self._admit_seq = 0
         self._mean_plen = 16.0                              # EMA of admitted prompt lengths
+        # realtime lane: requests of tiers < fast_tiers are prefilled ahead of
+        # every other admitted prompt (their admission order key is shifted
+        # below all others), and the dispatcher may admit them past the
+        # step's prefill headroom (``lane_capacity``)
+        self.fast_tiers = 1
+        self.warmed_shapes = 0
         self.page = page
         self.gpu_index = gpu_index
         self.max_inflight = max(1, max_inflight)
@@ -194,6 +200,12 @@ class BackendEngine:
         # cost is quantised in 256-row tiles, the tail rows are nearly free
         return min(free, max(1, -(-head // max(1, int(round(self._mean_plen))))))
 
+    def lane_capacity(self) -> int:
+        """Slots a realtime request may take beyond ``admit_capacity``: every
+        free (or parked) slot.  Its prefill goes first in the next step, so
+        it starts computing there instead of waiting for headroom."""
+        return len(self.free) + len(self.conv_lru)
+
     def admit(self, reqs: Sequence[Request]) -> List[Request]:
         now = time.monotonic_ns()
         out = []
@@ -234,7 +246,8 @@ class BackendEngine:
             self.s_pref[s] = base
             self.s_gen[s] = 0
             self.s_gmax[s] = r.gen_tokens
-            self.s_seq[s] = self._admit_seq
+            # prefill order key: realtime-lane tiers sort before everything else
+            self.s_seq[s] = self._admit_seq - (1 << 48 if 0 <= r.tier < self.fast_tiers else 0)
             self._admit_seq += 1
             self.s_active[s] = True
             self.s_conv[s] = r.conv
@@ -305,6 +318,48 @@ class BackendEngine:
             tiles[D:, 3] = a0[trep] + toff
         self.s_pref[pre] += take
         return toks, pos, slot, samp, samp_slots, dec_rows, dec_src, tiles, n_pre, D
+
+    def warm_shapes(self, sizes: Optional[Sequence[int]] = None) -> int:
+        """Run one throw-away forward at every token count a cold start can
+        produce, before serving.
+
+        A saturated warm-up only ever runs ~token_budget-token steps; the
+        first SMALL step afterwards (a gateway going idle -> busy, or the first
+        requests after start) used to pay the one-time GEMM kernel selection /
+        code-object load of small-M shapes -- measured at ~135 ms for the
+        first T = 1 forward of the 8B stub (``bench/cold_shapes.py``,
+        ``profiles/r2_cold_shapes.md``) -- on live requests.  Every T in
+        1..32 is run (lm_head rows = T), then a geometric ladder up to the
+        token budget.  Must be called on an idle engine (uses scratch rows of
+        free slots; nothing it writes is ever read by a request)."""
+        if not self.cuda:
+            return 0
+        if self.active or self.conv_lru or self._q:
+            raise RuntimeError("warm_shapes needs an idle engine")
+        if sizes is None:
+            ladder, t = [], 48
+            while t < self.token_budget:
+                ladder.append(t)
+                t = t * 3 // 2
+            sizes = list(range(1, 33)) + ladder + [self.token_budget]
+        dev = self.device
+        n = 0
+        for T in sizes:
+            T = int(min(max(1, T), self.token_budget))
+            r = torch.arange(T, device=dev, dtype=torch.int32)
+            seg = min(16, self.max_ctx)
+            slot = (r // seg) % self.slots
+            pos = r % seg
+            t0 = torch.arange(0, T, seg, device=dev, dtype=torch.int32)
+            tiles = torch.stack([t0, torch.clamp(T - t0, max=seg), (t0 // seg) % self.slots,
+                                 torch.zeros_like(t0)], 1).contiguous() if self.use_tiles else None
+            samp = torch.arange(min(T, self.slots), device=dev, dtype=torch.long)
+            self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(), slot.contiguous(),
+                               samp, tiles=tiles, n_dec=0)
+            n += 1
+        torch.cuda.synchronize(dev)
+        self.warmed_shapes = n
+        return n
 
     def inject(self, **fault) -> None:
         """Fault injection: ``fail_launch=n``, ``slow_ms=x``, ``drop_heartbeat=True``
@@ -464,6 +519,19 @@ class BackendEngine:
         if self.page is not None and not self.cuda and not self.fault.get("drop_heartbeat"):
             self.page.write_host(self.inflight(), self.free_slots(), f.T, f.step)
         return f
+
+    def queued_steps(self) -> int:
+        """Forward steps launched and not yet reaped."""
+        return len(self._q)
+
+    def poll_one(self) -> bool:
+        """Reap the oldest queued step if the GPU finished it (non-blocking);
+        its results are returned by the next ``finish``."""
+        f = self._reap(block=False)
+        if f is None:
+            return False
+        self._reaped.append(f)
+        return True
 
     def finish(self, block: bool = False) -> StepResult:
         """Reap finished steps.  Non-blocking unless ``block`` (then waits for

@@ -87,6 +87,7 @@ def cmd_serve(a, role: str = "serve") -> int:
         local = local_device_index()
         torch.cuda.set_device(local)
         engine, page = _build_engine(cfg, a.model, torch.device("cuda", local))
+        engine.warm_shapes()      # cold-start GEMM shapes before the first request (idle -> busy)
     ring, app_role = None, "serve"
     if role in ("api-gateway", "queue-manager") and not a.no_ring:
         # the split deployment shares ONE request queue through shared memory (D14)

@@ -168,6 +168,9 @@ class Gateway:
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0}
         # overload shedding (expire_queued) -> dead-letter queue
         self.shed_expired = bool(getattr(q, "shed_expired", True))
+        # realtime lane (tier 0 admitted past the step's prefill headroom and
+        # prefilled first): queue.realtime_lane, default on
+        self.realtime_lane = bool(getattr(q, "realtime_lane", True))
         self.dead_letter = dead_letter
         self.on_expire = None       # optional callback(msg)
         # failure detection: a backend error (HIP error / OOM), the telemetry
@@ -361,9 +364,21 @@ class Gateway:
         if self.engine is None or not self.healthy:
             return 0
         free = self.engine.admit_capacity()
-        if free <= 0:
-            return 0
-        msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets(), self.lifo_ns)
+        msgs, tier_idx = [], np.zeros(0, dtype=np.int32)
+        if free > 0:
+            msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets(),
+                                                    self.lifo_ns)
+        lane = self._lane_budget(len(msgs), int((np.asarray(tier_idx) == 0).sum()))
+        if lane > 0:
+            # realtime lane: tier-0 requests the step's prefill headroom could
+            # not take are admitted into any free slot; the engine prefills
+            # them first in the next step (engine.fast_tiers)
+            b = [0] * len(self.tiers)
+            b[0] = lane
+            m2, t2, _ = self.qm.pop_tiers(self.tiers, lane, [0] * len(self.tiers), b, None)
+            if m2:
+                msgs = list(msgs) + list(m2)
+                tier_idx = np.concatenate([np.asarray(tier_idx, dtype=np.int64), np.asarray(t2, dtype=np.int64)])
         if not msgs:
             return 0
         if self.shed_expired:     # expired requests behind a live tier head
@@ -401,6 +416,19 @@ class Gateway:
                 self.qm.requeue_after_failure(r.meta.queue_name, r.meta)
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
+
+    def _lane_budget(self, taken: int, taken0: int) -> int:
+        """How many more tier-0 requests the realtime lane may admit now
+        (``taken`` requests, ``taken0`` of them tier 0, already popped)."""
+        if not self.realtime_lane or self.engine is None or not self.tiers:
+            return 0
+        if self.qm.size(self.tiers[0]) <= 0:
+            return 0
+        room = self.engine.lane_capacity() - taken
+        b = self._budgets()[0]
+        if b >= 0:
+            room = min(room, b - taken0)
+        return max(0, room)
 
     def _dispatch_global(self) -> int:
         W, me = self.world, self.rank
@@ -687,6 +715,21 @@ class Gateway:
         if self.world == 1:
             did = self._dispatch_local() > 0 or did
         return did
+
+    def quiesce(self, pump=None, poll_s: float = 0.0002) -> None:
+        """Wait until no forward step is queued on the GPU, ingesting (and on
+        one rank dispatching) arrivals from ``pump`` meanwhile, then reap the
+        finished steps.  A following ``torch.cuda.synchronize`` returns at
+        once, so a synchronisation point (bench window edges) does not stall
+        live arrivals behind up to ``max_inflight`` forwards."""
+        with self._tick_lock:
+            eng = self.engine
+            if eng is None:
+                return
+            while eng.queued_steps():
+                if not eng.poll_one() and not self._while_waiting(pump):
+                    time.sleep(poll_s)
+            self.finish_backend()
 
     def _tick(self, pump=None):
         res = None

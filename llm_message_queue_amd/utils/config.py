@@ -141,6 +141,10 @@ class QueueConfig:
     # is shed at its deadline).  Off = the reference's FIFO-within-priority.
     adaptive_lifo: bool = False
     lifo_after: int = 0
+    # realtime lane: the highest tier may take any free GPU batch slot even
+    # when the next step's prefill headroom is spoken for, and is prefilled
+    # first in that step (docs/architecture.md:233 "realtime < 100 ms")
+    realtime_lane: bool = True
 
 
 @dataclass

@@ -36,6 +36,10 @@ def test_bench_single_rank_dry_run():
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 2 and d["scaling"] == "weak"
     assert "DRY RUN" in d["data"] and d["value"] > 0 and "gateway_only" in d
+    # the timed window starts in steady state: untimed serving ticks at the
+    # offered rate ran first (the driver's 20-step window used to
+    # start from the empty system the calibration drain left)
+    assert d["steady_ticks"] >= 60
 
 
 def test_bench_four_ranks_torchrun_dry_run():
