@@ -284,6 +284,9 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     for _ in range(a.steps):
         serve_tick()
+    # same at the closing edge: arrivals during the final device drain are
+    # ingested and admitted, not left waiting behind the synchronise
+    gw.quiesce(pump)
     sync_all()
     t1 = time.perf_counter()
     gc.enable()
