@@ -379,6 +379,19 @@ class LoadBalancer:
                     (ep.response_time * 9 + response_time_ns) // 10
             ep.error_rate = (ep.error_rate * 9 + 1) / 10 if is_error else ep.error_rate * 0.9
 
+    def note_dispatch(self, endpoint_id: str, n: int = 1) -> None:
+        """``n`` requests were placed on this endpoint by the multi-GPU
+        planner (the batch equivalent of ``n`` GetEndpoint picks): count them
+        as connections until their completions ``release_endpoint``."""
+        with self._lock:
+            ep = self._find(endpoint_id)
+            if ep is None:
+                return
+            if ep.page is not None:
+                ep.pending += n
+            else:
+                ep.connections += n
+
     def mark_admitted(self, endpoint_id: str, n: int = 1) -> None:
         """GPU endpoints: ``n`` dispatched requests are now counted by the page."""
         with self._lock:

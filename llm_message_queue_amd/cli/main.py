@@ -96,8 +96,14 @@ def cmd_serve(a, role: str = "serve") -> int:
         app_role = "ingress" if role == "api-gateway" else "dispatcher"
     gapp = GatewayApp(cfg, use_gpu=use_gpu, engine=engine, comm=comm, start=False, role=app_role, ring=ring)
     if engine is not None:
-        gapp.lb.add_endpoint(Endpoint(id=f"gpu{rank}", type="llm", gpu_index=rank, page=page,
-                                      max_connections=cfg.gpu.slots_per_gpu))
+        # every rank's balancer lists EVERY GPU of the job (its own bound to
+        # the zero-copy load page): the multi-GPU planner reads the view of
+        # these endpoints -- an operator or the autoscaler removing /
+        # marking one on rank 0 takes that GPU out of placement everywhere
+        world = comm.world if comm is not None else 1
+        for j in range(world):
+            gapp.lb.add_endpoint(Endpoint(id=f"gpu{j}", type="llm", gpu_index=j, page=page if j == rank else None,
+                                          max_connections=cfg.gpu.slots_per_gpu))
         gapp.resources.register_gpu(rank, a.model, cfg.gpu.slots_per_gpu,
                                     torch.cuda.get_device_properties(engine.device).total_memory,
                                     cfg.gpu.slots_per_gpu * cfg.backend.max_ctx)

@@ -118,6 +118,11 @@ class GatewayApp:
                                state_manager=self.state, use_gpu_preprocess=self.preprocessor.gpu_enabled(),
                                queue_manager=self.standard, dead_letter=self.factory.dead_letter_queue)
         self.gateway.on_complete = self._on_complete
+        if engine is not None:
+            # per-GPU usage (in-flight slots, HBM) from every tick's load
+            # exchange -> /api/v1/resources (multi-rank; one rank keeps its
+            # own resource current through the same path)
+            self.gateway.resources = self.resources
         self.batcher = MicroBatcher(self._flush, cfg.preprocessor.batch_window_us, cfg.preprocessor.max_batch)
         self._stop = threading.Event()
         self._wake = threading.Event()

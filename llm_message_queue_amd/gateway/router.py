@@ -158,14 +158,27 @@ class Gateway:
         self._inbox: List[Message] = []
         self._inbox_lock = threading.Lock()
         self.inflight_by_tier = np.zeros(len(self.tiers), dtype=np.int64)
-        self.pinned = np.zeros(self.world, dtype=np.int64)   # queued requests per home GPU
+        # queued requests per (home GPU, tier): KV-residency pins (planner L_PIN)
+        self.pinned = np.zeros((self.world, planner.NTIERS), dtype=np.int64)
+        # multi-GPU placement follows loadbalancer.algorithm (planner.PlanState;
+        # identical on every rank, advanced identically by every plan)
+        self.plan_state = planner.PlanState(strategy=str(getattr(cfg.loadbalancer, "algorithm", "")))
+        self.resources = None          # optional ResourceScheduler: per-GPU usage from the load exchange
+        self._res_next_ns = 0
+        self.hbm_fn = None             # optional () -> (used MiB, total MiB) of this rank's GPU
+        self._hbm_cache = (0, 0, 0)    # (used, total, refreshed at ns)
+        self._rt_ewma_us = 0.0         # service time (admit -> done) EWMA of this GPU
+        self._err_ewma = 0.0           # backend error EWMA of this GPU
+        self.epoch = 0                 # KV migrations completed by this rank
+        self.loads = None              # last all-gathered load matrix
         self.local: Dict[int, Message] = {}          # handle -> msg dispatched to my engine (my origin)
         self.remote_out: Dict[int, Message] = {}      # handle -> msg I sent to another rank
         self.foreign: Dict[int, Tuple[int, int, int]] = {}  # my engine req id -> (origin, handle, tier)
         self._done_owed: Dict[int, List[Tuple[int, int, int, int]]] = {r: [] for r in range(self.world)}
         self.rec = LatencyRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
-                         "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0}
+                         "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
+                         "overcommit": 0}
         # overload shedding (expire_queued) -> dead-letter queue
         self.shed_expired = bool(getattr(q, "shed_expired", True))
         # realtime lane (tier 0 admitted past the step's prefill headroom and
@@ -187,6 +200,8 @@ class Gateway:
         self.cluster_idle = False     # every rank idle at the last load exchange
         self._tick_lock = threading.RLock()     # set_healthy from a telemetry thread waits for the tick
         self.unhealthy_peers: set = set()
+        self.excluded_peers: set = set()    # parked / operator-excluded GPUs (balancer view)
+        self._gpu_eps_seen: set = set()     # GPU endpoints this rank's balancer has registered
         self.on_complete = None     # optional callback(msg)
         self.tracer = None          # optional utils.tracing.RequestTracer
         self.rec_done = LatencyRecorder(len(self.tiers))   # arrival -> completion (end to end)
@@ -233,9 +248,7 @@ class Gateway:
         out = []
         for m, e in zip(batch, errs):
             if e is None and self.world > 1:
-                h = self._home(m)
-                if 0 <= h < self.world:
-                    self.pinned[h] += 1
+                self._pin(m, +1)
             if e is not None:
                 m.status = MessageStatus.FAILED
                 self.counters["rejected"] += 1
@@ -305,6 +318,8 @@ class Gateway:
         if self.shed_expired:
             self.expire_queued()
         if self.world == 1:
+            if self.resources is not None and self.engine is not None and time.monotonic_ns() >= self._res_next_ns:
+                self._observe_loads(self._my_load()[None, :])
             return self._dispatch_local()
         return self._dispatch_global()
 
@@ -329,9 +344,7 @@ class Gateway:
                     m = self.qm.pop_message(name)
                 except QueueError:
                     break
-                h = self._home(m)
-                if 0 <= h < self.world and self.pinned[h] > 0:
-                    self.pinned[h] -= 1
+                self._pin(m, -1)
                 out.append(m)
         self._shed(out)
         return len(out)
@@ -430,22 +443,126 @@ class Gateway:
             room = min(room, b - taken0)
         return max(0, room)
 
-    def _dispatch_global(self) -> int:
-        W, me = self.world, self.rank
+    def _pin(self, m: Message, delta: int) -> None:
+        """Count a queued request against its (home GPU, tier) pin."""
+        h = self._home(m)
+        if 0 <= h < self.world:
+            t = self.tier_of_queue.get(m.queue_name, 2) if m.tier < 0 else m.tier
+            t = min(max(int(t), 0), planner.NTIERS - 1)
+            self.pinned[h, t] = max(0, int(self.pinned[h, t]) + delta)
+
+    def _exclude_mask(self) -> int:
+        """GPUs this rank's balancer view rules out for new work: parked by
+        the autoscaler (endpoint removed), or marked unhealthy by an operator
+        or a health probe.  Only GPU endpoints (``gpu<j>``) count; a rank
+        without a balancer excludes nothing."""
+        lb = self.lb
+        if lb is None:
+            return 0
+        mask = 0
+        for j in range(self.world):
+            try:
+                ep = lb.get_endpoint_by_id(f"gpu{j}")
+            except Exception:
+                if j in self._gpu_eps_seen:       # registered once, now removed (parked)
+                    mask |= 1 << j
+                continue
+            self._gpu_eps_seen.add(j)
+            if not lb._eligible(ep):
+                mask |= 1 << j
+        return mask
+
+    def _weights(self) -> List[int]:
+        lb = self.lb
+        out = []
+        for j in range(self.world):
+            try:
+                out.append(max(1, int(lb.get_endpoint_by_id(f"gpu{j}").weight)) if lb is not None else 1)
+            except Exception:
+                out.append(1)
+        return out
+
+    def _hbm_mib(self) -> Tuple[int, int]:
+        """(used, total) MiB of this rank's GPU: the telemetry page (amd-smi)
+        when the poller fills it, else the HIP allocator's view, refreshed at
+        most every 250 ms (a device query per tick would cost more than the
+        tick's planning)."""
+        eng = self.engine
+        page = getattr(eng, "page", None) if eng is not None else None
+        if page is not None:
+            try:
+                w = page.words
+                if int(w[6]) > 0:
+                    return int(w[5]) >> 20, int(w[6]) >> 20
+            except Exception:
+                pass
+        now = time.monotonic_ns()
+        used, total, at = self._hbm_cache
+        if now - at < 250_000_000:
+            return used, total
+        if self.hbm_fn is not None:
+            used, total = self.hbm_fn()
+        elif eng is not None and getattr(eng, "cuda", False):
+            import torch
+            free_b, tot_b = torch.cuda.mem_get_info(eng.device)
+            used, total = (tot_b - free_b) >> 20, tot_b >> 20
+        self._hbm_cache = (int(used), int(total), now)
+        return int(used), int(total)
+
+    def _my_load(self) -> np.ndarray:
+        W = self.world
         depth, age = self._queue_state()
-        free = self.engine.admit_capacity() if self.engine is not None else 0
-        inflight = self.engine.inflight() if self.engine is not None else 0
-        done_for = [len(self._done_owed[r]) for r in range(W)]
-        load = planner.make_load(free, inflight, depth, age, healthy=self.engine is not None and self.healthy,
-                                 done_for=done_for, pinned=[int(x) for x in self.pinned], stopping=self.stopping)
-        loads = self.comm.all_gather_i64(load)
+        eng = self.engine
+        up = eng is not None and self.healthy
+        free = eng.admit_capacity() if up else 0
+        slots_free = eng.lane_capacity() if (up and self.realtime_lane) else free
+        inflight = eng.inflight() if eng is not None else 0
+        used, total = self._hbm_mib() if eng is not None else (0, 0)
+        return planner.make_load(
+            free, inflight, depth, age, hbm_used_mib=used, hbm_total_mib=total, healthy=up, epoch=self.epoch,
+            done_for=[len(self._done_owed[r]) for r in range(W)], pinned=self.pinned, stopping=self.stopping,
+            slots_free=slots_free, slots_total=eng.slots if eng is not None else 0,
+            exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
+            weights=self._weights())
+
+    def _observe_loads(self, loads: np.ndarray) -> None:
+        """Per-tick bookkeeping on the gathered load matrix: peers' health and
+        stop flags, and (at most every 100 ms) the ResourceScheduler's
+        per-GPU usage -- in-flight slots, HBM, KV tokens -- so
+        ``/api/v1/resources/stats`` tracks real GPU use on every rank."""
+        W = self.world
+        self.loads = loads
         if loads[:, planner.L_STOP].any():
             self.peers_stopping = True
         self.cluster_idle = not (loads[:, planner.L_INFLIGHT].any()
                                  or loads[:, planner.L_DEPTH:planner.L_DEPTH + planner.NTIERS].any()
                                  or loads[:, planner.L_DONE:planner.L_DONE + W].any())
         self.unhealthy_peers = {i for i in range(W) if loads[i, planner.L_HEALTHY] == 0}
-        quota = planner.plan_dispatch(loads, [a // 1000 for a in self.aging_ns])
+        ex = planner.eligible(loads)
+        self.excluded_peers = {i for i in range(W) if not ex[i] and loads[i, planner.L_HEALTHY] != 0}
+        rs = self.resources
+        now = time.monotonic_ns()
+        if rs is None or now < self._res_next_ns:
+            return
+        self._res_next_ns = now + 100_000_000
+        from ..scheduler.resource_scheduler import ResourceType
+        for j in range(W):
+            rid = f"gpu{j}"
+            slots = int(loads[j, planner.L_SLOTS_TOTAL])
+            cap = {ResourceType.GPU: slots, ResourceType.MEMORY: int(loads[j, planner.L_HBM_TOTAL]) << 20}
+            used = {ResourceType.GPU: int(loads[j, planner.L_INFLIGHT]),
+                    ResourceType.MEMORY: int(loads[j, planner.L_HBM_USED]) << 20}
+            try:
+                rs.heartbeat(rid, used=used, capacity=cap)
+            except Exception:            # first sight of a peer GPU: register it
+                rs.register_gpu(j, "llm", slots, cap[ResourceType.MEMORY], 0)
+                rs.heartbeat(rid, used=used, capacity=cap)
+
+    def _dispatch_global(self) -> int:
+        W, me = self.world, self.rank
+        loads = self.comm.all_gather_i64(self._my_load())
+        self._observe_loads(loads)
+        quota = planner.plan_dispatch(loads, [a // 1000 for a in self.aging_ns], self.plan_state)
         # pop exactly my per-tier grant
         mine = quota[me]                              # [W, 4]
         per_tier = mine.sum(axis=0)
@@ -453,41 +570,44 @@ class Gateway:
                                                 [int(x) for x in per_tier], self.lifo_ns)
         by_tier: Dict[int, List[Message]] = {t: [] for t in range(len(self.tiers))}
         for m, t in zip(msgs, tier_idx):
+            self._pin(m, -1)                          # (counted under its queue's tier)
             m.tier = int(t)
             by_tier[int(t)].append(m)
-            h = self._home(m)
-            if 0 <= h < W and self.pinned[h] > 0:
-                self.pinned[h] -= 1
         cap = self.prompt_cap
         width = DESC_HDR + cap
-        send = []
-        local_msgs: List[Message] = []
-        for j in range(W):
-            rows = []
-            for t in range(len(self.tiers)):
-                n = int(mine[j, t])
-                if n <= 0:
-                    continue
-                # KV-residency affinity: fill destination j's quota with the
-                # conversations homed on GPU j first, then in queue order
-                pool = by_tier[t]
-                pref = [m for m in pool if self._home(m, effective=True) == j][:n]
-                if len(pref) < n:
-                    pick = set(id(m) for m in pref)
-                    pref += [m for m in pool if id(m) not in pick][:n - len(pref)]
-                chosen = set(id(m) for m in pref)
-                take, by_tier[t] = pref, [m for m in pool if id(m) not in chosen]
-                if j == me:
-                    local_msgs.extend(take)
+        # destinations: KV-residency first (a turn goes to its home GPU while
+        # that GPU's quota lasts), then queue order fills the rest
+        dest: Dict[int, List[Message]] = {j: [] for j in range(W)}
+        for t, pool in by_tier.items():
+            room = [int(mine[j, t]) for j in range(W)]
+            rest = []
+            for m in pool:
+                h = self._home(m, effective=True)
+                if 0 <= h < W and room[h] > 0:
+                    dest[h].append(m)
+                    room[h] -= 1
                 else:
-                    rows.extend(take)
+                    rest.append(m)
+            k = 0
+            for j in range(W):
+                n = room[j]
+                if n > 0:
+                    dest[j].extend(rest[k:k + n])
+                    k += n
+        done_for = [len(self._done_owed[r]) for r in range(W)]
+        send = []
+        now_ns = time.monotonic_ns()
+        for j in range(W):
+            rows = dest[j] if j != me else []
             buf = np.zeros((len(rows) + done_for[j], width), dtype=np.int32)
             for k, m in enumerate(rows):
                 self._fill_desc(buf[k], m, me, cap)
                 self.remote_out[m.handle] = m
                 self.inflight_by_tier[m.tier] += 1
                 m.endpoint_id = f"gpu{j}"
-                m.dispatched_at = time.monotonic_ns()
+                m.dispatched_at = now_ns
+            if rows and self.lb is not None:
+                self.lb.note_dispatch(f"gpu{j}", len(rows))
             for k, rec in enumerate(self._done_owed[j]):
                 row = buf[len(rows) + k]
                 row[0] = rec[4]
@@ -504,9 +624,8 @@ class Gateway:
         send[me] = np.zeros((0, width), dtype=np.int32)
         got = self.comm.all_to_all_rows(send, recv_counts, width)
         # admit: my own first, then foreign descriptors
-        reqs: List[Request] = []
-        for m in local_msgs:
-            reqs.append(self._make_request(m, m.tier))
+        local_msgs = dest[me]
+        reqs: List[Request] = [self._make_request(m, m.tier) for m in local_msgs]
         for src in range(W):
             for row in got[src]:
                 if row[0] == K_DISPATCH:
@@ -515,7 +634,7 @@ class Gateway:
                     self._remote_done(row)
                 elif row[0] == K_FAIL:
                     self._remote_fail(row)
-        admitted = self.engine.admit(reqs) if (self.engine is not None and reqs) else []
+        admitted = self.engine.admit(reqs) if (self.engine is not None and reqs and self.healthy) else []
         now = time.monotonic_ns()
         tiers, arr, enqs = [], [], []
         for r in admitted:
@@ -535,7 +654,22 @@ class Gateway:
             m.endpoint_id = f"gpu{me}"
         self._record(tiers, arr, enqs, now)
         if len(admitted) < len(reqs):
-            raise RuntimeError(f"rank {me}: plan over-committed backend ({len(reqs)} > {len(admitted)})")
+            # the plan only grants what the engine reported it could take, so
+            # this is a bug or a concurrent health change -- never a reason to
+            # take the rank (and with it every peer's collective) down:
+            # requeue my own, hand foreign ones back to their router
+            self.counters["overcommit"] += len(reqs) - len(admitted)
+            self.log.warning("plan over-committed backend; re-routing", rank=me, planned=len(reqs),
+                             admitted=len(admitted))
+            got_ids = {id(r) for r in admitted}
+            for r in reqs:
+                if id(r) in got_ids:
+                    continue
+                if isinstance(r.meta, Message):
+                    self._requeue(r.meta)
+                else:
+                    origin, handle, tier, _a, _e = r.meta
+                    self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
 
@@ -550,7 +684,8 @@ class Gateway:
         if h is None and m.conversation_id:
             h = self.conv_home.get(m.conversation_id)
         h = -1 if h is None else int(h)
-        if effective and (h in self.unhealthy_peers or (h == self.rank and not self.healthy)):
+        if effective and (h in self.unhealthy_peers or h in self.excluded_peers
+                          or (h == self.rank and not self.healthy)):
             return -1
         return h
 
@@ -594,9 +729,8 @@ class Gateway:
         m.endpoint_id = ""
         m.dispatched_at = 0
         self.qm.requeue_after_failure(m.queue_name, m)
-        h = self._home(m)
-        if self.world > 1 and 0 <= h < self.world:
-            self.pinned[h] += 1
+        if self.world > 1:
+            self._pin(m, +1)
 
     # ------------------------------------------------------------------ health
     def set_healthy(self, healthy: bool, reason: str = "") -> int:
@@ -613,6 +747,7 @@ class Gateway:
         if healthy or not was or self.engine is None:
             return 0
         self.log.warning("GPU backend unhealthy; evacuating", rank=self.rank, reason=reason)
+        self._err_ewma = 0.9 * self._err_ewma + 0.1
         n = 0
         for r in self.engine.abort_all():
             n += 1
@@ -639,7 +774,7 @@ class Gateway:
         adm = int(_join64(row[5:6], row[6:7])[0])
         done = int(_join64(row[7:8], row[8:9])[0])
         self._remember_dialog(m, int(row[3]))
-        self._complete(m, done - adm)
+        self._complete(m, done - adm)     # (releases the balancer's gpu<j> endpoint with this RT)
 
     # ------------------------------------------------------------------ backend step
     def _complete(self, m: Message, process_ns: int) -> None:
@@ -669,6 +804,15 @@ class Gateway:
         if self.engine is None:
             return None
         res = self.engine.finish(block=block)
+        if res.completed:
+            # this GPU's service-time EWMA (alpha 0.1 per completion, as the
+            # reference's ReleaseEndpoint): published in the load vector for
+            # the adaptive strategy on every rank
+            st = np.fromiter((r.done_ns - r.admitted_ns for r in res.completed), dtype=np.float64)
+            a = 1.0 - 0.9 ** len(st)
+            self._rt_ewma_us = (1 - a) * self._rt_ewma_us + a * float(st.mean()) / 1e3 \
+                if self._rt_ewma_us > 0 else float(st.mean()) / 1e3
+            self._err_ewma *= 0.9 ** len(st)
         for r in res.completed:
             if isinstance(r.meta, Message):
                 m = r.meta

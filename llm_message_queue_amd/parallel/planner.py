@@ -1,54 +1,119 @@
 """Deterministic global dispatch / rebalance plan (N10).
 
 Every rank all-gathers the same ``[world, LOAD_WIDTH]`` load matrix and runs
-``plan_dispatch`` on it, so all ranks agree on the plan without a leader.
-The plan answers: how many tier-t requests does router i hand to backend j
-this tick?
+``plan_dispatch`` on it with the same ``PlanState``, so all ranks agree on the
+plan without a leader round-trip (collectives are issued in the same order
+everywhere).  The plan answers: how many tier-t requests does router i hand
+to backend j this tick?
 
 Policy (the gateway-level generalisation of the reference's strict-priority
-poll, `cmd/queue-manager/main.go:112-124`, plus the anti-starvation it lacks):
+poll, `cmd/queue-manager/main.go:112-124`, plus the anti-starvation it lacks,
+and of its per-request endpoint choice, `internal/loadbalancer/load_balancer.go:234-294`):
   1. tiers whose oldest request is past its ``max_wait_time`` are served
      first (aging), then tiers in priority order;
   2. within a tier, scarce capacity is split between routers in proportion to
      their demand (largest remainder, ties to the lower rank);
-  3. a router's grant is placed on its LOCAL backend first (no transfer),
-     then on the backend with the most free slots (least-connections),
-     skipping unhealthy backends; ties go to the lower index.
+  3. conversations homed on GPU j (KV residency, ``L_PIN``) go to j while it
+     has room -- the reference's session affinity (`load_balancer.go:501-558`)
+     made real: the KV of the dialog lives there;
+  4. the rest of the tier's grant is spread over the ELIGIBLE GPUs by the
+     configured ``loadbalancer.algorithm`` -- the reference's selectors
+     (`load_balancer.go:381-498`) applied to a batch of identical requests:
+       * round_robin: a cursor over the GPUs (persisted in ``PlanState``),
+         one request per GPU per turn -> an exact 1/W split over time;
+       * least_connections: water-filling on slot utilisation
+         (in-flight + assigned) / slots, ties to lower HBM use, then index;
+       * weighted_random: multinomial draw (seeded by the shared tick
+         counter, identical on every rank) with weight = endpoint weight x
+         free-slot fraction x free-HBM fraction;
+       * adaptive_load: water-filling on the reference's score
+         0.4 load + 0.4 min(rt_s, 10) + 0.2 (10 err) plus an HBM-pressure
+         term; the reference's 10 % runner-up exploration is a seeded draw;
+       * local_first (MI355X addition): every router keeps what its own GPU
+         can take, the excess goes least-connections;
+  5. the per-GPU counts from step 4 are matched to routers LOCAL FIRST
+     (a router's requests go to its own GPU when the strategy sends work
+     there), so the all_to_all only carries the imbalance.
+A GPU is eligible when it is healthy, not excluded by any rank's balancer
+view (parked by the autoscaler, removed, or marked unhealthy by an operator:
+``L_EXCLUDE`` bitmask) and not shutting down.  Tier 0 may use every free slot
+(the realtime lane, ``L_SLOTS``); the other tiers only the next step's prefill
+headroom (``L_FREE``).
 """
 from __future__ import annotations
 
-from typing import Sequence
+from dataclasses import dataclass
+from typing import Optional, Sequence
 
 import numpy as np
 
 MAX_WORLD = 8
-# [16 + r] = completion records this rank owes router r
-# [24 + j] = queued requests at this router whose conversation is homed on GPU j
-LOAD_WIDTH = 16 + 2 * MAX_WORLD
-L_PIN = 16 + MAX_WORLD
-L_FREE, L_INFLIGHT = 0, 1
-L_DEPTH = 2          # 4 tiers: 2..5
-L_AGE_US = 6         # 4 tiers: 6..9 (oldest head wait, microseconds)
-L_HBM_USED, L_HBM_TOTAL, L_HEALTHY, L_EPOCH = 10, 11, 12, 13
-L_STOP = 14          # the rank is shutting down: every rank leaves after this same tick
-L_DONE = 16
 NTIERS = 4
+# ---- load vector layout (int64)
+L_FREE, L_INFLIGHT = 0, 1        # admits the next step's prefill headroom takes; slots in use
+L_DEPTH = 2                      # 4 tiers: 2..5 queued (within tier budget)
+L_AGE_US = 6                     # 4 tiers: 6..9 (oldest head wait, microseconds)
+L_HBM_USED, L_HBM_TOTAL = 10, 11  # MiB (telemetry page / device memory info)
+L_HEALTHY, L_EPOCH = 12, 13      # epoch: KV migrations this rank has completed
+L_STOP = 14                      # the rank is shutting down: every rank leaves after this same tick
+L_SLOTS = 15                     # free batch slots (realtime lane capacity)
+L_DONE = 16                      # [16 + r] completion records this rank owes router r
+L_PIN = L_DONE + MAX_WORLD       # [24 + 4 j + t] queued tier-t requests here whose conversation is homed on GPU j
+L_EXCLUDE = L_PIN + MAX_WORLD * NTIERS   # 56: bitmask of GPUs this rank's balancer view excludes
+L_RT_US = L_EXCLUDE + 1          # EWMA service time (admit -> done) on this GPU, microseconds
+L_ERR_PPM = L_EXCLUDE + 2        # EWMA backend error rate, parts per million
+L_SLOTS_TOTAL = L_EXCLUDE + 3    # batch slots of this GPU
+L_WEIGHT = L_EXCLUDE + 8         # [64 + j] endpoint weight of GPU j in this rank's balancer (rank 0 row is used)
+LOAD_WIDTH = L_WEIGHT + MAX_WORLD
+
+STRATEGIES = ("round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first")
 
 
 def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[int], hbm_used_mib: int = 0,
               hbm_total_mib: int = 0, healthy: bool = True, epoch: int = 0,
-              done_for: Sequence[int] = (), pinned: Sequence[int] = (), stopping: bool = False) -> np.ndarray:
+              done_for: Sequence[int] = (), pinned=None, stopping: bool = False,
+              slots_free: Optional[int] = None, slots_total: int = 0, exclude_mask: int = 0,
+              rt_us: int = 0, err_ppm: int = 0, weights: Sequence[int] = ()) -> np.ndarray:
+    """``pinned``: [W, 4] (home GPU x tier) queued counts, or a [W] vector
+    (all counted as tier 2, normal -- legacy callers)."""
     v = np.zeros(LOAD_WIDTH, dtype=np.int64)
     v[L_FREE], v[L_INFLIGHT] = free, inflight
     v[L_DEPTH:L_DEPTH + NTIERS] = list(depth)[:NTIERS]
     v[L_AGE_US:L_AGE_US + NTIERS] = list(age_us)[:NTIERS]
     v[L_HBM_USED], v[L_HBM_TOTAL], v[L_HEALTHY], v[L_EPOCH] = hbm_used_mib, hbm_total_mib, int(healthy), epoch
     v[L_STOP] = int(stopping)
+    v[L_SLOTS] = free if slots_free is None else slots_free
     for r, n in enumerate(done_for):
         v[L_DONE + r] = n
-    for j, n in enumerate(pinned):
-        v[L_PIN + j] = n
+    if pinned is not None:
+        p = np.asarray(pinned, dtype=np.int64)
+        if p.ndim == 1:
+            q = np.zeros((len(p), NTIERS), dtype=np.int64)
+            q[:, 2] = p
+            p = q
+        for j in range(min(MAX_WORLD, p.shape[0])):
+            v[L_PIN + NTIERS * j:L_PIN + NTIERS * (j + 1)] = p[j, :NTIERS]
+    v[L_EXCLUDE] = exclude_mask
+    v[L_RT_US], v[L_ERR_PPM], v[L_SLOTS_TOTAL] = rt_us, err_ppm, slots_total
+    for j, w in enumerate(list(weights)[:MAX_WORLD]):
+        v[L_WEIGHT + j] = w
     return v
+
+
+@dataclass
+class PlanState:
+    """Plan inputs that persist across ticks; every rank holds an identical
+    copy and advances it identically (``plan_dispatch`` mutates it)."""
+    strategy: str = "least_connections"
+    rr_cursor: int = 0
+    tick: int = 0
+    seed: int = 0x5EED
+
+    def __post_init__(self):
+        if self.strategy not in STRATEGIES:
+            # the reference falls back to round robin for unknown names
+            # (`load_balancer.go:272-275`; its shipped "weighted_round_robin")
+            self.strategy = "round_robin"
 
 
 def _split(cap: int, demand: np.ndarray) -> np.ndarray:
@@ -66,50 +131,195 @@ def _split(cap: int, demand: np.ndarray) -> np.ndarray:
     return np.minimum(g, demand)
 
 
-def plan_dispatch(loads: np.ndarray, aging_us: Sequence[int]) -> np.ndarray:
-    """Returns quota[i, j, t] (int64, shape [W, W, 4])."""
+def _waterfill(n: int, cap: np.ndarray, level0: np.ndarray, slope: np.ndarray, tie: np.ndarray) -> np.ndarray:
+    """Place ``n`` identical units on bins with capacity ``cap`` so the bins'
+    levels ``level0 + slope * units`` rise evenly (each unit goes to the
+    currently lowest bin; ties by ``tie`` then index).  Exact batch
+    equivalent of repeated argmin selection, O(W log) instead of O(n W)."""
+    W = len(cap)
+    out = np.zeros(W, dtype=np.int64)
+    cap = np.maximum(cap, 0)
+    n = int(min(n, cap.sum()))
+    if n <= 0:
+        return out
+    live = cap > 0
+    lo = float(level0[live].min())
+    hi = float((level0 + slope * cap)[live].max()) + 1.0
+
+    def fill(L):
+        # units each bin takes to reach level L (strictly below L)
+        k = np.ceil((L - level0) / slope - 1e-12)
+        return np.clip(k, 0, cap).astype(np.int64)
+
+    for _ in range(64):
+        mid = 0.5 * (lo + hi)
+        if fill(mid).sum() <= n:
+            lo = mid
+        else:
+            hi = mid
+    out = fill(lo)
+    rem = n - int(out.sum())
+    if rem > 0:
+        # the next units go to the bins whose next level is lowest
+        nxt = level0 + slope * out
+        order = sorted((j for j in range(W) if out[j] < cap[j]), key=lambda j: (nxt[j], tie[j], j))
+        while rem > 0 and order:
+            progressed = False
+            for j in list(order):
+                if rem <= 0:
+                    break
+                if out[j] < cap[j]:
+                    out[j] += 1
+                    rem -= 1
+                    progressed = True
+                if out[j] >= cap[j]:
+                    order.remove(j)
+            if not progressed:
+                break
+    return out
+
+
+def _targets(G: int, cap: np.ndarray, loads: np.ndarray, assigned: np.ndarray, elig: np.ndarray,
+             st: PlanState, t: int, demand_local: np.ndarray) -> np.ndarray:
+    """Per-GPU counts for ``G`` units of tier t under the strategy."""
+    W = len(cap)
+    cap = np.where(elig, cap, 0)
+    G = int(min(G, cap.sum()))
+    if G <= 0:
+        return np.zeros(W, dtype=np.int64)
+    slots = np.maximum(loads[:, L_SLOTS_TOTAL], 1).astype(np.float64)
+    inflight = (loads[:, L_INFLIGHT] + assigned).astype(np.float64)
+    hbm_tot = loads[:, L_HBM_TOTAL].astype(np.float64)
+    hbm_frac = np.where(hbm_tot > 0, loads[:, L_HBM_USED] / np.maximum(hbm_tot, 1), 0.0)
+    s = st.strategy
+    if s == "round_robin":
+        # the cursor walks the FULL GPU list (a GPU leaving does not shift
+        # everybody's turn, as in balancer.load_balancer); per pass every
+        # live GPU gets left // live, the remainder goes to the next ones
+        # from the cursor, which then moves past the last of them
+        out = np.zeros(W, dtype=np.int64)
+        left = G
+        while left > 0:
+            live = [(st.rr_cursor + k) % W for k in range(W) if out[(st.rr_cursor + k) % W] < cap[(st.rr_cursor + k) % W]]
+            if not live:
+                break
+            q, r = divmod(left, len(live))
+            for k, j in enumerate(live):
+                add = min(q + (1 if k < r else 0), int(cap[j] - out[j]))
+                out[j] += add
+                left -= add
+            if r:
+                st.rr_cursor = (live[r - 1] + 1) % W
+        return out
+    if s == "weighted_random":
+        w0 = loads[0, L_WEIGHT:L_WEIGHT + W].astype(np.float64)
+        w0 = np.where(w0 > 0, w0, 1.0)
+        free = np.clip(slots - inflight, 0, None) / slots
+        w = np.where(cap > 0, w0 * free * (1.0 - hbm_frac), 0.0)
+        if w.sum() <= 0:
+            w = (cap > 0).astype(np.float64)
+        rng = np.random.default_rng([st.seed, st.tick, t])
+        out = np.minimum(rng.multinomial(G, w / w.sum()), cap)
+        short = G - int(out.sum())
+        if short > 0:                    # overflow of a full GPU: least-connections
+            out += _waterfill(short, cap - out, inflight / slots + out / slots, 1.0 / slots, hbm_frac)
+        return out
+    if s == "adaptive_load":
+        rt_s = np.minimum(loads[:, L_RT_US] / 1e6, 10.0)
+        err = loads[:, L_ERR_PPM] / 1e6
+        score = 0.4 * inflight / slots + 0.4 * rt_s + 0.2 * (10.0 * err) + 0.2 * hbm_frac
+        out = _waterfill(G, cap, score, 0.4 / slots, hbm_frac)
+        # the reference sends 10 % of picks to the runner-up (exploration)
+        live = np.flatnonzero(cap > 0)
+        if len(live) > 1 and G >= 10:
+            rng = np.random.default_rng([st.seed, st.tick, t, 1])
+            k = int(rng.binomial(G, 0.1))
+            best = live[np.argsort(score[live], kind="stable")]
+            a, b = int(best[0]), int(best[1])
+            k = min(k, int(out[a]), int(cap[b] - out[b]))
+            out[a] -= k
+            out[b] += k
+        return out
+    if s == "local_first":
+        out = np.minimum(demand_local, cap)
+        rest = G - int(out.sum())
+        if rest > 0:
+            out += _waterfill(rest, cap - out, (inflight + out) / slots, 1.0 / slots, hbm_frac)
+        return out
+    # least_connections (default)
+    return _waterfill(G, cap, inflight / slots, 1.0 / slots, hbm_frac)
+
+
+def eligible(loads: np.ndarray) -> np.ndarray:
+    W = loads.shape[0]
+    mask = 0
+    for i in range(W):
+        mask |= int(loads[i, L_EXCLUDE])
+    ex = np.array([(mask >> j) & 1 for j in range(W)], dtype=bool)
+    return (loads[:, L_HEALTHY] > 0) & (loads[:, L_STOP] == 0) & ~ex
+
+
+def plan_dispatch(loads: np.ndarray, aging_us: Sequence[int], state: Optional[PlanState] = None) -> np.ndarray:
+    """Returns quota[i, j, t] (int64, shape [W, W, 4]).  ``state`` defaults
+    to least-connections with no memory across ticks."""
+    st = state if state is not None else PlanState()
     loads = np.asarray(loads, dtype=np.int64)
     W = loads.shape[0]
-    cap = np.where(loads[:, L_HEALTHY] > 0, loads[:, L_FREE], 0).astype(np.int64)
+    elig = eligible(loads)
+    cap_head = np.where(elig, loads[:, L_FREE], 0).astype(np.int64)
+    cap_slot = np.where(elig, np.maximum(loads[:, L_SLOTS], loads[:, L_FREE]), 0).astype(np.int64)
     depth = loads[:, L_DEPTH:L_DEPTH + NTIERS].copy()
     age = loads[:, L_AGE_US:L_AGE_US + NTIERS]
     quota = np.zeros((W, W, NTIERS), dtype=np.int64)
-    pin = loads[:, L_PIN:L_PIN + W].copy() if loads.shape[1] >= L_PIN + W else np.zeros((W, W), np.int64)
+    pin = loads[:, L_PIN:L_PIN + NTIERS * W].reshape(W, W, NTIERS).copy()      # [router, home, tier]
+    assigned = np.zeros(W, dtype=np.int64)
     overdue = [t for t in range(NTIERS)
                if aging_us[t] > 0 and (age[:, t] > aging_us[t]).any() and depth[:, t].sum() > 0]
     order = overdue + [t for t in range(NTIERS) if t not in overdue]
     for t in order:
+        cap = np.minimum(cap_slot, cap_head) if t > 0 else cap_slot.copy()
         total_cap = int(cap.sum())
         if total_cap <= 0:
-            break
+            continue
         grant = _split(total_cap, depth[:, t])
+        left = grant.copy()
+        # 3) KV-residency affinity
         for i in range(W):
-            g = int(grant[i])
-            if g <= 0:
-                continue
-            # KV-residency affinity: conversations homed on GPU j go to j
             for j in range(W):
-                if g <= 0:
+                if left[i] <= 0:
                     break
-                take = min(g, int(pin[i, j]), int(cap[j]))
+                take = min(int(left[i]), int(pin[i, j, t]), int(cap[j]))
                 if take > 0:
                     quota[i, j, t] += take
                     cap[j] -= take
-                    pin[i, j] -= take
-                    g -= take
-            # then local first
-            take = min(g, int(cap[i]))
-            if take:
-                quota[i, i, t] += take
-                cap[i] -= take
-                g -= take
-            while g > 0:
-                j = int(np.argmax(cap))          # most free slots, lowest index on ties
-                if cap[j] <= 0:
-                    break
-                take = min(g, int(cap[j]))
-                quota[i, j, t] += take
-                cap[j] -= take
-                g -= take
-            depth[i, t] -= int(grant[i]) - g
+                    pin[i, j, t] -= take
+                    left[i] -= take
+                    assigned[j] += take
+        # 4) strategy: per-GPU counts for the rest of the tier's grant
+        G = int(left.sum())
+        if G > 0:
+            tgt = _targets(G, cap, loads, assigned, elig, st, t, left)
+            # 5) match routers to those counts, local first
+            for i in range(W):
+                take = min(int(left[i]), int(tgt[i]))
+                if take > 0:
+                    quota[i, i, t] += take
+                    tgt[i] -= take
+                    left[i] -= take
+            for i in range(W):
+                for j in range(W):
+                    if left[i] <= 0:
+                        break
+                    take = min(int(left[i]), int(tgt[j]))
+                    if take > 0:
+                        quota[i, j, t] += take
+                        tgt[j] -= take
+                        left[i] -= take
+        used = quota[:, :, t].sum(axis=0)
+        cap_slot = np.maximum(cap_slot - used, 0)
+        # a realtime request's prefill goes first, so it eats headroom too
+        cap_head = np.maximum(cap_head - used, 0)
+        assigned = quota.sum(axis=(0, 2))
+        depth[:, t] -= quota[:, :, t].sum(axis=1)
+    st.tick += 1
     return quota

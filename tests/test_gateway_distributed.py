@@ -94,15 +94,21 @@ def test_poisson_arrivals_rate():
 
 
 # ---------------------------------------------------------------- planner
-def load(free, depth, age=(0, 0, 0, 0), healthy=True):
-    return planner.make_load(free, 0, depth, age, healthy=healthy)
+def load(free, depth, age=(0, 0, 0, 0), healthy=True, slots=10, **kw):
+    return planner.make_load(free, slots - free, depth, age, healthy=healthy, slots_total=slots, **kw)
 
 
 def test_plan_local_first_then_least_loaded():
+    # GPU0 has 2 free of 10, GPU1 8, GPU2 5: router 0 keeps 2 locally, the
+    # other 8 water-fill slot utilisation (GPU1 0.2 -> 0.5 first, then both)
     loads = np.stack([load(2, [0, 0, 10, 0]), load(8, [0, 0, 0, 0]), load(5, [0, 0, 0, 0])])
-    q = planner.plan_dispatch(loads, [0] * 4)
-    assert q[0, 0, 2] == 2 and q[0, 1, 2] == 8 and q[0, 2, 2] == 0
+    q = planner.plan_dispatch(loads, [0] * 4, planner.PlanState("local_first"))
+    assert q[0, 0, 2] == 2 and q[0, 1, 2] == 6 and q[0, 2, 2] == 2
     assert q.sum() == 10
+    # least_connections: water-fill every GPU's utilisation (0.8 / 0.2 /
+    # 0.5): GPU1 to 0.5, GPU1+GPU2 to 0.8, the last unit to the lowest index
+    q = planner.plan_dispatch(loads, [0] * 4, planner.PlanState("least_connections"))
+    assert q.sum() == 10 and list(q[0, :, 2]) == [1, 6, 3]
 
 
 def test_plan_strict_priority_and_proportional_split():
