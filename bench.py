@@ -72,6 +72,13 @@ def parse(argv=None):
     ap.add_argument("--trace-sample", type=int, default=20, help="trace every Nth completed request")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="rehearse the multi-rank control flow on CPU (gloo, tiny model); not a measurement")
+    ap.add_argument("--ingress", default="per-rank", choices=["per-rank", "rank0"],
+                    help="per-rank: every GPU process fronts its own Poisson stream (weak scaling, one ingress "
+                         "per GPU); rank0: rank 0 alone receives N x the per-GPU rate and the planner spreads it "
+                         "over all GPUs with all_to_all (the `cli serve` topology: HTTP on rank 0)")
+    ap.add_argument("--lb", default="least_connections",
+                    choices=["round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first"],
+                    help="multi-GPU placement strategy (loadbalancer.algorithm)")
     ap.add_argument("--control-plane", default="gloo", choices=["gloo", "nccl"],
                     help="per-tick load/descriptor exchange: host gloo group or RCCL on a side stream")
     ap.add_argument("--gateway-only-s", type=float, default=3.0,
@@ -114,6 +121,7 @@ def main(argv=None) -> int:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         comm = init_from_env(control=a.control_plane)
+    comm_kind = "solo" if world == 1 else str(getattr(comm, "backend", a.control_plane))
 
     def dsync():
         if not dry:
@@ -142,12 +150,13 @@ def main(argv=None) -> int:
                            residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
-    lbcfg.algorithm = "least_connections"
+    lbcfg.algorithm = a.lb
     lbcfg.health_check_interval = 0
     lb = LoadBalancer(lbcfg)
-    lb.add_endpoint(Endpoint(id=f"gpu{rank}", type="llm", gpu_index=rank, page=page,
-                             max_connections=a.slots))
-    gw = Gateway(cfg, preprocessor=pre, engine=engine, comm=comm, load_balancer=lb if world == 1 else None,
+    for j in range(world):          # every rank's balancer lists every GPU (cli serve does the same)
+        lb.add_endpoint(Endpoint(id=f"gpu{j}", type="llm", gpu_index=j, page=page if j == rank else None,
+                                 max_connections=a.slots))
+    gw = Gateway(cfg, preprocessor=pre, engine=engine, comm=comm, load_balancer=lb,
                  use_gpu_preprocess=not dry, prompt_cap=a.prompt_cap, gen_tokens=a.gen_tokens)
     wl = Workload(seed=a.seed * 1000 + rank)
     # one throw-away forward per cold-start shape (small T / small lm_head
@@ -199,6 +208,8 @@ def main(argv=None) -> int:
     # slowest member) is what the offered load is sized against
     capacity = float(np.mean(caps))
     rate = a.rate if a.rate > 0 else a.util * capacity
+    # rank0 ingress: one front door takes the whole job's traffic
+    my_rate = (rate * world if rank == 0 else 0.0) if a.ingress == "rank0" else rate
     # drain the calibration backlog (untimed)
     gw.drop_pending()
 
@@ -215,7 +226,7 @@ def main(argv=None) -> int:
     gw.rec.reset()
     gw.flush_latency()
     gw.rec_done.reset()
-    arrivals = PoissonArrivals(rate, seed=a.seed * 1000 + rank)
+    arrivals = PoissonArrivals(my_rate, seed=a.seed * 1000 + rank)
     tick_s = a.tick_ms / 1e3
     clock = {"next_tick": 0.0}
 
@@ -236,7 +247,7 @@ def main(argv=None) -> int:
         now = time.monotonic()
         if tick_s > 0 and now < clock["next_tick"]:
             time.sleep(clock["next_tick"] - now)
-        elif engine.inflight() == 0 and gw.pending() == 0 and arrivals.t_next > now:
+        elif world == 1 and engine.inflight() == 0 and gw.pending() == 0 and arrivals.t_next > now:
             time.sleep(min(arrivals.t_next - now, 0.05))
         clock["next_tick"] = max(clock["next_tick"] + tick_s, time.monotonic())
         pump()
@@ -256,6 +267,7 @@ def main(argv=None) -> int:
     # from the empty one the calibration drain leaves.  The arrival clock
     # keeps running into the timed window.
     steady = a.steady_ticks if a.steady_ticks >= 0 else max(60, 4 * a.warmup)
+    c0 = {k: gw.counters[k] for k in ("submitted", "completed", "rejected", "expired")}
     sync_all()
     mono0 = time.monotonic()
     arrivals.reset(mono0)
@@ -294,6 +306,19 @@ def main(argv=None) -> int:
         gw.tracer = engine.tracer = None
         tracer.dump(a.trace_out if world == 1 else f"{a.trace_out}.rank{rank}")
     elapsed_local = t1 - t0
+    # untimed: finish every request offered since the steady phase began and
+    # account for all of them (served, rejected or shed -- none lost)
+    pump_stop = arrivals.rate
+    arrivals.rate = 0.0
+    busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
+    n_drain = 0
+    while busy.max() > 0 and n_drain < 2000:
+        gw.tick()
+        n_drain += 1
+        busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
+    arrivals.rate = pump_stop
+    acct = comm.all_gather_i64(np.array([gw.counters[k] - c0[k] for k in ("submitted", "completed", "rejected",
+                                                                          "expired")], dtype=np.int64)).sum(axis=0)
     dispatched_local = gw.counters["dispatched"] - d0
     tokens_local = engine.total_tokens - tok0
 
@@ -325,7 +350,8 @@ def main(argv=None) -> int:
                 "synthetic (Poisson arrivals, 10/30/40/20 tier mix, random-init weights)",
         "config": {"model": f"{a.model}-stub (32L, random bf16)" if a.model == "llama3-8b" else a.model,
                    "global_batch": a.slots * world, "seq_len": a.max_ctx,
-                   "parallelism": f"dp{world}", "token_budget": a.token_budget,
+                   "parallelism": f"dp{world}", "ingress": a.ingress, "placement": a.lb,
+                   "control_plane": comm_kind, "token_budget": a.token_budget,
                    "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap, "inflight": a.inflight,
                    "aging_ms": a.aging_ms, "util": a.util,
                    "classifier": not a.no_classifier, "residual_in_gemm": not a.no_residual_gemm,
@@ -347,7 +373,10 @@ def main(argv=None) -> int:
         # stricter still: arrival -> last generated token of the 8B backend
         "p99_e2e_target_met": bool(lat_done["p99_ms"] <= P99_TARGET_MS),
         "offered_rate_per_gpu": round(rate, 2),
+        "remote_dispatched": int(comm.all_gather_i64(np.array([gw.counters["remote_sent"]], dtype=np.int64)).sum()),
         "steady_ticks": steady,
+        "requests_accounted": {"offered": int(acct[0]), "completed": int(acct[1]), "rejected": int(acct[2]),
+                               "shed": int(acct[3]), "lost": int(acct[0] - acct[1] - acct[2] - acct[3])},
         "warm_shapes": warmed,
         "calibrated_capacity_per_gpu": round(capacity, 2),
         "backend_tokens_per_s": round(tokens / elapsed, 1) if elapsed > 0 else 0.0,

@@ -113,6 +113,13 @@ def cmd_serve(a, role: str = "serve") -> int:
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
+
+    def _watch_fatal():            # a lost peer rank ends this process too
+        while not stop.is_set():
+            if gapp.fatal is not None:
+                stop.set()
+            stop.wait(0.2)
+    threading.Thread(target=_watch_fatal, daemon=True).start()
     if rank == 0 and role in ("serve", "api-gateway", "queue-manager"):
         # queue-manager serves the full API too: with a native ingress in
         # front, status / conversation / admin routes live with the dispatcher
@@ -143,6 +150,9 @@ def cmd_serve(a, role: str = "serve") -> int:
     gapp.stop()
     if page is not None:
         page.close(unlink=True)
+    if gapp.fatal is not None:
+        print(json.dumps({"event": "fatal", "error": str(gapp.fatal)}), flush=True)
+        return 3
     return 0
 
 

@@ -91,6 +91,7 @@ class GatewayApp:
         self._snap_thread: Optional[threading.Thread] = None
         self.telemetry = None
         self._accepted = 0
+        self.fatal: Optional[BaseException] = None     # PeerLost from the serve loop
         self.cfg = cfg
         self.log = get_logger("app")
         self.metrics: QueueMetrics = default_metrics()
@@ -338,13 +339,22 @@ class GatewayApp:
 
     # ------------------------------------------------------------------ dispatch
     def _serve_loop(self) -> None:
+        from ..parallel.comm import PeerLost
         gw = self.gateway
         while True:
             if self._stop.is_set():
                 gw.request_stop()
             if gw.peers_stopping:
                 break
-            gw.tick()
+            try:
+                gw.tick()
+            except PeerLost as e:
+                # a peer rank died: this job cannot tick any more; leave with
+                # a failure status so the launcher restarts a fresh group
+                self.fatal = e
+                self.log.error("peer rank lost; stopping", error=str(e))
+                self._stop.set()
+                break
             self._dispatch_times.append((time.monotonic(), gw.counters["dispatched"]))
             idle = (gw.cluster_idle if gw.world > 1 else
                     self.engine.inflight() == 0 and gw.pending() == 0)

@@ -26,6 +26,16 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 
+class PeerLost(RuntimeError):
+    """A control-plane collective did not complete within the group's
+    timeout: a peer rank died or hung.  Every tick is a collective, so the
+    survivors cannot make progress; the serving loop exits non-zero and the
+    launcher (``torchrun --max-restarts``) starts fresh processes."""
+
+
+DEFAULT_TIMEOUT_S = 60.0
+
+
 class Comm:
     rank: int = 0
     world: int = 1
@@ -123,7 +133,24 @@ class TorchComm(Comm):
         import contextlib
         return self.torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
+    def _guard(self, fn, *args):
+        try:
+            return fn(*args)
+        except PeerLost:
+            raise
+        except Exception as e:      # gloo timeout / connection reset, RCCL DistBackendError
+            raise PeerLost(f"rank {self.rank}: control-plane collective failed ({type(e).__name__}: {e})") from e
+
     def all_gather_i64(self, vec):
+        return self._guard(self._all_gather_i64, vec)
+
+    def all_to_all_rows(self, send, recv_counts, width):
+        return self._guard(self._all_to_all_rows, send, recv_counts, width)
+
+    def broadcast_i64(self, vec, root=0):
+        return self._guard(self._broadcast_i64, vec, root)
+
+    def _all_gather_i64(self, vec):
         torch = self.torch
         with self._ctx():
             v = self._put(np.asarray(vec, dtype=np.int64).reshape(-1))
@@ -131,7 +158,7 @@ class TorchComm(Comm):
             self.dist.all_gather_into_tensor(out, v, group=self.group)
             return self._get(out).reshape(self.world, -1)
 
-    def all_to_all_rows(self, send, recv_counts, width):
+    def _all_to_all_rows(self, send, recv_counts, width):
         torch = self.torch
         send_counts = [int(np.asarray(s).size // width) for s in send]
         flat = np.concatenate([np.asarray(s, dtype=np.int32).reshape(-1) for s in send]) \
@@ -149,7 +176,7 @@ class TorchComm(Comm):
             a += c
         return res
 
-    def broadcast_i64(self, vec, root=0):
+    def _broadcast_i64(self, vec, root=0):
         with self._ctx():
             v = self._put(np.asarray(vec, dtype=np.int64).reshape(-1))
             self.dist.broadcast(v, src=root, group=self.group)
@@ -163,14 +190,15 @@ class TorchComm(Comm):
 
     def barrier(self):
         if self.backend == "nccl":
-            self.dist.barrier(group=self.group, device_ids=[self.device.index])
+            self._guard(lambda: self.dist.barrier(group=self.group, device_ids=[self.device.index]))
         else:
-            self.dist.barrier(group=self.group)
+            self._guard(lambda: self.dist.barrier(group=self.group))
 
 
 class _Hub:
-    def __init__(self, world: int):
+    def __init__(self, world: int, timeout_s: Optional[float] = None):
         self.world = world
+        self.timeout_s = timeout_s
         self.bar = threading.Barrier(world)
         self.slots: List[object] = [None] * world
         self.mail = {}
@@ -184,17 +212,24 @@ class FakeComm(Comm):
         self.hub, self.rank, self.world = hub, rank, hub.world
 
     @staticmethod
-    def make(world: int) -> List["FakeComm"]:
-        hub = _Hub(world)
+    def make(world: int, timeout_s: Optional[float] = None) -> List["FakeComm"]:
+        hub = _Hub(world, timeout_s)
         return [FakeComm(hub, r) for r in range(world)]
+
+    def _wait(self):
+        try:
+            self.hub.bar.wait(self.hub.timeout_s)
+        except threading.BrokenBarrierError as e:
+            raise PeerLost(f"rank {self.rank}: peer did not reach the collective within "
+                           f"{self.hub.timeout_s} s") from e
 
     def _exchange(self, obj):
         h = self.hub
-        h.bar.wait()
+        self._wait()
         h.slots[self.rank] = obj
-        h.bar.wait()
+        self._wait()
         got = list(h.slots)
-        h.bar.wait()
+        self._wait()
         return got
 
     def all_gather_i64(self, vec):
@@ -226,7 +261,7 @@ class FakeComm(Comm):
             t.copy_(h.mail[(src, self.rank)].pop(0))
 
     def barrier(self):
-        self.hub.bar.wait()
+        self._wait()
 
 
 def local_device_index() -> int:
@@ -249,7 +284,7 @@ def gpus_oversubscribed() -> bool:
     return 0 < n < int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
 
 
-def init_from_env(backend: Optional[str] = None, control: str = "gloo"):
+def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_s: Optional[float] = None):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...).
 
     The default process group is ``backend`` (nccl = RCCL when a GPU is
@@ -257,12 +292,20 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo"):
     control plane uses a ``control`` group: "gloo" (host TCP, default --
     decoupled from the GPU streams) or "nccl" (RCCL on a high-priority
     stream, see ``TorchComm``)."""
+    import datetime
     import os
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return SoloComm()
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("LLMQ_COLLECTIVE_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+    # bounded collectives: a dead or hung peer surfaces as PeerLost within
+    # timeout_s instead of blocking every survivor for the backend default
+    # (10-30 min); RCCL's watchdog aborts a timed-out communicator
+    to = datetime.timedelta(seconds=timeout_s)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -276,10 +319,10 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo"):
             local = local_device_index()
             torch.cuda.set_device(local)
             kw["device_id"] = torch.device("cuda", local)
-        dist.init_process_group(backend=backend, **kw)
+        dist.init_process_group(backend=backend, timeout=to, **kw)
     default_backend = dist.get_backend()
     if control == default_backend or (control == "gloo" and default_backend == "gloo"):
         return TorchComm()
-    ctrl = dist.new_group(backend=control)
+    ctrl = dist.new_group(backend=control, timeout=to)
     return TorchComm(group=ctrl, data_group=dist.group.WORLD,
                      device=torch.device("cpu") if control == "gloo" else None)

@@ -133,50 +133,51 @@ def _split(cap: int, demand: np.ndarray) -> np.ndarray:
 
 def _waterfill(n: int, cap: np.ndarray, level0: np.ndarray, slope: np.ndarray, tie: np.ndarray) -> np.ndarray:
     """Place ``n`` identical units on bins with capacity ``cap`` so the bins'
-    levels ``level0 + slope * units`` rise evenly (each unit goes to the
-    currently lowest bin; ties by ``tie`` then index).  Exact batch
-    equivalent of repeated argmin selection, O(W log) instead of O(n W)."""
+    levels ``level0 + slope * units`` rise evenly: the batch equivalent of
+    giving each unit to the currently lowest bin (ties by ``tie``, then
+    index).  Exact and O(W^2) in plain Python floats (W <= 8 bins: numpy
+    per-call overhead would dominate): the fill level is found between the
+    bins' start/saturation breakpoints, whole units are taken below it and
+    the remainder goes to the lowest next levels."""
     W = len(cap)
-    out = np.zeros(W, dtype=np.int64)
-    cap = np.maximum(cap, 0)
-    n = int(min(n, cap.sum()))
+    capl = [max(0, int(c)) for c in cap]
+    l0 = [float(x) for x in level0]
+    sl = [max(float(x), 1e-12) for x in slope]
+    n = min(int(n), sum(capl))
+    out = [0] * W
     if n <= 0:
-        return out
-    live = cap > 0
-    lo = float(level0[live].min())
-    hi = float((level0 + slope * cap)[live].max()) + 1.0
+        return np.zeros(W, dtype=np.int64)
+    live = [j for j in range(W) if capl[j] > 0]
+    pts = sorted({l0[j] for j in live} | {l0[j] + sl[j] * capl[j] for j in live})
 
-    def fill(L):
-        # units each bin takes to reach level L (strictly below L)
-        k = np.ceil((L - level0) / slope - 1e-12)
-        return np.clip(k, 0, cap).astype(np.int64)
+    def units(L):                      # continuous units below level L
+        return sum(min(capl[j], max(0.0, (L - l0[j]) / sl[j])) for j in live)
 
-    for _ in range(64):
-        mid = 0.5 * (lo + hi)
-        if fill(mid).sum() <= n:
-            lo = mid
-        else:
-            hi = mid
-    out = fill(lo)
-    rem = n - int(out.sum())
-    if rem > 0:
-        # the next units go to the bins whose next level is lowest
-        nxt = level0 + slope * out
-        order = sorted((j for j in range(W) if out[j] < cap[j]), key=lambda j: (nxt[j], tie[j], j))
-        while rem > 0 and order:
-            progressed = False
-            for j in list(order):
-                if rem <= 0:
-                    break
-                if out[j] < cap[j]:
-                    out[j] += 1
-                    rem -= 1
-                    progressed = True
-                if out[j] >= cap[j]:
-                    order.remove(j)
-            if not progressed:
-                break
-    return out
+    L = pts[-1]
+    for k in range(1, len(pts)):
+        if units(pts[k]) >= n:
+            lo, hi = pts[k - 1], pts[k]
+            ulo = units(lo)
+            rate = sum(1.0 / sl[j] for j in live if l0[j] <= lo and l0[j] + sl[j] * capl[j] > lo)
+            L = lo + (n - ulo) / rate if rate > 0 else hi
+            break
+    for j in live:                     # whole units strictly below L
+        k = int(np.ceil((L - l0[j]) / sl[j] - 1e-9))
+        out[j] = min(capl[j], max(0, k))
+    over = sum(out) - n
+    while over > 0:                    # integer rounding: undo the last-placed units
+        j = max((j for j in live if out[j] > 0), key=lambda j: (l0[j] + sl[j] * (out[j] - 1), float(tie[j]), j))
+        out[j] -= 1
+        over -= 1
+    rem = n - sum(out)
+    while rem > 0:
+        cand = [j for j in live if out[j] < capl[j]]
+        if not cand:
+            break
+        j = min(cand, key=lambda j: (l0[j] + sl[j] * out[j], float(tie[j]), j))
+        out[j] += 1
+        rem -= 1
+    return np.asarray(out, dtype=np.int64)
 
 
 def _targets(G: int, cap: np.ndarray, loads: np.ndarray, assigned: np.ndarray, elig: np.ndarray,
@@ -261,65 +262,77 @@ def eligible(loads: np.ndarray) -> np.ndarray:
 
 def plan_dispatch(loads: np.ndarray, aging_us: Sequence[int], state: Optional[PlanState] = None) -> np.ndarray:
     """Returns quota[i, j, t] (int64, shape [W, W, 4]).  ``state`` defaults
-    to least-connections with no memory across ticks."""
+    to least-connections with no memory across ticks.  (Inner loops run on
+    Python ints: W <= 8, so numpy scalar indexing would dominate.)"""
     st = state if state is not None else PlanState()
     loads = np.asarray(loads, dtype=np.int64)
     W = loads.shape[0]
     elig = eligible(loads)
-    cap_head = np.where(elig, loads[:, L_FREE], 0).astype(np.int64)
-    cap_slot = np.where(elig, np.maximum(loads[:, L_SLOTS], loads[:, L_FREE]), 0).astype(np.int64)
-    depth = loads[:, L_DEPTH:L_DEPTH + NTIERS].copy()
-    age = loads[:, L_AGE_US:L_AGE_US + NTIERS]
-    quota = np.zeros((W, W, NTIERS), dtype=np.int64)
-    pin = loads[:, L_PIN:L_PIN + NTIERS * W].reshape(W, W, NTIERS).copy()      # [router, home, tier]
-    assigned = np.zeros(W, dtype=np.int64)
+    el = [bool(x) for x in elig]
+    cap_head = [int(loads[j, L_FREE]) if el[j] else 0 for j in range(W)]
+    cap_slot = [max(int(loads[j, L_SLOTS]), int(loads[j, L_FREE])) if el[j] else 0 for j in range(W)]
+    depth = loads[:, L_DEPTH:L_DEPTH + NTIERS].tolist()
+    age = loads[:, L_AGE_US:L_AGE_US + NTIERS].tolist()
+    pin = loads[:, L_PIN:L_PIN + NTIERS * W].reshape(W, W, NTIERS).tolist()      # [router][home][tier]
+    quota = [[[0] * NTIERS for _ in range(W)] for _ in range(W)]
+    assigned = [0] * W
     overdue = [t for t in range(NTIERS)
-               if aging_us[t] > 0 and (age[:, t] > aging_us[t]).any() and depth[:, t].sum() > 0]
+               if aging_us[t] > 0 and any(age[i][t] > aging_us[t] for i in range(W))
+               and sum(depth[i][t] for i in range(W)) > 0]
     order = overdue + [t for t in range(NTIERS) if t not in overdue]
     for t in order:
-        cap = np.minimum(cap_slot, cap_head) if t > 0 else cap_slot.copy()
-        total_cap = int(cap.sum())
+        cap = list(cap_slot) if t == 0 else [min(a, b) for a, b in zip(cap_slot, cap_head)]
+        total_cap = sum(cap)
         if total_cap <= 0:
             continue
-        grant = _split(total_cap, depth[:, t])
-        left = grant.copy()
+        dem = [depth[i][t] for i in range(W)]
+        if sum(dem) <= 0:
+            continue
+        left = [int(x) for x in _split(total_cap, np.asarray(dem, dtype=np.int64))]
+        used = [0] * W
         # 3) KV-residency affinity
         for i in range(W):
+            if left[i] <= 0:
+                continue
             for j in range(W):
-                if left[i] <= 0:
-                    break
-                take = min(int(left[i]), int(pin[i, j, t]), int(cap[j]))
+                take = min(left[i], pin[i][j][t], cap[j])
                 if take > 0:
-                    quota[i, j, t] += take
+                    quota[i][j][t] += take
                     cap[j] -= take
-                    pin[i, j, t] -= take
+                    pin[i][j][t] -= take
                     left[i] -= take
-                    assigned[j] += take
+                    used[j] += take
+                    if left[i] <= 0:
+                        break
         # 4) strategy: per-GPU counts for the rest of the tier's grant
-        G = int(left.sum())
+        G = sum(left)
         if G > 0:
-            tgt = _targets(G, cap, loads, assigned, elig, st, t, left)
+            tgt = [int(x) for x in _targets(G, np.asarray(cap, dtype=np.int64), loads,
+                                            np.asarray([a + u for a, u in zip(assigned, used)], dtype=np.int64),
+                                            elig, st, t,
+                                            np.asarray(left, dtype=np.int64))]
             # 5) match routers to those counts, local first
             for i in range(W):
-                take = min(int(left[i]), int(tgt[i]))
+                take = min(left[i], tgt[i])
                 if take > 0:
-                    quota[i, i, t] += take
+                    quota[i][i][t] += take
                     tgt[i] -= take
                     left[i] -= take
+                    used[i] += take
             for i in range(W):
                 for j in range(W):
                     if left[i] <= 0:
                         break
-                    take = min(int(left[i]), int(tgt[j]))
+                    take = min(left[i], tgt[j])
                     if take > 0:
-                        quota[i, j, t] += take
+                        quota[i][j][t] += take
                         tgt[j] -= take
                         left[i] -= take
-        used = quota[:, :, t].sum(axis=0)
-        cap_slot = np.maximum(cap_slot - used, 0)
-        # a realtime request's prefill goes first, so it eats headroom too
-        cap_head = np.maximum(cap_head - used, 0)
-        assigned = quota.sum(axis=(0, 2))
-        depth[:, t] -= quota[:, :, t].sum(axis=1)
+                        used[j] += take
+        for j in range(W):
+            cap_slot[j] = max(cap_slot[j] - used[j], 0)
+            # a realtime request's prefill goes first, so it eats headroom too
+            cap_head[j] = max(cap_head[j] - used[j], 0)
+            assigned[j] += used[j]
     st.tick += 1
-    return quota
+    return np.asarray(quota, dtype=np.int64).reshape(W, W, NTIERS)

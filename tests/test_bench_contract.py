@@ -47,3 +47,22 @@ def test_bench_four_ranks_torchrun_dry_run():
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "4",
               "--cpu-dry-run", "--steps", "5", "--warmup", "2", "--gateway-only-s", "0"])
     assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["value"] > 0
+
+
+def _rank0_ingress(world):
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(world),
+              "--cpu-dry-run", "--steps", "6", "--warmup", "2", "--steady-ticks", "8", "--gateway-only-s", "0",
+              "--ingress", "rank0", "--lb", "round_robin"], timeout=420)
+    assert d["n_gpus"] == world and d["config"]["ingress"] == "rank0"
+    assert d["remote_dispatched"] > 0                  # the planner spread rank 0's traffic
+    acc = d["requests_accounted"]
+    assert acc["offered"] > 0 and acc["lost"] == 0 and acc["completed"] > 0, acc
+
+
+def test_bench_rank0_ingress_world4_dry_run():
+    _rank0_ingress(4)
+
+
+def test_bench_rank0_ingress_world8_dry_run():
+    _rank0_ingress(8)

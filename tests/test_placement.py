@@ -208,3 +208,52 @@ def test_overcommit_requeues_instead_of_raising(monkeypatch):
         if gws[0].counters["completed"] >= 8:
             break
     assert gws[0].counters["completed"] == 8
+
+
+def test_dead_peer_surfaces_as_peer_lost_within_timeout():
+    """Every tick is a collective: when one rank dies the survivors must
+    fail fast (PeerLost -> serve loop exits non-zero), not hang."""
+    import time
+    from llm_message_queue_amd.parallel.comm import PeerLost
+    W = 4
+    comms = FakeComm.make(W, timeout_s=1.0)
+    gws = []
+    for r in range(W):
+        eng = BackendEngine(MICRO, slots=4, max_ctx=64, token_budget=64, device="cpu", impl="ref", seed=r)
+        gws.append(Gateway(_cfg("local_first"), engine=eng, comm=comms[r], use_gpu_preprocess=False,
+                           prompt_cap=8, gen_tokens=2))
+    _tick_all(gws)                                          # all alive
+    errs, took = {}, {}
+
+    def survivor(r):
+        t0 = time.monotonic()
+        try:
+            for _ in range(50):
+                gws[r].tick()
+        except PeerLost as e:
+            errs[r] = e
+        took[r] = time.monotonic() - t0
+
+    ths = [threading.Thread(target=survivor, args=(r,)) for r in range(W - 1)]   # rank 3 is dead
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(10)
+    assert set(errs) == {0, 1, 2}
+    assert max(took.values()) < 5.0
+
+
+def test_serve_loop_exits_on_peer_lost():
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    from llm_message_queue_amd.parallel.comm import PeerLost
+    c = _cfg("local_first")
+    eng = BackendEngine(MICRO, slots=4, max_ctx=64, token_budget=64, device="cpu", impl="ref")
+    app = GatewayApp(c, use_gpu=False, engine=eng, start=False)
+
+    def boom(*a, **k):
+        raise PeerLost("rank 1 gone")
+    app.gateway.tick = boom
+    app.start()
+    app._loop_thread.join(5)
+    assert isinstance(app.fatal, PeerLost) and app._stop.is_set()
+    app.stop()
