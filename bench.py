@@ -217,7 +217,7 @@ def main(argv=None) -> int:
         # the stop decision must be GLOBAL: every tick is a collective, so all
         # ranks have to run the same number of them
         return (engine.inflight() + len(gw.remote_out) + sum(len(v) for v in gw._done_owed.values())
-                + gw.pending())
+                + gw.pending() + gw.inbox_size())
 
     busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
     while busy.max() > 0:

@@ -939,6 +939,11 @@ class Gateway:
     def pending(self) -> int:
         return self.qm.total_pending()
 
+    def inbox_size(self) -> int:
+        """Submitted, not yet ingested (preprocessed + queued)."""
+        with self._inbox_lock:
+            return len(self._inbox)
+
     def drop_pending(self) -> int:
         n = 0
         for t in self.tiers:
