@@ -108,6 +108,7 @@ class BackendEngine:
         self.s_cached = np.zeros(slots, dtype=np.int64)
         self.kv_reused_tokens = 0
         self.kv_evictions = 0
+        self.kv_imported = 0
         # per-slot host state (the batch builder is vectorised over these)
         self.s_prompt = np.zeros((slots, max_ctx), dtype=np.int32)
         self.s_plen = np.zeros(slots, dtype=np.int64)
@@ -199,6 +200,38 @@ class BackendEngine:
         # (chunked prefill), so a saturated step fills its token budget -- GEMM
         # cost is quantised in 256-row tiles, the tail rows are nearly free
         return min(free, max(1, -(-head // max(1, int(round(self._mean_plen))))))
+
+    # ------------------------------------------------------------------ KV migration (N11)
+    def export_kv(self, conv: int):
+        """(slot, tokens) of conversation ``conv``'s parked KV, or (-1, 0)
+        when it is not resident here (evicted, or a turn is in flight)."""
+        s = self.conv_lru.get(conv)
+        if s is None:
+            return -1, 0
+        return s, int(self.s_cached[s])
+
+    def drop_parked(self, conv: int) -> None:
+        """Forget a parked conversation (its KV moved to another GPU); the
+        slot is free for the next admission (stream order keeps the pending
+        pack copy ahead of any later write to it)."""
+        s = self.conv_lru.pop(conv, None)
+        if s is not None:
+            self.s_conv[s] = -1
+            self.s_cached[s] = 0
+            self.free.append(s)
+
+    def import_kv(self, conv: int, tokens: int) -> int:
+        """Park an incoming conversation's KV (``tokens`` positions) in a
+        slot; returns the slot the caller unpacks into.  The conversation's
+        turn is then admitted like any resident turn (prefills only its new
+        tokens)."""
+        self.drop_parked(conv)
+        s = self._take_slot()
+        self.s_conv[s] = conv
+        self.s_cached[s] = int(tokens)
+        self.conv_lru[conv] = s
+        self.kv_imported += 1
+        return s
 
     def lane_capacity(self) -> int:
         """Slots a realtime request may take beyond ``admit_capacity``: every

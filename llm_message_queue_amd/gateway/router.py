@@ -97,7 +97,9 @@ class LatencyRecorder:
 
 # --------------------------------------------------------------------------- descriptors
 K_DISPATCH, K_DONE, K_FAIL = 1, 2, 3     # K_FAIL: an evacuating backend hands a request back
-DESC_HDR = 14       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, -, conv lo/hi]
+DESC_HDR = 16       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
+#                    dialog history length, -]; flags = (home GPU + 1) | KV_MIGRATE
+KV_MIGRATE = 1 << 8     # descriptor flag: hold the turn until its KV arrives from the home GPU
 
 
 def conv_key(conversation_id: str) -> int:
@@ -171,6 +173,16 @@ class Gateway:
         self._err_ewma = 0.0           # backend error EWMA of this GPU
         self.epoch = 0                 # KV migrations completed by this rank
         self.loads = None              # last all-gathered load matrix
+        # KV migration (N11): a turn placed away from its (alive) home GPU
+        # moves the dialog's KV there instead of replaying the dialog
+        self.kv_migrate = bool(getattr(cfg.gpu, "kv_migration", True))
+        self._mig_out: List[Tuple[int, int, int]] = []       # orders to publish in the next load vector
+        self._await_kv: Dict[int, List[Request]] = {}         # conv key -> turns held for their KV
+        self.migrator = None
+        if self.world > 1 and engine is not None and self.kv_migrate and hasattr(engine, "model"):
+            from ..parallel.migration import KVMigrator
+            self.migrator = KVMigrator(engine.model, self.comm)
+            self.comm.warm_data_plane()
         self.local: Dict[int, Message] = {}          # handle -> msg dispatched to my engine (my origin)
         self.remote_out: Dict[int, Message] = {}      # handle -> msg I sent to another rank
         self.foreign: Dict[int, Tuple[int, int, int]] = {}  # my engine req id -> (origin, handle, tier)
@@ -178,7 +190,7 @@ class Gateway:
         self.rec = LatencyRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
-                         "overcommit": 0}
+                         "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0}
         # overload shedding (expire_queued) -> dead-letter queue
         self.shed_expired = bool(getattr(q, "shed_expired", True))
         # realtime lane (tier 0 admitted past the step's prefill headroom and
@@ -514,16 +526,17 @@ class Gateway:
         depth, age = self._queue_state()
         eng = self.engine
         up = eng is not None and self.healthy
-        free = eng.admit_capacity() if up else 0
-        slots_free = eng.lane_capacity() if (up and self.realtime_lane) else free
-        inflight = eng.inflight() if eng is not None else 0
+        held = self.awaiting_kv()
+        free = max(0, eng.admit_capacity() - held) if up else 0
+        slots_free = max(0, eng.lane_capacity() - held) if (up and self.realtime_lane) else free
+        inflight = (eng.inflight() if eng is not None else 0) + held
         used, total = self._hbm_mib() if eng is not None else (0, 0)
         return planner.make_load(
             free, inflight, depth, age, hbm_used_mib=used, hbm_total_mib=total, healthy=up, epoch=self.epoch,
             done_for=[len(self._done_owed[r]) for r in range(W)], pinned=self.pinned, stopping=self.stopping,
             slots_free=slots_free, slots_total=eng.slots if eng is not None else 0,
             exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
-            weights=self._weights())
+            weights=self._weights(), migrations=self._mig_out)
 
     def _observe_loads(self, loads: np.ndarray) -> None:
         """Per-tick bookkeeping on the gathered load matrix: peers' health and
@@ -561,7 +574,9 @@ class Gateway:
     def _dispatch_global(self) -> int:
         W, me = self.world, self.rank
         loads = self.comm.all_gather_i64(self._my_load())
+        self._mig_out = []                               # published; every rank now executes them
         self._observe_loads(loads)
+        ready = self._migrate(loads)                     # turns whose KV arrived (or replays)
         quota = planner.plan_dispatch(loads, [a // 1000 for a in self.aging_ns], self.plan_state)
         # pop exactly my per-tier grant
         mine = quota[me]                              # [W, 4]
@@ -594,6 +609,7 @@ class Gateway:
                 if n > 0:
                     dest[j].extend(rest[k:k + n])
                     k += n
+        migrate = self._plan_migrations(dest)         # id(msg) -> home GPU sending its KV
         done_for = [len(self._done_owed[r]) for r in range(W)]
         send = []
         now_ns = time.monotonic_ns()
@@ -601,7 +617,7 @@ class Gateway:
             rows = dest[j] if j != me else []
             buf = np.zeros((len(rows) + done_for[j], width), dtype=np.int32)
             for k, m in enumerate(rows):
-                self._fill_desc(buf[k], m, me, cap)
+                self._fill_desc(buf[k], m, me, cap, migrate.get(id(m), -1))
                 self.remote_out[m.handle] = m
                 self.inflight_by_tier[m.tier] += 1
                 m.endpoint_id = f"gpu{j}"
@@ -625,11 +641,21 @@ class Gateway:
         got = self.comm.all_to_all_rows(send, recv_counts, width)
         # admit: my own first, then foreign descriptors
         local_msgs = dest[me]
-        reqs: List[Request] = [self._make_request(m, m.tier) for m in local_msgs]
+        reqs: List[Request] = list(ready)
+        for m in local_msgs:
+            r = self._make_request(m, m.tier)
+            if id(m) in migrate:                      # my own turn, its KV comes next tick
+                self._await_kv.setdefault(r.conv, []).append(r)
+            else:
+                reqs.append(r)
         for src in range(W):
             for row in got[src]:
                 if row[0] == K_DISPATCH:
-                    reqs.append(self._foreign_request(row, cap))
+                    r = self._foreign_request(row, cap)
+                    if int(row[11]) & KV_MIGRATE:
+                        self._await_kv.setdefault(r.conv, []).append(r)
+                    else:
+                        reqs.append(r)
                 elif row[0] == K_DONE:
                     self._remote_done(row)
                 elif row[0] == K_FAIL:
@@ -673,6 +699,59 @@ class Gateway:
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
 
+    def awaiting_kv(self) -> int:
+        """Turns dispatched here that wait for their KV (next tick)."""
+        return sum(len(v) for v in self._await_kv.values())
+
+    def _plan_migrations(self, dest: Dict[int, List[Message]]) -> Dict[int, int]:
+        """Turns placed on a GPU other than their (alive) home GPU move their
+        dialog KV with them: record the order (published in the next load
+        vector) and re-home the conversation now.  At most
+        ``planner.MAX_MIGRATIONS`` per router per tick; the rest replay."""
+        out: Dict[int, int] = {}
+        if self.migrator is None or not self.kv_migrate:
+            return out
+        W = self.world
+        for j in range(W):
+            for m in dest[j]:
+                if not m.conversation_id or len(self._mig_out) >= planner.MAX_MIGRATIONS:
+                    continue
+                h = self._home(m)
+                if not 0 <= h < W or h == j or h in self.unhealthy_peers or (h == self.rank and not self.healthy):
+                    continue
+                ck = conv_key(m.conversation_id)
+                if any(o[0] == ck for o in self._mig_out):
+                    continue                               # one move per conversation per tick
+                out[id(m)] = h
+                self._mig_out.append((ck, h, j))
+                self.conv_home[m.conversation_id] = j
+                if m.metadata and "home_gpu" in m.metadata:
+                    m.metadata["home_gpu"] = j
+        return out
+
+    def _migrate(self, loads: np.ndarray) -> List[Request]:
+        """Execute every router's published orders (same list on every
+        rank), then release the turns held here for them: resident KV if it
+        arrived, else a dialog replay."""
+        orders = planner.migration_orders(loads)
+        imported: Dict[int, int] = {}
+        if orders and self.migrator is not None:
+            imported = self.migrator.execute(orders, self.engine, self.rank)
+            if any(self.rank in (s, d) for _, s, d in orders):
+                self.epoch += 1
+        ready: List[Request] = []
+        if self._await_kv:
+            for ck, rs in self._await_kv.items():
+                got = imported.get(ck, 0)
+                for r in rs:
+                    if got > 0:
+                        self.counters["kv_migrated"] += 1
+                    else:
+                        self.counters["kv_migrate_replays"] += 1
+                ready.extend(rs)
+            self._await_kv = {}
+        return ready
+
     def _home(self, m: Message, effective: bool = False) -> int:
         """GPU holding the conversation's KV (-1: none).  ``effective``: -1
         as well when that GPU is unhealthy (the conversation is re-homed)."""
@@ -689,7 +768,7 @@ class Gateway:
             return -1
         return h
 
-    def _fill_desc(self, row: np.ndarray, m: Message, origin: int, cap: int) -> None:
+    def _fill_desc(self, row: np.ndarray, m: Message, origin: int, cap: int, migrate_from: int = -1) -> None:
         row[0] = K_DISPATCH
         lo, hi = _split64(np.array([m.handle, m.arrival_ns, m.enqueued_at], dtype=np.int64))
         row[1], row[2] = lo[0], hi[0]
@@ -701,6 +780,9 @@ class Gateway:
         row[10] = len(p)
         ck = conv_key(m.conversation_id) if self.kv_residency else -1
         row[12], row[13] = _split64(np.array([ck]))[0][0], _split64(np.array([ck]))[1][0]
+        row[11] = (migrate_from + 1) | KV_MIGRATE if migrate_from >= 0 else 0
+        hist = self.conv_hist.get(m.conversation_id) if m.conversation_id else None
+        row[14] = 0 if hist is None else len(hist)
         row[DESC_HDR:DESC_HDR + len(p)] = p.view(np.int32)
 
     def _foreign_request(self, row: np.ndarray, cap: int) -> Request:
@@ -711,8 +793,13 @@ class Gateway:
         prompt = row[DESC_HDR:DESC_HDR + max(1, plen)].copy()
         ck = int(_join64(row[12:13], row[13:14])[0])
         self._next_req += 1
+        # a non-resident turn replays its dialog: the origin router holds the
+        # history, the descriptor carries its length (the replay's prefill
+        # cost; generated tokens are placeholders there as well)
+        hl = int(row[14])
         return Request(req_id=self._next_req, prompt=prompt, gen_tokens=gen, tier=tier,
-                       meta=(origin, handle, tier, arrival, enq), conv=ck)
+                       meta=(origin, handle, tier, arrival, enq), conv=ck,
+                       history=np.zeros(hl, dtype=np.int32) if hl > 0 else None)
 
     def _remote_fail(self, row: np.ndarray) -> None:
         """The backend my request was sent to evacuated it: queue it again."""
@@ -749,6 +836,15 @@ class Gateway:
         self.log.warning("GPU backend unhealthy; evacuating", rank=self.rank, reason=reason)
         self._err_ewma = 0.9 * self._err_ewma + 0.1
         n = 0
+        held = [r for rs in self._await_kv.values() for r in rs]
+        self._await_kv = {}
+        for r in held:                                  # turns waiting for a KV that will not be used here
+            n += 1
+            if isinstance(r.meta, Message):
+                self._requeue(r.meta)
+            else:
+                origin, handle, tier, _a, _e = r.meta
+                self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
         for r in self.engine.abort_all():
             n += 1
             if isinstance(r.meta, Message):

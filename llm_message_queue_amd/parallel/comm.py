@@ -55,6 +55,17 @@ class Comm:
     def recv_tensor(self, t, src: int) -> None:
         raise NotImplementedError
 
+    def exchange_p2p(self, sends, recvs) -> None:
+        """Point-to-point: post every ``(dst, tensor)`` send and every
+        ``(src, tensor)`` receive, then wait for all of them.  Per peer pair,
+        messages match in issue order (RCCL semantics).  Deadlock-free for
+        any pattern, since nothing waits before everything is posted."""
+        raise NotImplementedError
+
+    def warm_data_plane(self) -> None:
+        """One collective on the data group on every rank (RCCL builds its
+        communicator on the first collective, which p2p batches must not be)."""
+
     def barrier(self) -> None:
         pass
 
@@ -79,6 +90,10 @@ class SoloComm(Comm):
         raise RuntimeError("no peer in a world of one")
 
     recv_tensor = send_tensor
+
+    def exchange_p2p(self, sends, recvs):
+        if sends or recvs:
+            raise RuntimeError("no peer in a world of one")
 
 
 class TorchComm(Comm):
@@ -182,6 +197,30 @@ class TorchComm(Comm):
             self.dist.broadcast(v, src=root, group=self.group)
             return self._get(v)
 
+    def exchange_p2p(self, sends, recvs):
+        if not sends and not recvs:
+            return
+        dist = self.dist
+        g = self.data_group
+        # group ranks -> global ranks for P2POp
+        def peer(r):
+            return dist.get_global_rank(g, r) if g is not None and g is not dist.group.WORLD else r
+        ops = [dist.P2POp(dist.isend, t, peer(d), g) for d, t in sends]
+        ops += [dist.P2POp(dist.irecv, t, peer(s), g) for s, t in recvs]
+        try:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        except Exception as e:
+            raise PeerLost(f"rank {self.rank}: p2p exchange failed ({type(e).__name__}: {e})") from e
+
+    def warm_data_plane(self):
+        torch = self.torch
+        dist = self.dist
+        dev = torch.device("cuda", torch.cuda.current_device()) \
+            if dist.get_backend(self.data_group) == "nccl" else torch.device("cpu")
+        t = torch.zeros(1, device=dev)
+        self._guard(lambda: dist.all_reduce(t, group=self.data_group))
+
     def send_tensor(self, t, dst):
         self.dist.send(t, dst=dst, group=self.data_group)
 
@@ -257,8 +296,15 @@ class FakeComm(Comm):
     def recv_tensor(self, t, src):
         h = self.hub
         with h.cv:
-            h.cv.wait_for(lambda: h.mail.get((src, self.rank)))
+            if not h.cv.wait_for(lambda: h.mail.get((src, self.rank)), timeout=h.timeout_s):
+                raise PeerLost(f"rank {self.rank}: nothing from rank {src} within {h.timeout_s} s")
             t.copy_(h.mail[(src, self.rank)].pop(0))
+
+    def exchange_p2p(self, sends, recvs):
+        for d, t in sends:            # mailbox sends never block
+            self.send_tensor(t, d)
+        for s_, t in recvs:
+            self.recv_tensor(t, s_)
 
     def barrier(self):
         self._wait()

@@ -228,6 +228,9 @@ class GPUConfig:
     telemetry_period_ms: int = 20
     comm_backend: str = "nccl"        # RCCL on ROCm; "gloo" for CPU tests
     control_plane: str = "gloo"       # per-tick load/descriptor exchange: gloo (host) or nccl (RCCL)
+    # move a conversation's KV to the GPU its next turn is placed on (RCCL
+    # send/recv over xGMI) instead of replaying the dialog there
+    kv_migration: bool = True
     rebalance_interval_ms: int = 100
 
 
