@@ -176,6 +176,9 @@ class Gateway:
         # KV migration (N11): a turn placed away from its (alive) home GPU
         # moves the dialog's KV there instead of replaying the dialog
         self.kv_migrate = bool(getattr(cfg.gpu, "kv_migration", True))
+        # conversation affinity in multi-GPU placement (pins); off = every
+        # turn is placed by the strategy alone (bench/migrate_bench.py)
+        self.affinity = True
         self._mig_out: List[Tuple[int, int, int]] = []       # orders to publish in the next load vector
         self._await_kv: Dict[int, List[Request]] = {}         # conv key -> turns held for their KV
         self.migrator = None
@@ -533,7 +536,8 @@ class Gateway:
         used, total = self._hbm_mib() if eng is not None else (0, 0)
         return planner.make_load(
             free, inflight, depth, age, hbm_used_mib=used, hbm_total_mib=total, healthy=up, epoch=self.epoch,
-            done_for=[len(self._done_owed[r]) for r in range(W)], pinned=self.pinned, stopping=self.stopping,
+            done_for=[len(self._done_owed[r]) for r in range(W)],
+            pinned=self.pinned if self.affinity else None, stopping=self.stopping,
             slots_free=slots_free, slots_total=eng.slots if eng is not None else 0,
             exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
             weights=self._weights(), migrations=self._mig_out)
@@ -597,7 +601,7 @@ class Gateway:
             room = [int(mine[j, t]) for j in range(W)]
             rest = []
             for m in pool:
-                h = self._home(m, effective=True)
+                h = self._home(m, effective=True) if self.affinity else -1
                 if 0 <= h < W and room[h] > 0:
                     dest[h].append(m)
                     room[h] -= 1

@@ -97,10 +97,11 @@ class KVMigrator:
             return {}
         self.comm.exchange_p2p(sends, recvs)                  # phase 1: token counts
         sends, recvs, land = [], [], []
+        host = not self._p2p_on_device() and dev.type == "cuda"   # gloo data plane: stage via host
         for dst, conv, slot, n in out_items:
             if n > 0:
                 buf = self.pack(slot, n)
-                sends.append((dst, buf))
+                sends.append((dst, buf.cpu() if host else buf))
                 engine.drop_parked(conv)                     # the KV lives on dst from now on
                 self.bytes_sent += buf.numel() * buf.element_size()
                 self.sent += 1
@@ -109,13 +110,14 @@ class KVMigrator:
             n = int(h.item())
             imported[conv] = 0
             if n > 0:
-                buf = torch.empty(self._shape(n), dtype=self.model.kcache[0].dtype, device=dev)
+                buf = torch.empty(self._shape(n), dtype=self.model.kcache[0].dtype,
+                                  device=torch.device("cpu") if host else dev)
                 recvs.append((src, buf))
                 land.append((conv, buf, n))
         self.comm.exchange_p2p(sends, recvs)                  # phase 2: packed K/V
         for conv, buf, n in land:
             slot = engine.import_kv(conv, n)
-            self.unpack(buf, slot)
+            self.unpack(buf.to(dev, non_blocking=False) if host else buf, slot)
             imported[conv] = n
             self.bytes_recv += buf.numel() * buf.element_size()
             self.received += 1
