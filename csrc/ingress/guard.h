@@ -336,7 +336,8 @@ class Guard {
 
   // Authenticate + authorise + rate-limit one request.  `api_key` is the
   // value of key_header(), `authorization` the Authorization header,
-  // `user_hint` the request's user id when the body names one (per-user
+  // `user_hint` the request's user id when the body names one (ignored for
+  // rate limiting since r2: only an authenticated subject keys the per-user
   // limits fall back to it when the caller is anonymous).
   GuardResult check(const std::string& method, const std::string& path, const std::string& ip,
                     const std::string& api_key, const std::string& authorization, const std::string& user_hint,
@@ -359,11 +360,18 @@ class Guard {
       }
       if (!role_allows(r.role, perm)) return fail(r, G_FORBIDDEN, "role '" + r.role + "' lacks " + perm);
     }
+    // Most specific bucket first: a request one IP's or one user's limit
+    // refuses must not have drained the shared global bucket on its way
+    // (one abusive client could otherwise exhaust global capacity for all).
+    // The per-user bucket is keyed on the AUTHENTICATED subject only; an
+    // anonymous caller is limited by its address (per-IP bucket) -- a body's
+    // user_id is a claim anyone can make, so keying on it would let a
+    // client spend another user's quota.
+    (void)user_hint;
     double ra = 0;
-    if (!global_.allow("*", now_ns, &ra)) return limited(r, "global", ra);
     if (!ip.empty() && !per_ip_.allow(ip, now_ns, &ra)) return limited(r, "per_ip", ra);
-    const std::string& user = !r.subject.empty() ? r.subject : user_hint;
-    if (!user.empty() && !per_user_.allow(user, now_ns, &ra)) return limited(r, "per_user", ra);
+    if (!r.subject.empty() && !per_user_.allow(r.subject, now_ns, &ra)) return limited(r, "per_user", ra);
+    if (!global_.allow("*", now_ns, &ra)) return limited(r, "global", ra);
     return r;
   }
 

@@ -60,6 +60,7 @@ struct Scan {
   bool ok = false;
   std::string id, user_id;
   int priority = 0;
+  std::string error;   // why the body was refused (400 text)
 };
 
 struct JsonScanner {
@@ -69,36 +70,143 @@ struct JsonScanner {
   void ws() {
     while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
   }
+  static int hexv(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  bool hex4(unsigned* cp) {
+    if (e - p < 4) return false;
+    unsigned v = 0;
+    for (int k = 0; k < 4; ++k) {
+      const int h = hexv(p[k]);
+      if (h < 0) return false;
+      v = v * 16 + (unsigned)h;
+    }
+    p += 4;
+    *cp = v;
+    return true;
+  }
+  static void put_utf8(std::string* out, unsigned cp) {
+    if (!out) return;
+    if (cp < 0x80) {
+      out->push_back((char)cp);
+    } else if (cp < 0x800) {
+      out->push_back((char)(0xC0 | (cp >> 6)));
+      out->push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+      out->push_back((char)(0xE0 | (cp >> 12)));
+      out->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      out->push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      out->push_back((char)(0xF0 | (cp >> 18)));
+      out->push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      out->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      out->push_back((char)(0x80 | (cp & 0x3F)));
+    }
+  }
+  // one well-formed UTF-8 sequence (what Python's strict utf-8 decoder
+  // accepts: no overlongs, no encoded surrogates, <= U+10FFFF)
+  bool utf8(std::string* out) {
+    const unsigned char c = (unsigned char)*p;
+    int n;
+    unsigned cp;
+    if (c < 0x80) { n = 0; cp = c; }
+    else if (c >= 0xC2 && c <= 0xDF) { n = 1; cp = c & 0x1F; }
+    else if (c >= 0xE0 && c <= 0xEF) { n = 2; cp = c & 0x0F; }
+    else if (c >= 0xF0 && c <= 0xF4) { n = 3; cp = c & 0x07; }
+    else return false;
+    if (e - p < n + 1) return false;
+    for (int k = 1; k <= n; ++k) {
+      const unsigned char d = (unsigned char)p[k];
+      if ((d & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (d & 0x3F);
+    }
+    if ((n == 2 && cp < 0x800) || (n == 3 && (cp < 0x10000 || cp > 0x10FFFF)) || (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    if (out) out->append(p, (size_t)n + 1);
+    p += n + 1;
+    return true;
+  }
+  // RFC 8259 string: valid escapes only (\uXXXX decoded, surrogate pairs
+  // joined; a lone surrogate is kept as Python keeps it, but callers that
+  // need a printable id reject it), well-formed UTF-8, no raw controls
   bool str(std::string* out) {
     if (p >= e || *p != '"') return false;
     ++p;
     while (p < e && *p != '"') {
       if (*p == '\\') {
         if (p + 1 >= e) return false;
-        if (out) out->push_back(p[1] == 'n' ? '\n' : p[1] == 't' ? '\t' : p[1]);
-        p += (p[1] == 'u') ? 6 : 2;
+        const char c = p[1];
+        p += 2;
+        switch (c) {
+          case '"': if (out) out->push_back('"'); break;
+          case '\\': if (out) out->push_back('\\'); break;
+          case '/': if (out) out->push_back('/'); break;
+          case 'b': if (out) out->push_back('\b'); break;
+          case 'f': if (out) out->push_back('\f'); break;
+          case 'n': if (out) out->push_back('\n'); break;
+          case 'r': if (out) out->push_back('\r'); break;
+          case 't': if (out) out->push_back('\t'); break;
+          case 'u': {
+            unsigned cp;
+            if (!hex4(&cp)) return false;
+            if (cp >= 0xD800 && cp <= 0xDBFF && e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+              const char* save = p;
+              p += 2;
+              unsigned lo;
+              if (!hex4(&lo)) return false;
+              if (lo >= 0xDC00 && lo <= 0xDFFF) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+              else p = save;
+            }
+            if (cp >= 0xD800 && cp <= 0xDFFF) lone_surrogate = true;
+            put_utf8(out, cp);
+            break;
+          }
+          default: return false;
+        }
         continue;
       }
       if ((unsigned char)*p < 0x20) return false;
-      if (out) out->push_back(*p);
-      ++p;
+      if (!utf8(out)) return false;
     }
     if (p >= e) return false;
     ++p;
     return true;
   }
+  // RFC 8259 number: -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
   bool num(double* out) {
     const char* s = p;
-    if (p < e && (*p == '-' || *p == '+')) ++p;
-    bool any = false;
-    while (p < e && ((*p >= '0' && *p <= '9') || *p == '.' || *p == 'e' || *p == 'E' || *p == '-' || *p == '+')) {
+    if (p < e && *p == '-') ++p;
+    if (p >= e) return false;
+    if (*p == '0') {
       ++p;
-      any = true;
+    } else if (*p >= '1' && *p <= '9') {
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    } else {
+      return false;
     }
-    if (!any) return false;
+    bool is_int = true;
+    if (p < e && *p == '.') {
+      ++p;
+      is_int = false;
+      if (p >= e || *p < '0' || *p > '9') return false;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    }
+    if (p < e && (*p == 'e' || *p == 'E')) {
+      ++p;
+      is_int = false;
+      if (p < e && (*p == '+' || *p == '-')) ++p;
+      if (p >= e || *p < '0' || *p > '9') return false;
+      while (p < e && *p >= '0' && *p <= '9') ++p;
+    }
+    last_is_int = is_int;
     if (out) *out = strtod(std::string(s, p - s).c_str(), nullptr);
     return true;
   }
+  bool last_is_int = true;
+  bool lone_surrogate = false;
   bool lit(const char* w) {
     size_t n = strlen(w);
     if ((size_t)(e - p) < n || memcmp(p, w, n) != 0) return false;
@@ -159,8 +267,84 @@ int priority_from_string(const std::string& s) {
   return -1;
 }
 
+// Go duration text as utils/duration.parse_duration_ns accepts it:
+// [+-]? ( [0-9]*\.?[0-9]+ (ns|us|µs|μs|ms|s|m|h) )+  , or "" / "0"
+bool go_duration(const std::string& raw) {
+  size_t a = 0, b = raw.size();
+  while (a < b && isspace((unsigned char)raw[a])) ++a;
+  while (b > a && isspace((unsigned char)raw[b - 1])) --b;
+  std::string s = raw.substr(a, b - a);
+  if (s.empty() || s == "0") return true;
+  size_t i = 0;
+  if (s[i] == '+' || s[i] == '-') ++i;
+  if (i >= s.size()) return false;
+  while (i < s.size()) {
+    const size_t d0 = i;
+    while (i < s.size() && isdigit((unsigned char)s[i])) ++i;
+    if (i < s.size() && s[i] == '.') {
+      ++i;
+      const size_t f0 = i;
+      while (i < s.size() && isdigit((unsigned char)s[i])) ++i;
+      if (i == f0) return false;
+    } else if (i == d0) {
+      return false;
+    }
+    static const char* units[] = {"ns", "us", "\xC2\xB5s", "\xCE\xBCs", "ms", "s", "m", "h"};
+    bool hit = false;
+    for (const char* u : units) {
+      const size_t L = strlen(u);
+      if (s.compare(i, L, u) == 0) {
+        i += L;
+        hit = true;
+        break;
+      }
+    }
+    if (!hit) return false;
+  }
+  return true;
+}
+
+// RFC 3339 timestamp as models.message.parse_time reads it back
+// (YYYY-MM-DDTHH:MM:SS[.frac](Z|+HH:MM|-HH:MM), real calendar dates)
+bool rfc3339(const std::string& s) {
+  auto dig = [&](size_t i, size_t n) {
+    if (i + n > s.size()) return false;
+    for (size_t k = i; k < i + n; ++k)
+      if (!isdigit((unsigned char)s[k])) return false;
+    return true;
+  };
+  auto num = [&](size_t i, size_t n) { return atoi(s.substr(i, n).c_str()); };
+  if (s.size() < 20 || !dig(0, 4) || s[4] != '-' || !dig(5, 2) || s[7] != '-' || !dig(8, 2) || s[10] != 'T' ||
+      !dig(11, 2) || s[13] != ':' || !dig(14, 2) || s[16] != ':' || !dig(17, 2))
+    return false;
+  const int y = num(0, 4), mo = num(5, 2), d = num(8, 2);
+  static const int mdays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  if (y < 1 || mo < 1 || mo > 12 || d < 1 || d > mdays[mo - 1] + (mo == 2 && leap ? 1 : 0)) return false;
+  if (num(11, 2) > 23 || num(14, 2) > 59 || num(17, 2) > 59) return false;
+  size_t i = 19;
+  if (i < s.size() && s[i] == '.') {
+    ++i;
+    const size_t f0 = i;
+    while (i < s.size() && isdigit((unsigned char)s[i])) ++i;
+    if (i == f0) return false;
+  }
+  if (i < s.size() && s[i] == 'Z') return i + 1 == s.size();
+  return i + 6 == s.size() && (s[i] == '+' || s[i] == '-') && dig(i + 1, 2) && s[i + 3] == ':' && dig(i + 4, 2) &&
+         num(i + 1, 2) <= 23 && num(i + 4, 2) <= 59;
+}
+
+// id / user_id travel into the 202 JSON and the ring record unescaped:
+// printable ASCII without quote or backslash only
+bool plain_token(const std::string& s) {
+  for (unsigned char c : s)
+    if (c < 0x20 || c > 0x7E || c == '"' || c == '\\') return false;
+  return true;
+}
+
 Scan scan_message(const char* b, size_t n) {
   Scan r;
+  r.error = "Invalid message format";
   JsonScanner js{b, b + n};
   js.ws();
   if (js.p >= js.e || *js.p != '{') return r;
@@ -179,27 +363,79 @@ Scan scan_message(const char* b, size_t n) {
     if (js.p >= js.e || *js.p != ':') return r;
     ++js.p;
     js.ws();
+    const char c0 = js.p < js.e ? *js.p : 0;
     if (key == "id" || key == "user_id") {
       std::string v;
-      if (js.p < js.e && *js.p == '"') {
+      if (c0 == '"') {
         if (!js.str(&v)) return r;
+        if (js.lone_surrogate || !plain_token(v)) {
+          r.error = key + " must be printable ASCII without quotes or backslashes";
+          return r;
+        }
         (key == "id" ? r.id : r.user_id) = v;
-      } else if (!js.value()) {
+      } else if (c0 == 'n') {
+        if (!js.lit("null")) return r;
+      } else {
+        r.error = key + " must be a string";
         return r;
       }
     } else if (key == "priority") {
-      if (js.p < js.e && *js.p == '"') {
+      if (c0 == '"') {
         std::string v;
         if (!js.str(&v)) return r;
-        r.priority = v.empty() ? 0 : priority_from_string(v);
-        if (r.priority < 0) return r;                 // unknown priority name -> 400
-      } else if (js.p < js.e && *js.p == 'n') {
+        r.priority = priority_from_string(v);
+        if (r.priority < 0) {                          // unknown priority name -> 400
+          r.error = "invalid priority";
+          return r;
+        }
+      } else if (c0 == 'n') {
         if (!js.lit("null")) return r;
       } else {
         double d = 0;
-        if (!js.num(&d)) return r;
+        if (!js.num(&d) || d != (double)(int64_t)d || d < 0 || d > 4) {
+          r.error = "invalid priority";
+          return r;
+        }
         r.priority = (int)d;
-        if (r.priority < 0 || r.priority > 4) return r;
+      }
+    } else if (key == "metadata") {                    // Message.from_dict: object (or null)
+      if (c0 != '{' && c0 != 'n') {
+        r.error = "metadata must be an object";
+        return r;
+      }
+      if (!js.value()) return r;
+    } else if (key == "timeout" || key == "max_retries" || key == "retry_count") {
+      // numbers (finite, int64 range) or null; timeout also a Go duration string
+      if (c0 == 'n') {
+        if (!js.lit("null")) return r;
+      } else if (c0 == '"' && key == "timeout") {
+        std::string v;
+        if (!js.str(&v) || !go_duration(v)) {
+          r.error = "invalid timeout";
+          return r;
+        }
+      } else {
+        double d = 0;
+        if (!js.num(&d) || !(d > -9.2e18 && d < 9.2e18)) {
+          r.error = "invalid " + key;
+          return r;
+        }
+      }
+    } else if (key == "created_at" || key == "updated_at" || key == "scheduled_at" || key == "completed_at") {
+      if (c0 == 'n') {
+        if (!js.lit("null")) return r;
+      } else if (c0 == '"') {
+        std::string v;
+        if (!js.str(&v) || !(v.empty() || rfc3339(v))) {
+          r.error = "invalid " + key;
+          return r;
+        }
+      } else {
+        double d = 0;
+        if (!js.num(&d) || !(d > -9.2e18 && d < 9.2e18)) {
+          r.error = "invalid " + key;
+          return r;
+        }
       }
     } else if (!js.value()) {
       return r;
@@ -213,6 +449,7 @@ Scan scan_message(const char* b, size_t n) {
       ++js.p;
       js.ws();
       r.ok = js.p == js.e;
+      if (r.ok) r.error.clear();
       return r;
     }
     return r;
@@ -225,6 +462,7 @@ struct Conn {
   size_t out_off = 0;
   bool close_after = false;
   bool continued = false;   // "100 Continue" already sent for the pending request
+  bool out_armed = false;   // EPOLLOUT registered (a write hit EAGAIN)
   int64_t last_ns = 0;      // last byte received (idle / slow-client reaping)
 };
 
@@ -406,6 +644,15 @@ class HttpIngress {
           if (eof) cn.close_after = true;
         }
         if (!dead && !cn.out.empty()) dead = !flush(fd, cn, ep);
+        if (!dead && cn.out.empty() && cn.out_armed) {
+          // drained: back to read interest only (level-triggered EPOLLOUT on
+          // an idle writable socket would wake this thread forever)
+          epoll_event ce{};
+          ce.events = EPOLLIN | EPOLLRDHUP;
+          ce.data.fd = fd;
+          epoll_ctl(ep, EPOLL_CTL_MOD, fd, &ce);
+          cn.out_armed = false;
+        }
         if (dead || (cn.close_after && cn.out.empty())) {
           epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
           ::close(fd);
@@ -427,10 +674,13 @@ class HttpIngress {
         continue;
       }
       if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-        epoll_event ce{};
-        ce.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
-        ce.data.fd = fd;
-        epoll_ctl(ep, EPOLL_CTL_MOD, fd, &ce);
+        if (!cn.out_armed) {
+          epoll_event ce{};
+          ce.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
+          ce.data.fd = fd;
+          epoll_ctl(ep, EPOLL_CTL_MOD, fd, &ce);
+          cn.out_armed = true;
+        }
         return true;
       }
       return false;
@@ -590,7 +840,7 @@ class HttpIngress {
           // rejected by the guard (401 / 403 / 429)
         } else if (!s.ok) {
           bad_++;
-          respond(cn, 400, "Bad Request", "{\"error\":\"Invalid message format\"}", keep);
+          respond(cn, 400, "Bad Request", "{\"error\":\"" + s.error + "\"}", keep);
         } else {
           std::string id = s.id.empty() ? uuid4(rng) : s.id;
           std::string rec(8 + 36 + 4 + clen, '\0');
@@ -693,6 +943,6 @@ PYBIND11_MODULE(_ingress, m) {
   m.def("scan_message", [](py::bytes b) {
     std::string s = b;
     Scan r = scan_message(s.data(), s.size());
-    return py::make_tuple(r.ok, r.id, r.priority, r.user_id);
+    return py::make_tuple(r.ok, r.id, r.priority, r.user_id, r.error);
   });
 }

@@ -170,10 +170,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
                 return JSONResponse({"error": "bad Content-Length"}, status_code=400)
             if int(cl) > MAX_BODY:
                 return JSONResponse({"error": "body exceeds 4 MiB"}, status_code=413)
-        elif request.headers.get("transfer-encoding", "").lower() == "chunked":
-            if len(await request.body()) > MAX_BODY:     # cached: the route reads it again
-                return JSONResponse({"error": "body exceeds 4 MiB"}, status_code=413)
-        return await call_next(request)
+        return await call_next(request)       # chunked bodies: ChunkedBodyCap (raw ASGI, below)
 
     # ------------------------------------------------------------------ CORS
     @app.middleware("http")
@@ -569,4 +566,41 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
     def get_config():
         return redact_config(dataclasses.asdict(G.cfg))
 
+    app.add_middleware(ChunkedBodyCap)
     return app
+
+
+class ChunkedBodyCap:
+    """Raw-ASGI cap for bodies without a Content-Length (chunked transfer
+    encoding): the stream is read incrementally and refused with 413 as soon
+    as the running total passes ``MAX_BODY`` -- at most 4 MiB plus one chunk
+    is ever buffered (``await request.body()`` buffered the whole
+    stream first).  An accepted body is replayed to the app unchanged."""
+
+    def __init__(self, app):
+        self.app = app
+
+    async def __call__(self, scope, receive, send):
+        if scope.get("type") != "http":
+            return await self.app(scope, receive, send)
+        hdrs = {k.lower(): v for k, v in scope.get("headers") or []}
+        if b"content-length" in hdrs or hdrs.get(b"transfer-encoding", b"").lower() != b"chunked":
+            return await self.app(scope, receive, send)
+        chunks, total = [], 0
+        while True:
+            msg = await receive()
+            if msg["type"] == "http.disconnect":
+                return
+            body = msg.get("body", b"")
+            total += len(body)
+            if total > MAX_BODY:
+                resp = JSONResponse({"error": "body exceeds 4 MiB"}, status_code=413)
+                return await resp(scope, receive, send)
+            chunks.append(body)
+            if not msg.get("more_body", False):
+                break
+        replay = [{"type": "http.request", "body": b"".join(chunks), "more_body": False}]
+
+        async def again():
+            return replay.pop() if replay else await receive()
+        return await self.app(scope, again, send)

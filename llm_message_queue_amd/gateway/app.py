@@ -293,12 +293,19 @@ class GatewayApp:
                 continue
             now = time.time_ns()
             ready, raw, bad = [], [], []
+            undecodable: List[Message] = []
             for tag, b in recs:
                 if tag == TAG_RAW:
                     try:
                         m = decode_raw(b)
-                    except Exception:
-                        continue                  # the ingress validated the JSON; drop garbage
+                    except Exception as e:
+                        # the native scanner already refuses what json.loads /
+                        # Message.from_dict refuse (400 at the door); a record
+                        # that still fails here was acknowledged (202), so it
+                        # is accounted for, never silently dropped: status
+                        # failed, dead-letter queue, metric, event to the ingress
+                        undecodable.append(self._undecodable(b, e))
+                        continue
                     m.created_at = m.updated_at = now
                     raw.append(m)
                 else:
@@ -320,7 +327,20 @@ class GatewayApp:
                     bad.append(m)
             if bad:
                 self.ring.put_events(bad, error="queue full")
+            if undecodable:
+                self.factory.dead_letter_queue.push_many(undecodable, "undecodable request body", "ingress")
+                self.metrics.requests_rejected.labels("undecodable").inc(len(undecodable))
+                for m in undecodable:
+                    self.messages.put(m)
+                self.ring.put_events(undecodable, error="undecodable request body")
             self._wake.set()
+
+    @staticmethod
+    def _undecodable(b: bytes, err: BaseException) -> Message:
+        mid = b[8:44].rstrip(b"\x00").decode("ascii", "replace") if len(b) >= 44 else ""
+        m = Message(id=mid, status=MessageStatus.FAILED, metadata={"error": f"undecodable body: {err}"})
+        m.arrival_ns = int.from_bytes(b[0:8], "little", signed=True) if len(b) >= 8 else 0
+        return m
 
     def _event_loop(self) -> None:
         """Ingress: apply status events from the dispatcher to the message store."""

@@ -75,6 +75,30 @@ def test_bad_bodies(client):
     assert client.post("/api/v1/messages", content=iter([b'{"content":', b'"chunked ok"}'])).status_code == 202
 
 
+def test_chunked_body_cap_reads_incrementally():
+    """a huge chunked stream is cut off at the 4 MiB cap, not
+    buffered whole before the check (raw ASGI receive, no client in between)."""
+    import asyncio
+    from llm_message_queue_amd.api.server import ChunkedBodyCap
+    pulled, sent, reached = [0], [], []
+
+    async def receive():
+        pulled[0] += 1
+        return {"type": "http.request", "body": b"x" * (1 << 20), "more_body": pulled[0] < 1000}   # 1 GB
+
+    async def send(msg):
+        sent.append(msg)
+
+    async def app(scope, rcv, snd):
+        reached.append(True)
+
+    scope = {"type": "http", "method": "POST", "path": "/api/v1/messages",
+             "headers": [(b"transfer-encoding", b"chunked")]}
+    asyncio.run(ChunkedBodyCap(app)(scope, receive, send))
+    assert pulled[0] == 5 and not reached                       # 5 MiB read, then 413
+    assert sent[0]["status"] == 413
+
+
 def test_conversation_flow(client):
     r = client.post("/api/v1/conversations", json={"user_id": "alice", "metadata": {"topic": "t"}})
     assert r.status_code == 201

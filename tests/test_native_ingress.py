@@ -26,9 +26,9 @@ def _post(port, body, raw=False):
 
 def test_json_scanner():
     scan = _native.ingress().scan_message
-    assert scan(b'{"content":"hi","priority":"urgent","id":"abc"}') == (True, "abc", 2, "")
+    assert scan(b'{"content":"hi","priority":"urgent","id":"abc"}')[:4] == (True, "abc", 2, "")
     assert scan(b'{"content":"a\\"b","metadata":{"x":[1,{"y":null}]},"priority":4,"user_id":"u"}')[0:3:2] == (True, 4)
-    assert scan(b'{}') == (True, "", 0, "")
+    assert scan(b'{}')[:4] == (True, "", 0, "")
     for bad in (b'', b'[1]', b'{"content":}', b'{"priority":"bogus"}', b'{"a":1,}', b'{"a":1} x', b'{"priority":9}'):
         assert not scan(bad)[0], bad
 
@@ -154,7 +154,8 @@ def test_json_scanner_properties():
         | st.text(max_size=20)
     val = st.recursive(leaf, lambda c: st.lists(c, max_size=4) | st.dictionaries(st.text(max_size=8), c, max_size=4),
                        max_leaves=12)
-    reserved = {"id", "priority", "user_id", "content"}
+    reserved = {"id", "priority", "user_id", "content", "metadata", "timeout", "max_retries", "retry_count",
+                "created_at", "updated_at", "scheduled_at", "completed_at"}
 
     @settings(max_examples=300, deadline=None)
     @given(st.binary(max_size=200))
@@ -328,3 +329,122 @@ def test_native_ingress_reaps_idle_and_stalled_connections(stack):
     assert ing.stats()["idle_closed"] >= 2
     for s in (idle, stalled, busy):
         s.close()
+
+
+STRICT_BAD = [
+    b'{"content":"x","n":1.2.3}', b'{"n":+1}', b'{"n":01}', b'{"n":1.}', b'{"n":.5}', b'{"n":1e}', b'{"n":-}',
+    b'{"n":NaN}', b'{"n":Infinity}', b'{"c":"bad \\q escape"}', b'{"c":"\\u12G4"}', b'{"c":"\xff\xfe"}',
+    b'{"c":"\xc0\xaf"}', b'{"c":"\xed\xa0\x80"}', b'{"metadata":5}', b'{"metadata":"x"}', b'{"metadata":[1]}',
+    b'{"timeout":"abc"}', b'{"timeout":"5"}', b'{"timeout":true}', b'{"timeout":1e400}', b'{"max_retries":"x"}',
+    b'{"retry_count":[1]}', b'{"created_at":"yesterday"}', b'{"created_at":"2024-02-30T00:00:00Z"}',
+    b'{"id":"a\\"b"}', b'{"id":"a\\\\b"}', b'{"id":"\\u00e9"}', b'{"id":5}', b'{"user_id":"x\\ny"}',
+    b'{"priority":""}', b'{"priority":2.5}', b'{"priority":"bogus"}',
+]
+
+
+def test_json_scanner_strict_refusals():
+    """every body the dispatcher's json.loads / Message.from_dict
+    would refuse is refused at the door (400), so a 202 is never followed by
+    a silent drop; the reason is reported."""
+    scan = _native.ingress().scan_message
+    for bad in STRICT_BAD:
+        r = scan(bad)
+        assert not r[0] and r[4], bad
+    ok = [b'{"timeout":"1m30s","max_retries":5,"retry_count":0,"metadata":null}',
+          b'{"timeout":30000000000,"created_at":"2024-02-29T12:00:00.5+02:00","c":"\\u00e9\\ud83d\\ude00 \xc3\xa9"}',
+          b'{"id":"abc-123_X.y","user_id":"u 1","priority":null,"timeout":null}']
+    for good in ok:
+        assert scan(good)[0], good
+
+
+def test_scan_ok_implies_dispatcher_decodes():
+    """Property: whenever the native scanner accepts a body, the dispatcher's
+    decode (json.loads + Message.from_dict) succeeds on the same bytes."""
+    from hypothesis import given, settings, strategies as st
+    from llm_message_queue_amd.gateway.shm_bridge import decode_raw
+    scan = _native.ingress().scan_message
+    leaf = st.none() | st.booleans() | st.integers(-10**20, 10**20) | st.floats() | st.text(max_size=12)
+    val = st.recursive(leaf, lambda c: st.lists(c, max_size=3) | st.dictionaries(st.text(max_size=6), c, max_size=3),
+                       max_leaves=8)
+    typed = st.sampled_from(["id", "user_id", "priority", "metadata", "timeout", "max_retries", "retry_count",
+                             "created_at", "scheduled_at", "content", "conversation_id", "status"])
+    special = st.sampled_from(["1m", "10ms", "1.5h", "abc", "", "0", "2024-01-31T10:00:00Z", "2023-02-29T00:00:00Z",
+                               "urgent", "realtime", "4", " 3 ", "+2", "x\\y", "ok-id"])
+
+    def record(body: bytes) -> bytes:
+        return (123).to_bytes(8, "little", signed=True) + b"id-1".ljust(36, b"\0") + \
+            len(body).to_bytes(4, "little") + body
+
+    @settings(max_examples=400, deadline=None)
+    @given(st.dictionaries(typed, val | special, max_size=6), st.booleans())
+    def prop(d, ascii_only):
+        try:
+            body = json.dumps(d, ensure_ascii=ascii_only).encode("utf-8", "surrogatepass")
+        except (ValueError, UnicodeEncodeError):
+            return
+        if scan(body)[0]:
+            decode_raw(record(body))            # must not raise
+
+    @settings(max_examples=400, deadline=None)
+    @given(st.binary(max_size=120))
+    def raw(b):
+        if scan(b)[0]:
+            decode_raw(record(b))
+
+    prop()
+    raw()
+
+
+def test_undecodable_record_is_dead_lettered_not_dropped(stack):
+    """A RAW ring record the dispatcher cannot decode (the scanner let it
+    through) is accounted for: failed status, dead-letter queue, metric."""
+    from llm_message_queue_amd.gateway.shm_bridge import TAG_RAW
+    disp, ing, port = stack
+    body = b'{"content": "x", "created_at": "not a time"}'
+    rec = (5).to_bytes(8, "little", signed=True) + b"bad-rec-1".ljust(36, b"\0") + len(body).to_bytes(4, "little") + body
+    disp.ring.requests.push_many([rec], TAG_RAW)
+    t0 = time.time()
+    while time.time() - t0 < 5 and disp.messages.get("bad-rec-1") is None:
+        time.sleep(0.02)
+    m = disp.messages.get("bad-rec-1")
+    assert m is not None and m.status == "failed" and "undecodable" in m.metadata["error"]
+    assert any(it.message.id == "bad-rec-1" for it in disp.factory.dead_letter_queue.get_all())
+
+
+def test_slow_reader_does_not_spin_ingress_thread():
+    """after a write hit EAGAIN the connection's EPOLLOUT interest
+    must be dropped again once the output drained -- otherwise the ingress
+    thread busy-polls the idle writable socket for the connection's life."""
+    import resource
+    name = f"pyt-spin-{os.getpid()}"
+    ring = RingPair(name, 1 << 20, "create")
+    ing = NativeIngress(0, name, threads=1, host="127.0.0.1")
+    port = ing.start()
+    try:
+        s = socket.create_connection(("127.0.0.1", port))
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 16)
+        req = b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n"
+        n = 40000
+        s.sendall(req * n)                      # pipelined; responses pile up unread
+        time.sleep(0.5)                         # server hits EAGAIN with EPOLLOUT armed
+        s.settimeout(10)
+        seen, tail = 0, b""
+        while seen < n:
+            chunk = s.recv(1 << 20)
+            if not chunk:
+                break
+            buf = tail + chunk
+            seen += buf.count(b"HTTP/1.1 200")
+            tail = buf[-11:]                    # a status line split across reads
+            seen -= tail.count(b"HTTP/1.1 200")
+        assert seen == n
+        time.sleep(0.2)
+        c0 = resource.getrusage(resource.RUSAGE_SELF)
+        time.sleep(1.0)                         # idle keep-alive connection
+        c1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu = (c1.ru_utime - c0.ru_utime) + (c1.ru_stime - c0.ru_stime)
+        assert cpu < 0.3, f"ingress burned {cpu:.2f} s CPU on an idle connection"
+        s.close()
+    finally:
+        ing.stop()
+        ring.close(unlink=True)

@@ -47,11 +47,25 @@ def test_per_ip_and_per_user_buckets_are_independent():
     code, *_, reason, _ = g.check("GET", "/api/v1/queues/stats", ip="1.1.1.1", now_ns=t)
     assert code == 429 and "per_ip" in reason
     assert g.check("GET", "/api/v1/queues/stats", ip="2.2.2.2", now_ns=t)[0] == 0
-    assert g.check("POST", "/api/v1/messages", ip="3.3.3.3", user="alice", now_ns=t)[0] == 0
-    code, *_, reason, _ = g.check("POST", "/api/v1/messages", ip="4.4.4.4", user="alice", now_ns=t)
-    assert code == 429 and "per_user" in reason
-    assert g.check("POST", "/api/v1/messages", ip="5.5.5.5", user="bob", now_ns=t)[0] == 0
+    # anonymous callers are limited per address; a body's user_id claim never
+    # keys a per-user bucket (naming "alice" must not spend alice's quota)
+    for ip in ("3.3.3.3", "4.4.4.4", "5.5.5.5"):
+        assert g.check("POST", "/api/v1/messages", ip=ip, user="alice", now_ns=t)[0] == 0
     assert g.allow_user("carol")[0] and not g.allow_user("carol")[0]
+
+
+def test_specific_limits_checked_before_the_global_bucket():
+    """a request refused by its IP's bucket must not drain the
+    global bucket shared by everyone."""
+    g = _guard(global_rps=0.001, global_burst=3.0, ip_rps=0.001, ip_burst=1.0)
+    t = 7_000_000_000
+    assert g.check("POST", "/api/v1/messages", ip="6.6.6.6", now_ns=t)[0] == 0
+    for _ in range(10):                                   # the abusive IP is refused ...
+        code, *_, reason, _ = g.check("POST", "/api/v1/messages", ip="6.6.6.6", now_ns=t)
+        assert code == 429 and "per_ip" in reason
+    # ... without spending the 2 global tokens left for other clients
+    assert g.check("POST", "/api/v1/messages", ip="7.7.7.7", now_ns=t)[0] == 0
+    assert g.check("POST", "/api/v1/messages", ip="8.8.8.8", now_ns=t)[0] == 0
 
 
 def test_api_key_auth_and_rbac():
