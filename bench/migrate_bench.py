@@ -2,9 +2,9 @@
 (N11; BASELINE config 4 "long-dialog replay routed across GPUs").
 
 C concurrent conversations, T turns each, closed loop, all entering at rank 0
-(the `cli serve` ingress).  Placement ignores conversation affinity and uses
-round robin, so consecutive turns of a dialog keep landing on a GPU that does
-NOT hold its KV -- the worst case for re-homing (a rebalance on every turn).
+(the `cli serve` ingress).  In the migrate and replay modes every turn after the first is placed on a GPU
+other than the one holding its KV (``Gateway.rehome_every_turn``) -- the
+worst case for re-homing (a rebalance on every turn).
 Modes (one per launch, the job's collectives stop together):
 
   * migrate -- the turn's KV moves from its home GPU (two-phase p2p on the
@@ -39,8 +39,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="migrate", choices=["migrate", "replay", "pinned"])
-    ap.add_argument("--convs", type=int, default=256)
-    ap.add_argument("--turns", type=int, default=4)
+    ap.add_argument("--convs", type=int, default=512)
+    ap.add_argument("--turns", type=int, default=8)
     ap.add_argument("--slots", type=int, default=768)
     ap.add_argument("--max-ctx", type=int, default=512)
     ap.add_argument("--token-budget", type=int, default=4096)
@@ -86,6 +86,7 @@ def main() -> int:
     gw = Gateway(cfg, preprocessor=pre, engine=engine, comm=comm, use_gpu_preprocess=not a.cpu,
                  prompt_cap=a.prompt_cap, gen_tokens=a.gen_tokens)
     gw.affinity = a.mode == "pinned"
+    gw.rehome_every_turn = a.mode != "pinned"
     wl = Workload(seed=11)
     done_turns = {c: 0 for c in range(a.convs)}
     due = []

@@ -177,8 +177,11 @@ class Gateway:
         # moves the dialog's KV there instead of replaying the dialog
         self.kv_migrate = bool(getattr(cfg.gpu, "kv_migration", True))
         # conversation affinity in multi-GPU placement (pins); off = every
-        # turn is placed by the strategy alone (bench/migrate_bench.py)
+        # turn is placed by the strategy alone.  ``rehome_every_turn``
+        # (bench/migrate_bench.py): a turn goes to any GPU but its home --
+        # the worst case of rebalancing, for measuring migration vs replay
         self.affinity = True
+        self.rehome_every_turn = False
         self._mig_out: List[Tuple[int, int, int]] = []       # orders to publish in the next load vector
         self._await_kv: Dict[int, List[Request]] = {}         # conv key -> turns held for their KV
         self.migrator = None
@@ -607,6 +610,8 @@ class Gateway:
                     room[h] -= 1
                 else:
                     rest.append(m)
+            if self.rehome_every_turn:
+                rest = self._avoid_home(rest, room, dest)
             k = 0
             for j in range(W):
                 n = room[j]
@@ -702,6 +707,24 @@ class Gateway:
                     self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
+
+    def _avoid_home(self, pool: List[Message], room: List[int], dest: Dict[int, List[Message]]) -> List[Message]:
+        """Place each homed turn on a GPU other than its home (bench knob);
+        returns the turns still unplaced."""
+        left = []
+        for m in pool:
+            h = self._home(m)
+            if h < 0:
+                left.append(m)
+                continue
+            js = [j for j in range(self.world) if j != h and room[j] > 0]
+            if not js:
+                left.append(m)
+                continue
+            j = max(js, key=lambda x: room[x])
+            dest[j].append(m)
+            room[j] -= 1
+        return left
 
     def awaiting_kv(self) -> int:
         """Turns dispatched here that wait for their KV (next tick)."""

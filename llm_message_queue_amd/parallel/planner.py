@@ -66,7 +66,7 @@ L_SLOTS_TOTAL = L_EXCLUDE + 3    # batch slots of this GPU
 L_WEIGHT = L_EXCLUDE + 8         # [64 + j] endpoint weight of GPU j in this rank's balancer (rank 0 row is used)
 # KV migration orders this router decided LAST tick (executed this tick by
 # every rank from the gathered loads): count, then (conv key, src << 8 | dst)
-MAX_MIGRATIONS = 8
+MAX_MIGRATIONS = 64
 L_MIG_N = L_WEIGHT + MAX_WORLD   # 72
 L_MIG = L_MIG_N + 1              # 73 .. 73 + 2 * MAX_MIGRATIONS
 LOAD_WIDTH = L_MIG + 2 * MAX_MIGRATIONS

@@ -40,8 +40,35 @@ def category(name: str) -> str:
     return "other"
 
 
-def main(prefix: str) -> None:
-    stats = list(csv.DictReader(open(prefix + "_kernel_stats.csv")))
+def from_db(path: str, tail_frac: float = 1.0):
+    """rocprofv3 SQLite output (``run_results.db``): per-kernel stats and
+    the dispatch intervals, optionally only the last ``tail_frac`` of the
+    trace (the serving loop after calibration)."""
+    import sqlite3
+    c = sqlite3.connect(path)
+    rows = list(c.execute("select name, start, end from kernels"))
+    if not rows:
+        return [], []
+    t_lo = min(r[1] for r in rows)
+    t_hi = max(r[2] for r in rows)
+    cut = t_hi - tail_frac * (t_hi - t_lo)
+    rows = [r for r in rows if r[1] >= cut]
+    agg = defaultdict(lambda: [0, 0])
+    for n, a, b in rows:
+        agg[n][0] += 1
+        agg[n][1] += b - a
+    total = sum(v[1] for v in agg.values()) or 1
+    stats = [{"Name": n, "Calls": str(v[0]), "TotalDurationNs": str(v[1]), "AverageNs": str(v[1] / v[0]),
+              "Percentage": str(100.0 * v[1] / total)} for n, v in sorted(agg.items(), key=lambda kv: -kv[1][1])]
+    trace = [{"Start_Timestamp": str(a), "End_Timestamp": str(b)} for _, a, b in rows]
+    return stats, trace
+
+
+def main(prefix: str, tail_frac: float = 1.0) -> None:
+    if prefix.endswith(".db"):
+        stats, tr_db = from_db(prefix, tail_frac)
+    else:
+        stats, tr_db = list(csv.DictReader(open(prefix + "_kernel_stats.csv"))), None
     total = sum(int(r["TotalDurationNs"]) for r in stats) or 1
     print(f"# Kernel profile: `{prefix.split('/')[-1]}`\n")
     print(f"Total kernel time {total / 1e6:.1f} ms over {sum(int(r['Calls']) for r in stats)} dispatches.\n")
@@ -55,10 +82,13 @@ def main(prefix: str) -> None:
     print("\n## By category\n\n| category | total ms | % |\n|---|---:|---:|")
     for c, v in sorted(cats.items(), key=lambda kv: -kv[1]):
         print(f"| {c} | {v / 1e6:.1f} | {100 * v / total:.1f} |")
-    try:
-        tr = list(csv.DictReader(open(prefix + "_kernel_trace.csv")))
-    except FileNotFoundError:
-        return
+    if tr_db is not None:
+        tr = tr_db
+    else:
+        try:
+            tr = list(csv.DictReader(open(prefix + "_kernel_trace.csv")))
+        except FileNotFoundError:
+            return
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in tr)
     if not iv:
         return
@@ -82,4 +112,4 @@ def main(prefix: str) -> None:
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 1.0)
