@@ -107,12 +107,12 @@ static void summarise_project(uintptr_t pooled, uintptr_t seg_off, int C, uintpt
 
 static void salient_topk(uintptr_t hashes, int L, uintptr_t ntok, int stride, uintptr_t seg_off, int C,
                          uintptr_t stop, int nstop, int K, uintptr_t out_hash, uintptr_t out_cnt,
-                         uintptr_t stream) {
+                         uintptr_t out_overflow, uintptr_t stream) {
   require(K >= 0 && K <= 64, "K out of range");
   if (C == 0 || K == 0) return;
   hipLaunchKernelGGL(salient_topk_kernel, dim3(C), dim3(256), 0, S(stream), P<const uint32_t>(hashes), L,
                      P<const int32_t>(ntok), stride, P<const int32_t>(seg_off), P<const uint32_t>(stop),
-                     nstop, K, P<uint32_t>(out_hash), P<int32_t>(out_cnt));
+                     nstop, K, P<uint32_t>(out_hash), P<int32_t>(out_cnt), P<int32_t>(out_overflow));
   check_launch();
 }
 

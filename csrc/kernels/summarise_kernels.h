@@ -108,8 +108,10 @@ constexpr int SAL_TABLE = 2048;
 __global__ void __launch_bounds__(256)
 salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __restrict__ ntok,
                     int stride, const int32_t* __restrict__ seg_off, const uint32_t* __restrict__ stop,
-                    int nstop, int K, uint32_t* __restrict__ out_hash, int32_t* __restrict__ out_cnt) {
+                    int nstop, int K, uint32_t* __restrict__ out_hash, int32_t* __restrict__ out_cnt,
+                    int32_t* __restrict__ out_overflow) {
   __shared__ uint32_t key[SAL_TABLE];
+  __shared__ int overflow;  // a token found no table slot (> SAL_TABLE distinct): result is partial
   __shared__ int32_t cnt[SAL_TABLE];
   __shared__ int32_t first[SAL_TABLE];
   __shared__ uint64_t best_s[4];
@@ -117,6 +119,7 @@ salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* _
   const int tid = threadIdx.x;
   const int c = blockIdx.x;
   for (int i = tid; i < SAL_TABLE; i += 256) { key[i] = 0u; cnt[i] = 0; first[i] = 0x7FFFFFFF; }
+  if (tid == 0) overflow = 0;
   __syncthreads();
   const int a = seg_off[c], b = seg_off[c + 1];
   int ord = 0;  // running token order across the conversation's messages
@@ -129,15 +132,18 @@ salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* _
       if (is_stop) continue;
       if (h == 0u) h = 1u;  // 0 marks an empty slot
       uint32_t slot = (h * 2654435761u) & (SAL_TABLE - 1);
+      bool placed = false;
       for (int probe = 0; probe < SAL_TABLE; ++probe) {
         const uint32_t prev = atomicCAS(&key[slot], 0u, h);
         if (prev == 0u || prev == h) {
           atomicAdd(&cnt[slot], 1);
           atomicMin(&first[slot], ord + t);
+          placed = true;
           break;
         }
         slot = (slot + 1) & (SAL_TABLE - 1);
       }
+      if (!placed) overflow = 1;  // benign race: every writer stores 1
     }
     ord += n;
   }
@@ -175,6 +181,9 @@ salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* _
     }
     __syncthreads();
   }
+  // the host recomputes a flagged conversation exactly (never a silently
+  // truncated top-k)
+  if (tid == 0) out_overflow[c] = overflow;
 }
 
 }  // namespace llmq

@@ -32,6 +32,7 @@ class SummaryEngine:
         self._sm = None
         self._cpu_w = None
         self.batches = 0
+        self.salient_overflows = 0      # conversations recomputed on the host (kernel table overflow)
 
     # --------------------------------------------------------------- GPU
     def _gpu_parts(self):
@@ -108,9 +109,16 @@ class SummaryEngine:
                 seg_d, st_d, fi_d, ntok = link.upload([seg, state, first,
                                                        np.ascontiguousarray(res.stats[:, 5], dtype=np.int32)])
                 sm.project(res.pooled, seg_d, st_d, fi_d)
-                hs, cs = sm.salient(res.hashes, ntok, seg_d, k=self.k, link=link)
+                hs, cs, ovf = sm.salient(res.hashes, ntok, seg_d, k=self.k, link=link)
                 new_state = link.download([st_d])[0]
             sal = [[(int(h), int(n)) for h, n in zip(hs[c], cs[c]) if n > 0] for c in range(C)]
+            for c in np.flatnonzero(ovf):
+                # > 2048 distinct tokens overflowed the kernel's LDS table:
+                # exact top-k on the host for that conversation
+                self.salient_overflows += 1
+                a, b = int(seg[c]), int(seg[c + 1])
+                toks = [oracle.token_hashes(oracle.sanitize(x), self.cfg.max_tokens) for x in contents[a:b]]
+                sal[c] = _topk_host(toks, self.k)
             return [(new_state[c], sal[c]) for c in range(C)]
         # CPU reference
         pooled, toks = self._pool_cpu(contents)
@@ -122,15 +130,26 @@ class SummaryEngine:
             mean = pooled[a:b].mean(0).to(torch.bfloat16).float() if b > a else torch.zeros(pooled.shape[1])
             proj = (Pt.float() @ mean).numpy()
             s = proj if first[c] else self.alpha * state[c] + (1 - self.alpha) * proj
-            flat = [t for m in range(a, b) for t in toks[m] if t not in stop]
-            cnt, firstpos = {}, {}
-            for i, t in enumerate(flat):
-                t = t or 1
-                cnt[t] = cnt.get(t, 0) + 1
-                firstpos.setdefault(t, i)
-            sal = sorted(cnt.items(), key=lambda kv: (-kv[1], firstpos[kv[0]]))[:self.k]
-            out.append((s.astype(np.float32), sal))
+            out.append((s.astype(np.float32), _topk_host(toks[a:b], self.k, stop)))
         return out
+
+
+def _topk_host(toks: Sequence[Sequence[int]], k: int, stop=None) -> List[Tuple[int, int]]:
+    """Exact salient top-k: non-stop-word token hashes by (count desc,
+    first occurrence asc); hash 0 is folded to 1 as in the kernel."""
+    stop = set(_stop_hashes()) if stop is None else stop
+    cnt, firstpos = {}, {}
+    i = 0
+    for msg in toks:
+        for t in msg:
+            if t in stop:
+                i += 1
+                continue
+            t = t or 1
+            cnt[t] = cnt.get(t, 0) + 1
+            firstpos.setdefault(t, i)
+            i += 1
+    return sorted(cnt.items(), key=lambda kv: (-kv[1], firstpos[kv[0]]))[:k]
 
 
 def _stop_hashes():

@@ -59,18 +59,22 @@ class Summariser:
         return state
 
     def salient(self, hashes: torch.Tensor, ntok: torch.Tensor, seg_off: torch.Tensor, k: int = 8,
-                stop: Optional[torch.Tensor] = None, ntok_stride: int = 1, link=None) -> Tuple[np.ndarray, np.ndarray]:
-        """Top-k salient token hashes per segment.  ``link`` (an
-        ``ops.hostlink.HostLink`` on the current stream) reads the result
-        back without waiting for other streams."""
+                stop: Optional[torch.Tensor] = None, ntok_stride: int = 1, link=None
+                ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Top-k salient token hashes per segment, plus a per-segment
+        overflow flag (more distinct tokens than the kernel's 2048-entry LDS
+        table: that segment's top-k is partial and must be recomputed).
+        ``link`` (an ``ops.hostlink.HostLink`` on the current stream) reads the
+        result back without waiting for other streams."""
         C = seg_off.numel() - 1
         L = hashes.shape[1]
         stop = self._stop if stop is None else stop
         oh = torch.zeros((C, k), dtype=torch.int32, device=self.device)
         oc = torch.zeros((C, k), dtype=torch.int32, device=self.device)
+        ov = torch.zeros(max(C, 1), dtype=torch.int32, device=self.device)
         self.k.salient_topk(hashes.data_ptr(), L, ntok.data_ptr(), ntok_stride, seg_off.data_ptr(), C,
-                            stop.data_ptr(), stop.numel(), k, oh.data_ptr(), oc.data_ptr(), self._s())
+                            stop.data_ptr(), stop.numel(), k, oh.data_ptr(), oc.data_ptr(), ov.data_ptr(), self._s())
         if link is not None:
-            h, c = link.download([oh, oc])
-            return h.view(np.uint32), c
-        return oh.cpu().numpy().view(np.uint32), oc.cpu().numpy()
+            h, c, o = link.download([oh, oc, ov])
+            return h.view(np.uint32), c, o[:C]
+        return oh.cpu().numpy().view(np.uint32), oc.cpu().numpy(), ov.cpu().numpy()[:C]
