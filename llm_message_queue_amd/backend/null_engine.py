@@ -28,6 +28,18 @@ class NullEngine:
     def admit_capacity(self) -> int:
         return self.free_slots()
 
+    def lane_capacity(self) -> int:
+        return self.free_slots()
+
+    def queued_steps(self) -> int:
+        return 0
+
+    def poll_one(self) -> bool:
+        return False
+
+    def warm_shapes(self, sizes=None) -> int:
+        return 0
+
     def inflight(self) -> int:
         return len(self.active)
 

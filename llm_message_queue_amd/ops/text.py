@@ -159,6 +159,35 @@ class TextResult:
                 out[p] += int(self.extra_scores[j, s])
         return out
 
+    def decide(self, default_priority: int) -> Dict[str, list]:
+        """Whole-batch decisions as Python lists (one numpy pass each):
+        keyword priority = the oracle's ``pick_priority`` (highest strictly
+        positive score, ties to the more urgent level -- slots are in
+        ascending priority order, so argmax's first maximum is that level),
+        sentiment, question string, fallback flag, token counts."""
+        st = self.stats
+        nslot = len(self.slot_prio)
+        out: Dict[str, list] = {}
+        if nslot:
+            sc = st[:, ST_SCORES:ST_SCORES + nslot].astype(np.int64)
+            if self.extra_scores is not None:
+                sc = sc + self.extra_scores[:, :nslot]
+            best = sc.max(axis=1)
+            prio = np.asarray(self.slot_prio, dtype=np.int64)[sc.argmax(axis=1)]
+            out["priority"] = np.where(best > 0, prio, default_priority).tolist()
+        else:
+            out["priority"] = [default_priority] * len(st)
+        pos, neg = st[:, ST_POS], st[:, ST_NEG]
+        out["sentiment"] = np.where(pos > neg, "positive", np.where(neg > pos, "negative", "neutral")).tolist()
+        out["question"] = np.where(st[:, ST_QUESTION] != 0, "true", "false").tolist()
+        out["word_count"] = st[:, ST_WORDS].tolist()
+        out["fallback"] = ((st[:, ST_FLAGS] & FLAG_FOLD) != 0).tolist()
+        ntok = st[:, ST_NTOK]
+        if self.prompt_hashes is not None:
+            ntok = np.minimum(ntok, self.prompt_hashes.shape[1])
+        out["ntok"] = ntok.tolist()
+        return out
+
     def priority(self, j: int, default_priority: int) -> int:
         return oracle.pick_priority(self.scores(j), default_priority)
 

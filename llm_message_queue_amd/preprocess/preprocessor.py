@@ -28,6 +28,8 @@ from ..models.message import (Message, PRIORITY_NORMAL, level_priority_from_name
                               priority_name)
 from . import oracle
 
+_PNAME = {p: priority_name(p) for p in range(0, 6)}
+
 
 class Preprocessor:
     def __init__(self, cfg=None, *, use_gpu: Optional[bool] = None, device: str = "cuda"):
@@ -114,6 +116,29 @@ class Preprocessor:
             return False
         return True
 
+    def _head_fast(self, msg: Message, udefs) -> Optional[bool]:
+        """``_resolve_priority_head`` against a per-batch snapshot of the user
+        defaults (one lock per batch, not per message)."""
+        md = msg.metadata
+        if md is None:
+            md = msg.metadata = {}
+        if msg.priority != PRIORITY_NORMAL and msg.priority != 0:
+            return None
+        up = md.get("user_priority")
+        if isinstance(up, str):
+            p = level_priority_from_name(up)
+            if p is not None:
+                msg.priority = p
+                md["priority_reason"] = "user_override"
+            return False
+        if udefs:
+            udef = udefs.get(msg.user_id)
+            if udef is not None:
+                msg.priority = udef
+                md["priority_reason"] = "user_default"
+                return False
+        return True
+
     def _finish(self, msg: Message, now_ns: int) -> None:
         msg.metadata["analyzed"] = True
         if not msg.queue_name:
@@ -193,7 +218,14 @@ class Preprocessor:
                 if prompt_cap:
                     m.prompt_ids = oracle.token_hashes(m.content, prompt_cap)
             return msgs
-        heads = [self._resolve_priority_head(m) for m in msgs]
+        # Per-message Python is the ingest ceiling at tens of thousands of
+        # requests/s, so everything the kernels return is decided for the
+        # whole batch in numpy first (keyword priority argmax with the
+        # oracle's tie-break, sentiment, question, fallback flags); the loop
+        # below only stores the decided values.
+        with self._lock:
+            udefs = dict(self._user_priorities) if self._user_priorities else None
+        heads = [self._head_fast(m, udefs) for m in msgs]
         work = [i for i, h in enumerate(heads) if h is not None and msgs[i].content]
         now = time.time_ns()
         if work:
@@ -206,41 +238,49 @@ class Preprocessor:
             self.stats["gpu_messages"] += len(work)
             self.stats["last_gpu_ms"] = res.elapsed_ms
             self.stats["gpu_ms_total"] = self.stats.get("gpu_ms_total", 0.0) + res.elapsed_ms
+            d = res.decide(self.default_priority)
+            fb, kp, wc, sent, qs, ntok = d["fallback"], d["priority"], d["word_count"], d["sentiment"], \
+                d["question"], d["ntok"]
+            ml = res.ml_priority.tolist() if res.has_classifier else None
+            use_ml = self.cfg.use_classifier_priority
+            ph = res.prompt_hashes if prompt_cap else None
             for j, i in enumerate(work):
                 m = msgs[i]
-                if res.fallback[j]:
+                md = m.metadata
+                if fb[j]:
                     # fold-special characters / non-literal patterns: oracle
                     self.stats["oracle_fallbacks"] += 1
                     if heads[i]:
                         original = m.priority
                         m.priority = self._analyze_priority_cpu(m)
                         if m.priority != original:
-                            m.metadata["priority_reason"] = "content_keywords"
-                    wc, sent, q = oracle.content_analysis(m.content)
+                            md["priority_reason"] = "content_keywords"
+                    w, se, q = oracle.content_analysis(m.content)
+                    md["word_count"] = w
+                    md["sentiment"] = se
+                    md["contains_question"] = "true" if q else "false"
                 else:
                     if heads[i]:
-                        original = m.priority
-                        m.priority = res.priority(j, self.default_priority)
-                        if m.priority != original:
-                            m.metadata["priority_reason"] = "content_keywords"
-                    wc, sent, q = res.word_count[j], res.sentiment(j), bool(res.question[j])
-                self._content_metadata(m, int(wc), sent, q)
-                if prompt_cap:
-                    m.prompt_ids = res.prompt_ids(j)
-                if res.has_classifier:
-                    m.metadata["ml_priority"] = int(res.ml_priority[j])
-                    if (self.cfg.use_classifier_priority and heads[i]
-                            and m.metadata.get("priority_reason") is None):
-                        m.priority = int(res.ml_priority[j])
-                        m.metadata["priority_reason"] = "classifier"
-        for i, m in enumerate(msgs):
-            h = heads[i]
-            if h is None:
-                continue
-            if h and not m.content:
-                original = m.priority
-                m.priority = self._analyze_priority_cpu(m)
-                if m.priority != original:
-                    m.metadata["priority_reason"] = "content_keywords"
-            self._finish(m, now)
+                        p = kp[j]
+                        if p != m.priority:
+                            m.priority = p
+                            md["priority_reason"] = "content_keywords"
+                    md["word_count"] = wc[j]
+                    md["sentiment"] = sent[j]
+                    md["contains_question"] = qs[j]
+                if ph is not None:
+                    m.prompt_ids = ph[j, :ntok[j]]
+                if ml is not None:
+                    md["ml_priority"] = ml[j]
+                    if use_ml and heads[i] and md.get("priority_reason") is None:
+                        m.priority = ml[j]
+                        md["priority_reason"] = "classifier"
+                # _finish, inlined (analysed, queue name, timestamps)
+                md["analyzed"] = True
+                if not m.queue_name:
+                    m.queue_name = _PNAME.get(m.priority) or priority_name(m.priority)
+                if not m.created_at:
+                    m.created_at = now
+                m.updated_at = now
+                heads[i] = None                     # finished
         return msgs

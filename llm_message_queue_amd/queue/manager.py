@@ -152,14 +152,20 @@ class QueueManager:
 
     def push_routed(self, messages: Sequence[Message]) -> List[Optional[QueueError]]:
         """Push each message to ``message.queue_name`` (gateway ingress path)."""
-        for m in messages:
-            self.apply_priority_rules(m)
+        if self.config.priority_adjust_rules:
+            for m in messages:
+                self.apply_priority_rules(m)
         errs = self.mlq.push_many([m.queue_name for m in messages], messages)
         if self.metrics:
-            pend = self.metrics.pending
+            # one labelled increment per (queue, priority), not per message
+            cnt: Dict[tuple, int] = {}
             for m, e in zip(messages, errs):
                 if e is None:
-                    pend.labels(self.name, m.queue_name, priority_name(m.priority)).inc()
+                    k = (m.queue_name, m.priority)
+                    cnt[k] = cnt.get(k, 0) + 1
+            pend = self.metrics.pending
+            for (q, p), n in cnt.items():
+                pend.labels(self.name, q, priority_name(p)).inc(n)
         return errs
 
     def pop_message(self, queue_name: str) -> Message:
@@ -189,10 +195,14 @@ class QueueManager:
                   budget: Sequence[int], lifo_ns: Optional[Sequence[int]] = None):
         msgs, tier_idx, enq = self.mlq.pop_tiers(tiers, count, aging_ns, budget, lifo_ns)
         if self.metrics and msgs:
+            cnt: Dict[tuple, int] = {}
             for m in msgs:
-                p = priority_name(m.priority)
-                self.metrics.pending.labels(self.name, m.queue_name, p).dec()
-                self.metrics.processing.labels(self.name, m.queue_name, p).inc()
+                k = (m.queue_name, m.priority)
+                cnt[k] = cnt.get(k, 0) + 1
+            for (q, pr), n in cnt.items():
+                p = priority_name(pr)
+                self.metrics.pending.labels(self.name, q, p).dec(n)
+                self.metrics.processing.labels(self.name, q, p).inc(n)
         return msgs, tier_idx, enq
 
     def peek_message(self, queue_name: str) -> Message:

@@ -45,8 +45,11 @@ def test_bench_single_rank_dry_run():
 def test_bench_four_ranks_torchrun_dry_run():
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "4",
-              "--cpu-dry-run", "--steps", "5", "--warmup", "2", "--gateway-only-s", "0"])
+              "--cpu-dry-run", "--steps", "5", "--warmup", "2", "--gateway-only-s", "0.5",
+              "--gateway-only-rate", "200"])
     assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["value"] > 0
+    # the secondary null-backend phase runs multi-rank too (the driver's 8-GPU run does it)
+    assert d["gateway_only"]["requests_per_s"] > 0
 
 
 def _rank0_ingress(world):
