@@ -216,8 +216,9 @@ def main(argv=None) -> int:
     def busy_local():
         # the stop decision must be GLOBAL: every tick is a collective, so all
         # ranks have to run the same number of them
-        return (engine.inflight() + len(gw.remote_out) + sum(len(v) for v in gw._done_owed.values())
-                + gw.pending() + gw.inbox_size())
+        return (engine.inflight() + engine.queued_steps() + len(gw.remote_out)
+                + sum(len(v) for v in gw._done_owed.values()) + gw.pending() + gw.inbox_size()
+                + gw.awaiting_kv())
 
     busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
     while busy.max() > 0:

@@ -109,6 +109,7 @@ class BackendEngine:
         self.kv_reused_tokens = 0
         self.kv_evictions = 0
         self.kv_imported = 0
+        self.kv_stale = 0                                   # parked copies found outdated at admission
         # per-slot host state (the batch builder is vectorised over these)
         self.s_prompt = np.zeros((slots, max_ctx), dtype=np.int32)
         self.s_plen = np.zeros(slots, dtype=np.int64)
@@ -256,6 +257,11 @@ class BackendEngine:
             s = self.conv_lru.pop(r.conv, None) if r.conv >= 0 else None
             if s is not None:
                 base = int(self.s_cached[s])
+                if r.history is not None and base < len(r.history):
+                    # a stale copy: this GPU served an earlier turn, later turns
+                    # ran elsewhere -- attending over it would drop them
+                    base = 0
+                    self.kv_stale += 1
                 if base + len(r.prompt) + r.gen_tokens > cap + 1:
                     base = 0                                  # context window full: restart the dialog KV
             else:

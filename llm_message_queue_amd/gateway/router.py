@@ -97,6 +97,7 @@ class LatencyRecorder:
 
 # --------------------------------------------------------------------------- descriptors
 K_DISPATCH, K_DONE, K_FAIL = 1, 2, 3     # K_FAIL: an evacuating backend hands a request back
+K_MIGRATE = 4       # [kind, conv lo/hi, dest]: to a conversation's home GPU -- send its KV to dest this tick
 DESC_HDR = 16       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
 #                    dialog history length, -]; flags = (home GPU + 1) | KV_MIGRATE
 KV_MIGRATE = 1 << 8     # descriptor flag: hold the turn until its KV arrives from the home GPU
@@ -182,8 +183,11 @@ class Gateway:
         # the worst case of rebalancing, for measuring migration vs replay
         self.affinity = True
         self.rehome_every_turn = False
-        self._mig_out: List[Tuple[int, int, int]] = []       # orders to publish in the next load vector
-        self._await_kv: Dict[int, List[Request]] = {}         # conv key -> turns held for their KV
+        # orders (conv, home, dest) decided this tick; their K_MIGRATE rows go
+        # to the home GPUs in the next tick's all_to_all (counts announced in
+        # that tick's load vector), when home and dest both execute them
+        self._mig_out: List[Tuple[int, int, int]] = []
+        self._await_kv: Dict[int, List[Tuple[Request, int]]] = {}   # conv -> [(held turn, home GPU)]
         self.migrator = None
         if self.world > 1 and engine is not None and self.kv_migrate and hasattr(engine, "model"):
             from ..parallel.migration import KVMigrator
@@ -196,7 +200,7 @@ class Gateway:
         self.rec = LatencyRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
-                         "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0}
+                         "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0, "realtime_local": 0}
         # overload shedding (expire_queued) -> dead-letter queue
         self.shed_expired = bool(getattr(q, "shed_expired", True))
         # realtime lane (tier 0 admitted past the step's prefill headroom and
@@ -543,7 +547,8 @@ class Gateway:
             pinned=self.pinned if self.affinity else None, stopping=self.stopping,
             slots_free=slots_free, slots_total=eng.slots if eng is not None else 0,
             exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
-            weights=self._weights(), migrations=self._mig_out)
+            weights=self._weights(),
+            migrate_rows=[sum(1 for _, h, _ in self._mig_out if h == j and j != self.rank) for j in range(W)])
 
     def _observe_loads(self, loads: np.ndarray) -> None:
         """Per-tick bookkeeping on the gathered load matrix: peers' health and
@@ -581,9 +586,9 @@ class Gateway:
     def _dispatch_global(self) -> int:
         W, me = self.world, self.rank
         loads = self.comm.all_gather_i64(self._my_load())
-        self._mig_out = []                               # published; every rank now executes them
+        orders_prev, self._mig_out = self._mig_out, []   # decided last tick: sent / executed now
+        held_prev, self._await_kv = self._await_kv, {}   # turns flagged last tick
         self._observe_loads(loads)
-        ready = self._migrate(loads)                     # turns whose KV arrived (or replays)
         quota = planner.plan_dispatch(loads, [a // 1000 for a in self.aging_ns], self.plan_state)
         # pop exactly my per-tier grant
         mine = quota[me]                              # [W, 4]
@@ -633,6 +638,13 @@ class Gateway:
                 m.dispatched_at = now_ns
             if rows and self.lb is not None:
                 self.lb.note_dispatch(f"gpu{j}", len(rows))
+            mig_rows = [(c, d) for c, h, d in orders_prev if h == j] if j != me else []
+            if mig_rows:
+                extra = np.zeros((len(mig_rows), width), dtype=np.int32)
+                for k, (c, d) in enumerate(mig_rows):
+                    extra[k, 0] = K_MIGRATE
+                    extra[k, 1], extra[k, 2] = _split64(np.array([c]))[0][0], _split64(np.array([c]))[1][0]
+                    extra[k, 3] = d
             for k, rec in enumerate(self._done_owed[j]):
                 row = buf[len(rows) + k]
                 row[0] = rec[4]
@@ -641,34 +653,51 @@ class Gateway:
                 row[5], row[6] = _split64(np.array([rec[2]]))[0][0], _split64(np.array([rec[2]]))[1][0]
                 row[7], row[8] = _split64(np.array([rec[3]]))[0][0], _split64(np.array([rec[3]]))[1][0]
             self._done_owed[j] = []
-            send.append(buf)
+            send.append(np.concatenate([buf, extra]) if mig_rows else buf)
             if j != me:
                 self.counters["remote_sent"] += len(rows)
-        recv_counts = [int(quota[i, me].sum()) + int(loads[i, planner.L_DONE + me]) if i != me else 0
-                       for i in range(W)]
+        recv_counts = [int(quota[i, me].sum()) + int(loads[i, planner.L_DONE + me])
+                       + int(loads[i, planner.L_MIGC + me]) if i != me else 0 for i in range(W)]
         send[me] = np.zeros((0, width), dtype=np.int32)
         got = self.comm.all_to_all_rows(send, recv_counts, width)
-        # admit: my own first, then foreign descriptors
+        # orders where I am the home GPU: K_MIGRATE rows from the routers, plus
+        # my own router's orders for my own KV
+        src_orders = [(c, me, d) for c, h, d in orders_prev if h == me]
         local_msgs = dest[me]
-        reqs: List[Request] = list(ready)
+        newly_held: List[Tuple[Request, int]] = []
         for m in local_msgs:
             r = self._make_request(m, m.tier)
-            if id(m) in migrate:                      # my own turn, its KV comes next tick
-                self._await_kv.setdefault(r.conv, []).append(r)
+            if id(m) in migrate:                      # my own turn: its KV comes next tick
+                newly_held.append((r, migrate[id(m)]))
             else:
-                reqs.append(r)
+                newly_held.append((r, -1))
+        fresh: List[Request] = []
         for src in range(W):
             for row in got[src]:
-                if row[0] == K_DISPATCH:
+                kind = row[0]
+                if kind == K_DISPATCH:
                     r = self._foreign_request(row, cap)
-                    if int(row[11]) & KV_MIGRATE:
-                        self._await_kv.setdefault(r.conv, []).append(r)
+                    fl = int(row[11])
+                    if fl & KV_MIGRATE:
+                        newly_held.append((r, (fl & 0xFF) - 1))
                     else:
-                        reqs.append(r)
-                elif row[0] == K_DONE:
+                        fresh.append(r)
+                elif kind == K_DONE:
                     self._remote_done(row)
-                elif row[0] == K_FAIL:
+                elif kind == K_FAIL:
                     self._remote_fail(row)
+                elif kind == K_MIGRATE:
+                    src_orders.append((int(_join64(row[1:2], row[2:3])[0]), me, int(row[3])))
+        # execute last tick's orders (home side: send; dest side: receive),
+        # then admit the turns that waited for them, ahead of new work
+        ready = self._migrate(loads, src_orders, held_prev)
+        reqs: List[Request] = list(ready)
+        for r, h in newly_held:
+            if h < 0:
+                reqs.append(r)
+            else:
+                self._await_kv.setdefault(r.conv, []).append((r, h))
+        reqs.extend(fresh)
         admitted = self.engine.admit(reqs) if (self.engine is not None and reqs and self.healthy) else []
         now = time.monotonic_ns()
         tiers, arr, enqs = [], [], []
@@ -728,27 +757,28 @@ class Gateway:
 
     def awaiting_kv(self) -> int:
         """Turns dispatched here that wait for their KV (next tick)."""
-        return sum(len(v) for v in self._await_kv.values())
+        return sum(len(v) for v in self._await_kv.values())   # (turn, home) pairs
 
     def _plan_migrations(self, dest: Dict[int, List[Message]]) -> Dict[int, int]:
         """Turns placed on a GPU other than their (alive) home GPU move their
-        dialog KV with them: record the order (published in the next load
-        vector) and re-home the conversation now.  At most
-        ``planner.MAX_MIGRATIONS`` per router per tick; the rest replay."""
+        dialog KV with them: record the order (sent to the home GPU in the next
+        tick's all_to_all) and re-home the conversation now."""
         out: Dict[int, int] = {}
         if self.migrator is None or not self.kv_migrate:
             return out
         W = self.world
+        seen = set()
         for j in range(W):
             for m in dest[j]:
-                if not m.conversation_id or len(self._mig_out) >= planner.MAX_MIGRATIONS:
+                if not m.conversation_id:
                     continue
                 h = self._home(m)
                 if not 0 <= h < W or h == j or h in self.unhealthy_peers or (h == self.rank and not self.healthy):
                     continue
                 ck = conv_key(m.conversation_id)
-                if any(o[0] == ck for o in self._mig_out):
+                if ck in seen:
                     continue                               # one move per conversation per tick
+                seen.add(ck)
                 out[id(m)] = h
                 self._mig_out.append((ck, h, j))
                 self.conv_home[m.conversation_id] = j
@@ -756,27 +786,28 @@ class Gateway:
                     m.metadata["home_gpu"] = j
         return out
 
-    def _migrate(self, loads: np.ndarray) -> List[Request]:
-        """Execute every router's published orders (same list on every
-        rank), then release the turns held here for them: resident KV if it
-        arrived, else a dialog replay."""
-        orders = planner.migration_orders(loads)
+    def _migrate(self, loads: np.ndarray, src_orders: List[Tuple[int, int, int]],
+                 held: Dict[int, List[Tuple[Request, int]]]) -> List[Request]:
+        """Execute last tick's migration orders -- as the home GPU
+        (``src_orders``) and as the destination (the turns ``held`` for their
+        KV) -- then release the held turns: resident KV if it arrived, else a
+        dialog replay.  A home GPU that is down (by this tick's loads, the
+        view every rank shares) neither sends nor is waited for."""
+        up = [bool(x) for x in loads[:, planner.L_HEALTHY]]
+        orders = [o for o in src_orders if up[self.rank]]
+        for ck, rs in held.items():
+            srcs = {h for _, h in rs if 0 <= h < self.world and up[h]}
+            orders.extend((ck, h, self.rank) for h in srcs)
         imported: Dict[int, int] = {}
         if orders and self.migrator is not None:
             imported = self.migrator.execute(orders, self.engine, self.rank)
-            if any(self.rank in (s, d) for _, s, d in orders):
-                self.epoch += 1
+            self.epoch += 1
         ready: List[Request] = []
-        if self._await_kv:
-            for ck, rs in self._await_kv.items():
-                got = imported.get(ck, 0)
-                for r in rs:
-                    if got > 0:
-                        self.counters["kv_migrated"] += 1
-                    else:
-                        self.counters["kv_migrate_replays"] += 1
-                ready.extend(rs)
-            self._await_kv = {}
+        for ck, rs in held.items():
+            got = imported.get(ck, 0)
+            for r, _h in rs:
+                self.counters["kv_migrated" if got > 0 else "kv_migrate_replays"] += 1
+                ready.append(r)
         return ready
 
     def _home(self, m: Message, effective: bool = False) -> int:
@@ -863,7 +894,7 @@ class Gateway:
         self.log.warning("GPU backend unhealthy; evacuating", rank=self.rank, reason=reason)
         self._err_ewma = 0.9 * self._err_ewma + 0.1
         n = 0
-        held = [r for rs in self._await_kv.values() for r in rs]
+        held = [r for rs in self._await_kv.values() for r, _h in rs]
         self._await_kv = {}
         for r in held:                                  # turns waiting for a KV that will not be used here
             n += 1
@@ -981,7 +1012,57 @@ class Gateway:
         did = bool(self.ingest())
         if self.world == 1:
             did = self._dispatch_local() > 0 or did
+        else:
+            did = self._dispatch_realtime_local() > 0 or did
         return did
+
+    def _dispatch_realtime_local(self) -> int:
+        """Multi-rank realtime lane: between the per-tick collectives a router
+        admits its realtime-tier requests straight into free slots of its OWN
+        GPU.  A local placement needs no cross-rank decision (the next load
+        vector reports the slots taken), so realtime dispatch is not paced by
+        the tick.  Skipped while realtime turns homed on another GPU are
+        queued here -- those follow their KV through the planner."""
+        eng = self.engine
+        if not self.realtime_lane or eng is None or not self.healthy or not self.tiers:
+            return 0
+        if self.qm.size(self.tiers[0]) <= 0:
+            return 0
+        homed_elsewhere = int(self.pinned[:, 0].sum()) - int(self.pinned[self.rank, 0])
+        if homed_elsewhere > 0:
+            return 0
+        room = eng.lane_capacity() - self.awaiting_kv()
+        b = self._budgets()[0]
+        if b >= 0:
+            room = min(room, b)
+        if room <= 0:
+            return 0
+        budgets = [0] * len(self.tiers)
+        budgets[0] = room
+        msgs, _t, _e = self.qm.pop_tiers(self.tiers, room, [0] * len(self.tiers), budgets, None)
+        if not msgs:
+            return 0
+        reqs = []
+        for m in msgs:
+            self._pin(m, -1)
+            m.tier = 0
+            reqs.append(self._make_request(m, 0))
+        admitted = eng.admit(reqs)
+        now = time.monotonic_ns()
+        for r in admitted:
+            m = r.meta
+            m.dispatched_at = now
+            m.status = MessageStatus.PROCESSING
+            m.endpoint_id = f"gpu{self.rank}"
+            self.local[m.handle] = m
+            self.inflight_by_tier[0] += 1
+        for r in reqs[len(admitted):]:             # cannot happen (room was counted); requeue defensively
+            self._requeue(r.meta)
+        self._record([0] * len(admitted), [r.meta.arrival_ns for r in admitted],
+                     [r.meta.enqueued_at for r in admitted], now)
+        self.counters["dispatched"] += len(admitted)
+        self.counters["realtime_local"] += len(admitted)
+        return len(admitted)
 
     def quiesce(self, pump=None, poll_s: float = 0.0002) -> None:
         """Wait until no forward step is queued on the GPU, ingesting (and on

@@ -64,12 +64,11 @@ L_RT_US = L_EXCLUDE + 1          # EWMA service time (admit -> done) on this GPU
 L_ERR_PPM = L_EXCLUDE + 2        # EWMA backend error rate, parts per million
 L_SLOTS_TOTAL = L_EXCLUDE + 3    # batch slots of this GPU
 L_WEIGHT = L_EXCLUDE + 8         # [64 + j] endpoint weight of GPU j in this rank's balancer (rank 0 row is used)
-# KV migration orders this router decided LAST tick (executed this tick by
-# every rank from the gathered loads): count, then (conv key, src << 8 | dst)
-MAX_MIGRATIONS = 64
-L_MIG_N = L_WEIGHT + MAX_WORLD   # 72
-L_MIG = L_MIG_N + 1              # 73 .. 73 + 2 * MAX_MIGRATIONS
-LOAD_WIDTH = L_MIG + 2 * MAX_MIGRATIONS
+# KV migration: [72 + h] = K_MIGRATE rows this router sends rank h in THIS
+# tick's all_to_all (orders decided last tick; h = the conversation's home,
+# which sends the KV) -- announced here so every receiver knows its row count
+L_MIGC = L_WEIGHT + MAX_WORLD
+LOAD_WIDTH = L_MIGC + MAX_WORLD
 
 STRATEGIES = ("round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first")
 
@@ -79,7 +78,7 @@ def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[i
               done_for: Sequence[int] = (), pinned=None, stopping: bool = False,
               slots_free: Optional[int] = None, slots_total: int = 0, exclude_mask: int = 0,
               rt_us: int = 0, err_ppm: int = 0, weights: Sequence[int] = (),
-              migrations: Sequence[Sequence[int]] = ()) -> np.ndarray:
+              migrate_rows: Sequence[int] = ()) -> np.ndarray:
     """``pinned``: [W, 4] (home GPU x tier) queued counts, or a [W] vector
     (all counted as tier 2, normal -- legacy callers)."""
     v = np.zeros(LOAD_WIDTH, dtype=np.int64)
@@ -103,28 +102,9 @@ def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[i
     v[L_RT_US], v[L_ERR_PPM], v[L_SLOTS_TOTAL] = rt_us, err_ppm, slots_total
     for j, w in enumerate(list(weights)[:MAX_WORLD]):
         v[L_WEIGHT + j] = w
-    mig = list(migrations)[:MAX_MIGRATIONS]
-    v[L_MIG_N] = len(mig)
-    for k, (conv, src, dst) in enumerate(mig):
-        v[L_MIG + 2 * k] = conv
-        v[L_MIG + 2 * k + 1] = (int(src) << 8) | int(dst)
+    for h, n in enumerate(list(migrate_rows)[:MAX_WORLD]):
+        v[L_MIGC + h] = n
     return v
-
-
-def migration_orders(loads: np.ndarray):
-    """Every router's published orders ``(conv, src, dst)``, in rank order;
-    orders whose source GPU is down are dropped (its KV is gone: the turn
-    replays), identically on every rank."""
-    out = []
-    W = loads.shape[0]
-    for i in range(W):
-        for k in range(int(min(loads[i, L_MIG_N], MAX_MIGRATIONS))):
-            conv = int(loads[i, L_MIG + 2 * k])
-            sd = int(loads[i, L_MIG + 2 * k + 1])
-            src, dst = sd >> 8, sd & 0xFF
-            if 0 <= src < W and 0 <= dst < W and loads[src, L_HEALTHY] > 0:
-                out.append((conv, src, dst))
-    return out
 
 
 @dataclass

@@ -139,3 +139,25 @@ def test_dead_home_replays():
     assert gws[1].counters["completed"] == 2
     assert gws[0].engine.kv_imported == 0
     assert sum(g.counters["kv_migrated"] for g in gws) == 0
+
+
+def test_stale_parked_copy_is_not_reused():
+    """A GPU that served an earlier turn still parks that turn's KV; when a
+    later turn ran elsewhere (no migration), the parked copy misses it and
+    must not be attended over: the engine replays the dialog instead."""
+    e = _eng()
+    conv = 99
+    _run(e, Request(1, np.arange(5, 15, dtype=np.int32), 3, conv=conv))
+    parked = e.export_kv(conv)[1]
+    assert parked == 12
+    # the gateway's dialog is longer than the parked copy (a turn ran elsewhere)
+    hist = np.zeros(parked + 9, dtype=np.int32)
+    r = Request(2, np.arange(20, 26, dtype=np.int32), 3, conv=conv, history=hist)
+    e.admit([r])
+    assert r.reused == 0 and e.kv_stale == 1 and len(r.prompt) == len(hist) + 6
+    # an up-to-date copy is reused
+    e2 = _eng()
+    _run(e2, Request(1, np.arange(5, 15, dtype=np.int32), 3, conv=conv))
+    r2 = Request(2, np.arange(20, 26, dtype=np.int32), 3, conv=conv, history=np.zeros(parked, dtype=np.int32))
+    e2.admit([r2])
+    assert r2.reused == parked and e2.kv_stale == 0

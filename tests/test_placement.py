@@ -257,3 +257,23 @@ def test_serve_loop_exits_on_peer_lost():
     app._loop_thread.join(5)
     assert isinstance(app.fatal, PeerLost) and app._stop.is_set()
     app.stop()
+
+
+def test_multirank_realtime_lane_dispatches_between_ticks():
+    """World > 1: dispatch is a per-tick collective, but realtime requests
+    are admitted into the router's own GPU while it waits for the forward
+    (no tick needed), and the next load vector accounts for them."""
+    from llm_message_queue_amd.models.message import Message
+    W = 2
+    gws, _ = _cluster(W, "least_connections", slots=16)
+    rt = [Message(id=f"rt{i}", content="outage now", priority=1, user_id="u") for i in range(3)]
+    gws[0].submit(rt)
+    gws[0]._last_ingest_ns = 0
+    assert gws[0]._while_waiting(None)                   # ingest + local realtime admission, no collective
+    assert all(m.dispatched_at > 0 and m.endpoint_id == "gpu0" for m in rt)
+    assert gws[0].counters["realtime_local"] == 3
+    for _ in range(30):
+        _tick_all(gws)
+        if gws[0].counters["completed"] >= 3:
+            break
+    assert gws[0].counters["completed"] == 3
