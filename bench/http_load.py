@@ -97,6 +97,23 @@ def _wait_up(url, timeout=120.0):
     return False
 
 
+def _bench_config_file() -> str:
+    """configs/config.yaml plus the serving settings bench.py measures."""
+    import yaml
+    with open(os.path.join(ROOT, "configs", "config.yaml")) as fh:
+        c = yaml.safe_load(fh)
+    for lv, ms in zip(sorted(c["queue"]["levels"], key=lambda x: x["priority"]), (50, 100, 150, 200)):
+        lv["max_concurrent"] = 1536
+        lv["max_wait_time"] = f"{ms}ms"
+    c.setdefault("gpu", {})["slots_per_gpu"] = 1536
+    c.setdefault("backend", {}).update({"token_budget": 4096, "max_ctx": 512, "prompt_tokens": 32, "gen_tokens": 4})
+    c.setdefault("logging", {})["level"] = "warning"
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"llmq_bench_config_{os.getpid()}.yaml")
+    with open(path, "w") as fh:
+        yaml.safe_dump(c, fh)
+    return path
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--url", default="")
@@ -110,6 +127,12 @@ def main() -> None:
     ap.add_argument("--client", choices=["python", "native"], default="python",
                     help="native = csrc/tools/http_bench.cpp (open-loop, keep-alive, no coordinated omission)")
     ap.add_argument("--conns", type=int, default=16, help="native client: connections per thread")
+    ap.add_argument("--warmup", type=float, default=0.0,
+                    help="seconds of load before the measured window (the dispatcher's latency window is reset "
+                         "after it)")
+    ap.add_argument("--bench-config", action="store_true",
+                    help="spawned GPU dispatcher runs bench.py's serving config (1536 slots, 4096-token steps, "
+                         "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
     a = ap.parse_args()
     procs, urls = [], []
     api_url = ""
@@ -117,6 +140,9 @@ def main() -> None:
                LLMQ_QUEUE__WORKER__MAX_CONCURRENT="512", LLMQ_QUEUE__WORKER__MAX_BATCH_SIZE="256",
                LLMQ_QUEUE__WORKER__PROCESS_INTERVAL="5ms")
     gpu = [] if a.gpu else ["--no-gpu"]
+    cfg_args = []
+    if a.bench_config:
+        cfg_args = ["--config", _bench_config_file()]
     try:
         if a.spawn == "serve":
             port = _port()
@@ -143,7 +169,8 @@ def main() -> None:
             api_port = _port()
             api_url = f"http://127.0.0.1:{api_port}"
             procs.append(subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "queue-manager",
-                                           "--ring", ring, "--port", str(api_port), "--host", "127.0.0.1"] + gpu,
+                                           "--ring", ring, "--port", str(api_port), "--host", "127.0.0.1"]
+                                          + gpu + cfg_args,
                                           cwd=ROOT, env=env,
                                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                           start_new_session=True))
@@ -164,16 +191,35 @@ def main() -> None:
             subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", os.path.join(ROOT, "csrc", "tools", "http_bench.cpp"),
                             "-o", exe], check=True)
             host, port = urls[0].split("//")[1].split(":")
+            import threading
+            import urllib.request
+            if a.warmup > 0:
+                subprocess.run([exe, host, port, str(a.rate), str(a.warmup), str(a.procs), str(a.conns)],
+                               capture_output=True, text=True, timeout=a.warmup + 60)
+            # the measured window: the load keeps running while the
+            # dispatcher's latency histograms restart (reset ~1 s in)
+            if api_url and a.warmup > 0:
+                def _reset():
+                    time.sleep(1.0)
+                    req = urllib.request.Request(api_url + "/api/v1/admin/stats/reset", method="POST", data=b"")
+                    urllib.request.urlopen(req, timeout=10).read()
+                threading.Thread(target=_reset, daemon=True).start()
             r = subprocess.run([exe, host, port, str(a.rate), str(a.duration), str(a.procs), str(a.conns)],
                                capture_output=True, text=True, timeout=a.duration + 60)
+            st_end = None
+            if api_url:                         # latency window closes with the load (before the drain)
+                with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
+                    st_end = json.loads(rr.read())
             os.unlink(exe)
             out = json.loads(r.stdout.strip().splitlines()[-1])
             if api_url:
-                import urllib.request
                 time.sleep(2.0)
                 with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
                     st = json.loads(rr.read())
-                out["dispatcher"] = {"dispatch": st.get("dispatch"), "latency": st.get("latency")}
+                out["dispatcher"] = {"dispatch": st.get("dispatch"), "latency": st_end.get("latency"),
+                                     "latency_e2e": st_end.get("latency_e2e"),
+                                     "note": "latency: HTTP arrival (native ingress clock) -> GPU slot admission; "
+                                             "latency_e2e: -> last generated token; window = the measured run"}
             out["mode"] = a.spawn or "url"
             print(json.dumps(out))
             return

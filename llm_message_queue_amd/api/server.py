@@ -558,6 +558,13 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         n = G.factory.dead_letter_queue.requeue_all(G.standard)
         return {"status": "requeued", "count": n}
 
+    @app.post("/api/v1/admin/stats/reset")
+    def reset_stats():
+        """Open a new latency window (arrival->dispatch and ->completion
+        histograms); counters are cumulative and stay."""
+        gw_app.reset_latency()
+        return {"status": "reset"}
+
     @app.get("/api/v1/admin/dead-letter")
     def list_dead_letter():
         return {"items": [it.to_dict() for it in G.factory.dead_letter_queue.get_all()]}

@@ -342,6 +342,12 @@ class GatewayApp:
         m.arrival_ns = int.from_bytes(b[0:8], "little", signed=True) if len(b) >= 8 else 0
         return m
 
+    def reset_latency(self) -> None:
+        """Start a fresh latency window (operators / load tests)."""
+        self.gateway.flush_latency()
+        self.gateway.rec.reset()
+        self.gateway.rec_done.reset()
+
     def _event_loop(self) -> None:
         """Ingress: apply status events from the dispatcher to the message store."""
         while not self._stop.is_set():
@@ -426,7 +432,9 @@ class GatewayApp:
             out[name] = {q: s.to_dict() for q, s in mgr.get_all_queue_stats().items()}
         out["workers"] = {q: [w.to_dict() for w in ws] for q, ws in self.factory.get_worker_stats().items()}
         out["dispatch"] = dict(self.gateway.counters)
-        out["latency"] = self.gateway.rec.summary()
+        out["latency"] = self.gateway.rec.summary()          # arrival -> dispatch (and enqueue -> dispatch)
+        self.gateway.flush_latency()
+        out["latency_e2e"] = self.gateway.rec_done.summary()  # arrival -> completion
         out["dead_letter"] = self.factory.dead_letter_queue.size()
         if self.ring is not None:
             out["rings"] = self.ring.stats()
