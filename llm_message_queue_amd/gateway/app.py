@@ -364,10 +364,32 @@ class GatewayApp:
                     m.metadata["error"] = ev["error"]
 
     # ------------------------------------------------------------------ dispatch
+    def _gc_maintenance(self, now: float) -> None:
+        """See ``server.gc_freeze_interval``: keep full GC scans off the
+        request path."""
+        import gc
+        sc = self.cfg.server
+        fi, fu = sc.gc_freeze_interval / 1e9, sc.gc_full_interval / 1e9
+        if fi <= 0:
+            return
+        if fu > 0 and now - self._gc_full_at >= fu:
+            gc.unfreeze()
+            gc.collect()
+            self._gc_full_at = now
+        if now - self._gc_freeze_at >= fi:
+            gc.freeze()
+            self._gc_freeze_at = now
+
     def _serve_loop(self) -> None:
+        import gc
         from ..parallel.comm import PeerLost
         gw = self.gateway
+        if self.cfg.server.gc_freeze_interval > 0:
+            gc.collect()
+            gc.freeze()
+        self._gc_freeze_at = self._gc_full_at = time.monotonic()
         while True:
+            self._gc_maintenance(time.monotonic())
             if self._stop.is_set():
                 gw.request_stop()
             if gw.peers_stopping:

@@ -49,6 +49,13 @@ class ServerConfig:
     # native ingress: close connections silent this long (idle keep-alive,
     # slowloris); 0 = never
     idle_timeout: int = 60_000_000_000
+    # latency: a full cyclic-GC pass over a serving heap (hundreds of
+    # thousands of tracked messages) stalls every request for 100+ ms.  The
+    # serve loop freezes the heap (gc.freeze: survivors leave the scanned
+    # generations; refcounting still frees them) every gc_freeze_interval and
+    # runs a full collection only every gc_full_interval.  0 disables.
+    gc_freeze_interval: int = 1_000_000_000
+    gc_full_interval: int = 600_000_000_000
 
 
 @dataclass
@@ -324,7 +331,7 @@ _DURATION_FIELDS = {
     "max_wait_time", "monitor_interval", "cleanup_interval", "max_retention_period",
     "process_interval", "initial_backoff", "max_backoff", "check_interval", "timeout",
     "health_check_interval", "session_timeout", "heartbeat_timeout", "autoscale_cooldown",
-    "max_idle_time", "lifo_after", "idle_timeout",
+    "max_idle_time", "lifo_after", "idle_timeout", "gc_freeze_interval", "gc_full_interval",
 }
 
 
