@@ -218,6 +218,7 @@ def main(argv=None) -> int:
         # ranks have to run the same number of them
         return (engine.inflight() + engine.queued_steps() + len(gw.remote_out)
                 + sum(len(v) for v in gw._done_owed.values()) + gw.pending() + gw.inbox_size()
+                + gw.preprocessing()
                 + gw.awaiting_kv())
 
     busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))

@@ -130,6 +130,9 @@ def main() -> None:
     ap.add_argument("--warmup", type=float, default=0.0,
                     help="seconds of load before the measured window (the dispatcher's latency window is reset "
                          "after it)")
+    ap.add_argument("--workload", action="store_true",
+                    help="native client sends bench.py's synthetic 4-tier workload (gateway/workload.py) instead "
+                         "of four fixed bodies")
     ap.add_argument("--bench-config", action="store_true",
                     help="spawned GPU dispatcher runs bench.py's serving config (1536 slots, 4096-token steps, "
                          "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
@@ -193,8 +196,19 @@ def main() -> None:
             host, port = urls[0].split("//")[1].split(":")
             import threading
             import urllib.request
+            extra = []
+            if a.workload:
+                from llm_message_queue_amd.gateway.workload import Workload
+                bpath = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"llmq_bodies_{os.getpid()}.jsonl")
+                with open(bpath, "w") as fh:
+                    for m in Workload(seed=7).make(int(a.rate * (a.duration + a.warmup)) + 1000):
+                        b = {"content": m.content, "user_id": m.user_id}
+                        if m.priority:
+                            b["priority"] = m.priority
+                        fh.write(json.dumps(b) + "\n")
+                extra = [bpath]
             if a.warmup > 0:
-                subprocess.run([exe, host, port, str(a.rate), str(a.warmup), str(a.procs), str(a.conns)],
+                subprocess.run([exe, host, port, str(a.rate), str(a.warmup), str(a.procs), str(a.conns)] + extra,
                                capture_output=True, text=True, timeout=a.warmup + 60)
             # the measured window: the load keeps running while the
             # dispatcher's latency histograms restart (reset ~1 s in)
@@ -204,7 +218,7 @@ def main() -> None:
                     req = urllib.request.Request(api_url + "/api/v1/admin/stats/reset", method="POST", data=b"")
                     urllib.request.urlopen(req, timeout=10).read()
                 threading.Thread(target=_reset, daemon=True).start()
-            r = subprocess.run([exe, host, port, str(a.rate), str(a.duration), str(a.procs), str(a.conns)],
+            r = subprocess.run([exe, host, port, str(a.rate), str(a.duration), str(a.procs), str(a.conns)] + extra,
                                capture_output=True, text=True, timeout=a.duration + 60)
             st_end = None
             if api_url:                         # latency window closes with the load (before the drain)

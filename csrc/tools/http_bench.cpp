@@ -4,7 +4,11 @@
 // out of the measurement.
 //
 //   g++ -O2 -std=c++17 -pthread csrc/tools/http_bench.cpp -o /tmp/http_bench
-//   /tmp/http_bench <host> <port> <rate_total> <seconds> <threads> <conns_per_thread>
+//   /tmp/http_bench <host> <port> <rate_total> <seconds> <threads> <conns_per_thread> [bodies.jsonl]
+//
+// With a bodies file (one JSON body per line -- e.g. bench.py's synthetic
+// 4-tier workload, written by bench/http_load.py) requests cycle through it
+// in order; otherwise four fixed bodies are drawn with the 10/30/40/20 mix.
 //
 // Each thread owns `conns` keep-alive connections and issues requests on a
 // Poisson schedule at rate/threads, round-robin over its connections,
@@ -71,19 +75,29 @@ static int dial(const char* host, int port) {
   return fd;
 }
 
-static void worker(const char* host, int port, double rate, double secs, int nconn, uint64_t seed, Result* res) {
+static std::vector<std::string> g_file_bodies;
+
+static void worker(const char* host, int port, double rate, double secs, int nconn, uint64_t seed, Result* res,
+                   int tid, int nthreads) {
   std::vector<Conn> cs(nconn);
   for (auto& c : cs) c.fd = dial(host, port);
   std::mt19937_64 rng(seed);
   std::exponential_distribution<double> gap(rate);
   std::discrete_distribution<int> pick(kMix, kMix + 4);
   std::vector<std::string> reqs;
-  for (auto* b : kBodies) {
+  auto add = [&](const std::string& b) {
     char hdr[256];
     snprintf(hdr, sizeof hdr, "POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
-                              "Content-Length: %zu\r\n\r\n", strlen(b));
+                              "Content-Length: %zu\r\n\r\n", b.size());
     reqs.push_back(std::string(hdr) + b);
+  };
+  if (!g_file_bodies.empty()) {
+    for (size_t i = (size_t)tid; i < g_file_bodies.size(); i += (size_t)nthreads) add(g_file_bodies[i]);
+  } else {
+    for (auto* b : kBodies) add(b);
   }
+  const bool from_file = !g_file_bodies.empty() && !reqs.empty();
+  size_t next_body = 0;
   const int64_t t0 = now_ns(), t_end = t0 + (int64_t)(secs * 1e9);
   int64_t t_next = t0;
   size_t rr = 0;
@@ -103,7 +117,7 @@ static void worker(const char* host, int port, double rate, double secs, int nco
       if (c.fd < 0) {
         res->errors++;
       } else {
-        c.out += reqs[pick(rng)];
+        c.out += from_file ? reqs[next_body++ % reqs.size()] : reqs[pick(rng)];
         c.sent.push_back(t_next);
         res->sent++;
       }
@@ -165,11 +179,27 @@ int main(int argc, char** argv) {
   int port = atoi(argv[2]);
   double rate = atof(argv[3]), secs = atof(argv[4]);
   int threads = atoi(argv[5]), conns = atoi(argv[6]);
+  if (argc > 7) {
+    FILE* f = fopen(argv[7], "r");
+    if (!f) {
+      fprintf(stderr, "cannot open %s\n", argv[7]);
+      return 2;
+    }
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t n;
+    while ((n = getline(&line, &cap, f)) > 0) {
+      while (n > 0 && (line[n - 1] == '\n' || line[n - 1] == '\r')) --n;
+      if (n > 0) g_file_bodies.emplace_back(line, (size_t)n);
+    }
+    free(line);
+    fclose(f);
+  }
   std::vector<Result> rs(threads);
   std::vector<std::thread> th;
   const int64_t t0 = now_ns();
   for (int i = 0; i < threads; ++i)
-    th.emplace_back(worker, host, port, rate / threads, secs, conns, 1234567ull * (i + 1), &rs[i]);
+    th.emplace_back(worker, host, port, rate / threads, secs, conns, 1234567ull * (i + 1), &rs[i], i, threads);
   for (auto& t : th) t.join();
   const double wall = (now_ns() - t0) / 1e9;
   std::vector<int64_t> lat;

@@ -160,6 +160,7 @@ class Gateway:
         self.metrics = metrics
         self._inbox: List[Message] = []
         self._inbox_lock = threading.Lock()
+        self._pre_pending = None        # outstanding asynchronous preprocess batch (ingest_async)
         self.inflight_by_tier = np.zeros(len(self.tiers), dtype=np.int64)
         # queued requests per (home GPU, tier): KV-residency pins (planner L_PIN)
         self.pinned = np.zeros((self.world, planner.NTIERS), dtype=np.int64)
@@ -253,18 +254,60 @@ class Gateway:
         self.counters["submitted"] += len(msgs)
 
     def ingest(self) -> List[Tuple[Message, Optional[QueueError]]]:
+        """Synchronous ingest: finish any outstanding preprocess batch, then
+        preprocess + enqueue everything in the inbox."""
+        out = self._finish_pending(block=True)
         with self._inbox_lock:
             batch, self._inbox = self._inbox, []
         if not batch:
-            return []
+            return out
         t0 = time.perf_counter_ns()
         self.pre.process_batch(batch, use_gpu=self.use_gpu_pre, prompt_cap=self.prompt_cap)
+        self.ingest_ns[0] += time.perf_counter_ns() - t0
+        return out + self._enqueue(batch)
+
+    def ingest_async(self) -> bool:
+        """Overlapped ingest (GPU preprocess only): enqueue the outstanding
+        batch if its kernels finished, and launch the inbox as the next batch
+        without waiting for it.  The preprocess chain queues behind the
+        forward's GEMMs for CUs; the host keeps ingesting and dispatching
+        meanwhile.  True if anything was done."""
+        if not self.use_gpu_pre:
+            return bool(self.ingest())
+        did = False
+        if self._pre_pending is not None:
+            if not self.pre.batch_ready(self._pre_pending):
+                return False
+            did = bool(self._finish_pending(block=True))
+        with self._inbox_lock:
+            batch, self._inbox = self._inbox, []
+        if batch:
+            t0 = time.perf_counter_ns()
+            self._pre_pending = self.pre.begin_batch(batch, prompt_cap=self.prompt_cap)
+            self.ingest_ns[0] += time.perf_counter_ns() - t0
+            did = True
+        return did
+
+    def preprocessing(self) -> int:
+        """Messages inside an outstanding preprocess batch."""
+        return len(self._pre_pending["msgs"]) if self._pre_pending is not None else 0
+
+    def _finish_pending(self, block: bool) -> List[Tuple[Message, Optional[QueueError]]]:
+        tok = self._pre_pending
+        if tok is None or (not block and not self.pre.batch_ready(tok)):
+            return []
+        self._pre_pending = None
+        t0 = time.perf_counter_ns()
+        self.pre.end_batch(tok)
+        self.ingest_ns[0] += time.perf_counter_ns() - t0
+        return self._enqueue(tok["msgs"])
+
+    def _enqueue(self, batch) -> List[Tuple[Message, Optional[QueueError]]]:
         t1 = time.perf_counter_ns()
         for m in batch:
             if not m.queue_name:
                 m.queue_name = priority_name(m.priority)
         errs = self.qm.push_routed(batch)
-        self.ingest_ns[0] += t1 - t0
         self.ingest_ns[1] += time.perf_counter_ns() - t1
         self.ingest_ns[2] += len(batch)
         out = []
@@ -1006,10 +1049,18 @@ class Gateway:
         if pump is not None:
             pump()
         now = time.monotonic_ns()
+        if self._pre_pending is not None and self.pre.batch_ready(self._pre_pending):
+            # a finished preprocess batch is enqueued (and dispatched) at once
+            self._finish_pending(block=True)
+            if self.world == 1:
+                self._dispatch_local()
+            else:
+                self._dispatch_realtime_local()
+            return True
         if len(self._inbox) < self.WAIT_INGEST_MSGS and now - self._last_ingest_ns < self.WAIT_INGEST_NS:
             return False
         self._last_ingest_ns = now
-        did = bool(self.ingest())
+        did = self.ingest_async()
         if self.world == 1:
             did = self._dispatch_local() > 0 or did
         else:
@@ -1077,6 +1128,7 @@ class Gateway:
             while eng.queued_steps():
                 if not eng.poll_one() and not self._while_waiting(pump):
                     time.sleep(poll_s)
+            self._finish_pending(block=True)      # no preprocess kernels left on the GPU either
             self.finish_backend()
 
     def _tick(self, pump=None):
@@ -1088,7 +1140,10 @@ class Gateway:
             try:
                 self.engine.launch(wait_cb=lambda: self._while_waiting(pump))
                 t1 = pc()
-                self.ingest()
+                if self.engine.queued_steps():
+                    self.ingest_async()          # the GPU is busy: do not wait for the preprocess chain
+                else:
+                    self.ingest()
                 t2 = pc()
                 res = self.finish_backend()
                 t3 = pc()
@@ -1149,6 +1204,7 @@ class Gateway:
             return len(self._inbox)
 
     def drop_pending(self) -> int:
+        self._finish_pending(block=True)
         n = 0
         for t in self.tiers:
             n += self.qm.size(t)

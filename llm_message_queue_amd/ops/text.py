@@ -219,6 +219,8 @@ class TextPipeline:
         # GEMM workgroups -- otherwise every preprocess kernel queues behind a
         # full-chip GEMM and ingest latency grows with the backend's load
         self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+        import threading
+        self._inflight = threading.Lock()
 
     def _ensure_readback(self, n_int32: int) -> None:
         if self._rb is None or self._rb.numel() < n_int32:
@@ -249,10 +251,53 @@ class TextPipeline:
 
     def run(self, contents: Sequence[str], patterns: Dict[int, list], version: int = -1,
             classify: bool = True, keep_device: bool = False, prompt_cap: int = 0) -> TextResult:
-        with self.torch.cuda.stream(self.stream):
-            return self._run(contents, patterns, version, classify, keep_device, prompt_cap)
+        return self.collect(self.launch(contents, patterns, version, classify, keep_device, prompt_cap))
 
-    def _run(self, contents, patterns, version, classify, keep_device, prompt_cap) -> TextResult:
+    def launch(self, contents: Sequence[str], patterns: Dict[int, list], version: int = -1,
+               classify: bool = True, keep_device: bool = False, prompt_cap: int = 0):
+        """Enqueue the whole chain (H2D, kernels, readback into host-mapped
+        memory, event) and return at once; ``collect`` waits and decodes.  The
+        staging and readback buffers are single-buffered: collect a launch
+        before the next one (``ready`` tells whether ``collect`` would
+        block)."""
+        # one launch in flight per pipeline (single-buffered staging): a
+        # second caller -- e.g. the HTTP micro-batcher thread next to the
+        # serve loop -- waits here until the first batch is collected
+        self._inflight.acquire()
+        try:
+            with self.torch.cuda.stream(self.stream):
+                return self._launch(contents, patterns, version, classify, keep_device, prompt_cap)
+        except BaseException:
+            self._inflight.release()
+            raise
+
+    @staticmethod
+    def ready(pend) -> bool:
+        return pend["event"].query()
+
+    def collect(self, pend) -> TextResult:
+        try:
+            pend["event"].synchronize()
+        finally:
+            self._inflight.release()
+        B, cap, o_pred, o_ph = pend["B"], pend["cap"], pend["o_pred"], pend["o_ph"]
+        rbn = self._rb.numpy()
+        stats_h = rbn[:B * STAT_COLS].reshape(B, STAT_COLS).copy()
+        pred_h = rbn[o_pred:o_pred + B].copy() if pend["pred"] is not None else None
+        ph = rbn[o_ph:o_ph + B * cap].reshape(B, cap).view(np.uint32).copy() if cap else None
+        extra = None
+        pk, contents = pend["pk"], pend["contents"]
+        if pk.cpu_patterns:
+            extra = np.zeros((B, 8), dtype=np.int64)
+            for j, c in enumerate(contents):
+                for slot, p in pk.cpu_patterns:
+                    extra[j, slot] += p.count(c)
+        el = (time.perf_counter() - pend["t0"]) * 1e3
+        keep = pend["keep_device"]
+        return TextResult(stats_h, pred_h, el, pend["pred"] is not None, pk.slot_prio, extra,
+                          pend["pooled"] if keep else None, pend["hashes"] if keep else None, self.L, ph)
+
+    def _launch(self, contents, patterns, version, classify, keep_device, prompt_cap):
         torch = self.torch
         t0 = time.perf_counter()
         B = len(contents)
@@ -317,17 +362,7 @@ class TextPipeline:
             self.ops.copy_bytes(rd + 4 * o_ph, hc.data_ptr(), 4 * B * cap, stream)
         ev = torch.cuda.Event()
         ev.record(self.stream)
-        ev.synchronize()
-        rbn = self._rb.numpy()
-        stats_h = rbn[:B * STAT_COLS].reshape(B, STAT_COLS).copy()
-        pred_h = rbn[o_pred:o_pred + B].copy() if pred is not None else None
-        ph = rbn[o_ph:o_ph + B * cap].reshape(B, cap).view(np.uint32).copy() if cap else None
-        extra = None
-        if pk.cpu_patterns:
-            extra = np.zeros((B, 8), dtype=np.int64)
-            for j, c in enumerate(contents):
-                for slot, p in pk.cpu_patterns:
-                    extra[j, slot] += p.count(c)
-        el = (time.perf_counter() - t0) * 1e3
-        return TextResult(stats_h, pred_h, el, pred is not None, pk.slot_prio, extra,
-                          pooled if keep_device else None, hashes if keep_device else None, L, ph)
+        # device tensors stay referenced by the pending record until collect
+        return {"event": ev, "B": B, "cap": cap, "o_pred": o_pred, "o_ph": o_ph, "pred": pred, "pk": pk,
+                "contents": contents, "t0": t0, "keep_device": keep_device, "pooled": pooled, "hashes": hashes,
+                "stats": stats, "hc": hc if cap else None}

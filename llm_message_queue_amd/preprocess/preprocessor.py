@@ -223,17 +223,36 @@ class Preprocessor:
         # whole batch in numpy first (keyword priority argmax with the
         # oracle's tie-break, sentiment, question, fallback flags); the loop
         # below only stores the decided values.
+        return self.end_batch(self.begin_batch(msgs, classify=classify, prompt_cap=prompt_cap))
+
+    # ------------------------------------------------------------------ asynchronous batch (GPU)
+    def begin_batch(self, msgs: Sequence[Message], classify: Optional[bool] = None, prompt_cap: int = 0):
+        """Launch a micro-batch's GPU preprocess and return at once (the
+        host does not wait for the kernels, which queue behind the backend's
+        forward for CUs); ``end_batch`` applies the results.  One batch may be
+        outstanding per preprocessor."""
         with self._lock:
             udefs = dict(self._user_priorities) if self._user_priorities else None
         heads = [self._head_fast(m, udefs) for m in msgs]
         work = [i for i, h in enumerate(heads) if h is not None and msgs[i].content]
-        now = time.time_ns()
+        pend = None
         if work:
             pipe = self.gpu_pipeline()
             pats, ver = self.patterns_snapshot()
-            res = pipe.run([msgs[i].content for i in work], pats, ver,
-                           classify=self.cfg.classifier if classify is None else classify,
-                           prompt_cap=prompt_cap)
+            pend = pipe.launch([msgs[i].content for i in work], pats, ver,
+                               classify=self.cfg.classifier if classify is None else classify,
+                               prompt_cap=prompt_cap)
+        return {"msgs": msgs, "heads": heads, "work": work, "pend": pend, "prompt_cap": prompt_cap}
+
+    def batch_ready(self, tok) -> bool:
+        return tok["pend"] is None or self._gpu.ready(tok["pend"])
+
+    def end_batch(self, tok) -> Sequence[Message]:
+        msgs, heads, work, prompt_cap = tok["msgs"], tok["heads"], tok["work"], tok["prompt_cap"]
+        now = time.time_ns()
+        if work:
+            pipe = self.gpu_pipeline()
+            res = pipe.collect(tok["pend"])
             self.stats["gpu_batches"] += 1
             self.stats["gpu_messages"] += len(work)
             self.stats["last_gpu_ms"] = res.elapsed_ms

@@ -156,3 +156,33 @@ def test_overload_expiry_and_adaptive_lifo_on_gpu():
     assert gw.counters["expired"] == 16 and dlq.size() == 16
     assert all(m.status == "timeout" and not m.dispatched_at for m in msgs[:16])
     assert gw.counters["completed"] == 48
+
+
+def test_async_ingest_matches_sync():
+    """Overlapped ingest (launch the preprocess batch, enqueue when its
+    kernels finished) produces exactly the synchronous path's messages."""
+    from llm_message_queue_amd.backend.engine import BackendEngine
+    from llm_message_queue_amd.gateway.router import Gateway
+    from llm_message_queue_amd.gateway.workload import Workload
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.utils.config import default_config
+    cfg = default_config()
+    cfg.queue.enable_metrics = False
+    outs = []
+    for mode in ("sync", "async"):
+        eng = BackendEngine(LlamaConfig.tiny(), slots=8, max_ctx=64, token_budget=128, device="cuda:0", impl="hip")
+        gw = Gateway(cfg, engine=eng, use_gpu_preprocess=True, prompt_cap=16, gen_tokens=2)
+        msgs = Workload(seed=9).make(200)
+        gw.submit(msgs)
+        if mode == "sync":
+            gw.ingest()
+        else:
+            assert gw.ingest_async() and gw.preprocessing() == 200 and gw.pending() == 0
+            t0 = time.time()
+            while gw.preprocessing() and time.time() - t0 < 10:
+                gw.ingest_async()
+        assert gw.pending() == 200
+        outs.append([(m.priority, m.queue_name, m.metadata.get("word_count"), m.metadata.get("sentiment"),
+                      m.metadata.get("contains_question"), m.metadata.get("ml_priority"),
+                      tuple(int(x) for x in m.prompt_ids)) for m in msgs])
+    assert outs[0] == outs[1]
