@@ -302,4 +302,16 @@ class Preprocessor:
                     m.created_at = now
                 m.updated_at = now
                 heads[i] = None                     # finished
+        # messages the kernels never saw: empty content (the oracle's
+        # metadata-priority / default rule) and user-decided heads
+        for i, h in enumerate(heads):
+            if h is None:
+                continue
+            m = msgs[i]
+            if h:
+                original = m.priority
+                m.priority = self._analyze_priority_cpu(m)
+                if m.priority != original:
+                    m.metadata["priority_reason"] = "content_keywords"
+            self._finish(m, now)
         return msgs
