@@ -1,0 +1,123 @@
+"""A/B of the hand-written gfx950 GEMMs against hipBLASLt (F.linear).
+
+  python bench/gemm_fused.py [--rounds 7] [--tokens 37,1024,2048,4041,4096]
+
+* swiglu: F.linear(x, W_gu) + silu_mul (the model's unfused MLP front half)
+  vs gemm_swiglu(x, W_perm) (one launch, SwiGLU epilogue).
+* plain:  F.linear(x, W) vs gemm(x, W) for the qkv / o / gate_up / down shapes.
+
+Numerics against an fp32 reference are printed first.  Timings are
+interleaved rounds in one process (median of per-round means), random
+normal activations and std-0.02 weights as in the model.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+import torch.nn.functional as F
+
+from llm_message_queue_amd.ops import gemm as G
+from llm_message_queue_amd.ops.llama_ops import HipOps
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--tokens", default="37,1024,2048,4041,4096")
+    ap.add_argument("--plain", action="store_true", help="also time the plain GEMM shapes")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    d, ffn = 4096, 14336
+    ops = HipOps()
+    w_gu = (torch.randn(2 * ffn, d, device=dev) * 0.02).to(torch.bfloat16)
+    w_perm = G.swiglu_permute(w_gu)
+
+    # ---- numerics
+    for T in (1, 37, 300, 4041):
+        x = torch.randn(T, d, device=dev).to(torch.bfloat16)
+        ref = G.swiglu_reference(x, w_gu).float()
+        fused = G.gemm_swiglu(x, w_perm).float()
+        unf = ops.silu_mul(F.linear(x, w_gu)).float()
+        plain = G.gemm(x, w_gu).float()
+        pref = (x.float() @ w_gu.float().t())
+        scale = ref.abs().max().item()
+        print(json.dumps({"check": "numerics", "T": T,
+                          "fused_max_err": (fused - ref).abs().max().item(),
+                          "unfused_max_err": (unf - ref).abs().max().item(),
+                          "ref_absmax": scale,
+                          "plain_max_err": (plain - pref).abs().max().item(),
+                          "plain_ref_absmax": pref.abs().max().item()}), flush=True)
+
+    # ---- swiglu timing
+    for T in [int(t) for t in a.tokens.split(",")]:
+        x = torch.randn(T, d, device=dev).to(torch.bfloat16)
+        out = torch.empty(T, ffn, dtype=torch.bfloat16, device=dev)
+
+        def unfused():
+            ops.silu_mul(F.linear(x, w_gu), out=out)
+
+        def fused():
+            G.gemm_swiglu(x, w_perm, out=out)
+
+        def blas_only():
+            F.linear(x, w_gu)
+
+        fns = {"hipblaslt+silu_mul": unfused, "fused": fused, "hipblaslt_gemm_only": blas_only}
+        for f in fns.values():
+            f()
+        torch.cuda.synchronize()
+        res = {k: [] for k in fns}
+        for _ in range(a.rounds):
+            for k, f in fns.items():
+                res[k].append(timeit(f, a.iters))
+        med = {k: statistics.median(v) for k, v in res.items()}
+        flop = 2.0 * T * 2 * ffn * d
+        print(json.dumps({"bench": "swiglu", "T": T, **{k + "_ms": round(v, 4) for k, v in med.items()},
+                          "fused_tflops": round(flop / med["fused"] / 1e9, 1),
+                          "blas_tflops": round(flop / med["hipblaslt_gemm_only"] / 1e9, 1),
+                          "speedup_vs_unfused": round(med["hipblaslt+silu_mul"] / med["fused"], 3)}), flush=True)
+
+    if a.plain:
+        shapes = {"qkv": (6144, d), "o": (d, d), "gate_up": (2 * ffn, d), "down": (d, ffn)}
+        for name, (N, K) in shapes.items():
+            w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+            for T in (4041, 4096):
+                x = torch.randn(T, K, device=dev).to(torch.bfloat16)
+                y = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
+                fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "hip": lambda: G.gemm(x, w, out=y),
+                       "hip_r1sched": lambda: G._launch(x, w, y, G.EPI_STORE + 16),
+                       "hip_nostagger": lambda: G._launch(x, w, y, G.EPI_STORE + 32)}
+                for f in fns.values():
+                    f()
+                res = {k: [] for k in fns}
+                for _ in range(a.rounds):
+                    for k, f in fns.items():
+                        res[k].append(timeit(f, a.iters))
+                med = {k: statistics.median(v) for k, v in res.items()}
+                flop = 2.0 * T * N * K
+                print(json.dumps({"bench": "plain", "gemm": name, "T": T,
+                                  **{k + "_ms": round(v, 4) for k, v in med.items()},
+                                  **{k + "_tflops": round(flop / v / 1e9, 1) for k, v in med.items()}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,429 @@
+// Hand-written gfx950 bf16 GEMM for the backend's MLP: C = A · Wᵀ with
+// A [M][K] and W [N][K] both K-contiguous (the layout F.linear feeds
+// hipBLASLt), fp32 accumulation on v_mfma_f32_16x16x32_bf16, and three
+// epilogues:
+//
+//   GM_EPI_STORE   C[M][N] = A·Wᵀ                         (bf16)
+//   GM_EPI_SWIGLU  H[M][N/2] = silu(A·Wgᵀ) * (A·Wuᵀ)       (Llama gate/up)
+//
+// The SwiGLU form removes the separate silu_mul pass and the HBM round trip
+// of the [M][2F] gate/up product (profiles/r1_gemm_experiments.md): W rows are
+// pre-permuted (`swiglu_permute` in ops/gemm.py) so that each wave's 64
+// output columns are 32 gate features followed by the same 32 up features,
+// i.e. every lane holds g and u of one (row, feature) in the same register
+// slot of two accumulators -- the epilogue is pure register math.
+//
+// Structure (cdna_hip_programming.md §5, "the 256² 8-phase template"):
+//   * 256x256 output tile, BK = 64, 512 threads = 8 waves as 2 (M) x 4 (N),
+//     128x64 outputs per wave = 32 16x16 fp32 accumulators (128 AGPR/VGPR).
+//   * LDS 128 KiB = 2 K-tile buffers x {A0, A1, B0, B1} half-tiles of 128
+//     rows x 128 B.  A half h holds the rows of m-half h of BOTH wave rows,
+//     B half h the columns of n-half h of all four wave columns, so each
+//     half-tile is consumed in exactly one quadrant phase and can be
+//     restaged as soon as that phase's reads retire.
+//   * Staging by buffer_load_dwordx4 ... lds (16 B per lane, lane-linear LDS
+//     image; fixed per-lane VGPR offset + scalar K offset, no VALU per load); the bank swizzle p = c ^ ((row >> 1) & 7) on the 16-B chunk is
+//     applied to the per-lane SOURCE address and to the ds_read address
+//     (rule 21), which makes the 16 x b128 fragment reads conflict-free
+//     across the ds_read_b128 lane groups of the 128-B-row image.
+//   * 8 phases per 2 K-tiles: each phase reads one operand half, issues one
+//     half-tile prefetch (2 glds per lane), barrier, 16 MFMAs (one quadrant x
+//     K = 64), barrier.  The prefetch runs 3 half-tiles ahead; a counted
+//     `s_waitcnt vmcnt(6)` at phases 4 and 8 (never 0 in the steady state)
+//     retires exactly the buffer the next phase reads, and raw s_barrier is
+//     used throughout so no wait drains the DMA queue early.
+//   * XCD-aware block order: blocks that the dispatcher puts on one XCD take
+//     a contiguous run of tiles, grouped 8 M-tiles x N so concurrently
+//     running tiles share A and W panels in that XCD's L2.
+//   * M need not be a multiple of 256: A rows are clamped on load, rows >= M
+//     are not stored.  K % 64 == 0 and N % 256 == 0 are checked by the host.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace llmq {
+
+typedef __attribute__((ext_vector_type(8))) short gm_bf16x8;
+typedef __attribute__((ext_vector_type(4))) float gm_f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int gm_u32x4;
+
+constexpr int GM_BM = 256, GM_BN = 256, GM_BK = 64, GM_THREADS = 512;
+constexpr int GM_HALF_BYTES = 128 * GM_BK * 2;     // 16 KiB
+constexpr int GM_BUF_BYTES = 4 * GM_HALF_BYTES;    // A0 A1 B0 B1
+constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
+constexpr int GM_GROUP_M = 8;
+
+enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2 };
+enum { GM_A0 = 0, GM_A1 = 1, GM_B0 = 2, GM_B1 = 3 };
+
+__device__ __forceinline__ uint16_t gm_f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);                 // round to nearest even (finite inputs)
+  return (uint16_t)(u >> 16);
+}
+
+typedef __attribute__((address_space(3))) void* gm_lds_ptr;
+
+// One half-tile (128 rows x 64 bf16) global -> LDS: 2 buffer_load ... lds per
+// lane.  The per-lane row/chunk offset is a fixed VGPR, the K-tile offset a
+// scalar (soffset), so the K-loop spends no VALU on staging addresses.
+__device__ __forceinline__ void gm_stage(__amdgpu_buffer_rsrc_t rs, uint32_t v0, uint32_t v1, uint32_t soff,
+                                         uint8_t* smem, uint32_t dst0, uint32_t dst1) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (gm_lds_ptr)(smem + dst0), 16, v0, soff, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (gm_lds_ptr)(smem + dst1), 16, v1, soff, 0, 0);
+}
+
+#define GM_FENCE() __builtin_amdgcn_sched_barrier(0)
+#define GM_BARRIER()                  \
+  do {                                \
+    GM_FENCE();                       \
+    __builtin_amdgcn_s_barrier();     \
+    GM_FENCE();                       \
+  } while (0)
+
+template <int EPI, bool STAGGER = true, int SCHED = 1>
+__global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
+    int M, int N, int K) {
+  extern __shared__ __align__(16) uint8_t smem[];
+
+  const int tiles_m = (M + GM_BM - 1) / GM_BM;
+  const int tiles_n = N / GM_BN;
+  const int nwg = tiles_m * tiles_n;
+  // XCD-contiguous remap (bijective for any nwg), then 8-M-tile grouping
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int pid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int group = pid / (GM_GROUP_M * tiles_n);
+  const int first_m = group * GM_GROUP_M;
+  const int gsize = min(tiles_m - first_m, GM_GROUP_M);
+  const int tm = first_m + (pid % (GM_GROUP_M * tiles_n)) % gsize;
+  const int tn = (pid % (GM_GROUP_M * tiles_n)) / gsize;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  // ---- staging sources: half h, instruction i -> LDS local row lr = i*64 + w*8 + lane/8
+  const int srow = w * 8 + (lane >> 3);            // 0..63
+  const int schunk = (lane & 7) ^ ((srow >> 1) & 7);   // source chunk for LDS slot lane&7
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, M * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, N * K * 2, 0x00020000);
+  uint32_t va[2][2], vb[2][2];                     // byte offsets (row, chunk) of K-tile 0
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int row = tm * GM_BM + i * 128 + h * 64 + srow;
+      row = row < M ? row : M - 1;
+      va[h][i] = (uint32_t)row * (uint32_t)K * 2u + (uint32_t)schunk * 16u;
+      const int col = tn * GM_BN + (2 * i + (w >> 2)) * 64 + h * 32 + (w & 3) * 8 + (lane >> 3);
+      vb[h][i] = (uint32_t)col * (uint32_t)K * 2u + (uint32_t)schunk * 16u;
+    }
+  }
+  // LDS destination (wave-uniform) of instruction i inside a half-tile
+  const uint32_t dst_i0 = (uint32_t)(w * 8) * 128u;
+  const uint32_t dst_i1 = (uint32_t)(64 + w * 8) * 128u;
+
+  // ---- fragment read offsets (bytes inside a half-tile), per k-step kk
+  const int fr = lane & 15, fq = lane >> 4;
+  uint32_t aoff[2][2], boff[2][2];                 // [buffer][kk]; buffer 1 = +64 KiB (beyond ds offset:)
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int c = fq + 4 * kk;
+    aoff[0][kk] = (uint32_t)(wr * 64 + fr) * 128u + (uint32_t)((c ^ ((fr >> 1) & 7)) * 16);
+    boff[0][kk] = (uint32_t)(wc * 32 + fr) * 128u + (uint32_t)((c ^ ((fr >> 1) & 7)) * 16) + 2 * GM_HALF_BYTES;
+    aoff[1][kk] = aoff[0][kk] + GM_BUF_BYTES;
+    boff[1][kk] = boff[0][kk] + GM_BUF_BYTES;
+  }
+
+  gm_f32x4 acc[2][4][2][2];                        // [mh][m][nh][n]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) acc[a][b][c][d] = gm_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  gm_bf16x8 af[4][2];                              // one m-half: [m][kk]
+  gm_bf16x8 bfr[2][2][2];                          // both n-halves: [nh][n][kk]
+  gm_bf16x8 b0y[2][2];                             // SCHED 1: buffer-1 B0 fragments
+
+#define GM_STAGE(BUF, HALF, KT)                                                               \
+  do {                                                                                        \
+    const uint32_t _ko = (uint32_t)(KT) * (GM_BK * 2);                                        \
+    const uint32_t _b = (uint32_t)(BUF) * GM_BUF_BYTES + (uint32_t)(HALF) * GM_HALF_BYTES;   \
+    if constexpr ((HALF) < 2)                                                                 \
+      gm_stage(rsa, va[(HALF)][0], va[(HALF)][1], _ko, smem, _b + dst_i0, _b + dst_i1);       \
+    else                                                                                      \
+      gm_stage(rsw, vb[(HALF)-2][0], vb[(HALF)-2][1], _ko, smem, _b + dst_i0, _b + dst_i1);   \
+  } while (0)
+
+#define GM_READ_A(BUF, MH)                                                                     \
+  do {                                                                                         \
+    _Pragma("unroll") for (int m = 0; m < 4; ++m)                                              \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
+        af[m][kk] = *reinterpret_cast<const gm_bf16x8*>(smem + aoff[BUF][kk] + (MH) * GM_HALF_BYTES + m * 2048); \
+  } while (0)
+
+#define GM_READ_B(BUF, NH)                                                                     \
+  do {                                                                                         \
+    _Pragma("unroll") for (int n = 0; n < 2; ++n)                                              \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
+        bfr[NH][n][kk] = *reinterpret_cast<const gm_bf16x8*>(smem + boff[BUF][kk] + (NH) * GM_HALF_BYTES + n * 2048); \
+  } while (0)
+
+#define GM_MFMA(MH, NH)                                                                        \
+  do {                                                                                         \
+    __builtin_amdgcn_s_setprio(1);                                                             \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                           \
+      _Pragma("unroll") for (int m = 0; m < 4; ++m)                                            \
+        _Pragma("unroll") for (int n = 0; n < 2; ++n)                                          \
+          acc[MH][m][NH][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], bfr[NH][n][kk], \
+                                                                      acc[MH][m][NH][n], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                             \
+  } while (0)
+
+// SCHED 1 helpers: B0 fragments into an explicit register set, MFMA with it
+#define GM_READ_B0_INTO(BUF, DST)                                                              \
+  do {                                                                                         \
+    _Pragma("unroll") for (int n = 0; n < 2; ++n)                                              \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                         \
+        DST[n][kk] = *reinterpret_cast<const gm_bf16x8*>(smem + boff[BUF][kk] + n * 2048);     \
+  } while (0)
+
+#define GM_MFMA_WITH(MH, NH, BREG)                                                             \
+  do {                                                                                         \
+    __builtin_amdgcn_s_setprio(1);                                                             \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                           \
+      _Pragma("unroll") for (int m = 0; m < 4; ++m)                                            \
+        _Pragma("unroll") for (int n = 0; n < 2; ++n)                                          \
+          acc[MH][m][NH][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], BREG[n][kk],  \
+                                                                      acc[MH][m][NH][n], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                             \
+  } while (0)
+
+#define GM_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define GM_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
+
+  const int nt = K / GM_BK;                        // even (K % 128 == 0 checked by host)
+
+  if constexpr (SCHED == 1) {
+    // Balanced schedule: every phase retires the half-tile staged 3 phases
+    // earlier (vmcnt(6) each phase), so the NEXT buffer's B0 fragments can be
+    // read one phase early (phases 4 and 8, which otherwise read nothing):
+    // 8/4/8/4 fragment reads per phase instead of 12/4/8/0.  Stage order per
+    // buffer is B0, A0, B1, A1; every restage is >= 2 phases after the
+    // half-tile's last read (safe with the wave-row stagger).
+    GM_STAGE(0, GM_B0, 0);
+    GM_STAGE(0, GM_A0, 0);
+    GM_STAGE(0, GM_B1, 0);
+    GM_STAGE(0, GM_A1, 0);
+    GM_STAGE(1, GM_B0, 1);
+    GM_STAGE(1, GM_A0, 1);
+    GM_STAGE(1, GM_B1, 1);
+    GM_VMCNT(6);
+    GM_BARRIER();
+    GM_READ_B0_INTO(0, bfr[0]);
+    if (STAGGER && wr == 1) GM_BARRIER();
+
+#define GM_PHASE_END(MH, NH, BREG) \
+  do {                             \
+    GM_BARRIER();                  \
+    GM_LGKM(0);                    \
+    GM_MFMA_WITH(MH, NH, BREG);    \
+    GM_BARRIER();                  \
+  } while (0)
+
+    int t = 0;
+    for (; t < nt - 2; t += 2) {
+      {
+        GM_READ_A(0, 0); GM_STAGE(1, GM_A1, t + 1); GM_VMCNT(6); GM_PHASE_END(0, 0, bfr[0]);
+        GM_READ_B(0, 1); GM_STAGE(0, GM_B0, t + 2); GM_VMCNT(6); GM_PHASE_END(0, 1, bfr[1]);
+        GM_READ_A(0, 1); GM_STAGE(0, GM_A0, t + 2); GM_VMCNT(6); GM_PHASE_END(1, 1, bfr[1]);
+        GM_READ_B0_INTO(1, b0y); GM_STAGE(0, GM_B1, t + 2); GM_VMCNT(6); GM_PHASE_END(1, 0, bfr[0]);
+        GM_READ_A(1, 0); GM_STAGE(0, GM_A1, t + 2); GM_VMCNT(6); GM_PHASE_END(0, 0, b0y);
+        GM_READ_B(1, 1); GM_STAGE(1, GM_B0, t + 3); GM_VMCNT(6); GM_PHASE_END(0, 1, bfr[1]);
+        GM_READ_A(1, 1); GM_STAGE(1, GM_A0, t + 3); GM_VMCNT(6); GM_PHASE_END(1, 1, bfr[1]);
+        GM_READ_B0_INTO(0, bfr[0]); GM_STAGE(1, GM_B1, t + 3); GM_VMCNT(6); GM_PHASE_END(1, 0, b0y);
+      }
+    }
+    {                                              // last two K-tiles: drain
+        GM_READ_A(0, 0); GM_STAGE(1, GM_A1, t + 1); GM_VMCNT(6); GM_PHASE_END(0, 0, bfr[0]);
+        GM_READ_B(0, 1); GM_VMCNT(4); GM_PHASE_END(0, 1, bfr[1]);
+        GM_READ_A(0, 1); GM_VMCNT(2); GM_PHASE_END(1, 1, bfr[1]);
+        GM_READ_B0_INTO(1, b0y); GM_VMCNT(0); GM_PHASE_END(1, 0, bfr[0]);
+        GM_READ_A(1, 0); GM_PHASE_END(0, 0, b0y);
+        GM_READ_B(1, 1); GM_PHASE_END(0, 1, bfr[1]);
+        GM_READ_A(1, 1); GM_PHASE_END(1, 1, bfr[1]);
+        GM_PHASE_END(1, 0, b0y);
+    }
+#undef GM_PHASE_END
+  } else {
+    // prologue: tile 0 -> buffer 0 (all halves), tile 1 -> buffer 1 (B0, A0, B1)
+    GM_STAGE(0, GM_A0, 0);
+    GM_STAGE(0, GM_A1, 0);
+    GM_STAGE(0, GM_B0, 0);
+    GM_STAGE(0, GM_B1, 0);
+    GM_STAGE(1, GM_B0, 1);
+    GM_STAGE(1, GM_A0, 1);
+    GM_STAGE(1, GM_B1, 1);
+    GM_VMCNT(6);
+    GM_BARRIER();
+    // wave-row 1 runs half a phase behind wave-row 0: on every SIMD (one wave
+    // of each row) one wave's fragment reads + DMA issue overlap the other's
+    // MFMA cluster.  One extra barrier here, balanced after the loop.
+    if (STAGGER && wr == 1) GM_BARRIER();
+
+    for (int t = 0; t < nt; t += 2) {
+      const bool more = t + 2 < nt;                  // wave-uniform
+      // ---- phase 1: buffer 0 quadrant (0,0); stage buffer 1 A1 (tile t+1)
+      GM_READ_B(0, 0);
+      GM_FENCE();
+      GM_READ_A(0, 0);
+      GM_STAGE(1, GM_A1, t + 1);
+      GM_LGKM(8);
+      GM_BARRIER();
+      GM_LGKM(0);
+      GM_MFMA(0, 0);
+      GM_BARRIER();
+      // ---- phase 2: quadrant (0,1); stage buffer 0 B0 (tile t+2)
+      GM_READ_B(0, 1);
+      if (more) GM_STAGE(0, GM_B0, t + 2);
+      GM_BARRIER();
+      GM_LGKM(0);
+      GM_MFMA(0, 1);
+      GM_BARRIER();
+      // ---- phase 3: quadrant (1,1); stage buffer 0 A0
+      GM_READ_A(0, 1);
+      if (more) GM_STAGE(0, GM_A0, t + 2);
+      GM_BARRIER();
+      GM_LGKM(0);
+      GM_MFMA(1, 1);
+      GM_BARRIER();
+      // ---- phase 4: quadrant (1,0); stage buffer 0 B1; retire buffer 1
+      if (more) {
+        GM_STAGE(0, GM_B1, t + 2);
+        GM_VMCNT(6);
+      } else {
+        GM_VMCNT(0);
+      }
+      GM_BARRIER();
+      GM_MFMA(1, 0);
+      GM_BARRIER();
+      // ---- phase 5: buffer 1 quadrant (0,0); stage buffer 0 A1
+      GM_READ_B(1, 0);
+      GM_FENCE();
+      GM_READ_A(1, 0);
+      if (more) GM_STAGE(0, GM_A1, t + 2);
+      GM_LGKM(8);
+      GM_BARRIER();
+      GM_LGKM(0);
+      GM_MFMA(0, 0);
+      GM_BARRIER();
+      // ---- phase 6: quadrant (0,1); stage buffer 1 B0 (tile t+3)
+      GM_READ_B(1, 1);
+      if (more) GM_STAGE(1, GM_B0, t + 3);
+      GM_BARRIER();
+      GM_LGKM(0);
+      GM_MFMA(0, 1);
+      GM_BARRIER();
+      // ---- phase 7: quadrant (1,1); stage buffer 1 A0
+      GM_READ_A(1, 1);
+      if (more) GM_STAGE(1, GM_A0, t + 3);
+      GM_BARRIER();
+      GM_LGKM(0);
+      GM_MFMA(1, 1);
+      GM_BARRIER();
+      // ---- phase 8: quadrant (1,0); stage buffer 1 B1; retire buffer 0
+      if (more) {
+        GM_STAGE(1, GM_B1, t + 3);
+        GM_VMCNT(6);
+      }
+      GM_BARRIER();
+      GM_MFMA(1, 0);
+      GM_BARRIER();
+    }
+  }
+
+#undef GM_STAGE
+#undef GM_READ_A
+#undef GM_READ_B
+#undef GM_MFMA
+#undef GM_READ_B0_INTO
+#undef GM_MFMA_WITH
+
+  if (STAGGER && wr == 0) GM_BARRIER();
+
+  // ---- epilogue through LDS (the staging buffers are free after the last barrier)
+  const int row0 = tm * GM_BM + wr * 128;          // first output row of this wave
+  if (EPI == GM_EPI_SWIGLU) {
+    // wave w: 128 rows x 32 features bf16 = 8 KiB at w * 8 KiB
+    uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 8192);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float g = acc[mh][m][0][n][j];
+            const float u = acc[mh][m][1][n][j];
+            const float s = g / (1.0f + __expf(-g));
+            o[(mh * 64 + m * 16 + fq * 4 + j) * 32 + n * 16 + fr] = gm_f2bf(s * u);
+          }
+    GM_LGKM(0);
+    __builtin_amdgcn_wave_barrier();
+    const int F = N >> 1;
+    const int col0 = tn * (GM_BN / 2) + wc * 32;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int qd = it * 64 + lane;               // 16-B chunk: row qd/4, chunk qd%4
+      const int r = qd >> 2, cb = qd & 3;
+      const int grow = row0 + r;
+      const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(smem + w * 8192 + r * 64 + cb * 16);
+      if (grow < M) *reinterpret_cast<gm_u32x4*>(C + (int64_t)grow * F + col0 + cb * 8) = v;
+    }
+  } else {
+    // wave w: 128 rows x 64 columns bf16 = 16 KiB at w * 16 KiB
+    uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 16384);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              o[(mh * 64 + m * 16 + fq * 4 + j) * 64 + nh * 32 + n * 16 + fr] = gm_f2bf(acc[mh][m][nh][n][j]);
+    GM_LGKM(0);
+    __builtin_amdgcn_wave_barrier();
+    const int col0 = tn * GM_BN + wc * 64;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int qd = it * 64 + lane;               // row qd/8, chunk qd%8
+      const int r = qd >> 3, cb = qd & 7;
+      const int grow = row0 + r;
+      const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(smem + w * 16384 + r * 128 + cb * 16);
+      if (grow < M) {
+        uint16_t* dst = C + (int64_t)grow * N + col0 + cb * 8;
+        *reinterpret_cast<gm_u32x4*>(dst) = v;
+      }
+    }
+  }
+}
+
+
+#undef GM_LGKM
+#undef GM_VMCNT
+#undef GM_BARRIER
+#undef GM_FENCE
+
+}  // namespace llmq

@@ -15,6 +15,7 @@
 #include <string>
 
 #include "classify_kernels.h"
+#include "gemm_kernels.h"
 #include "llama_kernels.h"
 #include "summarise_kernels.h"
 #include "text_kernels.h"
@@ -128,12 +129,48 @@ static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T,
   check_launch();
 }
 
-static void silu_mul(uintptr_t gu, uintptr_t out, int T, int F, uintptr_t stream) {
+// C = A · Wᵀ (epi 0, C [M][N]) or H = silu(A·Wgᵀ) * (A·Wuᵀ) over a
+// swiglu-permuted W (epi 2, C [M][N/2]); A [M][K], W [N][K], bf16.
+template <int EPI, bool STAGGER = true, int SCHED = 1>
+static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, GM_LDS_BYTES));
+    attr = true;
+  }
+  const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c, M, N, K);
+}
+
+// epi: 0 / 2 = store / SwiGLU; 16 / 32 = store with the round-1 phase
+// schedule / without the wave-row stagger (A/B measurements only).
+static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t stream) {
+  require(M > 0 && N > 0 && K > 0, "gemm: empty operand");
+  require(N % GM_BN == 0, "gemm: N must be a multiple of 256");
+  require(K % (2 * GM_BK) == 0, "gemm: K must be a multiple of 128");
+  require((int64_t)M * K < (int64_t)1 << 30 && (int64_t)N * K < (int64_t)1 << 30, "gemm: operand too large (2 GiB buffer descriptors)");
+  require(a % 16 == 0 && w % 16 == 0 && c % 16 == 0, "gemm: pointers must be 16-byte aligned");
+  if (epi == GM_EPI_STORE)
+    launch_gemm<GM_EPI_STORE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+  else if (epi == GM_EPI_SWIGLU)
+    launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+  else if (epi == GM_EPI_STORE + 16)
+    launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+  else if (epi == GM_EPI_STORE + 32)
+    launch_gemm<GM_EPI_STORE, false, 1>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+  else
+    throw std::invalid_argument("gemm: unknown epilogue");
+  check_launch();
+}
+
+static void silu_mul(uintptr_t gu, uintptr_t out, int T, int F, uintptr_t stream, bool perm) {
   require(F % 8 == 0, "F must be a multiple of 8");
+  require(!perm || F % 128 == 0, "permuted silu_mul needs F % 128 == 0");
   const int64_t total = (int64_t)T * F / 8;
   if (total == 0) return;
   hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(stream),
-                     P<const uint16_t>(gu), P<uint16_t>(out), T, F);
+                     P<const uint16_t>(gu), P<uint16_t>(out), T, F, perm ? 1 : 0);
   check_launch();
 }
 
@@ -257,7 +294,11 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("summarise_project", &summarise_project);
   m.def("salient_topk", &salient_topk);
   m.def("rmsnorm", &rmsnorm);
-  m.def("silu_mul", &silu_mul);
+  m.def("silu_mul", &silu_mul, py::arg("gu"), py::arg("out"), py::arg("T"), py::arg("F"), py::arg("stream"),
+        py::arg("perm") = false);
+  m.def("gemm_bf16", &gemm_bf16);
+  m.attr("GEMM_EPI_STORE") = (int)GM_EPI_STORE;
+  m.attr("GEMM_EPI_SWIGLU") = (int)GM_EPI_SWIGLU;
   m.def("rope_kv", &rope_kv);
   m.def("attention", &attention);
   m.def("attention_tiles", &attention_tiles);

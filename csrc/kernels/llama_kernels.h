@@ -95,14 +95,19 @@ rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ res, const
 
 // out[t, i] = silu(gu[t, i]) * gu[t, F + i], 8 elements per thread.
 __global__ void __launch_bounds__(256)
-silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out, int T, int F) {
+silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out, int T, int F, int perm) {
   const int64_t idx = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   const int64_t total = (int64_t)T * F;
   if (idx >= total) return;
   const int64_t t = idx / F;
   const int64_t i = idx % F;
-  const u16x8 g = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + i);
-  const u16x8 u = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + F + i);
+  // perm: gu columns in the fused GEMM's swiglu order (ops/gemm.py
+  // swiglu_perm_index, half = 32): feature i sits at column
+  // (i/128)*256 + ((i%128)/32)*64 + i%32, its up value 32 columns later.
+  const int64_t gc = perm ? (i >> 7) * 256 + ((i & 127) >> 5) * 64 + (i & 31) : i;
+  const int64_t uc = perm ? gc + 32 : F + i;
+  const u16x8 g = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + gc);
+  const u16x8 u = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + uc);
   u16x8 o;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {

@@ -10,7 +10,11 @@ decode tokens mixed).  GEMMs: ``torch.nn.functional.linear`` (hipBLASLt).
 The o / down projections accumulate into the residual stream in the GEMM
 epilogue (beta = 1).  Everything else: hand-written HIP kernels
 (``ops.llama_ops.HipOps``): RMSNorm (optionally fused with the residual add), RoPE + KV-cache write, segment-tiled MFMA GQA attention
-over the slot KV cache (prefill chunks and decode tokens), SiLU*up.
+over the slot KV cache (prefill chunks and decode tokens), SiLU*up -- and,
+with ``fused_mlp`` (default with the HIP ops), the hand-written gfx950 GEMM
+with the SwiGLU epilogue for the gate/up projection (``ops.gemm``): the
+[T][2F] gate/up product never reaches HBM and the silu_mul pass disappears
+(``profiles/r2_gemm_swiglu.md``).
 """
 from __future__ import annotations
 
@@ -63,7 +67,8 @@ class LlamaConfig:
 
 class LlamaStub:
     def __init__(self, cfg: LlamaConfig, slots: int, max_ctx: int, device="cuda", impl: str = "hip",
-                 seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False):
+                 seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False,
+                 fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -86,6 +91,11 @@ class LlamaStub:
         # (profiles/r1_gemm_experiments.md), so it is off by default.  The
         # weight stays one tensor; its row slices are contiguous views.
         self.split_qkv = split_qkv
+        # gate/up weight kept in the fused kernel's swiglu row order (same
+        # random draw, rows permuted once at init) so the HIP path runs
+        # gemm_swiglu on steps of >= min_fused_tokens rows
+        self.fused_mlp = (impl == "hip") if fused_mlp is None else bool(fused_mlp)
+        self.min_fused_tokens = int(min_fused_tokens)
         g = torch.Generator(device=self.device).manual_seed(seed)
         std = 0.02
 
@@ -103,7 +113,7 @@ class LlamaStub:
                 "wqkv": w((hq + 2 * hkv) * hd, d),
                 "wo": w(d, hq * hd),
                 "mlp_norm": torch.ones(d, dtype=dtype, device=self.device),
-                "w_gu": w(2 * cfg.ffn, d),
+                "w_gu": self._gu_layout(w(2 * cfg.ffn, d)),
                 "w_down": w(d, cfg.ffn),
             })
         # KV cache: per layer [slots, kv_heads, max_ctx, head_dim]
@@ -113,6 +123,12 @@ class LlamaStub:
                        for _ in range(cfg.layers)]
         self.cos, self.sin = rope_tables(max_ctx, cfg.rope_theta, self.device)
         self.scale = 1.0 / math.sqrt(hd)
+
+    def _gu_layout(self, w_gu: torch.Tensor) -> torch.Tensor:
+        if not self.fused_mlp:
+            return w_gu
+        from ..ops.gemm import swiglu_permute
+        return swiglu_permute(w_gu)
 
     def weight_bytes(self) -> int:
         n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
@@ -172,8 +188,7 @@ class LlamaStub:
                 x2 = ops.rmsnorm(res, L["mlp_norm"], cfg.eps)
             else:
                 x2 = ops.rmsnorm(F.linear(a, L["wo"]), L["mlp_norm"], cfg.eps, residual=res)
-            gu = F.linear(x2, L["w_gu"])
-            act = ops.silu_mul(gu)
+            act = ops.mlp_up(x2, L["w_gu"], self.fused_mlp, self.min_fused_tokens)
             if fused:
                 res.addmm_(act, L["w_down"].t())
             else:

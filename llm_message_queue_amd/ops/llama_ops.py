@@ -48,13 +48,27 @@ class HipOps:
                        y.data_ptr(), T, D, float(eps), _stream(x))
         return y
 
-    def silu_mul(self, gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def silu_mul(self, gu: torch.Tensor, out: Optional[torch.Tensor] = None, perm: bool = False) -> torch.Tensor:
+        """silu(gate) * up; ``perm``: ``gu`` columns are in the fused GEMM's
+        swiglu order (``ops.gemm.swiglu_perm_index``) instead of [gate | up]."""
         _check(gu, torch.bfloat16, "gu")
         T, F2 = gu.shape
         F = F2 // 2
         y = out if out is not None else torch.empty((T, F), dtype=gu.dtype, device=gu.device)
-        self.k.silu_mul(gu.data_ptr(), y.data_ptr(), T, F, _stream(gu))
+        self.k.silu_mul(gu.data_ptr(), y.data_ptr(), T, F, _stream(gu), perm)
         return y
+
+    def mlp_up(self, x: torch.Tensor, w_gu: torch.Tensor, fused: bool, min_fused_tokens: int) -> torch.Tensor:
+        """silu(x·Wgᵀ) * (x·Wuᵀ).  ``fused``: ``w_gu`` is in swiglu order and
+        steps of >= ``min_fused_tokens`` rows run the hand-written GEMM with
+        the SwiGLU epilogue (one launch, no [T][2F] intermediate); smaller
+        steps keep hipBLASLt + the permuted silu_mul."""
+        if not fused:
+            return self.silu_mul(torch.nn.functional.linear(x, w_gu))
+        from . import gemm as G
+        if x.shape[0] >= min_fused_tokens and G.supported(x.shape[0], w_gu.shape[0], x.shape[1]):
+            return G.gemm_swiglu(x, w_gu)
+        return self.silu_mul(torch.nn.functional.linear(x, w_gu), perm=True)
 
     def rope_kv(self, qkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, q_out=None):
         _check(qkv, torch.bfloat16, "qkv")
@@ -124,14 +138,24 @@ class RefOps:
             return out
         return y
 
-    def silu_mul(self, gu, out=None):
+    def silu_mul(self, gu, out=None, perm: bool = False):
         F = gu.shape[1] // 2
+        if perm:
+            from .gemm import swiglu_perm_index
+            gu = gu.index_select(1, swiglu_perm_index(F, gu.device).argsort())
         g, u = gu[:, :F].float(), gu[:, F:].float()
         y = (torch.nn.functional.silu(g) * u).to(torch.bfloat16)
         if out is not None:
             out.copy_(y)
             return out
         return y
+
+    def mlp_up(self, x, w_gu, fused: bool, min_fused_tokens: int):
+        """Reference of ``HipOps.mlp_up`` (``w_gu`` in swiglu order if fused)."""
+        if fused:
+            from .gemm import swiglu_unpermute
+            w_gu = swiglu_unpermute(w_gu)
+        return self.silu_mul(torch.nn.functional.linear(x, w_gu))
 
     def rope_kv(self, qkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, q_out=None):
         T = qkv.shape[0]

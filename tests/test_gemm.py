@@ -1,0 +1,149 @@
+"""Hand-written gfx950 GEMM (csrc/kernels/gemm_kernels.h, ops/gemm.py).
+
+CPU: the swiglu weight permutation and the model's fused-MLP reference path.
+GPU: the kernel against fp32 PyTorch references at T in {1, 37, 300, 4096}
+(4096: the serving step), plain and SwiGLU epilogues, the permuted silu_mul,
+and a tiny model forward with the fused MLP against the ref ops.
+"""
+import pytest
+import torch
+
+from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
+from llm_message_queue_amd.ops import gemm as G
+from llm_message_queue_amd.ops.llama_ops import RefOps
+
+
+def test_swiglu_perm_index_is_a_permutation_in_kernel_layout():
+    ffn = 512
+    idx = G.swiglu_perm_index(ffn)
+    assert sorted(idx.tolist()) == list(range(2 * ffn))
+    # in every 256-column tile, each wave's 64 columns = 32 gate then the same 32 up
+    for r in (0, 31, 32, 63, 64, 255, 256, 300, 1023):
+        tn, rem = divmod(r, 256)
+        wc, rem2 = divmod(rem, 64)
+        nh, c = divmod(rem2, 32)
+        f = tn * 128 + wc * 32 + c
+        assert idx[r].item() == (f if nh == 0 else ffn + f)
+
+
+def test_swiglu_permute_roundtrip_and_reference():
+    torch.manual_seed(0)
+    w = torch.randn(2 * 256, 64)
+    wp = G.swiglu_permute(w)
+    assert torch.equal(G.swiglu_unpermute(wp), w)
+    x = torch.randn(5, 64)
+    ref = G.swiglu_reference(x, w).float()
+    # emulate the kernel's epilogue over the permuted product
+    p = x @ wp.t()
+    out = torch.empty(5, 256)
+    for f in range(256):
+        tn, r = divmod(f, 128)
+        wc, c = divmod(r, 32)
+        col = tn * 256 + wc * 64 + c
+        out[:, f] = torch.nn.functional.silu(p[:, col]) * p[:, col + 32]
+    assert torch.allclose(out, ref, atol=1e-5, rtol=1e-5)
+
+
+def test_ref_silu_mul_perm_matches_unpermuted():
+    torch.manual_seed(1)
+    F = 256
+    gu = torch.randn(7, 2 * F).to(torch.bfloat16)
+    idx = G.swiglu_perm_index(F)
+    gu_perm = gu.index_select(1, idx)
+    ops = RefOps()
+    assert torch.equal(ops.silu_mul(gu_perm, perm=True), ops.silu_mul(gu))
+
+
+def test_fused_mlp_model_matches_unfused_on_ref_ops():
+    cfg = LlamaConfig(vocab=512, dim=256, layers=2, heads=2, kv_heads=1, ffn=512)
+    a = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, fused_mlp=True)
+    b = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, fused_mlp=False)
+    assert not torch.equal(a.layers[0]["w_gu"], b.layers[0]["w_gu"])       # stored permuted
+    assert torch.equal(G.swiglu_unpermute(a.layers[0]["w_gu"]), b.layers[0]["w_gu"])
+    tok = torch.randint(0, cfg.vocab, (12,), generator=torch.Generator().manual_seed(0))
+    pos = torch.tensor(list(range(6)) * 2, dtype=torch.int32)
+    slot = torch.tensor([0] * 6 + [1] * 6, dtype=torch.int32)
+    assert torch.equal(a.hidden(tok, pos, slot), b.hidden(tok, pos, slot))
+
+
+def test_gemm_rejects_unsupported_shapes():
+    assert G.supported(37, 512, 256)
+    assert not G.supported(37, 500, 256)
+    assert not G.supported(37, 512, 200)
+    assert not G.supported(0, 512, 256)
+
+
+# ----------------------------------------------------------------------------- GPU
+DEV = "cuda"
+
+
+def _rand(T, K, N, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(T, K, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    return x, w
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 37, 300, 4096])
+def test_gemm_plain_matches_fp32(T):
+    x, w = _rand(T, 4096, 1024, seed=T)
+    ref = x.float() @ w.float().t()
+    out = G.gemm(x, w).float()
+    err = (out - ref).abs().max().item()
+    assert err <= 0.01 * ref.abs().max().item() + 1e-3, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 37, 300, 4096])
+def test_gemm_swiglu_matches_fp32(T):
+    x, w = _rand(T, 4096, 2 * 1536, seed=100 + T)
+    ref = G.swiglu_reference(x, w).float()
+    out = G.gemm_swiglu(x, G.swiglu_permute(w)).float()
+    err = (out - ref).abs().max().item()
+    # one bf16 rounding of the output (the unfused path rounds g and u too)
+    assert err <= 0.01 * ref.abs().max().item() + 1e-3, err
+    assert torch.isfinite(out).all()
+
+
+@pytest.mark.gpu
+def test_gemm_swiglu_rows_past_m_untouched():
+    """M not a multiple of 256: rows >= M of a larger output buffer stay as
+    they were (loads clamp, stores mask)."""
+    x, w = _rand(300, 512, 512, seed=7)
+    big = torch.full((512, 256), 7.0, dtype=torch.bfloat16, device=DEV)
+    G.gemm_swiglu(x, G.swiglu_permute(w), out=big[:300])
+    assert (big[300:] == 7.0).all()
+    ref = G.swiglu_reference(x, w).float()
+    assert (big[:300].float() - ref).abs().max().item() <= 0.01 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.gpu
+def test_silu_mul_perm_matches_ref():
+    from llm_message_queue_amd.ops.llama_ops import HipOps
+    F = 1024
+    g = torch.Generator(device=DEV).manual_seed(3)
+    gu = torch.randn(37, 2 * F, generator=g, device=DEV).to(torch.bfloat16)
+    gu_perm = gu.index_select(1, G.swiglu_perm_index(F, DEV))
+    hip = HipOps().silu_mul(gu_perm, perm=True).float()
+    ref = RefOps().silu_mul(gu).float()
+    assert (hip - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [37, 600])
+def test_tiny_model_fused_mlp_matches_ref(T):
+    """The HIP model with the fused MLP (GEMM+SwiGLU for T >= 512, permuted
+    silu_mul below) against the fp32-reference ops on the same weights."""
+    cfg = LlamaConfig.tiny()
+    hip = LlamaStub(cfg, slots=4, max_ctx=256, device=DEV, impl="hip", seed=3, min_fused_tokens=512)
+    ref = LlamaStub(cfg, slots=4, max_ctx=256, device=DEV, impl="ref", seed=3, residual_in_gemm=True)
+    assert hip.fused_mlp and not ref.fused_mlp
+    n = T // 4
+    tok = torch.randint(0, cfg.vocab, (4 * n,), device=DEV)
+    pos = torch.arange(n, device=DEV, dtype=torch.int32).repeat(4)
+    slot = torch.arange(4, device=DEV, dtype=torch.int32).repeat_interleave(n)
+    ha = hip.hidden(tok, pos, slot).float()
+    hb = ref.hidden(tok, pos, slot).float()
+    rel = (ha - hb).norm() / hb.norm()
+    assert rel < 2e-2, rel.item()
