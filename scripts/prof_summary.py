@@ -15,6 +15,7 @@ import sys
 from collections import defaultdict
 
 CATEGORIES = [
+    ("gemm+swiglu (HIP)", re.compile(r"gemm_bf16_kernel")),
     ("gemm (hipBLASLt)", re.compile(r"^(Custom_)?Cijk_|gemm|Gemm")),
     ("attention (HIP)", re.compile(r"attention|attn")),
     ("rmsnorm (HIP)", re.compile(r"rmsnorm")),
@@ -22,6 +23,7 @@ CATEGORIES = [
     ("rope_kv (HIP)", re.compile(r"rope")),
     ("text/classifier/summary (HIP)", re.compile(r"text_analyze|scan_rows|embed_pool|classify|summarise|salient")),
     ("slot census (HIP)", re.compile(r"census")),
+    ("host link copies (HIP)", re.compile(r"copy_bytes")),
     ("torch elementwise/index", re.compile(r"elementwise|index|gather|scatter|copy|fill|reduce|arange|cat")),
 ]
 
