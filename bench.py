@@ -64,6 +64,8 @@ def parse(argv=None):
     ap.add_argument("--no-classifier", action="store_true")
     ap.add_argument("--no-residual-gemm", action="store_true",
                     help="o/down as F.linear + fused residual-add RMSNorm (default: residual in the GEMM epilogue)")
+    ap.add_argument("--no-fused-qkv", action="store_true",
+                    help="qkv on hipBLASLt + rope_kv instead of the GEMM with the RoPE/KV epilogue (A/B)")
     ap.add_argument("--no-fused-mlp", action="store_true",
                     help="gate/up on hipBLASLt + silu_mul instead of the hand-written SwiGLU GEMM (A/B)")
     ap.add_argument("--split-qkv", action="store_true",
@@ -150,7 +152,8 @@ def main(argv=None) -> int:
                            token_budget=a.token_budget, device=dev, impl="ref" if dry else "hip", seed=1000 + rank,
                            page=page, gpu_index=rank, max_inflight=a.inflight,
                            residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv,
-                           fused_mlp=False if a.no_fused_mlp else None)
+                           fused_mlp=False if a.no_fused_mlp else None,
+                           fused_qkv=False if a.no_fused_qkv else None)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -360,7 +363,8 @@ def main(argv=None) -> int:
                    "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap, "inflight": a.inflight,
                    "aging_ms": a.aging_ms, "util": a.util,
                    "classifier": not a.no_classifier, "residual_in_gemm": not a.no_residual_gemm,
-                   "split_qkv": a.split_qkv, "fused_mlp": bool(engine.model.fused_mlp)},
+                   "split_qkv": a.split_qkv, "fused_mlp": bool(engine.model.fused_mlp),
+                   "fused_qkv": bool(engine.model.fused_qkv)},
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),
         "p99_enqueue_to_dispatch_ms": round(lat["p99_enq_ms"], 3),

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--tokens", default="37,1024,2048,4041,4096")
     ap.add_argument("--plain", action="store_true", help="also time the plain GEMM shapes")
+    ap.add_argument("--rope", action="store_true", help="also A/B the qkv GEMM with the RoPE/KV epilogue")
+    ap.add_argument("--groups", default="", help="e.g. 4,8,16: also time gemm_swiglu per block-order group size")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -82,6 +84,8 @@ def main():
             F.linear(x, w_gu)
 
         fns = {"hipblaslt+silu_mul": unfused, "fused": fused, "hipblaslt_gemm_only": blas_only}
+        for gm in [int(v) for v in a.groups.split(",") if v]:
+            fns[f"fused_g{gm}"] = (lambda gm=gm: G._launch(x, w_perm, out, G.EPI_SWIGLU, group_m=gm))
         for f in fns.values():
             f()
         torch.cuda.synchronize()
@@ -95,6 +99,36 @@ def main():
                           "fused_tflops": round(flop / med["fused"] / 1e9, 1),
                           "blas_tflops": round(flop / med["hipblaslt_gemm_only"] / 1e9, 1),
                           "speedup_vs_unfused": round(med["hipblaslt+silu_mul"] / med["fused"], 3)}), flush=True)
+
+    if a.rope:
+        from llm_message_queue_amd.ops.llama_ops import rope_tables
+        Hq, Hkv, max_ctx, S = 32, 8, 512, 1536
+        wqkv = (torch.randn((Hq + 2 * Hkv) * 128, d, device=dev) * 0.02).to(torch.bfloat16)
+        cos_t, sin_t = rope_tables(max_ctx, 500000.0, dev)
+        kc1 = torch.zeros(S, Hkv, max_ctx, 128, dtype=torch.bfloat16, device=dev)
+        vc1, kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(kc1), torch.zeros_like(kc1)
+        for T in (37, 1024, 4041):
+            x = torch.randn(T, d, device=dev).to(torch.bfloat16)
+            cell = torch.randperm(S * 64, device=dev)[:T]               # unique (slot, pos)
+            slot = (cell // 64).to(torch.int32)
+            pos = (cell % 64 * 7 % max_ctx).to(torch.int32)
+            q1 = ops.rope_kv(F.linear(x, wqkv), pos, slot, cos_t, sin_t, Hq, Hkv, kc1, vc1)
+            q2 = G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2)
+            sl, ps = slot.long(), pos.long()
+            print(json.dumps({"check": "qkv_rope", "T": T, "q_max_diff": (q1.float() - q2.float()).abs().max().item(),
+                              "q_absmax": q1.float().abs().max().item(),
+                              "k_max_diff": (kc1[sl, :, ps].float() - kc2[sl, :, ps].float()).abs().max().item(),
+                              "v_max_diff": (vc1[sl, :, ps].float() - vc2[sl, :, ps].float()).abs().max().item()}),
+                  flush=True)
+            fns = {"hipblaslt+rope_kv": lambda: ops.rope_kv(F.linear(x, wqkv), pos, slot, cos_t, sin_t, Hq, Hkv, kc1, vc1),
+                   "fused": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2)}
+            res = {k: [] for k in fns}
+            for _ in range(a.rounds):
+                for k, f in fns.items():
+                    res[k].append(timeit(f, a.iters))
+            med = {k: statistics.median(v) for k, v in res.items()}
+            print(json.dumps({"bench": "qkv_rope", "T": T, **{k + "_ms": round(v, 4) for k, v in med.items()},
+                              "speedup": round(med["hipblaslt+rope_kv"] / med["fused"], 3)}), flush=True)
 
     if a.plain:
         shapes = {"qkv": (6144, d), "o": (d, d), "gate_up": (2 * ffn, d), "down": (d, ffn)}

@@ -52,9 +52,24 @@ constexpr int GM_BM = 256, GM_BN = 256, GM_BK = 64, GM_THREADS = 512;
 constexpr int GM_HALF_BYTES = 128 * GM_BK * 2;     // 16 KiB
 constexpr int GM_BUF_BYTES = 4 * GM_HALF_BYTES;    // A0 A1 B0 B1
 constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
-constexpr int GM_GROUP_M = 8;
+constexpr int GM_GROUP_M = 8;                    // default M-tiles per block-order group
 
-enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2 };
+enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3 };
+
+// GM_EPI_ROPE: the fused qkv projection's epilogue = the rope_kv kernel
+// (llama_kernels.h): RoPE (rotate-half) on q and k, q to ``q``, k / v into
+// this layer's cache at (slot[row], pos[row]); W rows are the plain
+// [q heads | k heads | v heads] order (N = (Hq + 2 Hkv) * 128).
+struct GmRope {
+  const int32_t* pos;
+  const int32_t* slot;
+  const float* cos_t;                              // [max_ctx][64]
+  const float* sin_t;
+  uint16_t* q;                                     // [M][Hq * 128]
+  uint16_t* kc;                                    // [n_slots][Hkv][max_ctx][128]
+  uint16_t* vc;
+  int Hq, Hkv, max_ctx, n_slots;
+};
 enum { GM_A0 = 0, GM_A1 = 1, GM_B0 = 2, GM_B1 = 3 };
 
 __device__ __forceinline__ uint16_t gm_f2bf(float f) {
@@ -85,7 +100,7 @@ __device__ __forceinline__ void gm_stage(__amdgpu_buffer_rsrc_t rs, uint32_t v0,
 template <int EPI, bool STAGGER = true, int SCHED = 1>
 __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
-    int M, int N, int K) {
+    int M, int N, int K, int group_m, const GmRope rp) {
   extern __shared__ __align__(16) uint8_t smem[];
 
   const int tiles_m = (M + GM_BM - 1) / GM_BM;
@@ -95,11 +110,11 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int pid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int group = pid / (GM_GROUP_M * tiles_n);
-  const int first_m = group * GM_GROUP_M;
-  const int gsize = min(tiles_m - first_m, GM_GROUP_M);
-  const int tm = first_m + (pid % (GM_GROUP_M * tiles_n)) % gsize;
-  const int tn = (pid % (GM_GROUP_M * tiles_n)) / gsize;
+  const int group = pid / (group_m * tiles_n);
+  const int first_m = group * group_m;
+  const int gsize = min(tiles_m - first_m, group_m);
+  const int tm = first_m + (pid % (group_m * tiles_n)) % gsize;
+  const int tn = (pid % (group_m * tiles_n)) / gsize;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -403,23 +418,74 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               o[(mh * 64 + m * 16 + fq * 4 + j) * 64 + nh * 32 + n * 16 + fr] = gm_f2bf(acc[mh][m][nh][n][j]);
-    GM_LGKM(0);
-    __builtin_amdgcn_wave_barrier();
-    const int col0 = tn * GM_BN + wc * 64;
+    if (EPI == GM_EPI_STORE) {
+      GM_LGKM(0);
+      __builtin_amdgcn_wave_barrier();
+      const int col0 = tn * GM_BN + wc * 64;
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int qd = it * 64 + lane;               // row qd/8, chunk qd%8
-      const int r = qd >> 3, cb = qd & 7;
-      const int grow = row0 + r;
-      const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(smem + w * 16384 + r * 128 + cb * 16);
-      if (grow < M) {
-        uint16_t* dst = C + (int64_t)grow * N + col0 + cb * 8;
-        *reinterpret_cast<gm_u32x4*>(dst) = v;
+      for (int it = 0; it < 16; ++it) {
+        const int qd = it * 64 + lane;               // row qd/8, chunk qd%8
+        const int r = qd >> 3, cb = qd & 7;
+        const int grow = row0 + r;
+        const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(smem + w * 16384 + r * 128 + cb * 16);
+        if (grow < M) *reinterpret_cast<gm_u32x4*>(C + (int64_t)grow * N + col0 + cb * 8) = v;
+      }
+    } else {                                       // GM_EPI_ROPE
+      __syncthreads();                             // the rotary partner (d + 64) is another wave's column
+      // (tile row r, tile column c) -> byte offset of the bf16 element in LDS
+      auto at = [&](int r, int c) -> const uint8_t* {
+        return smem + ((r >> 7) * 4 + (c >> 6)) * 16384 + (r & 127) * 128 + (c & 63) * 2;
+      };
+      const int nq = rp.Hq / 2, nk = rp.Hkv / 2;   // 256-column tiles of q / of k heads
+      if (tn < nq + nk) {
+        for (int task = tid; task < GM_BM * 16; task += GM_THREADS) {
+          const int r = task >> 4, hh = (task >> 3) & 1, j = task & 7;
+          const int grow = tm * GM_BM + r;
+          if (grow >= M) continue;
+          const int p = rp.pos[grow], sl = rp.slot[grow];
+          if ((unsigned)sl >= (unsigned)rp.n_slots || (unsigned)p >= (unsigned)rp.max_ctx) continue;
+          const gm_u32x4 lo = *reinterpret_cast<const gm_u32x4*>(at(r, hh * 128 + 8 * j));
+          const gm_u32x4 hi = *reinterpret_cast<const gm_u32x4*>(at(r, hh * 128 + 64 + 8 * j));
+          const float4 c0 = *reinterpret_cast<const float4*>(rp.cos_t + (int64_t)p * 64 + 8 * j);
+          const float4 c1 = *reinterpret_cast<const float4*>(rp.cos_t + (int64_t)p * 64 + 8 * j + 4);
+          const float4 s0 = *reinterpret_cast<const float4*>(rp.sin_t + (int64_t)p * 64 + 8 * j);
+          const float4 s1 = *reinterpret_cast<const float4*>(rp.sin_t + (int64_t)p * 64 + 8 * j + 4);
+          const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+          const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          gm_u32x4 olo, ohi;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a0 = __uint_as_float(lo[e] << 16), a1 = __uint_as_float(lo[e] & 0xffff0000u);
+            const float b0 = __uint_as_float(hi[e] << 16), b1 = __uint_as_float(hi[e] & 0xffff0000u);
+            const float c_0 = cc[2 * e], c_1 = cc[2 * e + 1], s_0 = ss[2 * e], s_1 = ss[2 * e + 1];
+            olo[e] = (uint32_t)gm_f2bf(a0 * c_0 - b0 * s_0) | ((uint32_t)gm_f2bf(a1 * c_1 - b1 * s_1) << 16);
+            ohi[e] = (uint32_t)gm_f2bf(b0 * c_0 + a0 * s_0) | ((uint32_t)gm_f2bf(b1 * c_1 + a1 * s_1) << 16);
+          }
+          uint16_t* dst;
+          if (tn < nq) {
+            dst = rp.q + (int64_t)grow * rp.Hq * 128 + (2 * tn + hh) * 128;
+          } else {
+            const int kvh = 2 * (tn - nq) + hh;
+            dst = rp.kc + (((int64_t)sl * rp.Hkv + kvh) * rp.max_ctx + p) * 128;
+          }
+          *reinterpret_cast<gm_u32x4*>(dst + 8 * j) = olo;
+          *reinterpret_cast<gm_u32x4*>(dst + 64 + 8 * j) = ohi;
+        }
+      } else {
+        for (int task = tid; task < GM_BM * 32; task += GM_THREADS) {
+          const int r = task >> 5, hh = (task >> 4) & 1, cb = task & 15;
+          const int grow = tm * GM_BM + r;
+          if (grow >= M) continue;
+          const int p = rp.pos[grow], sl = rp.slot[grow];
+          if ((unsigned)sl >= (unsigned)rp.n_slots || (unsigned)p >= (unsigned)rp.max_ctx) continue;
+          const int kvh = 2 * (tn - nq - nk) + hh;
+          uint16_t* dst = rp.vc + (((int64_t)sl * rp.Hkv + kvh) * rp.max_ctx + p) * 128;
+          *reinterpret_cast<gm_u32x4*>(dst + 8 * cb) = *reinterpret_cast<const gm_u32x4*>(at(r, hh * 128 + 8 * cb));
+        }
       }
     }
   }
 }
-
 
 #undef GM_LGKM
 #undef GM_VMCNT

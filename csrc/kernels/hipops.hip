@@ -132,7 +132,8 @@ static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T,
 // C = A · Wᵀ (epi 0, C [M][N]) or H = silu(A·Wgᵀ) * (A·Wuᵀ) over a
 // swiglu-permuted W (epi 2, C [M][N/2]); A [M][K], W [N][K], bf16.
 template <int EPI, bool STAGGER = true, int SCHED = 1>
-static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st) {
+static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st,
+                        int group_m, const GmRope& rp = GmRope{}) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
@@ -140,27 +141,49 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
     attr = true;
   }
   const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c, M, N, K);
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c, M, N, K, group_m, rp);
 }
 
 // epi: 0 / 2 = store / SwiGLU; 16 / 32 = store with the round-1 phase
 // schedule / without the wave-row stagger (A/B measurements only).
-static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t stream) {
+static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t stream,
+                      int group_m) {
+  require(group_m >= 1 && group_m <= 64, "gemm: group_m out of range");
   require(M > 0 && N > 0 && K > 0, "gemm: empty operand");
   require(N % GM_BN == 0, "gemm: N must be a multiple of 256");
   require(K % (2 * GM_BK) == 0, "gemm: K must be a multiple of 128");
   require((int64_t)M * K < (int64_t)1 << 30 && (int64_t)N * K < (int64_t)1 << 30, "gemm: operand too large (2 GiB buffer descriptors)");
   require(a % 16 == 0 && w % 16 == 0 && c % 16 == 0, "gemm: pointers must be 16-byte aligned");
   if (epi == GM_EPI_STORE)
-    launch_gemm<GM_EPI_STORE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+    launch_gemm<GM_EPI_STORE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_SWIGLU)
-    launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+    launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_STORE + 16)
-    launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+    launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_STORE + 32)
-    launch_gemm<GM_EPI_STORE, false, 1>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream));
+    launch_gemm<GM_EPI_STORE, false, 1>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else
     throw std::invalid_argument("gemm: unknown epilogue");
+  check_launch();
+}
+
+// q = RoPE(x · Wq^T); K/V cache rows (slot, pos) = (RoPE(x · Wk^T), x · Wv^T):
+// the qkv projection with the rope_kv kernel as its epilogue (no [T][qkv]
+// intermediate).  W [N][K] in the plain [q | k | v] head order.
+static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr_t pos, uintptr_t slot,
+                          uintptr_t cos_t, uintptr_t sin_t, int Hq, int Hkv, int max_ctx, int n_slots,
+                          uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t stream) {
+  require(M > 0 && K > 0, "gemm_qkv_rope: empty operand");
+  require(Hq % 2 == 0 && Hkv % 2 == 0 && Hkv >= 2, "gemm_qkv_rope: head counts must be even");
+  require(N == (Hq + 2 * Hkv) * 128, "gemm_qkv_rope: N must be (Hq + 2 Hkv) * 128");
+  require(K % (2 * GM_BK) == 0, "gemm_qkv_rope: K must be a multiple of 128");
+  require((int64_t)M * K < (int64_t)1 << 30 && (int64_t)N * K < (int64_t)1 << 30, "gemm_qkv_rope: operand too large");
+  require(a % 16 == 0 && w % 16 == 0 && q % 16 == 0 && kc % 16 == 0 && vc % 16 == 0 && cos_t % 16 == 0 &&
+              sin_t % 16 == 0, "gemm_qkv_rope: pointers must be 16-byte aligned");
+  require(max_ctx > 0 && n_slots > 0, "gemm_qkv_rope: bad cache shape");
+  GmRope rp{P<const int32_t>(pos), P<const int32_t>(slot), P<const float>(cos_t), P<const float>(sin_t),
+            P<uint16_t>(q), P<uint16_t>(kc), P<uint16_t>(vc), Hq, Hkv, max_ctx, n_slots};
+  launch_gemm<GM_EPI_ROPE>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M, rp);
   check_launch();
 }
 
@@ -296,7 +319,9 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("rmsnorm", &rmsnorm);
   m.def("silu_mul", &silu_mul, py::arg("gu"), py::arg("out"), py::arg("T"), py::arg("F"), py::arg("stream"),
         py::arg("perm") = false);
-  m.def("gemm_bf16", &gemm_bf16);
+  m.def("gemm_bf16", &gemm_bf16, py::arg("a"), py::arg("w"), py::arg("c"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("epi"), py::arg("stream"), py::arg("group_m") = (int)GM_GROUP_M);
+  m.def("gemm_qkv_rope", &gemm_qkv_rope);
   m.attr("GEMM_EPI_STORE") = (int)GM_EPI_STORE;
   m.attr("GEMM_EPI_SWIGLU") = (int)GM_EPI_SWIGLU;
   m.def("rope_kv", &rope_kv);

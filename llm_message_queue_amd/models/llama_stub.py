@@ -25,6 +25,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from ..ops import gemm as G
 from ..ops.llama_ops import get_ops, rope_tables
 
 
@@ -68,7 +69,8 @@ class LlamaConfig:
 class LlamaStub:
     def __init__(self, cfg: LlamaConfig, slots: int, max_ctx: int, device="cuda", impl: str = "hip",
                  seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False,
-                 fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512):
+                 fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512,
+                 fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -96,6 +98,11 @@ class LlamaStub:
         # gemm_swiglu on steps of >= min_fused_tokens rows
         self.fused_mlp = (impl == "hip") if fused_mlp is None else bool(fused_mlp)
         self.min_fused_tokens = int(min_fused_tokens)
+        # qkv projection with the RoPE + K/V-cache-write epilogue (ops.gemm.qkv_rope)
+        # on steps of >= min_fused_qkv_tokens rows (3.5% faster than hipBLASLt +
+        # rope_kv at T = 4041, slower below ~2k rows: profiles/r2_gemm_swiglu.md)
+        self.fused_qkv = (impl == "hip" and not split_qkv) if fused_qkv is None else bool(fused_qkv)
+        self.min_fused_qkv_tokens = int(min_fused_qkv_tokens)
         g = torch.Generator(device=self.device).manual_seed(seed)
         std = 0.02
 
@@ -127,8 +134,7 @@ class LlamaStub:
     def _gu_layout(self, w_gu: torch.Tensor) -> torch.Tensor:
         if not self.fused_mlp:
             return w_gu
-        from ..ops.gemm import swiglu_permute
-        return swiglu_permute(w_gu)
+        return G.swiglu_permute(w_gu)
 
     def weight_bytes(self) -> int:
         n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
@@ -168,15 +174,20 @@ class LlamaStub:
             if i > 0:
                 x = ops.rmsnorm(res, L["attn_norm"], cfg.eps) if fused else \
                     ops.rmsnorm(out, L["attn_norm"], cfg.eps, residual=res)
-            if self.split_qkv:
+            if self.fused_qkv and x.shape[0] >= self.min_fused_qkv_tokens:
+                q = G.qkv_rope(x, L["wqkv"], pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
+                             self.kcache[i], self.vcache[i])
+            elif self.split_qkv:
                 nq = cfg.heads * cfg.head_dim
                 qkv = torch.empty((x.shape[0], L["wqkv"].shape[0]), dtype=x.dtype, device=x.device)
                 torch.mm(x, L["wqkv"][:nq].t(), out=qkv[:, :nq])
                 torch.mm(x, L["wqkv"][nq:].t(), out=qkv[:, nq:])
+                q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
+                                self.kcache[i], self.vcache[i])
             else:
                 qkv = F.linear(x, L["wqkv"])
-            q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
-                            self.kcache[i], self.vcache[i])
+                q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
+                                self.kcache[i], self.vcache[i])
             if tiles is not None:
                 a = ops.attention_tiles(q, self.kcache[i], self.vcache[i], tiles, cfg.heads, cfg.kv_heads,
                                         self.scale, n_dec=n_dec)

@@ -7,7 +7,9 @@ its rows permuted by :func:`swiglu_permute` so that, inside every 256-column
 output tile, each wave's 64 columns are 32 gate features followed by the same
 32 up features (the kernel's register layout puts g and u of one element in
 the same lane).  ``gemm(x, w)`` is the plain ``x·Wᵀ`` on the same kernel,
-kept for A/B measurements against hipBLASLt.
+kept for A/B measurements against hipBLASLt.  ``qkv_rope`` runs the qkv
+projection with the RoPE + K/V-cache-write epilogue (replacing F.linear +
+``rope_kv``).
 
 CPU / reference path: :func:`swiglu_reference` (fp32 math of the same op).
 """
@@ -73,7 +75,7 @@ def supported(M: int, N: int, K: int) -> bool:
     return M > 0 and N % TILE_N == 0 and K % 128 == 0
 
 
-def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int):
+def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group_m: int = 8):
     k = _native.require_hipops()
     M, K = x.shape
     N = w.shape[0]
@@ -82,7 +84,7 @@ def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int):
     if not supported(M, N, K):
         raise ValueError(f"gemm: unsupported shape M={M} N={N} K={K}")
     k.gemm_bf16(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, epi,
-                torch.cuda.current_stream(x.device).cuda_stream)
+                torch.cuda.current_stream(x.device).cuda_stream, group_m)
     return out
 
 
@@ -105,3 +107,34 @@ def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None)
     if y.shape != (x.shape[0], F):
         raise ValueError("gemm_swiglu: out shape mismatch")
     return _launch(x, w_perm, y, EPI_SWIGLU)
+
+
+def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
+             cos_t: torch.Tensor, sin_t: torch.Tensor, Hq: int, Hkv: int,
+             kc: torch.Tensor, vc: torch.Tensor, q_out: torch.Tensor = None) -> torch.Tensor:
+    """The qkv projection with RoPE + the K/V cache write as its epilogue:
+    returns q [T][Hq*128] (rotated) and writes this step's K/V rows into
+    ``kc`` / ``vc`` [slots][Hkv][max_ctx][128] -- the same result as
+    ``F.linear`` followed by ``HipOps.rope_kv``, without the [T][qkv]
+    intermediate or the second launch."""
+    _check(x, "x")
+    _check(wqkv, "wqkv")
+    for t, n in ((kc, "kc"), (vc, "vc")):
+        _check(t, n)
+    if pos.dtype != torch.int32 or slot.dtype != torch.int32 or not (pos.is_contiguous() and slot.is_contiguous()):
+        raise TypeError("pos / slot must be contiguous int32")
+    if cos_t.dtype != torch.float32 or sin_t.dtype != torch.float32 or cos_t.shape[1] != 64:
+        raise TypeError("cos / sin tables must be float32 [max_ctx][64]")
+    T, K = x.shape
+    S, hk, max_ctx, hd = kc.shape
+    if hk != Hkv or hd != 128 or vc.shape != kc.shape or cos_t.shape[0] < max_ctx:
+        raise ValueError("kv cache / rope table shape mismatch")
+    if pos.numel() != T or slot.numel() != T:
+        raise ValueError("pos / slot length must equal the token count")
+    q = q_out if q_out is not None else torch.empty((T, Hq * 128), dtype=x.dtype, device=x.device)
+    _check(q, "q_out")
+    k = _native.require_hipops()
+    k.gemm_qkv_rope(x.data_ptr(), wqkv.data_ptr(), T, wqkv.shape[0], K, pos.data_ptr(), slot.data_ptr(),
+                    cos_t.data_ptr(), sin_t.data_ptr(), Hq, Hkv, max_ctx, S, q.data_ptr(), kc.data_ptr(),
+                    vc.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
+    return q

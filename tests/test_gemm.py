@@ -131,14 +131,16 @@ def test_silu_mul_perm_matches_ref():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T", [37, 600])
+@pytest.mark.parametrize("T", [37, 600, 2400])
 def test_tiny_model_fused_mlp_matches_ref(T):
     """The HIP model with the fused MLP (GEMM+SwiGLU for T >= 512, permuted
-    silu_mul below) against the fp32-reference ops on the same weights."""
+    silu_mul below) and the fused qkv+RoPE GEMM (T >= 2048) against the
+    fp32-reference ops on the same weights."""
     cfg = LlamaConfig.tiny()
-    hip = LlamaStub(cfg, slots=4, max_ctx=256, device=DEV, impl="hip", seed=3, min_fused_tokens=512)
-    ref = LlamaStub(cfg, slots=4, max_ctx=256, device=DEV, impl="ref", seed=3, residual_in_gemm=True)
-    assert hip.fused_mlp and not ref.fused_mlp
+    hip = LlamaStub(cfg, slots=4, max_ctx=1024, device=DEV, impl="hip", seed=3, min_fused_tokens=512,
+                    min_fused_qkv_tokens=2048)
+    ref = LlamaStub(cfg, slots=4, max_ctx=1024, device=DEV, impl="ref", seed=3, residual_in_gemm=True)
+    assert hip.fused_mlp and hip.fused_qkv and not ref.fused_mlp and not ref.fused_qkv
     n = T // 4
     tok = torch.randint(0, cfg.vocab, (4 * n,), device=DEV)
     pos = torch.arange(n, device=DEV, dtype=torch.int32).repeat(4)
@@ -147,3 +149,30 @@ def test_tiny_model_fused_mlp_matches_ref(T):
     hb = ref.hidden(tok, pos, slot).float()
     rel = (ha - hb).norm() / hb.norm()
     assert rel < 2e-2, rel.item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [37, 300, 4096])
+def test_qkv_rope_matches_linear_plus_rope_kv(T):
+    """The qkv GEMM with the RoPE/KV epilogue == F.linear + the rope_kv
+    kernel (q rows, and the K/V cache rows written at (slot, pos)); cache
+    cells no token addresses stay zero."""
+    from llm_message_queue_amd.ops.llama_ops import HipOps, rope_tables
+    Hq, Hkv, max_ctx, S, d = 8, 2, 64, 96, 512
+    g = torch.Generator(device=DEV).manual_seed(T)
+    x = torch.randn(T, d, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn((Hq + 2 * Hkv) * 128, d, generator=g, device=DEV) * 0.05).to(torch.bfloat16)
+    cos_t, sin_t = rope_tables(max_ctx, 500000.0, DEV)
+    cell = torch.randperm(S * max_ctx, generator=g, device=DEV)[:T]
+    slot, pos = (cell // max_ctx).to(torch.int32), (cell % max_ctx).to(torch.int32)
+    kc1 = torch.zeros(S, Hkv, max_ctx, 128, dtype=torch.bfloat16, device=DEV)
+    vc1, kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(kc1), torch.zeros_like(kc1)
+    q1 = HipOps().rope_kv(torch.nn.functional.linear(x, w), pos, slot, cos_t, sin_t, Hq, Hkv, kc1, vc1)
+    q2 = G.qkv_rope(x, w, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2)
+    tol = 0.02 * q1.float().abs().max().item()
+    assert (q1.float() - q2.float()).abs().max().item() <= tol
+    assert (kc1.float() - kc2.float()).abs().max().item() <= tol
+    assert (vc1.float() - vc2.float()).abs().max().item() <= tol
+    untouched = torch.ones(S, max_ctx, dtype=torch.bool, device=DEV)
+    untouched[slot.long(), pos.long()] = False
+    assert (kc2.permute(0, 2, 1, 3)[untouched] == 0).all()
