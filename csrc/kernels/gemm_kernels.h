@@ -365,12 +365,6 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     }
   }
 
-#undef GM_STAGE
-#undef GM_READ_A
-#undef GM_READ_B
-#undef GM_MFMA
-#undef GM_READ_B0_INTO
-#undef GM_MFMA_WITH
 
   if (STAGGER && wr == 0) GM_BARRIER();
 
@@ -487,6 +481,13 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   }
 }
 
+
+#undef GM_STAGE
+#undef GM_READ_A
+#undef GM_READ_B
+#undef GM_MFMA
+#undef GM_READ_B0_INTO
+#undef GM_MFMA_WITH
 #undef GM_LGKM
 #undef GM_VMCNT
 #undef GM_BARRIER
