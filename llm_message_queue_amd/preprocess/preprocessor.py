@@ -234,7 +234,11 @@ class Preprocessor:
         with self._lock:
             udefs = dict(self._user_priorities) if self._user_priorities else None
         heads = [self._head_fast(m, udefs) for m in msgs]
-        work = [i for i, h in enumerate(heads) if h is not None and msgs[i].content]
+        # every message with content goes through the kernels: explicit-
+        # priority messages are returned unanalysed (ProcessMessage's early
+        # return) but the backend still needs their prompt token ids
+        work = [i for i in range(len(msgs)) if msgs[i].content] if prompt_cap else \
+            [i for i, h in enumerate(heads) if h is not None and msgs[i].content]
         pend = None
         if work:
             pipe = self.gpu_pipeline()
@@ -265,6 +269,10 @@ class Preprocessor:
             ph = res.prompt_hashes if prompt_cap else None
             for j, i in enumerate(work):
                 m = msgs[i]
+                if ph is not None:
+                    m.prompt_ids = ph[j, :ntok[j]]
+                if heads[i] is None:                 # explicit priority: tokens only
+                    continue
                 md = m.metadata
                 if fb[j]:
                     # fold-special characters / non-literal patterns: oracle
@@ -287,8 +295,6 @@ class Preprocessor:
                     md["word_count"] = wc[j]
                     md["sentiment"] = sent[j]
                     md["contains_question"] = qs[j]
-                if ph is not None:
-                    m.prompt_ids = ph[j, :ntok[j]]
                 if ml is not None:
                     md["ml_priority"] = ml[j]
                     if use_ml and heads[i] and md.get("priority_reason") is None:

@@ -437,3 +437,25 @@ def test_salient_topk_flags_table_overflow_and_host_recomputes():
     assert eng.salient_overflows == 1
     toks = [oracle.token_hashes(oracle.sanitize(c), eng.cfg.max_tokens) for c in contents]
     assert out[0][1] == _topk_host(toks, 6)
+
+
+@pytest.mark.gpu
+def test_gpu_preprocess_tokenizes_every_message():
+    """Explicit-priority messages skip content analysis (ProcessMessage's
+    early return) but still get their prompt token ids on the GPU path --
+    the same ids as the CPU oracle -- so every tier's request carries its
+    real prompt to the backend."""
+    from llm_message_queue_amd.gateway.workload import Workload
+    from llm_message_queue_amd.preprocess.preprocessor import Preprocessor
+    msgs = Workload(seed=11).make(300)
+    cpu = [m.copy() for m in msgs]
+    Preprocessor(use_gpu=True).process_batch(msgs, use_gpu=True, classify=True, prompt_cap=32)
+    Preprocessor(use_gpu=False).process_batch(cpu, use_gpu=False, prompt_cap=32)
+    explicit = 0
+    for a, b in zip(msgs, cpu):
+        assert a.priority == b.priority
+        assert a.prompt_ids is not None and list(a.prompt_ids) == list(b.prompt_ids)
+        if "analyzed" not in b.metadata:
+            explicit += 1
+            assert "analyzed" not in a.metadata and "word_count" not in a.metadata
+    assert explicit > 0
