@@ -83,7 +83,7 @@ def parse(argv=None):
     ap.add_argument("--lb", default="least_connections",
                     choices=["round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first"],
                     help="multi-GPU placement strategy (loadbalancer.algorithm)")
-    ap.add_argument("--control-plane", default="gloo", choices=["gloo", "nccl"],
+    ap.add_argument("--control-plane", default="shm", choices=["shm", "gloo", "nccl"],
                     help="per-tick load/descriptor exchange: host gloo group or RCCL on a side stream")
     ap.add_argument("--gateway-only-s", type=float, default=3.0,
                     help="seconds of the secondary null-backend gateway measurement (0 = skip)")
@@ -115,7 +115,7 @@ def main(argv=None) -> int:
         # CPU rehearsal of the exact control flow (collectives, tick counts,
         # reductions) with a tiny model and gloo -- never a measurement
         dev = torch.device("cpu")
-        comm = init_from_env(backend="gloo", control="gloo")
+        comm = init_from_env(backend="gloo", control="gloo" if a.control_plane == "nccl" else a.control_plane)
         a.model, a.slots, a.max_ctx, a.token_budget, a.prompt_cap = "tiny", 16, 64, 128, 16
     else:
         if not torch.cuda.is_available():

@@ -33,7 +33,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--remote-per-tick", type=int, default=16, help="descriptors sent to each peer per tick")
-    ap.add_argument("--control", default="gloo", choices=["gloo", "nccl"])
+    ap.add_argument("--control", default="gloo", choices=["gloo", "nccl", "shm"])
     ap.add_argument("--busy-gpu", action="store_true")
     ap.add_argument("--force-group", action="store_true")
     a = ap.parse_args()
@@ -57,6 +57,9 @@ def main() -> None:
             comm = TorchComm()
     else:
         comm = init_from_env(backend="nccl" if gpu else "gloo", control=a.control)
+    if a.control == "shm" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        from llm_message_queue_amd.parallel.comm import ShmComm
+        assert isinstance(comm, ShmComm), type(comm)
     W, me = comm.world, comm.rank
     width = DESC_HDR + 32
     rng = np.random.default_rng(me)

@@ -2,9 +2,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "queue/shm_coll.h"
 #include "queue/shm_ring.h"
 
 namespace py = pybind11;
+using llmq::ShmCollective;
 using llmq::ShmRing;
 
 PYBIND11_MODULE(_shmring, m) {
@@ -56,4 +58,65 @@ PYBIND11_MODULE(_shmring, m) {
       .def("wake_all", &ShmRing::wake_all)
       .def("close", &ShmRing::close)
       .def("unlink", &ShmRing::unlink);
+  py::register_exception<llmq::ShmCollTimeout>(m, "ShmCollTimeout", PyExc_TimeoutError);
+  py::class_<ShmCollective>(m, "ShmCollective")
+      .def(py::init<const std::string&, int, int, uint64_t, bool>(), py::arg("name"), py::arg("world"),
+           py::arg("rank"), py::arg("buf_bytes") = 4 << 20, py::arg("create") = false)
+      .def("all_gather",
+           [](ShmCollective& c, py::bytes b, double timeout_s) {
+             std::string s = b;
+             {
+               py::gil_scoped_release nogil;
+               c.exchange(s.data(), s.size(), timeout_s);
+             }
+             py::list out;
+             const int world = c.world();
+             for (int r = 0; r < world; ++r) {
+               uint64_t n = 0;
+               const uint8_t* p = c.payload(r, &n);
+               out.append(py::bytes(reinterpret_cast<const char*>(p), n));
+             }
+             return out;
+           },
+           py::arg("data"), py::arg("timeout_s") = 60.0)
+      .def("all_to_all",
+           [](ShmCollective& c, const std::vector<py::bytes>& parts, double timeout_s) {
+             const int world = c.world();
+             if ((int)parts.size() != world) throw std::invalid_argument("all_to_all: one part per rank");
+             // payload: world x u64 part sizes, then the parts back to back
+             std::string buf(sizeof(uint64_t) * world, '\0');
+             for (int r = 0; r < world; ++r) {
+               std::string s = parts[r];
+               const uint64_t n = s.size();
+               std::memcpy(&buf[sizeof(uint64_t) * r], &n, sizeof(n));
+               buf += s;
+             }
+             {
+               py::gil_scoped_release nogil;
+               c.exchange(buf.data(), buf.size(), timeout_s);
+             }
+             py::list out;
+             const int me = c.rank();
+             for (int r = 0; r < world; ++r) {
+               uint64_t total = 0;
+               const uint8_t* p = c.payload(r, &total);
+               uint64_t off = sizeof(uint64_t) * world, n = 0;
+               for (int d = 0; d < world; ++d) {
+                 uint64_t sz;
+                 std::memcpy(&sz, p + sizeof(uint64_t) * d, sizeof(sz));
+                 if (d == me) n = sz;
+                 if (d < me) off += sz;
+               }
+               if (off + n > total) throw std::runtime_error("all_to_all: corrupt payload");
+               out.append(py::bytes(reinterpret_cast<const char*>(p + off), n));
+             }
+             return out;
+           },
+           py::arg("parts"), py::arg("timeout_s") = 60.0)
+      .def("attached", &ShmCollective::attached)
+      .def("unlink", &ShmCollective::unlink)
+      .def_property_readonly("ops", &ShmCollective::ops)
+      .def_property_readonly("world", &ShmCollective::world)
+      .def_property_readonly("rank", &ShmCollective::rank)
+      .def_property_readonly("buf_bytes", &ShmCollective::buf_bytes);
 }

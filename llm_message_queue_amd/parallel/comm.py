@@ -15,6 +15,8 @@ every scheduler tick does
   * ``send``/``recv`` point-to-point for conversation KV/context migration
     (N11) -- one direct xGMI link per GPU pair, not a ring.
 
+``ShmComm`` carries the per-tick control messages through one shared-memory
+segment when every rank is on the node (the default for the serving job);
 ``FakeComm`` runs the same API between threads of one process so the
 multi-rank logic is testable on a CPU box at world sizes 2/4/8.
 """
@@ -234,6 +236,86 @@ class TorchComm(Comm):
             self._guard(lambda: self.dist.barrier(group=self.group))
 
 
+class ShmComm(Comm):
+    """Node-local control plane: the per-tick collectives (load-vector
+    ``all_gather``, descriptor ``all_to_all``, ``broadcast``, barrier) go
+    through one POSIX shared-memory segment (``csrc/queue/shm_coll.h``, a
+    slot per rank, release/acquire sequence numbers, two buffers by op
+    parity) instead of gloo's TCP round trips -- every rank of the serving
+    job lives on the same MI355X node.  The data plane (KV migration p2p,
+    RCCL over xGMI) stays on ``data`` (a ``TorchComm``).
+
+    A peer that stops answering surfaces as ``PeerLost`` after
+    ``timeout_s`` (the segment never blocks forever)."""
+
+    backend = "shm"
+
+    def __init__(self, data: "TorchComm", name: str, timeout_s: float = DEFAULT_TIMEOUT_S,
+                 buf_bytes: int = 4 << 20):
+        from .. import _native
+        mod = _native.shmring()
+        self.data = data
+        self.rank, self.world = data.rank, data.world
+        self.timeout_s = float(timeout_s)
+        self.name = name
+        if self.rank == 0:
+            self.c = mod.ShmCollective(name, self.world, 0, buf_bytes, True)
+        data.barrier()                                 # the segment exists
+        if self.rank != 0:
+            self.c = mod.ShmCollective(name, self.world, self.rank, buf_bytes, False)
+        data.barrier()                                 # everyone attached
+        if self.rank == 0:
+            self.c.unlink()                            # the mappings outlive the name
+
+    def _x(self, fn, arg):
+        try:
+            return fn(arg, self.timeout_s)
+        except TimeoutError as e:
+            raise PeerLost(f"rank {self.rank}: {e}") from e
+
+    def all_gather_i64(self, vec):
+        v = np.ascontiguousarray(vec, dtype=np.int64).reshape(-1)
+        parts = self._x(self.c.all_gather, v.tobytes())
+        return np.stack([np.frombuffer(p, dtype=np.int64) for p in parts])
+
+    def all_to_all_rows(self, send, recv_counts, width):
+        parts = [np.ascontiguousarray(x, dtype=np.int32).reshape(-1, width).tobytes() for x in send]
+        got = self._x(self.c.all_to_all, parts)
+        out = [np.frombuffer(g, dtype=np.int32).reshape(-1, width).copy() for g in got]
+        for src, c in enumerate(recv_counts):
+            if out[src].shape[0] != c:
+                raise RuntimeError(f"rank {self.rank}: expected {c} rows from {src}, got {out[src].shape[0]}")
+        return out
+
+    def broadcast_i64(self, vec, root=0):
+        v = np.ascontiguousarray(vec, dtype=np.int64).reshape(-1)
+        parts = self._x(self.c.all_gather, v.tobytes() if self.rank == root else b"")
+        return np.frombuffer(parts[root], dtype=np.int64).copy()
+
+    def barrier(self):
+        self._x(self.c.all_gather, b"")
+
+    # data plane: RCCL (or gloo) through the torch group
+    def send_tensor(self, t, dst):
+        self.data.send_tensor(t, dst)
+
+    def recv_tensor(self, t, src):
+        self.data.recv_tensor(t, src)
+
+    def exchange_p2p(self, sends, recvs):
+        self.data.exchange_p2p(sends, recvs)
+
+    def warm_data_plane(self):
+        self.data.warm_data_plane()
+
+
+def single_node() -> bool:
+    """Every rank of the job on this node (torchrun's LOCAL_WORLD_SIZE)."""
+    import os
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+
+
 class _Hub:
     def __init__(self, world: int, timeout_s: Optional[float] = None):
         self.world = world
@@ -335,9 +417,10 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_
 
     The default process group is ``backend`` (nccl = RCCL when a GPU is
     present): it carries the data plane (KV migration over xGMI).  The
-    control plane uses a ``control`` group: "gloo" (host TCP, default --
-    decoupled from the GPU streams) or "nccl" (RCCL on a high-priority
-    stream, see ``TorchComm``)."""
+    control plane uses a ``control`` group: "shm" (one shared-memory segment
+    on the node, ``ShmComm``; falls back to gloo when the ranks span nodes),
+    "gloo" (host TCP) or "nccl" (RCCL on a high-priority stream, see
+    ``TorchComm``)."""
     import datetime
     import os
     import torch
@@ -347,6 +430,14 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_
         return SoloComm()
     if timeout_s is None:
         timeout_s = float(os.environ.get("LLMQ_COLLECTIVE_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+    shm = control == "shm"
+    if shm:
+        if single_node():
+            control = "gloo"                   # the setup barriers and a host group for the data-less ops
+        else:
+            import sys
+            print("comm: ranks span nodes -- shm control plane needs one node, using gloo", file=sys.stderr)
+            control, shm = "gloo", False
     # bounded collectives: a dead or hung peer surfaces as PeerLost within
     # timeout_s instead of blocking every survivor for the backend default
     # (10-30 min); RCCL's watchdog aborts a timed-out communicator
@@ -368,7 +459,12 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_
         dist.init_process_group(backend=backend, timeout=to, **kw)
     default_backend = dist.get_backend()
     if control == default_backend or (control == "gloo" and default_backend == "gloo"):
-        return TorchComm()
-    ctrl = dist.new_group(backend=control, timeout=to)
-    return TorchComm(group=ctrl, data_group=dist.group.WORLD,
-                     device=torch.device("cpu") if control == "gloo" else None)
+        comm = TorchComm()
+    else:
+        ctrl = dist.new_group(backend=control, timeout=to)
+        comm = TorchComm(group=ctrl, data_group=dist.group.WORLD,
+                         device=torch.device("cpu") if control == "gloo" else None)
+    if shm:
+        job = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
+        return ShmComm(comm, f"/llmq_ctrl_{job}_{os.environ.get('MASTER_PORT', '0')}", timeout_s=timeout_s)
+    return comm

@@ -234,7 +234,8 @@ class GPUConfig:
     hbm_reserve_gb: float = 16.0
     telemetry_period_ms: int = 20
     comm_backend: str = "nccl"        # RCCL on ROCm; "gloo" for CPU tests
-    control_plane: str = "gloo"       # per-tick load/descriptor exchange: gloo (host) or nccl (RCCL)
+    control_plane: str = "shm"        # per-tick load/descriptor exchange: shm (node-local shared memory;
+                                      # gloo when ranks span nodes), gloo (host TCP) or nccl (RCCL)
     # move a conversation's KV to the GPU its next turn is placed on (RCCL
     # send/recv over xGMI) instead of replaying the dialog there
     kv_migration: bool = True

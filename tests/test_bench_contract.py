@@ -53,10 +53,12 @@ def test_bench_four_ranks_torchrun_dry_run():
 
 
 def _rank0_ingress(world):
+    # --tick-ms: with the shared-memory control plane a tiny-model CPU tick
+    # takes ~1 ms, so 14 unpaced ticks would see almost no Poisson arrivals
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(world),
               "--cpu-dry-run", "--steps", "6", "--warmup", "2", "--steady-ticks", "8", "--gateway-only-s", "0",
-              "--ingress", "rank0", "--lb", "round_robin"], timeout=420)
+              "--ingress", "rank0", "--lb", "round_robin", "--tick-ms", "20"], timeout=420)
     assert d["n_gpus"] == world and d["config"]["ingress"] == "rank0"
     assert d["remote_dispatched"] > 0                  # the planner spread rank 0's traffic
     acc = d["requests_accounted"]
