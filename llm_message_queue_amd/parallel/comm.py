@@ -236,6 +236,10 @@ class TorchComm(Comm):
             self._guard(lambda: self.dist.barrier(group=self.group))
 
 
+class ShmUnavailable(RuntimeError):
+    """The node-local control segment could not be set up on some rank."""
+
+
 class ShmComm(Comm):
     """Node-local control plane: the per-tick collectives (load-vector
     ``all_gather``, descriptor ``all_to_all``, ``broadcast``, barrier) go
@@ -252,20 +256,37 @@ class ShmComm(Comm):
 
     def __init__(self, data: "TorchComm", name: str, timeout_s: float = DEFAULT_TIMEOUT_S,
                  buf_bytes: int = 4 << 20):
+        """Collective over ``data``: rank 0 creates the segment, the others
+        attach.  Raises ``ShmUnavailable`` on EVERY rank if any rank failed
+        (no /dev/shm, out of space, ...), so the caller can fall back to the
+        torch group together.  The per-rank buffers are sparse: only the
+        bytes a tick actually sends are ever touched."""
         from .. import _native
         mod = _native.shmring()
         self.data = data
         self.rank, self.world = data.rank, data.world
         self.timeout_s = float(timeout_s)
         self.name = name
+        self.c = None
+        err = ""
         if self.rank == 0:
-            self.c = mod.ShmCollective(name, self.world, 0, buf_bytes, True)
-        data.barrier()                                 # the segment exists
+            try:
+                self.c = mod.ShmCollective(name, self.world, 0, buf_bytes, True)
+            except Exception as e:                     # noqa: BLE001 -- reported on every rank below
+                err = f"rank 0: {e}"
+        ok = data.all_gather_i64(np.array([0 if err else 1], dtype=np.int64))   # the segment exists
+        if ok.min() == 0:
+            raise ShmUnavailable(err or "rank 0 could not create the control segment")
         if self.rank != 0:
-            self.c = mod.ShmCollective(name, self.world, self.rank, buf_bytes, False)
-        data.barrier()                                 # everyone attached
+            try:
+                self.c = mod.ShmCollective(name, self.world, self.rank, buf_bytes, False)
+            except Exception as e:                     # noqa: BLE001
+                err = f"rank {self.rank}: {e}"
+        ok = data.all_gather_i64(np.array([0 if err else 1], dtype=np.int64))   # everyone attached
         if self.rank == 0:
             self.c.unlink()                            # the mappings outlive the name
+        if ok.min() == 0:
+            raise ShmUnavailable(err or f"ranks {np.flatnonzero(ok[:, 0] == 0).tolist()} could not attach")
 
     def _x(self, fn, arg):
         try:
@@ -466,5 +487,9 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_
                          device=torch.device("cpu") if control == "gloo" else None)
     if shm:
         job = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
-        return ShmComm(comm, f"/llmq_ctrl_{job}_{os.environ.get('MASTER_PORT', '0')}", timeout_s=timeout_s)
+        try:
+            return ShmComm(comm, f"/llmq_ctrl_{job}_{os.environ.get('MASTER_PORT', '0')}", timeout_s=timeout_s)
+        except ShmUnavailable as e:                    # raised on every rank together
+            import sys
+            print(f"comm: shared-memory control plane unavailable ({e}); using the torch group", file=sys.stderr)
     return comm

@@ -138,3 +138,30 @@ def test_gateway_dispatch_over_shm_control_plane():
     for _, done, g in res:
         assert done and sum(r[0] for r in g) == 24
     assert res[0][2][1][1] > 0                            # rank 1 received work from rank 0's ingress
+
+
+def _fallback_worker(rank, world, port, out):
+    _env(rank, world, port)
+    from llm_message_queue_amd.parallel import comm as C
+    real = C.ShmComm.__init__
+
+    def broken_attach(self, data, name, timeout_s=60.0, buf_bytes=4 << 20):
+        if data.rank == 1:                             # this rank cannot attach
+            name = name + "_missing"
+        real(self, data, name, timeout_s, buf_bytes)
+
+    if rank == 1:
+        C.ShmComm.__init__ = broken_attach
+    else:
+        C.ShmComm.__init__ = lambda self, data, name, timeout_s=60.0, buf_bytes=4 << 20: real(
+            self, data, name, timeout_s, buf_bytes)
+    comm = C.init_from_env(backend="gloo", control="shm", timeout_s=20)
+    g = comm.all_gather_i64(np.array([rank]))
+    out.put((rank, type(comm).__name__, g[:, 0].tolist()))
+
+
+def test_shm_setup_failure_falls_back_to_torch_group_on_every_rank():
+    res, codes = _run(_fallback_worker, 2, timeout=60)
+    assert len(res) == 2, codes
+    assert {kind for _, kind, _ in res} == {"TorchComm"}
+    assert all(g == [0, 1] for _, _, g in res)
