@@ -87,7 +87,7 @@ def parse(argv=None):
                     help="per-tick load/descriptor exchange: host gloo group or RCCL on a side stream")
     ap.add_argument("--gateway-only-s", type=float, default=3.0,
                     help="seconds of the secondary null-backend gateway measurement (0 = skip)")
-    ap.add_argument("--gateway-only-rate", type=float, default=20000.0)
+    ap.add_argument("--gateway-only-rate", type=float, default=50000.0)
     return ap.parse_args(argv)
 
 
