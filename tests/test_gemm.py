@@ -176,3 +176,34 @@ def test_qkv_rope_matches_linear_plus_rope_kv(T):
     untouched = torch.ones(S, max_ctx, dtype=torch.bool, device=DEV)
     untouched[slot.long(), pos.long()] = False
     assert (kc2.permute(0, 2, 1, 3)[untouched] == 0).all()
+
+
+@pytest.mark.gpu
+def test_serving_shapes_match_fp32():
+    """The exact serving shapes of the 8B stub at a step of 4,041 tokens
+    (M not a multiple of 256): gate/up + SwiGLU (N = 28672, K = 4096) and the
+    qkv + RoPE epilogue (32 / 8 heads) against fp32 references."""
+    from llm_message_queue_amd.ops.llama_ops import rope_tables
+    T, d, ffn = 4041, 4096, 14336
+    x, w = _rand(T, d, 2 * ffn, seed=77)
+    ref = G.swiglu_reference(x, w).float()
+    out = G.gemm_swiglu(x, G.swiglu_permute(w)).float()
+    assert (out - ref).abs().max().item() <= 0.01 * ref.abs().max().item() + 1e-3
+    del w, out, ref
+    Hq, Hkv, max_ctx, S = 32, 8, 64, 128
+    wqkv = (torch.randn((Hq + 2 * Hkv) * 128, d, generator=torch.Generator(device=DEV).manual_seed(5),
+                        device=DEV) * 0.02).to(torch.bfloat16)
+    cos_t, sin_t = rope_tables(max_ctx, 500000.0, DEV)
+    cell = torch.randperm(S * max_ctx, device=DEV)[:T]
+    slot, pos = (cell // max_ctx).to(torch.int32), (cell % max_ctx).to(torch.int32)
+    kc1 = torch.zeros(S, Hkv, max_ctx, 128, dtype=torch.bfloat16, device=DEV)
+    vc1, kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(kc1), torch.zeros_like(kc1)
+    qkv_ref = (x.float() @ wqkv.float().t()).to(torch.bfloat16)
+    from llm_message_queue_amd.ops.llama_ops import HipOps
+    # reference: an fp32-accumulated product rounded to bf16, then the rope_kv kernel
+    q1 = HipOps().rope_kv(qkv_ref, pos, slot, cos_t, sin_t, Hq, Hkv, kc1, vc1)
+    q2 = G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2)
+    tol = 0.02 * q1.float().abs().max().item()
+    assert (q1.float() - q2.float()).abs().max().item() <= tol
+    assert (kc1.float() - kc2.float()).abs().max().item() <= tol
+    assert (vc1.float() - vc2.float()).abs().max().item() <= tol
