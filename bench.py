@@ -55,7 +55,10 @@ def parse(argv=None):
     ap.add_argument("--aging-ms", default="50,100,150,200",
                     help="per-tier aging deadlines (realtime,high,normal,low), ms")
     ap.add_argument("--prompt-cap", type=int, default=32)
-    ap.add_argument("--util", type=float, default=0.95)
+    ap.add_argument("--util", type=float, default=0.98,
+                    help="offered load as a fraction of the calibrated capacity (profiles/r2_qps_sweep_*.jsonl: "
+                         "0.98 keeps every tier's p99 arrival->dispatch ~50 ms and e2e ~320 ms over 150-step "
+                         "windows; 1.0 pushes the low tier's e2e past 500 ms)")
     ap.add_argument("--steady-ticks", type=int, default=-1,
                     help="untimed serving ticks at the offered rate before the timed window, so it starts in "
                          "steady state (-1 = max(60, 4 x --warmup))")
