@@ -78,6 +78,26 @@ __device__ __forceinline__ uint16_t gm_f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// Per-row scales of this lane's 32 accumulator rows (row0 + mh*64 + m*16 +
+// fq*4 + j): eight 16-B loads issued together, one branch for the whole set
+// (a per-element load under a runtime condition makes hipcc wait for each
+// load in turn).  rs must hold ceil(M / 256) * 256 floats (ops/gemm.py pads).
+__device__ __forceinline__ void gm_load_row_scales(const float* __restrict__ rs, int row0, int fq,
+                                                   gm_f32x4 (&sc)[2][4]) {
+  if (rs) {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        sc[mh][m] = *reinterpret_cast<const gm_f32x4*>(rs + row0 + mh * 64 + m * 16 + fq * 4);
+  } else {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) sc[mh][m] = gm_f32x4{1.f, 1.f, 1.f, 1.f};
+  }
+}
+
 typedef __attribute__((address_space(3))) void* gm_lds_ptr;
 
 // One half-tile (128 rows x 64 bf16) global -> LDS: 2 buffer_load ... lds per
@@ -100,7 +120,7 @@ __device__ __forceinline__ void gm_stage(__amdgpu_buffer_rsrc_t rs, uint32_t v0,
 template <int EPI, bool STAGGER = true, int SCHED = 1>
 __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
-    int M, int N, int K, int group_m, const GmRope rp) {
+    int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp) {
   extern __shared__ __align__(16) uint8_t smem[];
 
   const int tiles_m = (M + GM_BM - 1) / GM_BM;
@@ -373,6 +393,8 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   if (EPI == GM_EPI_SWIGLU) {
     // wave w: 128 rows x 32 features bf16 = 8 KiB at w * 8 KiB
     uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 8192);
+    gm_f32x4 sc[2][4];
+    gm_load_row_scales(rs, row0, fq, sc);
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
@@ -381,8 +403,8 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         for (int n = 0; n < 2; ++n)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float g = acc[mh][m][0][n][j];
-            const float u = acc[mh][m][1][n][j];
+            const float g = acc[mh][m][0][n][j] * sc[mh][m][j];
+            const float u = acc[mh][m][1][n][j] * sc[mh][m][j];
             const float s = g / (1.0f + __expf(-g));
             o[(mh * 64 + m * 16 + fq * 4 + j) * 32 + n * 16 + fr] = gm_f2bf(s * u);
           }
@@ -401,6 +423,8 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   } else {
     // wave w: 128 rows x 64 columns bf16 = 16 KiB at w * 16 KiB
     uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 16384);
+    gm_f32x4 sc[2][4];
+    gm_load_row_scales(rs, row0, fq, sc);
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
@@ -411,7 +435,8 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
           for (int n = 0; n < 2; ++n)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              o[(mh * 64 + m * 16 + fq * 4 + j) * 64 + nh * 32 + n * 16 + fr] = gm_f2bf(acc[mh][m][nh][n][j]);
+              o[(mh * 64 + m * 16 + fq * 4 + j) * 64 + nh * 32 + n * 16 + fr] =
+                  gm_f2bf(acc[mh][m][nh][n][j] * sc[mh][m][j]);
     if (EPI == GM_EPI_STORE) {
       GM_LGKM(0);
       __builtin_amdgcn_wave_barrier();

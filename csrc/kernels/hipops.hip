@@ -133,7 +133,7 @@ static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T,
 // swiglu-permuted W (epi 2, C [M][N/2]); A [M][K], W [N][K], bf16.
 template <int EPI, bool STAGGER = true, int SCHED = 1>
 static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st,
-                        int group_m, const GmRope& rp = GmRope{}) {
+                        int group_m, const float* rs = nullptr, const GmRope& rp = GmRope{}) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
@@ -141,23 +141,26 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
     attr = true;
   }
   const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c, M, N, K, group_m, rp);
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c, M, N, K, group_m, rs, rp);
 }
 
 // epi: 0 / 2 = store / SwiGLU; 16 / 32 = store with the round-1 phase
 // schedule / without the wave-row stagger (A/B measurements only).
 static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t stream,
-                      int group_m) {
+                      int group_m, uintptr_t rs) {
   require(group_m >= 1 && group_m <= 64, "gemm: group_m out of range");
   require(M > 0 && N > 0 && K > 0, "gemm: empty operand");
   require(N % GM_BN == 0, "gemm: N must be a multiple of 256");
   require(K % (2 * GM_BK) == 0, "gemm: K must be a multiple of 128");
   require((int64_t)M * K < (int64_t)1 << 30 && (int64_t)N * K < (int64_t)1 << 30, "gemm: operand too large (2 GiB buffer descriptors)");
   require(a % 16 == 0 && w % 16 == 0 && c % 16 == 0, "gemm: pointers must be 16-byte aligned");
+  const float* rsp = rs ? P<const float>(rs) : nullptr;
   if (epi == GM_EPI_STORE)
-    launch_gemm<GM_EPI_STORE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
+    launch_gemm<GM_EPI_STORE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m,
+                              rsp);
   else if (epi == GM_EPI_SWIGLU)
-    launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
+    launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m,
+                               rsp);
   else if (epi == GM_EPI_STORE + 16)
     launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_STORE + 32)
@@ -172,7 +175,7 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
 // intermediate).  W [N][K] in the plain [q | k | v] head order.
 static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr_t pos, uintptr_t slot,
                           uintptr_t cos_t, uintptr_t sin_t, int Hq, int Hkv, int max_ctx, int n_slots,
-                          uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t stream) {
+                          uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t stream, uintptr_t rs) {
   require(M > 0 && K > 0, "gemm_qkv_rope: empty operand");
   require(Hq % 2 == 0 && Hkv % 2 == 0 && Hkv >= 2, "gemm_qkv_rope: head counts must be even");
   require(N == (Hq + 2 * Hkv) * 128, "gemm_qkv_rope: N must be (Hq + 2 Hkv) * 128");
@@ -183,7 +186,17 @@ static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr
   require(max_ctx > 0 && n_slots > 0, "gemm_qkv_rope: bad cache shape");
   GmRope rp{P<const int32_t>(pos), P<const int32_t>(slot), P<const float>(cos_t), P<const float>(sin_t),
             P<uint16_t>(q), P<uint16_t>(kc), P<uint16_t>(vc), Hq, Hkv, max_ctx, n_slots};
-  launch_gemm<GM_EPI_ROPE>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M, rp);
+  launch_gemm<GM_EPI_ROPE>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M,
+                           rs ? P<const float>(rs) : nullptr, rp);
+  check_launch();
+}
+
+static void row_rms(uintptr_t x, uintptr_t r, int T, int D, float eps, uintptr_t stream) {
+  require(T >= 0 && D > 0 && D % 512 == 0, "row_rms expects D % 512 == 0");
+  require(x % 16 == 0 && r % 4 == 0, "row_rms: misaligned pointers");
+  if (T == 0) return;
+  hipLaunchKernelGGL(row_rms_kernel, dim3((T + 3) / 4), dim3(256), 0, S(stream), P<const uint16_t>(x), P<float>(r), T,
+                     D, eps);
   check_launch();
 }
 
@@ -320,8 +333,12 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("silu_mul", &silu_mul, py::arg("gu"), py::arg("out"), py::arg("T"), py::arg("F"), py::arg("stream"),
         py::arg("perm") = false);
   m.def("gemm_bf16", &gemm_bf16, py::arg("a"), py::arg("w"), py::arg("c"), py::arg("M"), py::arg("N"),
-        py::arg("K"), py::arg("epi"), py::arg("stream"), py::arg("group_m") = (int)GM_GROUP_M);
-  m.def("gemm_qkv_rope", &gemm_qkv_rope);
+        py::arg("K"), py::arg("epi"), py::arg("stream"), py::arg("group_m") = (int)GM_GROUP_M, py::arg("rs") = 0);
+  m.def("gemm_qkv_rope", &gemm_qkv_rope, py::arg("a"), py::arg("w"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("pos"), py::arg("slot"), py::arg("cos_t"), py::arg("sin_t"), py::arg("Hq"), py::arg("Hkv"),
+        py::arg("max_ctx"), py::arg("n_slots"), py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("stream"),
+        py::arg("rs") = 0);
+  m.def("row_rms", &row_rms);
   m.attr("GEMM_EPI_STORE") = (int)GM_EPI_STORE;
   m.attr("GEMM_EPI_SWIGLU") = (int)GM_EPI_SWIGLU;
   m.def("rope_kv", &rope_kv);

@@ -93,6 +93,29 @@ rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ res, const
   }
 }
 
+// r[t] = 1 / sqrt(mean(x[t]^2) + eps): the RMSNorm scale only (one wave per
+// row, 4 rows per block).  The fused GEMMs apply it to their accumulator rows
+// with the norm weight folded into W, so the normalised activations are never
+// written (ops/gemm.py row_scale).
+__global__ void __launch_bounds__(256)
+row_rms_kernel(const uint16_t* __restrict__ x, float* __restrict__ r, int T, int D, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= T) return;
+  const int lane = threadIdx.x & 63;
+  const uint16_t* xr = x + (int64_t)row * D;
+  float ss = 0.f;
+  for (int c = lane * 8; c < D; c += 512) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(xr + c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a = bf(v[k]);
+      ss += a * a;
+    }
+  }
+  ss = wave_sum(ss);
+  if (lane == 0) r[row] = rsqrtf(ss / (float)D + eps);
+}
+
 // out[t, i] = silu(gu[t, i]) * gu[t, F + i], 8 elements per thread.
 __global__ void __launch_bounds__(256)
 silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out, int T, int F, int perm) {

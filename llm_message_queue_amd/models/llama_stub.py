@@ -70,7 +70,7 @@ class LlamaStub:
     def __init__(self, cfg: LlamaConfig, slots: int, max_ctx: int, device="cuda", impl: str = "hip",
                  seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False,
                  fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512,
-                 fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048):
+                 fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048, row_scale_norm: bool = True):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -103,6 +103,9 @@ class LlamaStub:
         # rope_kv at T = 4041, slower below ~2k rows: profiles/r2_gemm_swiglu.md)
         self.fused_qkv = (impl == "hip" and not split_qkv) if fused_qkv is None else bool(fused_qkv)
         self.min_fused_qkv_tokens = int(min_fused_qkv_tokens)
+        # fused paths take the raw residual rows + a per-row RMSNorm scale
+        # (True) or an rmsnorm'd copy of the rows (False, A/B)
+        self.row_scale_norm = bool(row_scale_norm)
         g = torch.Generator(device=self.device).manual_seed(seed)
         std = 0.02
 
@@ -115,14 +118,23 @@ class LlamaStub:
         self.final_norm = torch.ones(d, dtype=dtype, device=self.device)
         self.layers = []
         for _ in range(cfg.layers):
-            self.layers.append({
+            L = {
                 "attn_norm": torch.ones(d, dtype=dtype, device=self.device),
                 "wqkv": w((hq + 2 * hkv) * hd, d),
                 "wo": w(d, hq * hd),
                 "mlp_norm": torch.ones(d, dtype=dtype, device=self.device),
-                "w_gu": self._gu_layout(w(2 * cfg.ffn, d)),
+                "w_gu": w(2 * cfg.ffn, d),
                 "w_down": w(d, cfg.ffn),
-            })
+            }
+            # the fused paths read the raw residual rows: the RMSNorm weight
+            # moves into the projection's input columns (W' = W diag(g)) and
+            # the norm left on the small-step path becomes a unit-weight one
+            if self.fused_qkv:
+                L["wqkv"], L["attn_norm"] = self._fold_norm(L["wqkv"], L["attn_norm"])
+            if self.fused_mlp:
+                L["w_gu"], L["mlp_norm"] = self._fold_norm(L["w_gu"], L["mlp_norm"])
+            L["w_gu"] = self._gu_layout(L["w_gu"])
+            self.layers.append(L)
         # KV cache: per layer [slots, kv_heads, max_ctx, head_dim]
         self.kcache = [torch.zeros((slots, hkv, max_ctx, hd), dtype=dtype, device=self.device)
                        for _ in range(cfg.layers)]
@@ -130,6 +142,12 @@ class LlamaStub:
                        for _ in range(cfg.layers)]
         self.cos, self.sin = rope_tables(max_ctx, cfg.rope_theta, self.device)
         self.scale = 1.0 / math.sqrt(hd)
+
+    @staticmethod
+    def _fold_norm(w: torch.Tensor, g: torch.Tensor):
+        if not bool((g == 1).all()):
+            w = (w.float() * g.float()[None, :]).to(w.dtype)
+        return w, torch.ones_like(g)
 
     def _gu_layout(self, w_gu: torch.Tensor) -> torch.Tensor:
         if not self.fused_mlp:
@@ -163,46 +181,73 @@ class LlamaStub:
     def hidden(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
                tiles: Optional[torch.Tensor] = None, n_dec: int = 0) -> torch.Tensor:
         """The 32-layer trunk: final-normed hidden states [T, d] (writes the
-        step's K/V into the cache)."""
+        step's K/V into the cache).
+
+        The residual stream ``res`` is updated in place by the o / down GEMMs.
+        On steps large enough for the hand-written GEMMs, the RMSNorms before
+        the qkv and gate/up projections are never materialised: ``row_rms``
+        computes each row's scale, the norm weight is folded into W at init,
+        and the GEMM epilogue applies the scale to its accumulator rows."""
         cfg, ops = self.cfg, self.ops
-        h = F.embedding(tokens, self.embed)              # [T, d]
+        if not self.residual_in_gemm:
+            return self._hidden_residual_norm(tokens, pos, slot, tiles, n_dec)
+        res = F.embedding(tokens, self.embed)            # [T, d], updated in place
+        T = res.shape[0]
+        rows_qkv = self.fused_qkv and T >= self.min_fused_qkv_tokens
+        rows_mlp = self.fused_mlp and T >= self.min_fused_tokens
+        for i, L in enumerate(self.layers):
+            if rows_qkv and self.row_scale_norm:
+                q = ops.qkv_rope_rows(res, L["wqkv"], ops.row_rms(res, cfg.eps), pos, slot, self.cos, self.sin,
+                                      cfg.heads, cfg.kv_heads, self.kcache[i], self.vcache[i])
+            elif rows_qkv:
+                q = G.qkv_rope(ops.rmsnorm(res, L["attn_norm"], cfg.eps), L["wqkv"], pos, slot, self.cos,
+                               self.sin, cfg.heads, cfg.kv_heads, self.kcache[i], self.vcache[i])
+            else:
+                q = self._qkv(ops.rmsnorm(res, L["attn_norm"], cfg.eps), L, i, pos, slot)
+            res.addmm_(self._attend(q, i, pos, slot, tiles, n_dec), L["wo"].t())
+            if rows_mlp and self.row_scale_norm:
+                act = ops.swiglu_rows(res, L["w_gu"], ops.row_rms(res, cfg.eps))
+            elif rows_mlp:
+                act = G.gemm_swiglu(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"])
+            else:
+                act = ops.mlp_up(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"], self.fused_mlp,
+                                 self.min_fused_tokens)
+            res.addmm_(act, L["w_down"].t())
+        return ops.rmsnorm(res, self.final_norm, cfg.eps)
+
+    def _qkv(self, x, L, i, pos, slot):
+        """qkv projection (hipBLASLt) + RoPE / KV-cache write of normalised rows."""
+        cfg, ops = self.cfg, self.ops
+        if self.split_qkv:
+            nq = cfg.heads * cfg.head_dim
+            qkv = torch.empty((x.shape[0], L["wqkv"].shape[0]), dtype=x.dtype, device=x.device)
+            torch.mm(x, L["wqkv"][:nq].t(), out=qkv[:, :nq])
+            torch.mm(x, L["wqkv"][nq:].t(), out=qkv[:, nq:])
+        else:
+            qkv = F.linear(x, L["wqkv"])
+        return ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
+                           self.kcache[i], self.vcache[i])
+
+    def _attend(self, q, i, pos, slot, tiles, n_dec):
+        cfg, ops = self.cfg, self.ops
+        if tiles is not None:
+            return ops.attention_tiles(q, self.kcache[i], self.vcache[i], tiles, cfg.heads, cfg.kv_heads,
+                                       self.scale, n_dec=n_dec)
+        return ops.attention(q, self.kcache[i], self.vcache[i], pos, slot, cfg.heads, cfg.kv_heads, self.scale)
+
+    def _hidden_residual_norm(self, tokens, pos, slot, tiles, n_dec):
+        """residual_in_gemm=False (A/B only): F.linear o / down projections and
+        residual-add RMSNorm kernels instead of beta = 1 GEMM epilogues."""
+        cfg, ops = self.cfg, self.ops
+        h = F.embedding(tokens, self.embed)
         res = h.clone()
         x = ops.rmsnorm(h, self.layers[0]["attn_norm"], cfg.eps)
         out = None
-        fused = self.residual_in_gemm
         for i, L in enumerate(self.layers):
             if i > 0:
-                x = ops.rmsnorm(res, L["attn_norm"], cfg.eps) if fused else \
-                    ops.rmsnorm(out, L["attn_norm"], cfg.eps, residual=res)
-            if self.fused_qkv and x.shape[0] >= self.min_fused_qkv_tokens:
-                q = G.qkv_rope(x, L["wqkv"], pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
-                             self.kcache[i], self.vcache[i])
-            elif self.split_qkv:
-                nq = cfg.heads * cfg.head_dim
-                qkv = torch.empty((x.shape[0], L["wqkv"].shape[0]), dtype=x.dtype, device=x.device)
-                torch.mm(x, L["wqkv"][:nq].t(), out=qkv[:, :nq])
-                torch.mm(x, L["wqkv"][nq:].t(), out=qkv[:, nq:])
-                q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
-                                self.kcache[i], self.vcache[i])
-            else:
-                qkv = F.linear(x, L["wqkv"])
-                q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads,
-                                self.kcache[i], self.vcache[i])
-            if tiles is not None:
-                a = ops.attention_tiles(q, self.kcache[i], self.vcache[i], tiles, cfg.heads, cfg.kv_heads,
-                                        self.scale, n_dec=n_dec)
-            else:
-                a = ops.attention(q, self.kcache[i], self.vcache[i], pos, slot, cfg.heads, cfg.kv_heads,
-                                  self.scale)
-            if fused:
-                res.addmm_(a, L["wo"].t())
-                x2 = ops.rmsnorm(res, L["mlp_norm"], cfg.eps)
-            else:
-                x2 = ops.rmsnorm(F.linear(a, L["wo"]), L["mlp_norm"], cfg.eps, residual=res)
+                x = ops.rmsnorm(out, L["attn_norm"], cfg.eps, residual=res)
+            a = self._attend(self._qkv(x, L, i, pos, slot), i, pos, slot, tiles, n_dec)
+            x2 = ops.rmsnorm(F.linear(a, L["wo"]), L["mlp_norm"], cfg.eps, residual=res)
             act = ops.mlp_up(x2, L["w_gu"], self.fused_mlp, self.min_fused_tokens)
-            if fused:
-                res.addmm_(act, L["w_down"].t())
-            else:
-                out = F.linear(act, L["w_down"])
-        return ops.rmsnorm(res, self.final_norm, cfg.eps) if fused else \
-            ops.rmsnorm(out, self.final_norm, cfg.eps, residual=res)
+            out = F.linear(act, L["w_down"])
+        return ops.rmsnorm(out, self.final_norm, cfg.eps, residual=res)

@@ -75,7 +75,24 @@ def supported(M: int, N: int, K: int) -> bool:
     return M > 0 and N % TILE_N == 0 and K % 128 == 0
 
 
-def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group_m: int = 8):
+def row_scale_len(M: int) -> int:
+    """Floats a row_scale buffer must hold: the kernel reads whole 256-row
+    tiles of it (rows past M are read but never stored)."""
+    return (M + 255) // 256 * 256
+
+
+def _row_scale_ptr(rs, M: int) -> int:
+    if rs is None:
+        return 0
+    if rs.dtype != torch.float32 or not rs.is_contiguous() or rs.numel() < row_scale_len(M):
+        raise ValueError("row_scale must be a contiguous float32 tensor of >= ceil(M/256)*256 values "
+                         "(ops.llama_ops.HipOps.row_rms pads)")
+    if rs.data_ptr() % 16:
+        raise ValueError("row_scale must be 16-byte aligned")
+    return rs.data_ptr()
+
+
+def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group_m: int = 8, row_scale=None):
     k = _native.require_hipops()
     M, K = x.shape
     N = w.shape[0]
@@ -84,21 +101,25 @@ def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group
     if not supported(M, N, K):
         raise ValueError(f"gemm: unsupported shape M={M} N={N} K={K}")
     k.gemm_bf16(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, epi,
-                torch.cuda.current_stream(x.device).cuda_stream, group_m)
+                torch.cuda.current_stream(x.device).cuda_stream, group_m, _row_scale_ptr(row_scale, M))
     return out
 
 
-def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
-    """x [M][K] · w[N][K]ᵀ -> [M][N] bf16 on the hand-written kernel."""
+def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, row_scale=None) -> torch.Tensor:
+    """x [M][K] · w[N][K]ᵀ -> [M][N] bf16 on the hand-written kernel
+    (``row_scale`` [M] fp32: output row i is multiplied by row_scale[i])."""
     _check(x, "x")
     _check(w, "w")
     y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
     _check(y, "out")
-    return _launch(x, w, y, EPI_STORE)
+    return _launch(x, w, y, EPI_STORE, row_scale=row_scale)
 
 
-def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
-    """silu(x·Wgᵀ) * (x·Wuᵀ) -> [M][F] bf16, ``w_perm`` from :func:`swiglu_permute`."""
+def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None, row_scale=None) -> torch.Tensor:
+    """silu(x·Wgᵀ) * (x·Wuᵀ) -> [M][F] bf16, ``w_perm`` from :func:`swiglu_permute`.
+    ``row_scale`` [M] fp32 scales row i of both products first: with the
+    RMSNorm weight folded into W and row_scale = ``row_rms(x)`` this is the
+    MLP of rmsnorm(x) without materialising the normalised rows."""
     _check(x, "x")
     _check(w_perm, "w_perm")
     F = w_perm.shape[0] // 2
@@ -106,17 +127,18 @@ def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None)
     _check(y, "out")
     if y.shape != (x.shape[0], F):
         raise ValueError("gemm_swiglu: out shape mismatch")
-    return _launch(x, w_perm, y, EPI_SWIGLU)
+    return _launch(x, w_perm, y, EPI_SWIGLU, row_scale=row_scale)
 
 
 def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
              cos_t: torch.Tensor, sin_t: torch.Tensor, Hq: int, Hkv: int,
-             kc: torch.Tensor, vc: torch.Tensor, q_out: torch.Tensor = None) -> torch.Tensor:
+             kc: torch.Tensor, vc: torch.Tensor, q_out: torch.Tensor = None, row_scale=None) -> torch.Tensor:
     """The qkv projection with RoPE + the K/V cache write as its epilogue:
     returns q [T][Hq*128] (rotated) and writes this step's K/V rows into
     ``kc`` / ``vc`` [slots][Hkv][max_ctx][128] -- the same result as
     ``F.linear`` followed by ``HipOps.rope_kv``, without the [T][qkv]
-    intermediate or the second launch."""
+    intermediate or the second launch.  ``row_scale`` as in :func:`gemm_swiglu`
+    (applied to q, k and v before the rotation)."""
     _check(x, "x")
     _check(wqkv, "wqkv")
     for t, n in ((kc, "kc"), (vc, "vc")):
@@ -136,5 +158,5 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
     k = _native.require_hipops()
     k.gemm_qkv_rope(x.data_ptr(), wqkv.data_ptr(), T, wqkv.shape[0], K, pos.data_ptr(), slot.data_ptr(),
                     cos_t.data_ptr(), sin_t.data_ptr(), Hq, Hkv, max_ctx, S, q.data_ptr(), kc.data_ptr(),
-                    vc.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
+                    vc.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream, _row_scale_ptr(row_scale, T))
     return q

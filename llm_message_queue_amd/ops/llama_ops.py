@@ -58,6 +58,28 @@ class HipOps:
         self.k.silu_mul(gu.data_ptr(), y.data_ptr(), T, F, _stream(gu), perm)
         return y
 
+    def row_rms(self, x: torch.Tensor, eps: float) -> torch.Tensor:
+        """1 / sqrt(mean(x^2) + eps) per row (the RMSNorm scale), fp32.  The
+        buffer holds ceil(T/256)*256 floats -- the fused GEMMs read whole
+        256-row tiles of it with vector loads -- and its first T are the
+        scales."""
+        from .gemm import row_scale_len
+        _check(x, torch.bfloat16, "x")
+        T, D = x.shape
+        r = torch.empty(row_scale_len(T), dtype=torch.float32, device=x.device)
+        self.k.row_rms(x.data_ptr(), r.data_ptr(), T, D, float(eps), _stream(x))
+        return r
+
+    def swiglu_rows(self, x, w_perm, r):
+        """The MLP up-projection of rmsnorm(x): one GEMM over the raw rows,
+        the norm weight folded into ``w_perm``, ``r`` applied per row."""
+        from . import gemm as G
+        return G.gemm_swiglu(x, w_perm, row_scale=r)
+
+    def qkv_rope_rows(self, x, wqkv, r, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc):
+        from . import gemm as G
+        return G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, row_scale=r)
+
     def mlp_up(self, x: torch.Tensor, w_gu: torch.Tensor, fused: bool, min_fused_tokens: int) -> torch.Tensor:
         """silu(x·Wgᵀ) * (x·Wuᵀ).  ``fused``: ``w_gu`` is in swiglu order and
         steps of >= ``min_fused_tokens`` rows run the hand-written GEMM with
@@ -149,6 +171,22 @@ class RefOps:
             out.copy_(y)
             return out
         return y
+
+    def row_rms(self, x, eps):
+        xf = x.float()
+        return torch.rsqrt(xf.pow(2).mean(-1) + eps)
+
+    def swiglu_rows(self, x, w_perm, r):
+        """Reference of ``HipOps.swiglu_rows`` (fp32 math, one bf16 rounding)."""
+        from .gemm import swiglu_unpermute
+        w = swiglu_unpermute(w_perm).float()
+        F = w.shape[0] // 2
+        gu = (x.float() * r[:, None]) @ w.t()
+        return (torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]).to(torch.bfloat16)
+
+    def qkv_rope_rows(self, x, wqkv, r, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc):
+        qkv = ((x.float() * r[:, None]) @ wqkv.float().t()).to(torch.bfloat16)
+        return self.rope_kv(qkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc)
 
     def mlp_up(self, x, w_gu, fused: bool, min_fused_tokens: int):
         """Reference of ``HipOps.mlp_up`` (``w_gu`` in swiglu order if fused)."""

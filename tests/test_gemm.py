@@ -66,6 +66,29 @@ def test_fused_mlp_model_matches_unfused_on_ref_ops():
     assert torch.equal(a.hidden(tok, pos, slot), b.hidden(tok, pos, slot))
 
 
+def test_row_scaled_fused_paths_match_rmsnorm_on_ref_ops():
+    """The rows path (row_rms + norm weight folded into W + per-row scale in
+    the fused GEMMs) computes the same trunk as rmsnorm -> GEMM, here on the
+    fp32 reference ops with a non-trivial norm weight."""
+    cfg = LlamaConfig(vocab=512, dim=512, layers=2, heads=4, kv_heads=2, ffn=512)
+    a = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, fused_mlp=True, fused_qkv=True,
+                  min_fused_tokens=1, min_fused_qkv_tokens=1)
+    b = LlamaStub(cfg, slots=2, max_ctx=16, device="cpu", impl="ref", seed=5, fused_mlp=False, fused_qkv=False)
+    g = torch.Generator().manual_seed(3)
+    for La, Lb in zip(a.layers, b.layers):
+        for key in ("attn_norm", "mlp_norm"):
+            gw = (1 + 0.2 * torch.randn(cfg.dim, generator=g)).to(torch.bfloat16)
+            Lb[key] = gw
+        La["wqkv"], _ = LlamaStub._fold_norm(Lb["wqkv"], Lb["attn_norm"])
+        wg, _ = LlamaStub._fold_norm(Lb["w_gu"], Lb["mlp_norm"])
+        La["w_gu"] = G.swiglu_permute(wg)
+    tok = torch.randint(0, cfg.vocab, (12,), generator=torch.Generator().manual_seed(0))
+    pos = torch.tensor(list(range(6)) * 2, dtype=torch.int32)
+    slot = torch.tensor([0] * 6 + [1] * 6, dtype=torch.int32)
+    ha, hb = a.hidden(tok, pos, slot).float(), b.hidden(tok, pos, slot).float()
+    assert ((ha - hb).norm() / hb.norm()).item() < 2e-2
+
+
 def test_gemm_rejects_unsupported_shapes():
     assert G.supported(37, 512, 256)
     assert not G.supported(37, 500, 256)
@@ -207,3 +230,19 @@ def test_serving_shapes_match_fp32():
     assert (q1.float() - q2.float()).abs().max().item() <= tol
     assert (kc1.float() - kc2.float()).abs().max().item() <= tol
     assert (vc1.float() - vc2.float()).abs().max().item() <= tol
+
+
+@pytest.mark.gpu
+def test_row_rms_and_row_scaled_swiglu_match_rmsnorm_path():
+    from llm_message_queue_amd.ops.llama_ops import HipOps
+    ops = HipOps()
+    x, w = _rand(300, 4096, 2 * 1024, seed=21)
+    x = (x.float() * 3.0).to(torch.bfloat16)
+    r = ops.row_rms(x, 1e-5)
+    assert r.numel() == 512                                    # padded to whole 256-row tiles
+    ref_r = torch.rsqrt(x.float().pow(2).mean(-1) + 1e-5)
+    assert torch.allclose(r[:300], ref_r, rtol=1e-4, atol=1e-6)
+    ones = torch.ones(4096, dtype=torch.bfloat16, device=DEV)
+    ref = G.swiglu_reference(ops.rmsnorm(x, ones, 1e-5), w).float()
+    out = G.gemm_swiglu(x, G.swiglu_permute(w), row_scale=r).float()
+    assert (out - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-3
