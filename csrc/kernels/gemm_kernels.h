@@ -456,21 +456,37 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         return smem + ((r >> 7) * 4 + (c >> 6)) * 16384 + (r & 127) * 128 + (c & 63) * 2;
       };
       const int nq = rp.Hq / 2, nk = rp.Hkv / 2;   // 256-column tiles of q / of k heads
+      // Every thread keeps one (head, 8-dim chunk) and walks rows r0 + stride*k:
+      // all row metadata and rotary factors are loaded up front (independent
+      // loads in flight together, not one dependent round trip per row).
       if (tn < nq + nk) {
-        for (int task = tid; task < GM_BM * 16; task += GM_THREADS) {
-          const int r = task >> 4, hh = (task >> 3) & 1, j = task & 7;
+        const int hh = (tid >> 3) & 1, j = tid & 7, r0 = tid >> 4;   // rows r0 + 32k, k < 8
+        int pk[8], sk[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int grow = min(tm * GM_BM + r0 + 32 * k, M - 1);
+          pk[k] = rp.pos[grow];
+          sk[k] = rp.slot[grow];
+        }
+        float4 c0[8], c1[8], s0[8], s1[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int64_t o = (int64_t)min(max(pk[k], 0), rp.max_ctx - 1) * 64 + 8 * j;
+          c0[k] = *reinterpret_cast<const float4*>(rp.cos_t + o);
+          c1[k] = *reinterpret_cast<const float4*>(rp.cos_t + o + 4);
+          s0[k] = *reinterpret_cast<const float4*>(rp.sin_t + o);
+          s1[k] = *reinterpret_cast<const float4*>(rp.sin_t + o + 4);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = r0 + 32 * k;
           const int grow = tm * GM_BM + r;
-          if (grow >= M) continue;
-          const int p = rp.pos[grow], sl = rp.slot[grow];
-          if ((unsigned)sl >= (unsigned)rp.n_slots || (unsigned)p >= (unsigned)rp.max_ctx) continue;
+          const int p = pk[k], sl = sk[k];
+          if (grow >= M || (unsigned)sl >= (unsigned)rp.n_slots || (unsigned)p >= (unsigned)rp.max_ctx) continue;
           const gm_u32x4 lo = *reinterpret_cast<const gm_u32x4*>(at(r, hh * 128 + 8 * j));
           const gm_u32x4 hi = *reinterpret_cast<const gm_u32x4*>(at(r, hh * 128 + 64 + 8 * j));
-          const float4 c0 = *reinterpret_cast<const float4*>(rp.cos_t + (int64_t)p * 64 + 8 * j);
-          const float4 c1 = *reinterpret_cast<const float4*>(rp.cos_t + (int64_t)p * 64 + 8 * j + 4);
-          const float4 s0 = *reinterpret_cast<const float4*>(rp.sin_t + (int64_t)p * 64 + 8 * j);
-          const float4 s1 = *reinterpret_cast<const float4*>(rp.sin_t + (int64_t)p * 64 + 8 * j + 4);
-          const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-          const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float cc[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
+          const float ss[8] = {s0[k].x, s0[k].y, s0[k].z, s0[k].w, s1[k].x, s1[k].y, s1[k].z, s1[k].w};
           gm_u32x4 olo, ohi;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -491,13 +507,21 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
           *reinterpret_cast<gm_u32x4*>(dst + 64 + 8 * j) = ohi;
         }
       } else {
-        for (int task = tid; task < GM_BM * 32; task += GM_THREADS) {
-          const int r = task >> 5, hh = (task >> 4) & 1, cb = task & 15;
+        const int hh = (tid >> 4) & 1, cb = tid & 15, r0 = tid >> 5;  // rows r0 + 16k, k < 16
+        int pk[16], sk[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int grow = min(tm * GM_BM + r0 + 16 * k, M - 1);
+          pk[k] = rp.pos[grow];
+          sk[k] = rp.slot[grow];
+        }
+        const int kvh = 2 * (tn - nq - nk) + hh;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int r = r0 + 16 * k;
           const int grow = tm * GM_BM + r;
-          if (grow >= M) continue;
-          const int p = rp.pos[grow], sl = rp.slot[grow];
-          if ((unsigned)sl >= (unsigned)rp.n_slots || (unsigned)p >= (unsigned)rp.max_ctx) continue;
-          const int kvh = 2 * (tn - nq - nk) + hh;
+          const int p = pk[k], sl = sk[k];
+          if (grow >= M || (unsigned)sl >= (unsigned)rp.n_slots || (unsigned)p >= (unsigned)rp.max_ctx) continue;
           uint16_t* dst = rp.vc + (((int64_t)sl * rp.Hkv + kvh) * rp.max_ctx + p) * 128;
           *reinterpret_cast<gm_u32x4*>(dst + 8 * cb) = *reinterpret_cast<const gm_u32x4*>(at(r, hh * 128 + 8 * cb));
         }
