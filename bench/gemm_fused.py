@@ -107,7 +107,7 @@ def main():
         cos_t, sin_t = rope_tables(max_ctx, 500000.0, dev)
         kc1 = torch.zeros(S, Hkv, max_ctx, 128, dtype=torch.bfloat16, device=dev)
         vc1, kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(kc1), torch.zeros_like(kc1)
-        for T in (37, 1024, 4041):
+        for T in (37, 1024, 2600, 4041):
             x = torch.randn(T, d, device=dev).to(torch.bfloat16)
             cell = torch.randperm(S * 64, device=dev)[:T]               # unique (slot, pos)
             slot = (cell // 64).to(torch.int32)
@@ -121,7 +121,12 @@ def main():
                               "v_max_diff": (vc1[sl, :, ps].float() - vc2[sl, :, ps].float()).abs().max().item()}),
                   flush=True)
             fns = {"hipblaslt+rope_kv": lambda: ops.rope_kv(F.linear(x, wqkv), pos, slot, cos_t, sin_t, Hq, Hkv, kc1, vc1),
-                   "fused": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2)}
+                   "fused": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2),
+                   "fused_nosplit": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2,
+                                                       split=False)}
+            if T <= 1024:   # split every tile: the cost of a K-half + the handoff vs a whole tile
+                fns["fused_allsplit"] = lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2,
+                                                           split_full=0)
             res = {k: [] for k in fns}
             for _ in range(a.rounds):
                 for k, f in fns.items():

@@ -98,6 +98,20 @@ __device__ __forceinline__ void gm_load_row_scales(const float* __restrict__ rs,
   }
 }
 
+// Split-K for the last partial wave of tiles (GM_EPI_ROPE): with 384 tiles on
+// 256 CUs the second wave would run half empty.  Tiles [full, nwg) run as two
+// blocks each over one half of K; the first to finish publishes its fp32
+// accumulators (agent-scope release), the second adds them (acquire) and runs
+// the epilogue -- cdna_hip_programming.md §5 "Projection GEMM" item 2.
+#define GM_CPOL_SC1 16   // cache-policy bit: agent-scope coherent access
+typedef unsigned int gm_u32x4 __attribute__((ext_vector_type(4)));
+
+struct GmSplit {
+  int full;       // tiles [0, full) run whole
+  float* ws;      // [nwg - full][GM_THREADS * 128] fp32 accumulator slabs (nullptr: no split)
+  int* cnt;       // [nwg - full][2]: ticket, ready -- zero at launch; the second half re-zeroes them
+};
+
 typedef __attribute__((address_space(3))) void* gm_lds_ptr;
 
 // One half-tile (128 rows x 64 bf16) global -> LDS: 2 buffer_load ... lds per
@@ -120,16 +134,24 @@ __device__ __forceinline__ void gm_stage(__amdgpu_buffer_rsrc_t rs, uint32_t v0,
 template <int EPI, bool STAGGER = true, int SCHED = 1>
 __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
-    int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp) {
+    int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp) {
   extern __shared__ __align__(16) uint8_t smem[];
 
   const int tiles_m = (M + GM_BM - 1) / GM_BM;
   const int tiles_n = N / GM_BN;
   const int nwg = tiles_m * tiles_n;
-  // XCD-contiguous remap (bijective for any nwg), then 8-M-tile grouping
+  const int full = sp.ws ? sp.full : nwg;
+  // XCD-contiguous remap (bijective for any count) of the whole tiles, then
+  // 8-M-tile grouping; split tiles take two consecutive blocks
   const int bid = blockIdx.x;
-  const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
-  const int pid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  int pid, khalf = -1;
+  if (bid < full) {
+    const int xcd = bid & 7, loc = bid >> 3, q8 = full >> 3, r8 = full & 7;
+    pid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  } else {
+    pid = full + ((bid - full) >> 1);
+    khalf = (bid - full) & 1;
+  }
   const int group = pid / (group_m * tiles_n);
   const int first_m = group * group_m;
   const int gsize = min(tiles_m - first_m, group_m);
@@ -190,7 +212,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 
 #define GM_STAGE(BUF, HALF, KT)                                                               \
   do {                                                                                        \
-    const uint32_t _ko = (uint32_t)(KT) * (GM_BK * 2);                                        \
+    const uint32_t _ko = (uint32_t)((KT) + kt0) * (GM_BK * 2);                                \
     const uint32_t _b = (uint32_t)(BUF) * GM_BUF_BYTES + (uint32_t)(HALF) * GM_HALF_BYTES;   \
     if constexpr ((HALF) < 2)                                                                 \
       gm_stage(rsa, va[(HALF)][0], va[(HALF)][1], _ko, smem, _b + dst_i0, _b + dst_i1);       \
@@ -245,7 +267,9 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 #define GM_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
 #define GM_VMCNT(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
 
-  const int nt = K / GM_BK;                        // even (K % 128 == 0 checked by host)
+  // K-tiles of this block: all, or one half for a split tile (host: nt % 4 == 0)
+  const int nt = khalf < 0 ? K / GM_BK : K / GM_BK / 2;
+  const int kt0 = khalf > 0 ? nt : 0;
 
   if constexpr (SCHED == 1) {
     // Balanced schedule: every phase retires the half-tile staged 3 phases
@@ -387,6 +411,69 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 
 
   if (STAGGER && wr == 0) GM_BARRIER();
+
+  // ---- split tile: the first K-half to finish hands its accumulators over
+  if (khalf >= 0) {
+    const int tix = pid - full;
+    int* cnt = sp.cnt + 2 * tix;
+    if (tid == 0) *reinterpret_cast<int*>(smem) =
+        __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int ticket = *reinterpret_cast<volatile int*>(smem);
+    __syncthreads();
+    // The slab moves with agent-scope (sc1) stores / loads -- written through
+    // and read past this XCD's L2 (the halves run on different XCDs) -- so
+    // neither side needs the whole-L2 write-back / invalidate of an
+    // agent-scope fence (measured: 156 vs 160 us at T=4041, fences cost L2
+    // hits for every block on the XCD).  Order: all slab stores acknowledged
+    // (vmcnt 0) -> barrier -> ready flag; the reader sees the flag before
+    // its barrier and then loads.
+    float* slab = sp.ws + (size_t)tix * GM_THREADS * 128;
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, GM_THREADS * 32 * 16, 0x00020000);
+    if (ticket == 0) {                             // first: publish, then leave
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int d = 0; d < 2; ++d)
+            {
+              const int i = ((a * 4 + b) * 4 + c * 2 + d) * GM_THREADS + tid;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gm_u32x4, acc[a][b][c][d]), srs, i * 16,
+                                                     0, GM_CPOL_SC1);
+            }
+      GM_VMCNT(0);
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {                                // second: wait for the slab (bounded)
+      for (int spin = 0; spin < (1 << 24); ++spin) {
+        if (__hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      GM_VMCNT(0);
+      // both halves are done with the counters: leave them zeroed for the next launch
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int d = 0; d < 2; ++d)
+          {
+            const int i = ((a * 4 + b) * 4 + c * 2 + d) * GM_THREADS + tid;
+            acc[a][b][c][d] += __builtin_bit_cast(gm_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                   srs, i * 16, 0, GM_CPOL_SC1));
+          }
+  }
 
   // ---- epilogue through LDS (the staging buffers are free after the last barrier)
   const int row0 = tm * GM_BM + wr * 128;          // first output row of this wave

@@ -133,7 +133,8 @@ static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T,
 // swiglu-permuted W (epi 2, C [M][N/2]); A [M][K], W [N][K], bf16.
 template <int EPI, bool STAGGER = true, int SCHED = 1>
 static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st,
-                        int group_m, const float* rs = nullptr, const GmRope& rp = GmRope{}) {
+                        int group_m, const float* rs = nullptr, const GmRope& rp = GmRope{},
+                        const GmSplit& sp = GmSplit{0, nullptr, nullptr}) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
@@ -141,7 +142,9 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
     attr = true;
   }
   const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c, M, N, K, group_m, rs, rp);
+  const int grid = sp.ws ? sp.full + 2 * (tiles - sp.full) : tiles;
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(grid), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c,
+                     M, N, K, group_m, rs, rp, sp);
 }
 
 // epi: 0 / 2 = store / SwiGLU; 16 / 32 = store with the round-1 phase
@@ -175,7 +178,8 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
 // intermediate).  W [N][K] in the plain [q | k | v] head order.
 static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr_t pos, uintptr_t slot,
                           uintptr_t cos_t, uintptr_t sin_t, int Hq, int Hkv, int max_ctx, int n_slots,
-                          uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t stream, uintptr_t rs) {
+                          uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t stream, uintptr_t rs,
+                          int split_full, uintptr_t split_ws, uintptr_t split_cnt) {
   require(M > 0 && K > 0, "gemm_qkv_rope: empty operand");
   require(Hq % 2 == 0 && Hkv % 2 == 0 && Hkv >= 2, "gemm_qkv_rope: head counts must be even");
   require(N == (Hq + 2 * Hkv) * 128, "gemm_qkv_rope: N must be (Hq + 2 Hkv) * 128");
@@ -186,8 +190,16 @@ static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr
   require(max_ctx > 0 && n_slots > 0, "gemm_qkv_rope: bad cache shape");
   GmRope rp{P<const int32_t>(pos), P<const int32_t>(slot), P<const float>(cos_t), P<const float>(sin_t),
             P<uint16_t>(q), P<uint16_t>(kc), P<uint16_t>(vc), Hq, Hkv, max_ctx, n_slots};
+  GmSplit sp{0, nullptr, nullptr};
+  if (split_ws) {
+    const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+    require(split_full >= 0 && split_full < tiles, "gemm_qkv_rope: bad split");
+    require((K / GM_BK) % 4 == 0 && K / GM_BK >= 8, "gemm_qkv_rope: split-K needs K % 256 == 0 and K >= 512");
+    require(split_cnt != 0 && split_ws % 16 == 0, "gemm_qkv_rope: split workspace");
+    sp = GmSplit{split_full, P<float>(split_ws), P<int>(split_cnt)};
+  }
   launch_gemm<GM_EPI_ROPE>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M,
-                           rs ? P<const float>(rs) : nullptr, rp);
+                           rs ? P<const float>(rs) : nullptr, rp, sp);
   check_launch();
 }
 
@@ -337,7 +349,7 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("gemm_qkv_rope", &gemm_qkv_rope, py::arg("a"), py::arg("w"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("pos"), py::arg("slot"), py::arg("cos_t"), py::arg("sin_t"), py::arg("Hq"), py::arg("Hkv"),
         py::arg("max_ctx"), py::arg("n_slots"), py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("stream"),
-        py::arg("rs") = 0);
+        py::arg("rs") = 0, py::arg("split_full") = 0, py::arg("split_ws") = 0, py::arg("split_cnt") = 0);
   m.def("row_rms", &row_rms);
   m.attr("GEMM_EPI_STORE") = (int)GM_EPI_STORE;
   m.attr("GEMM_EPI_SWIGLU") = (int)GM_EPI_SWIGLU;

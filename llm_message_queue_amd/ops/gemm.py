@@ -15,6 +15,8 @@ CPU / reference path: :func:`swiglu_reference` (fp32 math of the same op).
 """
 from __future__ import annotations
 
+import functools
+
 import torch
 
 from .. import _native
@@ -130,15 +132,61 @@ def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None,
     return _launch(x, w_perm, y, EPI_SWIGLU, row_scale=row_scale)
 
 
+TILE_M = 256
+_SPLIT_WS = {}
+
+
+def split_plan(M: int, N: int, K: int, cus: int):
+    """Split-K for the last, partial wave of tiles: returns ``full`` (tiles
+    run whole) or None.  The kernel holds one block per CU, so ``tiles`` over
+    ``cus`` CUs is ceil(tiles / cus) waves; when the last wave is at most half
+    full its tiles run as two blocks over one K-half each (one wave of
+    ``cus`` becomes half a wave).  qkv at the serving shape: 16 x 24 = 384
+    tiles on 256 CUs -> 256 whole + 128 split."""
+    tiles = (M + TILE_M - 1) // TILE_M * (N // TILE_N)
+    tail = tiles % cus
+    if tiles <= cus or tail == 0 or 2 * tail > cus or K % 256 or K < 512:
+        return None
+    return tiles - tail
+
+
+def _split_workspace(device, n_split: int, cus: int):
+    """fp32 slabs (256 KiB per split tile) + zeroed ticket/ready counters,
+    cached per device and sized for the largest possible tail (cus / 2).
+    The kernel re-zeroes the counters it used, so launches on ONE stream
+    can share them; qkv_rope is only issued from the engine's stream."""
+    key = (device.type, device.index)
+    ws = _SPLIT_WS.get(key)
+    if ws is None:
+        cap = cus // 2
+        ws = (torch.empty(cap * 512 * 128, dtype=torch.float32, device=device),
+              torch.zeros(cap * 2, dtype=torch.int32, device=device))
+        _SPLIT_WS[key] = ws
+    if n_split > ws[1].numel() // 2:
+        raise ValueError("split workspace too small")
+    return ws
+
+
+@functools.lru_cache(maxsize=None)
+def _cu_count_idx(index: int) -> int:
+    return torch.cuda.get_device_properties(index).multi_processor_count
+
+
+def _cu_count(device) -> int:
+    return _cu_count_idx(device.index if device.index is not None else torch.cuda.current_device())
+
+
 def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
              cos_t: torch.Tensor, sin_t: torch.Tensor, Hq: int, Hkv: int,
-             kc: torch.Tensor, vc: torch.Tensor, q_out: torch.Tensor = None, row_scale=None) -> torch.Tensor:
+             kc: torch.Tensor, vc: torch.Tensor, q_out: torch.Tensor = None, row_scale=None,
+             split: bool = True, split_full: int = None) -> torch.Tensor:
     """The qkv projection with RoPE + the K/V cache write as its epilogue:
     returns q [T][Hq*128] (rotated) and writes this step's K/V rows into
     ``kc`` / ``vc`` [slots][Hkv][max_ctx][128] -- the same result as
     ``F.linear`` followed by ``HipOps.rope_kv``, without the [T][qkv]
     intermediate or the second launch.  ``row_scale`` as in :func:`gemm_swiglu`
-    (applied to q, k and v before the rotation)."""
+    (applied to q, k and v before the rotation).  ``split``: run a partial
+    last wave of tiles split-K (:func:`split_plan`)."""
     _check(x, "x")
     _check(wqkv, "wqkv")
     for t, n in ((kc, "kc"), (vc, "vc")):
@@ -156,7 +204,17 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
     q = q_out if q_out is not None else torch.empty((T, Hq * 128), dtype=x.dtype, device=x.device)
     _check(q, "q_out")
     k = _native.require_hipops()
-    k.gemm_qkv_rope(x.data_ptr(), wqkv.data_ptr(), T, wqkv.shape[0], K, pos.data_ptr(), slot.data_ptr(),
+    N = wqkv.shape[0]
+    full, ws, cnt = 0, 0, 0
+    if split:
+        cus = _cu_count(x.device)
+        f = split_plan(T, N, K, cus) if split_full is None else split_full
+        if f is not None:
+            n_split = (T + TILE_M - 1) // TILE_M * (N // TILE_N) - f
+            w_t, c_t = _split_workspace(x.device, n_split, cus)
+            full, ws, cnt = f, w_t.data_ptr(), c_t.data_ptr()
+    k.gemm_qkv_rope(x.data_ptr(), wqkv.data_ptr(), T, N, K, pos.data_ptr(), slot.data_ptr(),
                     cos_t.data_ptr(), sin_t.data_ptr(), Hq, Hkv, max_ctx, S, q.data_ptr(), kc.data_ptr(),
-                    vc.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream, _row_scale_ptr(row_scale, T))
+                    vc.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream, _row_scale_ptr(row_scale, T),
+                    full, ws, cnt)
     return q

@@ -232,6 +232,46 @@ def test_serving_shapes_match_fp32():
     assert (vc1.float() - vc2.float()).abs().max().item() <= tol
 
 
+def test_split_plan_only_splits_a_half_empty_last_wave():
+    assert G.split_plan(4041, 6144, 4096, 256) == 256          # 384 tiles: 256 whole + 128 split
+    assert G.split_plan(2600, 6144, 4096, 256) == 256          # 264 tiles: 8 split
+    assert G.split_plan(2048, 6144, 4096, 256) is None         # 192 tiles: one wave already
+    assert G.split_plan(4096, 8192, 4096, 256) is None         # 512 tiles: two full waves
+    assert G.split_plan(5000, 6144, 4096, 256) is None         # 480 tiles: tail 224 > half
+    assert G.split_plan(4041, 6144, 384, 256) is None          # K too short to halve
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [2600, 4041])
+def test_qkv_rope_split_k_tail_matches_unsplit(T):
+    """The split-K last wave (two blocks per tile over one K-half each,
+    fp32 handoff through a workspace) == the unsplit kernel, over repeated
+    launches (the counters are re-zeroed by the kernel itself)."""
+    from llm_message_queue_amd.ops.llama_ops import rope_tables
+    d, Hq, Hkv, max_ctx, S = 4096, 32, 8, 64, 128
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if G.split_plan(T, (Hq + 2 * Hkv) * 128, d, cus) is None:
+        pytest.skip(f"no split on {cus} CUs")
+    g = torch.Generator(device=DEV).manual_seed(T)
+    x = torch.randn(T, d, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn((Hq + 2 * Hkv) * 128, d, generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    cos_t, sin_t = rope_tables(max_ctx, 500000.0, DEV)
+    cell = torch.randperm(S * max_ctx, generator=g, device=DEV)[:T]
+    slot, pos = (cell // max_ctx).to(torch.int32), (cell % max_ctx).to(torch.int32)
+    kc1 = torch.zeros(S, Hkv, max_ctx, 128, dtype=torch.bfloat16, device=DEV)
+    vc1 = torch.zeros_like(kc1)
+    q1 = G.qkv_rope(x, w, pos, slot, cos_t, sin_t, Hq, Hkv, kc1, vc1, split=False)
+    for it in range(3):
+        kc2, vc2 = torch.zeros_like(kc1), torch.zeros_like(kc1)
+        q2 = G.qkv_rope(x, w, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2, split=True)
+        tol = 0.01 * q1.float().abs().max().item()
+        assert (q1.float() - q2.float()).abs().max().item() <= tol, it
+        assert (kc1.float() - kc2.float()).abs().max().item() <= tol, it
+        assert (vc1.float() - vc2.float()).abs().max().item() <= tol, it
+    _, cnt = G._SPLIT_WS[("cuda", 0)]
+    assert int(cnt.abs().sum()) == 0                             # left zeroed for the next launch
+
+
 @pytest.mark.gpu
 def test_row_rms_and_row_scaled_swiglu_match_rmsnorm_path():
     from llm_message_queue_amd.ops.llama_ops import HipOps
