@@ -20,6 +20,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="64,256,1024,4096")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--split", action="store_true",
+                    help="time begin_batch / end_batch host work separately (the serve loop's async ingest: "
+                         "the GPU wait is not on the host), plus a cProfile of both")
+    ap.add_argument("--profile", action="store_true", help="with --split: cProfile the host work")
     a = ap.parse_args()
     import torch
 
@@ -46,6 +50,44 @@ def main() -> None:
 
     th = threading.Thread(target=load, daemon=True)
     th.start()
+    if a.split:
+        import cProfile
+        import pstats
+        for B in [int(s) for s in a.sizes.split(",")]:
+            for mode in ("idle", "busy"):
+                (busy.set if mode == "busy" else busy.clear)()
+                time.sleep(0.05)
+                pre.process_batch(wl.make(B), use_gpu=True, prompt_cap=32)
+                tb = te = 0.0
+                prof = cProfile.Profile() if a.profile else None
+                for _ in range(a.reps):
+                    msgs = wl.make(B)
+                    t0 = time.perf_counter()
+                    if prof:
+                        prof.enable()
+                    tok = pre.begin_batch(msgs, prompt_cap=32)
+                    if prof:
+                        prof.disable()
+                    tb += time.perf_counter() - t0
+                    while not pre.batch_ready(tok):
+                        time.sleep(0.0002)
+                    t0 = time.perf_counter()
+                    if prof:
+                        prof.enable()
+                    pre.end_batch(tok)
+                    if prof:
+                        prof.disable()
+                    te += time.perf_counter() - t0
+                print(json.dumps({"batch": B, "gpu": mode, "begin_us": round(tb / a.reps * 1e6, 1),
+                                  "end_us": round(te / a.reps * 1e6, 1),
+                                  "host_us_per_msg": round((tb + te) / a.reps / B * 1e6, 2)}), flush=True)
+                if prof:
+                    st = pstats.Stats(prof)
+                    print(f"--- cProfile B={B} {mode} (tottime, per 1 batch = /{a.reps})")
+                    st.sort_stats("tottime").print_stats(14)
+        stop.set()
+        th.join(timeout=5)
+        return
     for B in [int(s) for s in a.sizes.split(",")]:
         for mode in ("idle", "busy"):
             (busy.set if mode == "busy" else busy.clear)()

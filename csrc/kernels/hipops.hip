@@ -42,7 +42,9 @@ static void require(bool cond, const char* what) {
 
 // ---------------------------------------------------------------------- text
 static void text_analyze(uintptr_t bytes, uintptr_t offsets, int B, int L, py::bytes table,
-                         uintptr_t stats, uintptr_t hashes, uintptr_t stream) {
+                         uintptr_t stats, uintptr_t hashes, uintptr_t stream, uintptr_t zero_rows = 0,
+                         int zero_len = 0) {
+  require(zero_rows == 0 || (zero_len > 0 && zero_len % 4 == 0 && zero_rows % 16 == 0), "bad zero_rows");
   std::string t = table;
   require(t.size() == sizeof(PatternTable), "pattern table size mismatch");
   require(B >= 0 && L > 0, "bad B/L");
@@ -56,7 +58,8 @@ static void text_analyze(uintptr_t bytes, uintptr_t offsets, int B, int L, py::b
   if (B == 0) return;
   const int grid = (B + TA_WAVES - 1) / TA_WAVES;
   hipLaunchKernelGGL(text_analyze_kernel, dim3(grid), dim3(256), 0, S(stream), P<const uint8_t>(bytes),
-                     P<const int64_t>(offsets), B, L, pt, P<int32_t>(stats), P<uint32_t>(hashes));
+                     P<const int64_t>(offsets), B, L, pt, P<int32_t>(stats), P<uint32_t>(hashes),
+                     P<float>(zero_rows), zero_len);
   check_launch();
 }
 
@@ -92,6 +95,37 @@ static void classify_head(uintptr_t pooled, int B, int H, uintptr_t W2, uintptr_
   if (B == 0) return;
   hipLaunchKernelGGL(classify_head_kernel, dim3((B + 3) / 4), dim3(256), 0, S(stream), P<const float>(pooled),
                      B, H, P<const float>(W2), P<const float>(b2), P<float>(logits), P<int32_t>(pred));
+  check_launch();
+}
+
+static void copy_bytes(uintptr_t dst, uintptr_t src, int64_t n, uintptr_t stream);
+
+// The whole GPU preprocess chain of one micro-batch in ONE host call (the
+// serve loop's ingest path: one pybind crossing, no per-batch tensor
+// allocations, six launches): copy from host-mapped staging, text_analyze
+// (zeroing the pooled rows), row scan, embed_pool, classify_head, one
+// readback kernel into host-mapped memory.  The caller records the event.
+static void text_batch(uintptr_t staging, uintptr_t dev_bytes, int64_t total, int64_t off_offsets, int B, int L,
+                       py::bytes table, uintptr_t stats, uintptr_t hashes, bool classify, uintptr_t row_off,
+                       int rows_upper, uintptr_t E, int V, uintptr_t W1t, uintptr_t b1, int H, uintptr_t pooled,
+                       uintptr_t W2, uintptr_t b2, uintptr_t logits, uintptr_t pred, int cap, uintptr_t rb,
+                       int64_t o_pred, int64_t o_ph, uintptr_t stream) {
+  require(B > 0 && cap >= 0 && cap <= L, "text_batch: bad B / cap");
+  require(off_offsets % 8 == 0 && off_offsets + 8 * (int64_t)(B + 1) <= total, "text_batch: offsets placement");
+  require(o_pred >= (int64_t)B * TA_STAT_COLS && o_ph >= o_pred + (classify ? B : 0), "text_batch: readback layout");
+  copy_bytes(dev_bytes, staging, total, stream);
+  text_analyze(dev_bytes, dev_bytes + off_offsets, B, L, table, stats, hashes, stream, classify ? pooled : 0,
+               classify ? H : 0);
+  if (classify) {
+    scan_rows(stats + 4 * ST_NTOK, TA_STAT_COLS, B, row_off, stream);
+    embed_pool(hashes, L, row_off, B, rows_upper, E, V, W1t, b1, H, pooled, stream);
+    classify_head(pooled, B, H, W2, b2, logits, pred, stream);
+  }
+  const int64_t n = (int64_t)B * TA_STAT_COLS + (classify ? B : 0) + (int64_t)B * cap;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(text_readback_kernel, dim3(blocks), dim3(256), 0, S(stream), P<const int32_t>(stats),
+                     classify ? P<const int32_t>(pred) : nullptr, P<const uint32_t>(hashes), B, L, cap,
+                     P<int32_t>(rb), o_pred, o_ph);
   check_launch();
 }
 
@@ -335,7 +369,10 @@ PYBIND11_MODULE(_hipops, m) {
   m.attr("STAT_COLS") = TA_STAT_COLS;
   m.attr("SLOTS") = TA_SLOTS;
   m.attr("MAX_TOKEN_BYTES") = TA_MAX_TOKEN_BYTES;
-  m.def("text_analyze", &text_analyze);
+  m.def("text_analyze", &text_analyze, py::arg("bytes"), py::arg("offsets"), py::arg("B"), py::arg("L"),
+        py::arg("table"), py::arg("stats"), py::arg("hashes"), py::arg("stream"), py::arg("zero_rows") = 0,
+        py::arg("zero_len") = 0);
+  m.def("text_batch", &text_batch);
   m.def("scan_rows", &scan_rows);
   m.def("embed_pool", &embed_pool);
   m.def("classify_head", &classify_head);

@@ -137,13 +137,17 @@ __device__ __forceinline__ bool word_prefix_eq(const uint32_t (&wl)[4], const Wo
 __global__ void __launch_bounds__(256)
 text_analyze_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
                     int B, int L, PatternTable pt, int32_t* __restrict__ stats,
-                    uint32_t* __restrict__ hashes) {
+                    uint32_t* __restrict__ hashes, float* __restrict__ zero_rows, int zero_len) {
   __shared__ uint32_t win32[TA_WAVES][TA_WIN / 4];
   __shared__ int32_t next_ok[TA_WAVES][TA_MAX_PAT];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int msg = blockIdx.x * TA_WAVES + wv;
   if (msg >= B) return;  // whole wave exits together (msg is wave-uniform)
+  if (zero_rows) {       // the classifier's pooled row of this message (embed_pool accumulates into it)
+    float4* z = reinterpret_cast<float4*>(zero_rows + (int64_t)msg * zero_len);
+    for (int i = lane; i < zero_len / 4; i += 64) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   uint8_t* win8 = reinterpret_cast<uint8_t*>(win32[wv]);
 
   const int64_t start = offsets[msg];
@@ -308,6 +312,33 @@ text_analyze_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict
 #pragma unroll
     for (int s = 0; s < TA_SLOTS; ++s) st[ST_SCORES + s] = score[s];
   }
+}
+
+// One readback of a preprocess batch into host-mapped memory: stats rows,
+// classifier predictions at o_pred, the first `cap` token hashes of every
+// message at o_ph (int32 offsets into dst).  Replaces three copies and the
+// strided-slice gather of the per-launch path.
+__global__ void __launch_bounds__(256)
+text_readback_kernel(const int32_t* __restrict__ stats, const int32_t* __restrict__ pred,
+                     const uint32_t* __restrict__ hashes, int B, int L, int cap, int32_t* __restrict__ dst,
+                     int64_t o_pred, int64_t o_ph) {
+  const int64_t n_st = (int64_t)B * TA_STAT_COLS;
+  const int64_t n_pr = pred ? B : 0;
+  const int64_t n_ph = (int64_t)B * cap;
+  const int64_t n = n_st + n_pr + n_ph;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    if (i < n_st) {
+      dst[i] = stats[i];
+    } else if (i < n_st + n_pr) {
+      dst[o_pred + (i - n_st)] = pred[i - n_st];
+    } else {
+      const int64_t k = i - n_st - n_pr;
+      const int64_t b = k / cap, c = k - b * cap;
+      dst[o_ph + k] = (int32_t)hashes[b * L + c];
+    }
+  }
+  __threadfence_system();   // visible to the host once the stream's event completes
 }
 
 }  // namespace llmq
