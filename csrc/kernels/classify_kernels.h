@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256)
 embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __restrict__ row_off,
                   int B, const uint16_t* __restrict__ E, uint32_t vmask,
                   const uint16_t* __restrict__ W1t, const float* __restrict__ b1, int H,
-                  float* __restrict__ pooled) {
+                  float* __restrict__ pooled, const int32_t* __restrict__ ntok_src, int ntok_stride) {
   extern __shared__ __align__(16) uint8_t smem[];
   uint16_t* At = reinterpret_cast<uint16_t*>(smem);                       // 64 x 256 bf16 (32 KiB)
   float* Hs = reinterpret_cast<float*>(smem + EP_TM * EP_D * 2);          // 64 x 260 f32 (65 KiB)
@@ -101,7 +101,36 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  const int total = row_off[B];
+  // row_off: the global scan, or (ntok_src != nullptr) this block's own
+  // exclusive scan of the B token counts in LDS -- every block redoes the
+  // few-hundred-element scan instead of a separate single-block launch
+  const int32_t* ro = row_off;
+  if (ntok_src) {
+    __shared__ int32_t wtot[4];
+    int32_t* roff = rinfo + EP_TM;                                          // [B + 1] ints
+    int carry = 0;
+    for (int base = 0; base < B; base += 256) {
+      const int i = base + tid;
+      const int v = i < B ? ntok_src[(int64_t)i * ntok_stride] : 0;
+      int x = v;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      if (lane == 63) wtot[wv] = x;
+      __syncthreads();
+      int wpre = 0;
+      for (int k = 0; k < wv; ++k) wpre += wtot[k];
+      if (i < B) roff[i] = carry + wpre + x - v;
+      carry += wtot[0] + wtot[1] + wtot[2] + wtot[3];
+      __syncthreads();                                                      // wtot reuse
+    }
+    if (tid == 0) roff[B] = carry;
+    __syncthreads();
+    ro = roff;
+  }
+  const int total = ro[B];
   const int tile0 = blockIdx.x * EP_TM;
   if (tile0 >= total) return;  // uniform across the block
   const int rows = min(EP_TM, total - tile0);
@@ -114,7 +143,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
       int lo = 0, hi = B - 1;
       while (lo < hi) {  // largest m with row_off[m] <= g
         const int mid = (lo + hi + 1) >> 1;
-        if (row_off[mid] <= g) lo = mid; else hi = mid - 1;
+        if (ro[mid] <= g) lo = mid; else hi = mid - 1;
       }
       m = lo;
     }
@@ -130,7 +159,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     const int m = rmsg[r];
     if (m >= 0) {
-      const int tok = tile0 + r - row_off[m];
+      const int tok = tile0 + r - ro[m];
       const uint32_t bucket = hashes[(int64_t)m * L + tok] & vmask;
       v = *reinterpret_cast<const uint4*>(E + (int64_t)bucket * EP_D + ch * 8);
     }
@@ -196,7 +225,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
       for (int r = 0; r < rows; ++r) {
         const int m = rmsg[r];
         if (m != cur) {
-          const int a = row_off[cur], b = row_off[cur + 1];
+          const int a = ro[cur], b = ro[cur + 1];
           const float v = run / (float)(b - a);
           float* dst = pooled + (int64_t)cur * H + n0 + col;
           if (a >= tile0 && b <= tile0 + rows) *dst = v; else atomicAdd(dst, v);
@@ -206,7 +235,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
         run += Hs[r * EP_HS_STRIDE + col];
       }
       if (cur >= 0) {
-        const int a = row_off[cur], b = row_off[cur + 1];
+        const int a = ro[cur], b = ro[cur + 1];
         const float v = run / (float)(b - a);
         float* dst = pooled + (int64_t)cur * H + n0 + col;
         if (a >= tile0 && b <= tile0 + rows) *dst = v; else atomicAdd(dst, v);
@@ -216,14 +245,30 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   }
 }
 
+// Optional readback into host-mapped memory (int32 offsets into dst): stats
+// rows at 0, predictions at o_pred, the first `cap` token hashes at o_ph.
+struct ClassifyReadback {
+  int32_t* dst;                 // nullptr: no readback
+  const int32_t* stats;
+  const uint32_t* hashes;
+  int stat_cols, L, cap;
+  int64_t o_pred, o_ph;
+};
+
 // logits[b, 0:8] = pooled[b] . W2 + b2 ; pred[b] = 1 + argmax(logits[b, 0:4])
 // One wave per message; lane l covers 16 hidden units.
 __global__ void __launch_bounds__(256)
 classify_head_kernel(const float* __restrict__ pooled, int B, int H, const float* __restrict__ W2,
-                     const float* __restrict__ b2, float* __restrict__ logits, int32_t* __restrict__ pred) {
+                     const float* __restrict__ b2, float* __restrict__ logits, int32_t* __restrict__ pred,
+                     const ClassifyReadback rb) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
+  if (rb.dst) {         // the batch's readback rides along: stats row + prompt hashes of message b
+    if (lane < rb.stat_cols) rb.dst[(int64_t)b * rb.stat_cols + lane] = rb.stats[(int64_t)b * rb.stat_cols + lane];
+    for (int c = lane; c < rb.cap; c += 64)
+      rb.dst[rb.o_ph + (int64_t)b * rb.cap + c] = (int32_t)rb.hashes[(int64_t)b * rb.L + c];
+  }
   float part[8];
 #pragma unroll
   for (int o = 0; o < 8; ++o) part[o] = 0.f;
@@ -249,7 +294,9 @@ classify_head_kernel(const float* __restrict__ pooled, int B, int H, const float
       if (o < 4 && v > bv) { bv = v; best = o; }
     }
     pred[b] = best + 1;
+    if (rb.dst) rb.dst[rb.o_pred + b] = best + 1;
   }
+  if (rb.dst) __threadfence_system();   // host-mapped: visible once the stream's event completes
 }
 
 }  // namespace llmq

@@ -71,30 +71,41 @@ static void scan_rows(uintptr_t ntok, int stride, int B, uintptr_t row_off, uint
 }
 
 static bool g_embed_attr = false;
+static constexpr size_t EP_SMEM_BASE = EP_TM * EP_D * 2 + EP_TM * EP_HS_STRIDE * 4 + 2 * EP_TM * 4 + 16;
+static constexpr size_t EP_SMEM_MAX = 160 * 1024 - 256;   // static __shared__ of the kernel counts too
+// largest batch whose row offsets fit in LDS next to the tile (in-block scan)
+static constexpr int EP_MAX_LDS_SCAN = (int)((EP_SMEM_MAX - EP_SMEM_BASE) / 4) - 1;
+
+// ntok_src != 0: row_off is not read; every block scans the B token counts
+// (ntok_src[i * ntok_stride]) into LDS itself (no scan_rows launch).
 static void embed_pool(uintptr_t hashes, int L, uintptr_t row_off, int B, int rows_upper, uintptr_t E,
-                       int V, uintptr_t W1t, uintptr_t b1, int H, uintptr_t pooled, uintptr_t stream) {
+                       int V, uintptr_t W1t, uintptr_t b1, int H, uintptr_t pooled, uintptr_t stream,
+                       uintptr_t ntok_src = 0, int ntok_stride = 0) {
   require(V > 0 && (V & (V - 1)) == 0, "vocab buckets must be a power of two");
   require(H % EP_NCHUNK == 0, "hidden dim must be a multiple of 256");
   require(B >= 0 && rows_upper >= 0, "bad sizes");
+  require(ntok_src == 0 || (ntok_stride >= 1 && B <= EP_MAX_LDS_SCAN), "embed_pool: in-block scan bounds");
+  require(ntok_src != 0 || row_off != 0, "embed_pool: row_off or ntok_src");
   if (B == 0 || rows_upper == 0) return;
-  const size_t smem = EP_TM * EP_D * 2 + EP_TM * EP_HS_STRIDE * 4 + 2 * EP_TM * 4 + 16;
+  const size_t smem = EP_SMEM_BASE + (ntok_src ? 4 * ((size_t)B + 1) : 0);
   if (!g_embed_attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)embed_pool_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)EP_SMEM_MAX));
     g_embed_attr = true;
   }
   const int grid = (rows_upper + EP_TM - 1) / EP_TM;
   hipLaunchKernelGGL(embed_pool_kernel, dim3(grid), dim3(256), smem, S(stream), P<const uint32_t>(hashes),
                      L, P<const int32_t>(row_off), B, P<const uint16_t>(E), (uint32_t)(V - 1),
-                     P<const uint16_t>(W1t), P<const float>(b1), H, P<float>(pooled));
+                     P<const uint16_t>(W1t), P<const float>(b1), H, P<float>(pooled),
+                     P<const int32_t>(ntok_src), ntok_stride);
   check_launch();
 }
 
 static void classify_head(uintptr_t pooled, int B, int H, uintptr_t W2, uintptr_t b2, uintptr_t logits,
-                          uintptr_t pred, uintptr_t stream) {
+                          uintptr_t pred, uintptr_t stream, const ClassifyReadback& rb = ClassifyReadback{}) {
   if (B == 0) return;
   hipLaunchKernelGGL(classify_head_kernel, dim3((B + 3) / 4), dim3(256), 0, S(stream), P<const float>(pooled),
-                     B, H, P<const float>(W2), P<const float>(b2), P<float>(logits), P<int32_t>(pred));
+                     B, H, P<const float>(W2), P<const float>(b2), P<float>(logits), P<int32_t>(pred), rb);
   check_launch();
 }
 
@@ -102,9 +113,10 @@ static void copy_bytes(uintptr_t dst, uintptr_t src, int64_t n, uintptr_t stream
 
 // The whole GPU preprocess chain of one micro-batch in ONE host call (the
 // serve loop's ingest path: one pybind crossing, no per-batch tensor
-// allocations, six launches): copy from host-mapped staging, text_analyze
-// (zeroing the pooled rows), row scan, embed_pool, classify_head, one
-// readback kernel into host-mapped memory.  The caller records the event.
+// allocations, four launches): copy from host-mapped staging, text_analyze
+// (zeroing the pooled rows), embed_pool (row scan in LDS per block),
+// classify_head with the readback into host-mapped memory riding along
+// (without the classifier: one readback kernel).  The caller records the event.
 static void text_batch(uintptr_t staging, uintptr_t dev_bytes, int64_t total, int64_t off_offsets, int B, int L,
                        py::bytes table, uintptr_t stats, uintptr_t hashes, bool classify, uintptr_t row_off,
                        int rows_upper, uintptr_t E, int V, uintptr_t W1t, uintptr_t b1, int H, uintptr_t pooled,
@@ -117,9 +129,17 @@ static void text_batch(uintptr_t staging, uintptr_t dev_bytes, int64_t total, in
   text_analyze(dev_bytes, dev_bytes + off_offsets, B, L, table, stats, hashes, stream, classify ? pooled : 0,
                classify ? H : 0);
   if (classify) {
-    scan_rows(stats + 4 * ST_NTOK, TA_STAT_COLS, B, row_off, stream);
-    embed_pool(hashes, L, row_off, B, rows_upper, E, V, W1t, b1, H, pooled, stream);
-    classify_head(pooled, B, H, W2, b2, logits, pred, stream);
+    if (B <= EP_MAX_LDS_SCAN) {
+      embed_pool(hashes, L, 0, B, rows_upper, E, V, W1t, b1, H, pooled, stream, stats + 4 * ST_NTOK,
+                 TA_STAT_COLS);
+    } else {
+      scan_rows(stats + 4 * ST_NTOK, TA_STAT_COLS, B, row_off, stream);
+      embed_pool(hashes, L, row_off, B, rows_upper, E, V, W1t, b1, H, pooled, stream);
+    }
+    const ClassifyReadback crb{P<int32_t>(rb), P<const int32_t>(stats), P<const uint32_t>(hashes), TA_STAT_COLS,
+                               L, cap, o_pred, o_ph};
+    classify_head(pooled, B, H, W2, b2, logits, pred, stream, crb);   // + the readback
+    return;
   }
   const int64_t n = (int64_t)B * TA_STAT_COLS + (classify ? B : 0) + (int64_t)B * cap;
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
@@ -374,8 +394,18 @@ PYBIND11_MODULE(_hipops, m) {
         py::arg("zero_len") = 0);
   m.def("text_batch", &text_batch);
   m.def("scan_rows", &scan_rows);
-  m.def("embed_pool", &embed_pool);
-  m.def("classify_head", &classify_head);
+  m.def("embed_pool", [](uintptr_t hashes, int L, uintptr_t row_off, int B, int rows_upper, uintptr_t E, int V,
+                         uintptr_t W1t, uintptr_t b1, int H, uintptr_t pooled, uintptr_t stream, uintptr_t ntok_src,
+                         int ntok_stride) {
+          embed_pool(hashes, L, row_off, B, rows_upper, E, V, W1t, b1, H, pooled, stream, ntok_src, ntok_stride);
+        }, py::arg("hashes"), py::arg("L"), py::arg("row_off"), py::arg("B"), py::arg("rows_upper"), py::arg("E"),
+        py::arg("V"), py::arg("W1t"), py::arg("b1"), py::arg("H"), py::arg("pooled"), py::arg("stream"),
+        py::arg("ntok_src") = 0, py::arg("ntok_stride") = 0);
+  m.def("classify_head", [](uintptr_t pooled, int B, int H, uintptr_t W2, uintptr_t b2, uintptr_t logits,
+                            uintptr_t pred, uintptr_t stream) {
+    classify_head(pooled, B, H, W2, b2, logits, pred, stream);
+  });
+  m.attr("EMBED_POOL_MAX_LDS_SCAN") = EP_MAX_LDS_SCAN;
   m.def("summarise_project", &summarise_project);
   m.def("salient_topk", &salient_topk);
   m.def("rmsnorm", &rmsnorm);

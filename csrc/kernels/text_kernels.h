@@ -36,7 +36,7 @@ constexpr int TA_WIN = 96;               // staged bytes per wave per chunk
 
 enum : int32_t { FLAG_FOLD = 1 };
 enum : int32_t { ST_WORDS = 0, ST_POS = 1, ST_NEG = 2, ST_QUESTION = 3, ST_FLAGS = 4,
-                 ST_NTOK = 5, ST_SCORES = 8 };
+                 ST_NTOK = 5, ST_BEST_SLOT = 6, ST_CODE = 7, ST_SCORES = 8 };
 
 struct PatternTable {
   uint32_t text[TA_MAX_PAT][4];  // pattern bytes (lower-cased if case-insensitive)
@@ -309,8 +309,18 @@ text_analyze_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict
     st[ST_QUESTION] = question ? 1 : 0;
     st[ST_FLAGS] = fold ? FLAG_FOLD : 0;
     st[ST_NTOK] = ntok;
+    // the host's per-message decisions, precomputed: keyword slot with the
+    // highest strictly positive score (first maximum = the more urgent level,
+    // slots ascend in priority; unused slots score 0), and one code word
+    // (sentiment 0 neutral / 1 positive / 2 negative | question << 2 | fold << 3)
+    int best_slot = -1, best = 0;
 #pragma unroll
-    for (int s = 0; s < TA_SLOTS; ++s) st[ST_SCORES + s] = score[s];
+    for (int s = 0; s < TA_SLOTS; ++s) {
+      st[ST_SCORES + s] = score[s];
+      if (score[s] > best) { best = score[s]; best_slot = s; }
+    }
+    st[ST_BEST_SLOT] = best_slot;
+    st[ST_CODE] = (pos > neg ? 1 : (neg > pos ? 2 : 0)) | (question ? 4 : 0) | (fold ? 8 : 0);
   }
 }
 

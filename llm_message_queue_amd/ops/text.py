@@ -26,7 +26,13 @@ from ..preprocess import oracle
 MAX_PATTERNS = 32
 STAT_COLS = 16
 ST_WORDS, ST_POS, ST_NEG, ST_QUESTION, ST_FLAGS, ST_NTOK, ST_SCORES = 0, 1, 2, 3, 4, 5, 8
+ST_BEST_SLOT, ST_CODE = 6, 7          # kernel-side decisions (text_kernels.h)
 FLAG_FOLD = 1
+_SENT = ("neutral", "positive", "negative", "neutral")
+_QS = ("false", "true")
+_SENT_A = np.array(_SENT, dtype=object)
+_QS_A = np.array(_QS, dtype=object)
+SMALL_BATCH = 40                      # below: per-row Python beats numpy's fixed cost
 
 
 def _has_border(b: bytes) -> bool:
@@ -174,6 +180,21 @@ class TextResult:
         sentiment, question string, fallback flag, token counts."""
         st = self.stats
         nslot = len(self.slot_prio)
+        cap = self.prompt_hashes.shape[1] if self.prompt_hashes is not None else 1 << 30
+        if self.extra_scores is None:
+            # the kernel already picked the slot and coded sentiment / question / fold
+            sp = self.slot_prio
+            if len(st) <= SMALL_BATCH:
+                rows = [(sp[r[6]] if r[6] >= 0 else default_priority, _SENT[r[7] & 3], _QS[(r[7] >> 2) & 1],
+                         r[0], (r[7] & 8) != 0, r[5] if r[5] < cap else cap) for r in st[:, :8].tolist()]
+                cols = [list(c) for c in zip(*rows)] if rows else [[] for _ in range(6)]
+                return dict(zip(("priority", "sentiment", "question", "word_count", "fallback", "ntok"), cols))
+            bs, code = st[:, ST_BEST_SLOT], st[:, ST_CODE]
+            prio = (np.where(bs >= 0, np.asarray(sp, dtype=np.int64)[bs], default_priority) if nslot
+                    else np.full(len(st), default_priority))
+            return {"priority": prio.tolist(), "sentiment": _SENT_A[code & 3].tolist(),
+                    "question": _QS_A[(code >> 2) & 1].tolist(), "word_count": st[:, ST_WORDS].tolist(),
+                    "fallback": ((code & 8) != 0).tolist(), "ntok": np.minimum(st[:, ST_NTOK], cap).tolist()}
         out: Dict[str, list] = {}
         if nslot:
             sc = st[:, ST_SCORES:ST_SCORES + nslot].astype(np.int64)

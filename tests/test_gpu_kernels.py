@@ -163,6 +163,58 @@ def test_embed_pool_large_batch_spans_tiles():
         assert torch.allclose(res.pooled[j], Hd.mean(0), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("n", [1, 37, 1500])
+def test_one_call_text_batch_matches_per_launch_path(n):
+    """The serve path (``_hipops.text_batch``: reused buffers, row scan in
+    embed_pool's LDS, readback fused into classify_head) returns the same
+    stats, predictions and prompt hashes as the per-launch path."""
+    from llm_message_queue_amd.ops.text import TextPipeline
+    from llm_message_queue_amd.utils.config import PreprocessorConfig
+    texts = [" ".join(f"w{i}_{k}" for k in range(1 + (i * 7) % 90)) for i in range(n)]
+    if n > 3:
+        texts[1], texts[2] = "", "Is this URGENT?"
+    pipe = TextPipeline(PreprocessorConfig(max_tokens=128), device=DEV)
+    pats = oracle.default_patterns()
+    ref = pipe.run(texts, pats, classify=True, keep_device=True, prompt_cap=32)
+    cols = [0, 1, 2, 3, 4, 5] + list(range(8, 16))          # the columns text_analyze writes
+    # prompt hashes past a message's token count are never read (not zero-filled)
+    valid = np.arange(32)[None, :] < np.minimum(ref.stats[:, 5], 32)[:, None]
+    for _ in range(2):                                   # buffers reused across batches
+        got = pipe.run(texts, pats, classify=True, keep_device=False, prompt_cap=32)
+        assert (got.stats[:, cols] == ref.stats[:, cols]).all()
+        assert (got.prompt_hashes == ref.prompt_hashes)[valid].all()
+        assert (got.pred == ref.pred).mean() > 0.99     # f32 atomics may order differently
+    got = pipe.run(texts, pats, classify=False, keep_device=False, prompt_cap=32)
+    assert (got.stats[:, cols] == ref.stats[:, cols]).all() and got.pred is None
+    assert (got.prompt_hashes == ref.prompt_hashes)[valid].all()
+
+
+def test_embed_pool_in_block_scan_matches_row_off():
+    from llm_message_queue_amd.ops.text import TextPipeline
+    from llm_message_queue_amd.utils.config import PreprocessorConfig
+    texts = [" ".join(f"t{i}_{k}" for k in range(1 + (i * 13) % 70)) for i in range(900)]
+    pipe = TextPipeline(PreprocessorConfig(max_tokens=128), device=DEV)
+    res = pipe.run(texts, oracle.default_patterns(), classify=True, keep_device=True)
+    w, k = pipe.weights, pipe.ops
+    B, L = len(texts), 128
+    st = torch.as_tensor(res.stats, device=DEV)
+    ntok = st[:, 5].to(torch.int64)
+    row_off = torch.zeros(B + 1, dtype=torch.int32, device=DEV)
+    row_off[1:] = torch.cumsum(ntok, 0).to(torch.int32)
+    rows_upper = int(ntok.sum())
+    s = torch.cuda.current_stream().cuda_stream
+    out = []
+    for mode in ("global", "lds"):
+        pooled = torch.zeros(B, w.hidden, dtype=torch.float32, device=DEV)
+        k.embed_pool(res.hashes.data_ptr(), L, row_off.data_ptr() if mode == "global" else 0, B, rows_upper,
+                     w.E.data_ptr(), w.vocab, w.W1t.data_ptr(), w.b1.data_ptr(), w.hidden, pooled.data_ptr(), s,
+                     st.data_ptr() + 4 * 5 if mode == "lds" else 0, 16 if mode == "lds" else 0)
+        out.append(pooled)
+    torch.cuda.synchronize()
+    assert torch.allclose(out[0], out[1], atol=1e-5, rtol=1e-5)
+    assert torch.allclose(out[0], res.pooled, atol=1e-5, rtol=1e-5)
+
+
 # ----------------------------------------------------------------------------- llama ops
 @pytest.fixture(scope="module")
 def ops():

@@ -129,3 +129,30 @@ def test_token_hashes():
     h = oracle.token_hashes("Hello  WORLD x" + "y" * 40, 8)
     assert h[0] == oracle.fnv1a32(b"hello") and h[1] == oracle.fnv1a32(b"world")
     assert h[2] == oracle.fnv1a32(b"x" + b"y" * 31)
+
+
+@pytest.mark.parametrize("B", [0, 1, 17, 40, 41, 300])
+def test_kernel_side_decisions_match_score_argmax(B):
+    """TextResult.decide's fast paths (per-row for small batches, numpy for
+    large) read the slot / code words text_analyze writes into stats columns
+    6-7; they must equal the score-argmax decision of the general path."""
+    import numpy as np
+    from llm_message_queue_amd.ops.text import TextResult
+    rng = np.random.default_rng(B)
+    st = np.zeros((B, 16), dtype=np.int32)
+    st[:, 0] = rng.integers(0, 50, B)                    # words
+    st[:, 1:3] = rng.integers(0, 3, (B, 2))             # pos, neg
+    st[:, 3] = rng.integers(0, 2, B)                     # question
+    st[:, 4] = rng.integers(0, 2, B)                     # fold flag
+    st[:, 5] = rng.integers(0, 60, B)                    # ntok
+    st[:, 8:12] = rng.integers(0, 3, (B, 4))            # 4 keyword slots, ties common
+    for r in st:                                         # what the kernel writes
+        sc = r[8:16]
+        r[6] = int(np.argmax(sc)) if sc.max() > 0 else -1
+        r[7] = (1 if r[1] > r[2] else 2 if r[2] > r[1] else 0) | (4 if r[3] else 0) | (8 if r[4] else 0)
+    ph = np.zeros((B, 32), dtype=np.uint32)
+    fast = TextResult(st, None, 0.0, False, [0, 1, 2, 3], None, None, None, 128, ph).decide(2)
+    slow = TextResult(st, None, 0.0, False, [0, 1, 2, 3], np.zeros((B, 8), dtype=np.int64), None, None, 128,
+                      ph).decide(2)
+    for k in ("priority", "sentiment", "question", "word_count", "fallback", "ntok"):
+        assert list(fast[k]) == list(slow[k]), k
