@@ -84,6 +84,9 @@ def main() -> None:
             ms = timeit(lambda: ops.attention_tiles(q, kc, vc, tiles, Hq, Hkv, 128 ** -0.5, out=o, n_dec=768,
                                                     seg_keys=sk), a.reps)
             rec(f"attention_tiles_step_seg{sk}", ms, tokens=T, decode=768)
+            ms = timeit(lambda: ops.attention_tiles(q, kc, vc, tiles, Hq, Hkv, 128 ** -0.5, out=o, n_dec=768,
+                                                    seg_keys=sk, mixed=False), a.reps)
+            rec(f"attention_tiles_step_seg{sk}_two_launches", ms, tokens=T, decode=768)
             seg = tiles[768:].contiguous()
             ms = timeit(lambda: ops.attention_tiles(q, kc, vc, seg, Hq, Hkv, 128 ** -0.5, out=o, n_dec=0,
                                                     seg_keys=sk), a.reps)

@@ -303,11 +303,21 @@ static void attention(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, ui
 // kernel); the rest go to the MFMA segment kernel.  Rows are disjoint.
 static void attention_tiles(uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t tiles, int n_tiles, int n_dec,
                             int Hq, int Hkv, int max_ctx, int n_slots, int T, float scale, uintptr_t out,
-                            uintptr_t stream, int seg_keys) {
+                            uintptr_t stream, int seg_keys, bool mixed) {
   require(seg_keys == 32 || seg_keys == 64, "seg_keys must be 32 or 64");
   require(Hq == 4 * Hkv, "attention_tiles expects a GQA group of exactly 4 heads");
   require(0 <= n_dec && n_dec <= n_tiles, "n_dec out of range");
   const float scale_log2 = scale * 1.4426950408889634f;
+  if (mixed && n_dec > 0 && n_tiles > n_dec) {            // both kinds: one launch
+    const int seg_blocks = (n_tiles - n_dec) * Hkv;
+    const int dec_blocks = (n_dec * Hkv + 3) / 4;
+    auto kern = seg_keys == 32 ? attention_mixed_kernel<32> : attention_mixed_kernel<64>;
+    hipLaunchKernelGGL(kern, dim3(seg_blocks + dec_blocks), dim3(256), 0, S(stream), P<const uint16_t>(q),
+                       P<const uint16_t>(kc), P<const uint16_t>(vc), P<const int32_t>(tiles), n_dec, seg_blocks,
+                       Hq, Hkv, max_ctx, n_slots, T, scale_log2, P<uint16_t>(out));
+    check_launch();
+    return;
+  }
   if (n_dec > 0) {
     const int items = n_dec * Hkv;
     hipLaunchKernelGGL(attention_dec_kernel, dim3((items + 3) / 4), dim3(256), 0, S(stream), P<const uint16_t>(q),
@@ -422,7 +432,10 @@ PYBIND11_MODULE(_hipops, m) {
   m.attr("GEMM_EPI_SWIGLU") = (int)GM_EPI_SWIGLU;
   m.def("rope_kv", &rope_kv);
   m.def("attention", &attention);
-  m.def("attention_tiles", &attention_tiles);
+  m.def("attention_tiles", &attention_tiles, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("tiles"),
+        py::arg("n_tiles"), py::arg("n_dec"), py::arg("Hq"), py::arg("Hkv"), py::arg("max_ctx"), py::arg("n_slots"),
+        py::arg("T"), py::arg("scale"), py::arg("out"), py::arg("stream"), py::arg("seg_keys"),
+        py::arg("mixed") = true);
   m.def("register_host_page", &register_host_page);
   m.def("host_device_ptr", &host_device_ptr);
   m.def("copy_bytes", &copy_bytes);

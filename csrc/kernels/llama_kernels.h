@@ -316,27 +316,29 @@ attention_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc
 // halves the LDS and score registers: more workgroups resident per CU, and
 // this latency-bound kernel runs in fewer rounds.  Long dialog contexts loop
 // over more blocks.
+// LDS elements (bf16) of one segment-attention block: K tile | V^T tile |
+// per-wave P tiles; after the key loop the same bytes stage the output tiles
 template <int KEYS>
-__global__ void __launch_bounds__(256, KEYS == 32 ? 4 : 3)
-attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-                     const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int Hq, int Hkv,
-                     int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
+constexpr int seg_lds_elems() { return KEYS * 128 + 128 * (KEYS + 8) + 4 * 16 * (KEYS + 8); }
+
+template <int KEYS>
+__device__ __forceinline__ void attention_seg_block(int bid, uint16_t* __restrict__ smem,
+                                                    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                                                    const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles,
+                                                    int Hq, int Hkv, int max_ctx, int n_slots, int T,
+                                                    float scale_log2, uint16_t* __restrict__ out) {
   static_assert(KEYS == 32 || KEYS == 64, "key block");
   constexpr int SA_KEYS = KEYS;
   constexpr int SA_VROW = KEYS + 8;   // Vt row: KEYS keys + 8 pad
   constexpr int SA_PROW = KEYS + 8;   // P row
   constexpr int NJ = KEYS / 16;       // 16-key score tiles per block
   constexpr int NKS = KEYS / 32;      // 32-key PV k-steps per block
-  // one LDS array: K tile | V^T tile | per-wave P tiles; after the key loop
-  // the same bytes stage the output tiles for 16-B global stores
   constexpr int SA_OROW = 136;                        // O staging row: 128 dims + 8 pad
-  constexpr int SA_LDS = SA_KEYS * 128 + 128 * SA_VROW + 4 * 16 * SA_PROW;
-  static_assert(SA_LDS >= 4 * 16 * SA_OROW, "output staging must fit");
-  __shared__ __align__(16) uint16_t smem[SA_LDS];
+  static_assert(seg_lds_elems<KEYS>() >= 4 * 16 * SA_OROW, "output staging must fit");
   uint16_t* Ks = smem;
   uint16_t* Vt = smem + SA_KEYS * 128;
-  const int tile = blockIdx.x / Hkv;
-  const int g = blockIdx.x % Hkv;
+  const int tile = bid / Hkv;
+  const int g = bid % Hkv;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
@@ -475,6 +477,15 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
   }
 }
 
+template <int KEYS>
+__global__ void __launch_bounds__(256, KEYS == 32 ? 4 : 3)
+attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                     const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int Hq, int Hkv,
+                     int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
+  __shared__ __align__(16) uint16_t smem[seg_lds_elems<KEYS>()];
+  attention_seg_block<KEYS>(blockIdx.x, smem, q, kc, vc, tiles, Hq, Hkv, max_ctx, n_slots, T, scale_log2, out);
+}
+
 // ---------------------------------------------------------------------------
 // Decode attention (1-token tiles): one WAVE per (token, kv head), the GQA
 // group's 4 query heads handled together by that wave, 4 independent items
@@ -493,15 +504,15 @@ attention_seg_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
 //     8-B load per key; a half-wave reads a 256-B V row), so the serial key
 //     loop is half as long; the halves are summed with one xor-32 shuffle.
 // LDS: 1 KiB of scores/probabilities per wave.
-__global__ void __launch_bounds__(256)
-attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-                     const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int n_items, int Hq,
-                     int Hkv, int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
+__device__ __forceinline__ void attention_dec_block(int bid, float (*__restrict__ ps)[4][64],
+                                                    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                                                    const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles,
+                                                    int n_items, int Hq, int Hkv, int max_ctx, int n_slots, int T,
+                                                    float scale_log2, uint16_t* __restrict__ out) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  __shared__ float ps[4][4][64];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int item = blockIdx.x * 4 + wv;
+  const int item = bid * 4 + wv;
   if (item >= n_items) return;                 // whole wave; no block barrier below
   const int tile = item / Hkv;
   const int g = item % Hkv;
@@ -606,6 +617,37 @@ attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict_
       *reinterpret_cast<uint2*>(out + ((int64_t)row * Hq + g * 4 + h) * 128 + dp * 4) = o;
     }
   }
+}
+
+__global__ void __launch_bounds__(256)
+attention_dec_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                     const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int n_items, int Hq,
+                     int Hkv, int max_ctx, int n_slots, int T, float scale_log2, uint16_t* __restrict__ out) {
+  __shared__ float ps[4][4][64];
+  attention_dec_block(blockIdx.x, ps, q, kc, vc, tiles, n_items, Hq, Hkv, max_ctx, n_slots, T, scale_log2, out);
+}
+
+// Both kinds of tiles of a step in ONE launch: blocks [0, n_seg_blocks) run
+// segment (prefill-chunk) tiles, the rest decode items.  Each kernel alone is
+// latency-bound and leaves most of the chip idle for part of its run; in one
+// grid the decode blocks fill the CUs behind the segment blocks instead of
+// waiting for the segment kernel's last block (stream order).  The LDS array
+// is the segment block's; a decode block uses its first 4 KiB.
+template <int KEYS>
+__global__ void __launch_bounds__(256, KEYS == 32 ? 4 : 3)
+attention_mixed_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
+                       const uint16_t* __restrict__ vc, const int32_t* __restrict__ tiles, int n_dec_tiles,
+                       int n_seg_blocks, int Hq, int Hkv, int max_ctx, int n_slots, int T, float scale_log2,
+                       uint16_t* __restrict__ out) {
+  static_assert(seg_lds_elems<KEYS>() * 2 >= 4 * 4 * 64 * 4, "decode scores must fit");
+  __shared__ __align__(16) uint16_t smem[seg_lds_elems<KEYS>()];
+  const int bid = blockIdx.x;
+  if (bid < n_seg_blocks)
+    attention_seg_block<KEYS>(bid, smem, q, kc, vc, tiles + 4 * n_dec_tiles, Hq, Hkv, max_ctx, n_slots, T,
+                              scale_log2, out);
+  else
+    attention_dec_block(bid - n_seg_blocks, reinterpret_cast<float (*)[4][64]>(smem), q, kc, vc, tiles,
+                        n_dec_tiles * Hkv, Hq, Hkv, max_ctx, n_slots, T, scale_log2, out);
 }
 
 // Byte copy between device memory and host-mapped pinned memory, run as a

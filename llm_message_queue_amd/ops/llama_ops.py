@@ -10,6 +10,8 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import os
+
 import torch
 
 from .. import _native
@@ -117,19 +119,24 @@ class HipOps:
         return o
 
 
-    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None, n_dec: int = 0, seg_keys: int = 32):
+    MIXED_ATTENTION = os.environ.get("LLMQ_ATTN_MIXED", "1") != "0"
+
+    def attention_tiles(self, q, kc, vc, tiles, Hq, Hkv, scale, out=None, n_dec: int = 0, seg_keys: int = 32,
+                        mixed: bool = None):
         """Tiled attention; ``tiles`` int32 [n, 4] on the device = (first
         token row, n <= 16, slot, first position).  The first ``n_dec`` tiles
         must be 1-token (decode) tiles: they run on the wave-per-item decode
         kernel, the rest on the MFMA segment kernel (``seg_keys`` keys per
-        block: 32 or 64)."""
+        block: 32 or 64).  ``mixed`` (default on; env LLMQ_ATTN_MIXED=0
+        turns it off): a step with both kinds runs them in ONE launch."""
         _check(q, torch.bfloat16, "q")
         if tiles.dtype != torch.int32 or tiles.dim() != 2 or tiles.shape[1] != 4 or not tiles.is_contiguous():
             raise ValueError("tiles must be a contiguous int32 [n, 4] tensor")
         o = out if out is not None else torch.empty_like(q)
         self.k.attention_tiles(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), tiles.data_ptr(), tiles.shape[0],
                                int(n_dec), Hq, Hkv, kc.shape[2], kc.shape[0], q.shape[0], float(scale),
-                               o.data_ptr(), _stream(q), int(seg_keys))
+                               o.data_ptr(), _stream(q), int(seg_keys),
+                               self.MIXED_ATTENTION if mixed is None else bool(mixed))
         return o
 
 

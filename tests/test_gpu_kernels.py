@@ -311,6 +311,13 @@ def test_attention_tiles_mfma_vs_ref(ops):
     o4 = hip.attention_tiles(q, kc, vc, torch.from_numpy(tiles).to(DEV), Hq, Hkv, 128 ** -0.5, n_dec=5)
     err4 = (o4.float() - o2.float()).abs().max().item()
     assert err4 < 3e-2, err4
+    # the one-launch mixed kernel (default) == the two separate launches, bit for bit
+    o5 = hip.attention_tiles(q, kc, vc, torch.from_numpy(tiles).to(DEV), Hq, Hkv, 128 ** -0.5, n_dec=5,
+                             mixed=False)
+    assert torch.equal(o4, o5)
+    o6 = hip.attention_tiles(q, kc, vc, torch.from_numpy(tiles).to(DEV), Hq, Hkv, 128 ** -0.5, n_dec=5,
+                             seg_keys=64)
+    assert (o6.float() - o2.float()).abs().max().item() < 3e-2
 
 
 def test_tiny_model_forward_hip_vs_ref():
