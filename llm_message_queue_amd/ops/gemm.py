@@ -150,12 +150,12 @@ def split_plan(M: int, N: int, K: int, cus: int):
     return tiles - tail
 
 
-def _split_workspace(device, n_split: int, cus: int):
+def _split_workspace(device, stream: int, n_split: int, cus: int):
     """fp32 slabs (256 KiB per split tile) + zeroed ticket/ready counters,
-    cached per device and sized for the largest possible tail (cus / 2).
-    The kernel re-zeroes the counters it used, so launches on ONE stream
-    can share them; qkv_rope is only issued from the engine's stream."""
-    key = (device.type, device.index)
+    sized for the largest possible tail (cus / 2).  The kernel re-zeroes the
+    counters it used, so launches in stream order can share them; the cache
+    is keyed by (device, stream) so concurrent streams never do."""
+    key = (device.type, device.index, stream)
     ws = _SPLIT_WS.get(key)
     if ws is None:
         cap = cus // 2
@@ -206,15 +206,15 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
     k = _native.require_hipops()
     N = wqkv.shape[0]
     full, ws, cnt = 0, 0, 0
+    stream = torch.cuda.current_stream(x.device).cuda_stream
     if split:
         cus = _cu_count(x.device)
         f = split_plan(T, N, K, cus) if split_full is None else split_full
         if f is not None:
             n_split = (T + TILE_M - 1) // TILE_M * (N // TILE_N) - f
-            w_t, c_t = _split_workspace(x.device, n_split, cus)
+            w_t, c_t = _split_workspace(x.device, stream, n_split, cus)
             full, ws, cnt = f, w_t.data_ptr(), c_t.data_ptr()
     k.gemm_qkv_rope(x.data_ptr(), wqkv.data_ptr(), T, N, K, pos.data_ptr(), slot.data_ptr(),
                     cos_t.data_ptr(), sin_t.data_ptr(), Hq, Hkv, max_ctx, S, q.data_ptr(), kc.data_ptr(),
-                    vc.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream, _row_scale_ptr(row_scale, T),
-                    full, ws, cnt)
+                    vc.data_ptr(), stream, _row_scale_ptr(row_scale, T), full, ws, cnt)
     return q

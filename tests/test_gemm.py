@@ -268,7 +268,7 @@ def test_qkv_rope_split_k_tail_matches_unsplit(T):
         assert (q1.float() - q2.float()).abs().max().item() <= tol, it
         assert (kc1.float() - kc2.float()).abs().max().item() <= tol, it
         assert (vc1.float() - vc2.float()).abs().max().item() <= tol, it
-    _, cnt = G._SPLIT_WS[("cuda", 0)]
+    _, cnt = G._SPLIT_WS[("cuda", 0, torch.cuda.current_stream().cuda_stream)]
     assert int(cnt.abs().sum()) == 0                             # left zeroed for the next launch
 
 
