@@ -10,7 +10,10 @@
 // within a tier), DelayedQueue (concurrent schedule + wait_ready, no early
 // delivery), ShmRing (2 handles on one segment, MPMC exactly-once), Guard
 // (concurrent token buckets never admit more than burst + rate x elapsed;
-// concurrent JWT verification).
+// concurrent JWT verification), ShmCollective (4 ranks as threads: every
+// rank sees every other rank's payload of the same op over thousands of
+// variable-size exchanges, both buffer parities; a rank that stops makes the
+// others time out instead of hanging).
 #include <unistd.h>
 
 #include <algorithm>
@@ -18,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <memory>
 #include <random>
 #include <set>
 #include <string>
@@ -26,6 +30,7 @@
 
 #include "ingress/guard.h"
 #include "queue/mlq_core.h"
+#include "queue/shm_coll.h"
 #include "queue/shm_ring.h"
 
 #define CHECK(c)                                                              \
@@ -206,6 +211,54 @@ static void stress_ring() {
   std::printf("shm ring: %d records, 3 producers / 2 consumers OK\n", P * N);
 }
 
+static void stress_shm_coll() {
+  using llmq::ShmCollective;
+  const std::string name = "/llmq-coll-stress-" + std::to_string(getpid());
+  constexpr int W = 4, OPS = 3000;
+  std::vector<std::unique_ptr<ShmCollective>> c(W);
+  c[0] = std::make_unique<ShmCollective>(name, W, 0, 1 << 16, true);
+  for (int r = 1; r < W; ++r) c[r] = std::make_unique<ShmCollective>(name, W, r, 1 << 16, false);
+  CHECK(c[0]->attached() == W);
+  std::vector<std::thread> th;
+  for (int r = 0; r < W; ++r) {
+    th.emplace_back([&, r] {
+      std::vector<uint32_t> buf;
+      for (int op = 0; op < OPS; ++op) {
+        const int n = 1 + (r * 7 + op * 13) % 300;     // words this rank sends this op
+        buf.assign(n, 0);
+        for (int i = 0; i < n; ++i) buf[i] = (uint32_t)(r << 24) ^ (uint32_t)(op << 8) ^ (uint32_t)i;
+        c[r]->exchange(buf.data(), 4ull * n, 30.0);
+        for (int s = 0; s < W; ++s) {
+          uint64_t nb = 0;
+          const uint32_t* p = reinterpret_cast<const uint32_t*>(c[r]->payload(s, &nb));
+          const int ns = 1 + (s * 7 + op * 13) % 300;
+          CHECK(nb == 4ull * ns);
+          for (int i = 0; i < ns; ++i) CHECK(p[i] == ((uint32_t)(s << 24) ^ (uint32_t)(op << 8) ^ (uint32_t)i));
+        }
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r = 0; r < W; ++r) CHECK(c[r]->ops() == (uint64_t)OPS);
+  // rank W-1 stops: the others must give up within the timeout, not hang
+  std::atomic<int> timeouts{0};
+  th.clear();
+  for (int r = 0; r < W - 1; ++r) {
+    th.emplace_back([&, r] {
+      uint32_t v = (uint32_t)r;
+      try {
+        c[r]->exchange(&v, 4, 0.3);
+      } catch (const llmq::ShmCollTimeout&) {
+        ++timeouts;
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  CHECK(timeouts.load() == W - 1);
+  c[0]->unlink();
+  std::printf("shm collective: %d ranks x %d exchanges OK, dead-peer timeout OK\n", W, OPS);
+}
+
 static void stress_guard() {
   // 8 threads hammer one global bucket + per-user buckets with a fixed clock
   // window: admitted count must equal the token budget exactly.
@@ -276,6 +329,7 @@ int main() {
   stress_mlq();
   stress_delayed();
   stress_ring();
+  stress_shm_coll();
   stress_guard();
   fuzz_guard_parser();
   std::printf("ALL OK\n");
