@@ -75,6 +75,9 @@ static constexpr size_t EP_SMEM_BASE = EP_TM * EP_D * 2 + EP_TM * EP_HS_STRIDE *
 static constexpr size_t EP_SMEM_MAX = 160 * 1024 - 256;   // static __shared__ of the kernel counts too
 // largest batch whose row offsets fit in LDS next to the tile (in-block scan)
 static constexpr int EP_MAX_LDS_SCAN = (int)((EP_SMEM_MAX - EP_SMEM_BASE) / 4) - 1;
+// every block reads all B token counts, so the redundant scan costs
+// O(B x blocks) L2 traffic: above this batch size one scan_rows launch is cheaper
+static constexpr int EP_IN_BLOCK_SCAN_MAX_B = 2048;
 
 // ntok_src != 0: row_off is not read; every block scans the B token counts
 // (ntok_src[i * ntok_stride]) into LDS itself (no scan_rows launch).
@@ -129,7 +132,7 @@ static void text_batch(uintptr_t staging, uintptr_t dev_bytes, int64_t total, in
   text_analyze(dev_bytes, dev_bytes + off_offsets, B, L, table, stats, hashes, stream, classify ? pooled : 0,
                classify ? H : 0);
   if (classify) {
-    if (B <= EP_MAX_LDS_SCAN) {
+    if (B <= EP_IN_BLOCK_SCAN_MAX_B && B <= EP_MAX_LDS_SCAN) {
       embed_pool(hashes, L, 0, B, rows_upper, E, V, W1t, b1, H, pooled, stream, stats + 4 * ST_NTOK,
                  TA_STAT_COLS);
     } else {

@@ -103,14 +103,15 @@ class PoissonArrivals:
             self.rate = float(rate)
         self.t_next = t0 + self.rng.exponential(1.0 / self.rate) if self.rate > 0 else float("inf")
 
-    def due(self, now: float) -> List[float]:
-        """Arrival timestamps (s, monotonic) of every request due by ``now``."""
+    def due(self, now: float, limit: Optional[int] = None) -> List[float]:
+        """Arrival timestamps (s, monotonic) of every request due by ``now``
+        (at most ``limit``; the rest stay due for the next call)."""
         if self.t_next is None:
             self.reset(now)
         out = []
         if self.rate <= 0:
             return out
-        while self.t_next <= now:
+        while self.t_next <= now and (limit is None or len(out) < limit):
             out.append(self.t_next)
             self.t_next += self.rng.exponential(1.0 / self.rate)
         return out
