@@ -163,7 +163,7 @@ def test_embed_pool_large_batch_spans_tiles():
         assert torch.allclose(res.pooled[j], Hd.mean(0), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("n", [1, 37, 1500])
+@pytest.mark.parametrize("n", [1, 37, 1500, 3000])
 def test_one_call_text_batch_matches_per_launch_path(n):
     """The serve path (``_hipops.text_batch``: reused buffers, row scan in
     embed_pool's LDS, readback fused into classify_head) returns the same
