@@ -69,6 +69,8 @@ def parse(argv=None):
                     help="o/down as F.linear + fused residual-add RMSNorm (default: residual in the GEMM epilogue)")
     ap.add_argument("--no-row-scale", action="store_true",
                     help="fused GEMMs read rmsnorm'd rows instead of raw rows + a per-row scale (A/B)")
+    ap.add_argument("--no-fused-head", action="store_true",
+                    help="LM head on hipBLASLt + torch.argmax instead of the GEMM with the argmax epilogue")
     ap.add_argument("--no-fused-qkv", action="store_true",
                     help="qkv on hipBLASLt + rope_kv instead of the GEMM with the RoPE/KV epilogue (A/B)")
     ap.add_argument("--no-fused-mlp", action="store_true",
@@ -158,7 +160,8 @@ def main(argv=None) -> int:
                            page=page, gpu_index=rank, max_inflight=a.inflight,
                            residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv,
                            fused_mlp=False if a.no_fused_mlp else None,
-                           fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale)
+                           fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
+                           fused_head=False if a.no_fused_head else None)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -379,7 +382,8 @@ def main(argv=None) -> int:
                    "classifier": not a.no_classifier, "residual_in_gemm": not a.no_residual_gemm,
                    "split_qkv": a.split_qkv, "fused_mlp": bool(engine.model.fused_mlp),
                    "fused_qkv": bool(engine.model.fused_qkv),
-                   "row_scale_norm": bool(engine.model.row_scale_norm)},
+                   "row_scale_norm": bool(engine.model.row_scale_norm),
+                   "fused_head": bool(engine.model.fused_head)},
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),
         "p99_enqueue_to_dispatch_ms": round(lat["p99_enq_ms"], 3),

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--tokens", default="37,1024,2048,4041,4096")
     ap.add_argument("--plain", action="store_true", help="also time the plain GEMM shapes")
     ap.add_argument("--rope", action="store_true", help="also A/B the qkv GEMM with the RoPE/KV epilogue")
+    ap.add_argument("--head", action="store_true", help="also A/B the LM head: hipBLASLt + argmax vs argmax epilogue")
     ap.add_argument("--groups", default="", help="e.g. 4,8,16: also time gemm_swiglu per block-order group size")
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -134,6 +135,24 @@ def main():
             med = {k: statistics.median(v) for k, v in res.items()}
             print(json.dumps({"bench": "qkv_rope", "T": T, **{k + "_ms": round(v, 4) for k, v in med.items()},
                               "speedup": round(med["hipblaslt+rope_kv"] / med["fused"], 3)}), flush=True)
+
+    if a.head:
+        V = 128256
+        wh = (torch.randn(V, d, device=dev) * 0.02).to(torch.bfloat16)
+        for M in (256, 512, 900, 1200, 1536):
+            x = torch.randn(M, d, device=dev).to(torch.bfloat16)
+            fns = {"hipblaslt+argmax": lambda: torch.argmax(F.linear(x, wh), dim=-1),
+                   "fused": lambda: G.lm_head_argmax(x, wh)}
+            agree = (fns["hipblaslt+argmax"]().int() == fns["fused"]()).float().mean().item()
+            res = {k: [] for k in fns}
+            for _ in range(a.rounds):
+                for k, f in fns.items():
+                    res[k].append(timeit(f, a.iters))
+            med = {k: statistics.median(v) for k, v in res.items()}
+            print(json.dumps({"bench": "lm_head", "M": M, **{k + "_ms": round(v, 4) for k, v in med.items()},
+                              "speedup": round(med["hipblaslt+argmax"] / med["fused"], 3),
+                              "tflops_fused": round(2 * M * V * d / med["fused"] / 1e9, 1),
+                              "token_agreement": round(agree, 4)}), flush=True)
 
     if a.plain:
         shapes = {"qkv": (6144, d), "o": (d, d), "gate_up": (2 * ffn, d), "down": (d, ffn)}

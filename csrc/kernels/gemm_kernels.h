@@ -54,7 +54,18 @@ constexpr int GM_BUF_BYTES = 4 * GM_HALF_BYTES;    // A0 A1 B0 B1
 constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
 constexpr int GM_GROUP_M = 8;                    // default M-tiles per block-order group
 
-enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3 };
+enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4 };
+
+// GM_EPI_ARGMAX: the LM head's greedy sampling as the epilogue -- no [M][N]
+// logits tensor.  Each tile writes, per row, the max over its 256 columns and
+// the (global) column of its first occurrence into pv / pi [M][N / 256];
+// gemm_argmax_reduce_kernel picks the first maximum over the tiles (ties go
+// to the lower column, as torch.argmax does).  Values are the fp32
+// accumulators (not bf16-rounded logits).
+struct GmArgmax {
+  float* pv;
+  int32_t* pi;
+};
 
 // GM_EPI_ROPE: the fused qkv projection's epilogue = the rope_kv kernel
 // (llama_kernels.h): RoPE (rotate-half) on q and k, q to ``q``, k / v into
@@ -134,7 +145,8 @@ __device__ __forceinline__ void gm_stage(__amdgpu_buffer_rsrc_t rs, uint32_t v0,
 template <int EPI, bool STAGGER = true, int SCHED = 1>
 __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
-    int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp) {
+    int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp,
+    const GmArgmax am) {
   extern __shared__ __align__(16) uint8_t smem[];
 
   const int tiles_m = (M + GM_BM - 1) / GM_BM;
@@ -477,7 +489,52 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 
   // ---- epilogue through LDS (the staging buffers are free after the last barrier)
   const int row0 = tm * GM_BM + wr * 128;          // first output row of this wave
-  if (EPI == GM_EPI_SWIGLU) {
+  if (EPI == GM_EPI_ARGMAX) {
+    // per (row, wave): max over the wave's 64 columns -- 4 per lane, then the
+    // 16 lanes of a row group (xor butterfly; ties keep the lower column)
+    float* lv = reinterpret_cast<float*>(smem);                    // [256 rows][4 wave cols]
+    int* lc = reinterpret_cast<int*>(smem + GM_BM * 4 * 4);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = acc[mh][m][0][0][j];
+          int c = fr;
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+              const float x = acc[mh][m][nh][n][j];
+              if (x > v) { v = x; c = nh * 32 + n * 16 + fr; }
+            }
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) {
+            const float ov = __shfl_xor(v, off, 64);
+            const int oc = __shfl_xor(c, off, 64);
+            if (ov > v || (ov == v && oc < c)) { v = ov; c = oc; }
+          }
+          if (fr == 0) {
+            const int r = wr * 128 + mh * 64 + m * 16 + fq * 4 + j;
+            lv[r * 4 + wc] = v;
+            lc[r * 4 + wc] = wc * 64 + c;
+          }
+        }
+    __syncthreads();
+    if (tid < GM_BM) {                             // one thread per tile row: the 4 wave columns
+      const int grow = tm * GM_BM + tid;
+      float v = lv[tid * 4];
+      int c = lc[tid * 4];
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+        if (lv[tid * 4 + k] > v) { v = lv[tid * 4 + k]; c = lc[tid * 4 + k]; }
+      if (grow < M) {
+        am.pv[(int64_t)grow * tiles_n + tn] = v;
+        am.pi[(int64_t)grow * tiles_n + tn] = tn * GM_BN + c;
+      }
+    }
+  } else if (EPI == GM_EPI_SWIGLU) {
     // wave w: 128 rows x 32 features bf16 = 8 KiB at w * 8 KiB
     uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 8192);
     gm_f32x4 sc[2][4];
@@ -617,6 +674,28 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   }
 }
 
+
+// out[row] = column of the first maximum over the tiles' partials (one wave per row)
+__global__ __launch_bounds__(256) void gemm_argmax_reduce_kernel(const float* __restrict__ pv,
+                                                                 const int32_t* __restrict__ pi, int M, int tiles,
+                                                                 int32_t* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  float v = -__builtin_inff();
+  int c = 0x7fffffff;
+  for (int t = lane; t < tiles; t += 64) {         // ascending tiles: a later equal value never wins
+    const float x = pv[(int64_t)row * tiles + t];
+    if (x > v) { v = x; c = pi[(int64_t)row * tiles + t]; }
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oc = __shfl_xor(c, off, 64);
+    if (ov > v || (ov == v && oc < c)) { v = ov; c = oc; }
+  }
+  if (lane == 0) out[row] = c == 0x7fffffff ? 0 : c;   // all-NaN row: token 0
+}
 
 #undef GM_STAGE
 #undef GM_READ_A

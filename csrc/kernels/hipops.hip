@@ -191,7 +191,8 @@ static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T,
 template <int EPI, bool STAGGER = true, int SCHED = 1>
 static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st,
                         int group_m, const float* rs = nullptr, const GmRope& rp = GmRope{},
-                        const GmSplit& sp = GmSplit{0, nullptr, nullptr}) {
+                        const GmSplit& sp = GmSplit{0, nullptr, nullptr},
+                        const GmArgmax& am = GmArgmax{nullptr, nullptr}) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
@@ -201,7 +202,7 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
   const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
   const int grid = sp.ws ? sp.full + 2 * (tiles - sp.full) : tiles;
   hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(grid), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c,
-                     M, N, K, group_m, rs, rp, sp);
+                     M, N, K, group_m, rs, rp, sp, am);
 }
 
 // epi: 0 / 2 = store / SwiGLU; 16 / 32 = store with the round-1 phase
@@ -257,6 +258,20 @@ static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr
   }
   launch_gemm<GM_EPI_ROPE>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M,
                            rs ? P<const float>(rs) : nullptr, rp, sp);
+  check_launch();
+}
+
+// LM head + greedy sampling: out[m] = argmax_n (A[m] . W[n]) with the argmax
+// in the GEMM epilogue (no [M][N] logits); pv / pi: [M][N / 256] scratch.
+static void gemm_argmax(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr_t pv, uintptr_t pi,
+                        uintptr_t out, uintptr_t stream) {
+  require(M > 0 && N % GM_BN == 0 && K % (2 * GM_BK) == 0, "gemm_argmax: M > 0, N % 256, K % 128");
+  require((int64_t)M * K < (1LL << 30) && (int64_t)N * K < (1LL << 30), "gemm_argmax: operand > 2 GiB");
+  require(a % 16 == 0 && w % 16 == 0 && pv % 4 == 0 && pi % 4 == 0 && out % 4 == 0, "gemm_argmax: alignment");
+  launch_gemm<GM_EPI_ARGMAX>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M,
+                             nullptr, GmRope{}, GmSplit{0, nullptr, nullptr}, GmArgmax{P<float>(pv), P<int32_t>(pi)});
+  hipLaunchKernelGGL(gemm_argmax_reduce_kernel, dim3((M + 3) / 4), dim3(256), 0, S(stream), P<const float>(pv),
+                     P<const int32_t>(pi), M, N / GM_BN, P<int32_t>(out));
   check_launch();
 }
 
@@ -430,6 +445,7 @@ PYBIND11_MODULE(_hipops, m) {
         py::arg("pos"), py::arg("slot"), py::arg("cos_t"), py::arg("sin_t"), py::arg("Hq"), py::arg("Hkv"),
         py::arg("max_ctx"), py::arg("n_slots"), py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("stream"),
         py::arg("rs") = 0, py::arg("split_full") = 0, py::arg("split_ws") = 0, py::arg("split_cnt") = 0);
+  m.def("gemm_argmax", &gemm_argmax);
   m.def("row_rms", &row_rms);
   m.attr("GEMM_EPI_STORE") = (int)GM_EPI_STORE;
   m.attr("GEMM_EPI_SWIGLU") = (int)GM_EPI_SWIGLU;

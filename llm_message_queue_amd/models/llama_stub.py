@@ -70,7 +70,8 @@ class LlamaStub:
     def __init__(self, cfg: LlamaConfig, slots: int, max_ctx: int, device="cuda", impl: str = "hip",
                  seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False,
                  fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512,
-                 fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048, row_scale_norm: bool = True):
+                 fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048, row_scale_norm: bool = True,
+                 fused_head: Optional[bool] = None):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -103,6 +104,9 @@ class LlamaStub:
         # rope_kv at T = 4041, slower below ~2k rows: profiles/r2_gemm_swiglu.md)
         self.fused_qkv = (impl == "hip" and not split_qkv) if fused_qkv is None else bool(fused_qkv)
         self.min_fused_qkv_tokens = int(min_fused_qkv_tokens)
+        # LM head + greedy argmax in one hand-written GEMM (argmax epilogue, no
+        # [rows][vocab] logits) when the step samples >= 256 rows
+        self.fused_head = (impl == "hip") if fused_head is None else bool(fused_head)
         # fused paths take the raw residual rows + a per-row RMSNorm scale
         # (True) or an rmsnorm'd copy of the rows (False, A/B)
         self.row_scale_norm = bool(row_scale_norm)
@@ -174,8 +178,7 @@ class LlamaStub:
         per token."""
         xf = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec)
         sel = xf.index_select(0, sample_idx)
-        logits = F.linear(sel, self.lm_head)
-        return torch.argmax(logits, dim=-1).to(torch.int32)
+        return self.ops.greedy_head(sel, self.lm_head, self.fused_head)
 
     @torch.no_grad()
     def hidden(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,

@@ -218,3 +218,36 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
                     cos_t.data_ptr(), sin_t.data_ptr(), Hq, Hkv, max_ctx, S, q.data_ptr(), kc.data_ptr(),
                     vc.data_ptr(), stream, _row_scale_ptr(row_scale, T), full, ws, cnt)
     return q
+
+
+_ARGMAX_WS = {}
+
+
+def lm_head_argmax(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """Greedy next tokens ``argmax_n (x . w[n])`` -> int32 [M] with the argmax
+    in the GEMM epilogue: no [M][vocab] logits tensor is written or re-read
+    (the LM head of the serving step: ~1k rows x 128k vocab).  Ties resolve
+    to the lower index as torch.argmax does; the values compared are the fp32
+    accumulators, not bf16-rounded logits.  Scratch [M][N/256] (value, column)
+    partials are cached per (device, stream)."""
+    _check(x, "x")
+    _check(w, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K or not supported(M, N, K):
+        raise ValueError(f"lm_head_argmax: unsupported shape M={M} N={N} K={K}")
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    key = (x.device.type, x.device.index, stream)
+    need = M * (N // TILE_N)
+    ws = _ARGMAX_WS.get(key)
+    if ws is None or ws[0].numel() < need:
+        n = max(need, 2 * ws[0].numel() if ws is not None else 0)
+        ws = _ARGMAX_WS[key] = (torch.empty(n, dtype=torch.float32, device=x.device),
+                                torch.empty(n, dtype=torch.int32, device=x.device))
+    y = out if out is not None else torch.empty(M, dtype=torch.int32, device=x.device)
+    if y.dtype != torch.int32 or y.numel() < M or not y.is_contiguous():
+        raise ValueError("lm_head_argmax: out must be contiguous int32 [M]")
+    _native.require_hipops().gemm_argmax(x.data_ptr(), w.data_ptr(), M, N, K, ws[0].data_ptr(), ws[1].data_ptr(),
+                                         y.data_ptr(), stream)
+    return y
+

@@ -82,6 +82,15 @@ class HipOps:
         from . import gemm as G
         return G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, row_scale=r)
 
+    def greedy_head(self, x, w, fused: bool = True, min_rows: int = 256):
+        """Greedy tokens of the LM head (int32 [M]): the hand-written GEMM
+        with the argmax epilogue from ``min_rows`` rows (no logits tensor),
+        else hipBLASLt + torch.argmax."""
+        from . import gemm as G
+        if fused and x.shape[0] >= min_rows and G.supported(x.shape[0], w.shape[0], x.shape[1]):
+            return G.lm_head_argmax(x, w)
+        return torch.argmax(torch.nn.functional.linear(x, w), dim=-1).to(torch.int32)
+
     def mlp_up(self, x: torch.Tensor, w_gu: torch.Tensor, fused: bool, min_fused_tokens: int) -> torch.Tensor:
         """silu(x·Wgᵀ) * (x·Wuᵀ).  ``fused``: ``w_gu`` is in swiglu order and
         steps of >= ``min_fused_tokens`` rows run the hand-written GEMM with
@@ -194,6 +203,9 @@ class RefOps:
     def qkv_rope_rows(self, x, wqkv, r, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc):
         qkv = ((x.float() * r[:, None]) @ wqkv.float().t()).to(torch.bfloat16)
         return self.rope_kv(qkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc)
+
+    def greedy_head(self, x, w, fused: bool = True, min_rows: int = 256):
+        return torch.argmax(torch.nn.functional.linear(x, w), dim=-1).to(torch.int32)
 
     def mlp_up(self, x, w_gu, fused: bool, min_fused_tokens: int):
         """Reference of ``HipOps.mlp_up`` (``w_gu`` in swiglu order if fused)."""

@@ -286,3 +286,65 @@ def test_row_rms_and_row_scaled_swiglu_match_rmsnorm_path():
     ref = G.swiglu_reference(ops.rmsnorm(x, ones, 1e-5), w).float()
     out = G.gemm_swiglu(x, G.swiglu_permute(w), row_scale=r).float()
     assert (out - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [256, 300, 1000])
+def test_lm_head_argmax_matches_fp32_argmax(M):
+    """LM head with the argmax epilogue == argmax of the fp32 logits (a
+    mismatch is only allowed between near-tied logits)."""
+    V, d = 128256, 4096
+    g = torch.Generator(device=DEV).manual_seed(M)
+    x = torch.randn(M, d, generator=g, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(V, d, generator=g, device=DEV) * 0.02).to(torch.bfloat16)
+    got = G.lm_head_argmax(x, w).long()
+    ref = torch.empty(M, V, device=DEV)
+    for i in range(0, M, 128):                                   # fp32 logits in row chunks
+        ref[i:i + 128] = x[i:i + 128].float() @ w.float().t()
+    exp = ref.argmax(1)
+    bad = (got != exp).nonzero().flatten()
+    assert bad.numel() <= max(1, M // 100), bad.numel()
+    for i in bad.tolist():
+        gap = (ref[i, exp[i]] - ref[i, got[i]]).item()
+        assert 0 <= gap <= 1e-3 * ref[i].abs().max().item(), (i, gap)
+
+
+@pytest.mark.gpu
+def test_lm_head_argmax_ties_pick_the_lowest_column():
+    V, d = 128256, 256
+    x = torch.zeros(256, d, device=DEV)
+    w = torch.zeros(V, d, device=DEV)
+    x[0, 0] = 1.0
+    w[[300, 1000, 70000], 0] = 2.0                               # tie across tiles
+    x[1, 1] = 1.0
+    w[[515, 513, 77777], 1] = 3.0                                # tie inside one tile (513, 515) and across
+    x[2, 2] = -1.0
+    w[:, 2] = 1.0
+    w[12345, 2] = -5.0                                           # single maximum, negative logits
+    got = G.lm_head_argmax(x.to(torch.bfloat16), w.to(torch.bfloat16)).tolist()
+    assert got[0] == 300 and got[1] == 513 and got[2] == 12345
+    assert all(t == 0 for t in got[3:])                          # all-zero rows: every logit ties at 0
+
+
+@pytest.mark.gpu
+def test_tiny_model_fused_head_matches_fp32_argmax():
+    """The model's fused head returns the argmax of the fp32 logits of its
+    hidden states (the unfused path argmaxes bf16-rounded logits, which tie
+    often at this model's logit scale -- it is not the reference here)."""
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
+    cfg = LlamaConfig.tiny()
+    a = LlamaStub(cfg, slots=5, max_ctx=64, device=DEV, impl="hip", seed=3, fused_head=True)
+    T = 300                                                      # distinct (slot, pos) cells
+    tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
+    pos = (torch.arange(T, device=DEV) % 64).to(torch.int32)
+    slot = (torch.arange(T, device=DEV) // 64).to(torch.int32)
+    samp = torch.arange(T, device=DEV)
+    xf = a.hidden(tok, pos, slot)
+    ref = (xf.float() @ a.lm_head.float().t())
+    got = a.ops.greedy_head(xf, a.lm_head, True).long()
+    exp = ref.argmax(1)
+    for i in (got != exp).nonzero().flatten().tolist():
+        gap = (ref[i, exp[i]] - ref[i, got[i]]).item()
+        assert 0 <= gap <= 1e-3 * ref[i].abs().max().item(), (i, gap)
+    # forward() (hidden + the fused head) gives the same tokens: the trunk is deterministic
+    assert torch.equal(a.forward(tok, pos, slot, samp).long(), got)
