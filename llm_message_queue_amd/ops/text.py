@@ -359,7 +359,7 @@ class TextPipeline:
     def _launch_one_call(self, t0, B, pk, lens, ob, total, classify, prompt_cap, stream, contents):
         """The serve loop's path: the whole chain is one native call
         (``_hipops.text_batch``) over reused buffers -- no per-batch tensor
-        allocations, six launches instead of eleven."""
+        allocations, four launches instead of eleven."""
         ws = self._workspace(B, classify)
         L = self.L
         cap = min(prompt_cap, L) if prompt_cap > 0 else 0
