@@ -67,6 +67,13 @@ def _targets() -> Dict[str, dict]:
                    "-Wno-unused-command-line-argument", "-ffp-contract=fast"],
             libs=[f"-L{ROCM}/lib", "-lamdhip64"],
         ),
+        "_textcpu": dict(
+            compiler="g++",
+            sources=[os.path.join(CSRC, "text", "text_cpu.cpp")],
+            deps=[os.path.join(CSRC, "text", "text_cpu.h")],
+            flags=["-O3", "-std=c++17", "-fvisibility=hidden"],
+            libs=[],
+        ),
         "_telemetry": dict(
             compiler="g++",
             sources=[os.path.join(CSRC, "telemetry", "telemetry.cpp")],

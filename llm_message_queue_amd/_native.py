@@ -67,5 +67,10 @@ def shmring():
     return load("_shmring", autobuild=True)
 
 
+def textcpu():
+    """CPU twin of the text_analyze kernel (csrc/text/text_cpu.h)."""
+    return load("_textcpu", autobuild=True)
+
+
 def ingress():
     return load("_ingress", autobuild=True)

@@ -271,7 +271,8 @@ class TextPipeline:
             self._packed = pack_patterns(patterns, version)
         return self._packed
 
-    def pack(self, contents: Sequence[str]):
+    @staticmethod
+    def pack(contents: Sequence[str]):
         """UTF-8 bytes + offsets for a batch (host side)."""
         n = len(contents)
         if all(c.isascii() for c in contents):        # the common case: one encode for the batch
@@ -453,3 +454,59 @@ class TextPipeline:
         return {"event": ev, "B": B, "cap": cap, "o_pred": o_pred, "o_ph": o_ph, "pred": pred, "pk": pk,
                 "contents": contents, "t0": t0, "keep_device": keep_device, "pooled": pooled, "hashes": hashes,
                 "stats": stats, "hc": hc if cap else None}
+
+
+class CpuTextPipeline:
+    """The text pipeline on the CPU (no GPU on the host): the ``_textcpu``
+    module runs the same per-byte analysis as ``text_analyze_kernel`` over
+    the same packed batch and pattern table, and returns the same stats rows
+    and token hashes, so ``Preprocessor.end_batch`` decides priorities
+    exactly as on the GPU path (fold-special messages still go to the
+    oracle).  No classifier (the CPU oracle path has none either).  Same
+    launch / ready / collect interface as :class:`TextPipeline`; ``launch``
+    does the work."""
+
+    def __init__(self, cfg=None):
+        from ..utils.config import PreprocessorConfig
+        self.cfg = cfg or PreprocessorConfig()
+        self.L = int(self.cfg.max_tokens)
+        self.mod = _native.textcpu()
+        assert self.mod.PATTERN_TABLE_BYTES == 4 * (MAX_PATTERNS * 8 + MAX_PATTERNS * 3 + 1)
+        self._packed: Optional[PackedPatterns] = None
+
+    def _patterns(self, patterns, version) -> PackedPatterns:
+        if self._packed is None or self._packed.version != version or version < 0:
+            self._packed = pack_patterns(patterns, version)
+        return self._packed
+
+    def run(self, contents: Sequence[str], patterns: Dict[int, list], version: int = -1,
+            classify: bool = False, keep_device: bool = False, prompt_cap: int = 0) -> TextResult:
+        return self.collect(self.launch(contents, patterns, version, classify, keep_device, prompt_cap))
+
+    def launch(self, contents: Sequence[str], patterns: Dict[int, list], version: int = -1,
+               classify: bool = False, keep_device: bool = False, prompt_cap: int = 0):
+        t0 = time.perf_counter()
+        pk = self._patterns(patterns, version)
+        blob, offsets, _lens = TextPipeline.pack(contents)
+        B, L = len(contents), self.L
+        stats = np.empty((B, STAT_COLS), dtype=np.int32)
+        hashes = np.empty((B, L), dtype=np.uint32)
+        self.mod.analyze(np.frombuffer(blob, dtype=np.uint8), offsets, B, L, pk.table, stats, hashes)
+        extra = None
+        if pk.cpu_patterns:
+            extra = np.zeros((B, 8), dtype=np.int64)
+            for j, c in enumerate(contents):
+                for slot, pat in pk.cpu_patterns:
+                    extra[j, slot] += pat.count(c)
+        cap = min(prompt_cap, L) if prompt_cap > 0 else 0
+        res = TextResult(stats, None, (time.perf_counter() - t0) * 1e3, False, pk.slot_prio, extra, None, None, L,
+                         hashes[:, :cap] if cap else None)
+        return {"result": res}
+
+    @staticmethod
+    def ready(pend) -> bool:
+        return True
+
+    def collect(self, pend) -> TextResult:
+        return pend["result"]
+

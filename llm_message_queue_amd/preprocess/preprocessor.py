@@ -46,6 +46,7 @@ class Preprocessor:
         self._want_gpu = self.cfg.use_gpu if use_gpu is None else use_gpu
         self._device = device
         self._gpu = None           # lazily-built ops.text.TextPipeline
+        self._cpu = None           # lazily-built ops.text.CpuTextPipeline (False: unavailable)
         self._pattern_version = 0
         self.stats = {"gpu_batches": 0, "gpu_messages": 0, "oracle_fallbacks": 0,
                       "cpu_messages": 0, "last_gpu_ms": 0.0}
@@ -198,6 +199,22 @@ class Preprocessor:
             self._gpu = TextPipeline(self.cfg, device=self._device)
         return self._gpu
 
+    def cpu_pipeline(self):
+        """The native CPU twin of the text kernel, or None (disabled by
+        ``preprocessor.native_cpu`` or the module cannot be built/loaded --
+        then the per-message oracle runs, with a warning once)."""
+        if self._cpu is None:
+            self._cpu = False
+            if getattr(self.cfg, "native_cpu", True):
+                try:
+                    from ..ops.text import CpuTextPipeline
+                    self._cpu = CpuTextPipeline(self.cfg)
+                except Exception as e:              # no compiler / module on this host
+                    import logging
+                    logging.getLogger("preprocessor").warning("native CPU preprocess unavailable (%s); "
+                                                              "using the Python oracle", e)
+        return self._cpu or None
+
     def gpu_enabled(self) -> bool:
         if not self._want_gpu:
             return False
@@ -212,6 +229,9 @@ class Preprocessor:
         """Process a micro-batch.  Same results as ``process_message`` per
         message; on the GPU path one fused launch covers the whole batch."""
         use_gpu = self.gpu_enabled() if use_gpu is None else use_gpu
+        if not use_gpu and msgs and self.cpu_pipeline() is not None:
+            # the C++ twin of the GPU kernel, then the same batch decisions
+            return self.end_batch(self.begin_batch(msgs, classify=False, prompt_cap=prompt_cap, cpu=True))
         if not use_gpu:
             for m in msgs:
                 self.process_message(m)
@@ -226,7 +246,8 @@ class Preprocessor:
         return self.end_batch(self.begin_batch(msgs, classify=classify, prompt_cap=prompt_cap))
 
     # ------------------------------------------------------------------ asynchronous batch (GPU)
-    def begin_batch(self, msgs: Sequence[Message], classify: Optional[bool] = None, prompt_cap: int = 0):
+    def begin_batch(self, msgs: Sequence[Message], classify: Optional[bool] = None, prompt_cap: int = 0,
+                    cpu: bool = False):
         """Launch a micro-batch's GPU preprocess and return at once (the
         host does not wait for the kernels, which queue behind the backend's
         forward for CUs); ``end_batch`` applies the results.  One batch may be
@@ -239,28 +260,32 @@ class Preprocessor:
         # return) but the backend still needs their prompt token ids
         work = [i for i in range(len(msgs)) if msgs[i].content] if prompt_cap else \
             [i for i, h in enumerate(heads) if h is not None and msgs[i].content]
-        pend = None
+        pend = pipe = None
         if work:
-            pipe = self.gpu_pipeline()
+            pipe = self.cpu_pipeline() if cpu else self.gpu_pipeline()
             pats, ver = self.patterns_snapshot()
             pend = pipe.launch([msgs[i].content for i in work], pats, ver,
-                               classify=self.cfg.classifier if classify is None else classify,
+                               classify=False if cpu else (self.cfg.classifier if classify is None else classify),
                                prompt_cap=prompt_cap)
-        return {"msgs": msgs, "heads": heads, "work": work, "pend": pend, "prompt_cap": prompt_cap}
+        return {"msgs": msgs, "heads": heads, "work": work, "pend": pend, "prompt_cap": prompt_cap, "pipe": pipe,
+                "cpu": cpu}
 
     def batch_ready(self, tok) -> bool:
-        return tok["pend"] is None or self._gpu.ready(tok["pend"])
+        return tok["pend"] is None or tok["pipe"].ready(tok["pend"])
 
     def end_batch(self, tok) -> Sequence[Message]:
         msgs, heads, work, prompt_cap = tok["msgs"], tok["heads"], tok["work"], tok["prompt_cap"]
         now = time.time_ns()
         if work:
-            pipe = self.gpu_pipeline()
-            res = pipe.collect(tok["pend"])
-            self.stats["gpu_batches"] += 1
-            self.stats["gpu_messages"] += len(work)
-            self.stats["last_gpu_ms"] = res.elapsed_ms
-            self.stats["gpu_ms_total"] = self.stats.get("gpu_ms_total", 0.0) + res.elapsed_ms
+            res = tok["pipe"].collect(tok["pend"])
+            if tok.get("cpu"):
+                self.stats["cpu_native_batches"] = self.stats.get("cpu_native_batches", 0) + 1
+                self.stats["cpu_native_messages"] = self.stats.get("cpu_native_messages", 0) + len(work)
+            else:
+                self.stats["gpu_batches"] += 1
+                self.stats["gpu_messages"] += len(work)
+                self.stats["last_gpu_ms"] = res.elapsed_ms
+                self.stats["gpu_ms_total"] = self.stats.get("gpu_ms_total", 0.0) + res.elapsed_ms
             d = res.decide(self.default_priority)
             fb, kp, wc, sent, qs, ntok = d["fallback"], d["priority"], d["word_count"], d["sentiment"], \
                 d["question"], d["ntok"]

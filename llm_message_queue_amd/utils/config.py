@@ -221,6 +221,8 @@ class PreprocessorConfig:
     max_tokens: int = 128              # tokens per message fed to the classifier
     classifier: bool = True            # run the MFMA embedding classifier
     use_classifier_priority: bool = False  # let the classifier decide no-keyword msgs
+    native_cpu: bool = True            # without a GPU: the C++ twin of the text kernel (csrc/text/text_cpu.h)
+                                       # instead of the per-message Python oracle
     vocab_buckets: int = 65536
     embed_dim: int = 256
     hidden_dim: int = 1024
