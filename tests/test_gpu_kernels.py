@@ -41,6 +41,24 @@ def _check_batch(texts, patterns=None, L=64):
         assert list(hashes[j, :len(th)]) == th, repr(t)
 
 
+def test_cpu_twin_matches_gpu_kernel_bit_for_bit():
+    """csrc/text/text_cpu.h == text_analyze_kernel: every stats column
+    (including the precomputed decisions) and every token hash."""
+    from llm_message_queue_amd.ops.text import CpuTextPipeline, TextPipeline
+    from llm_message_queue_amd.utils.config import PreprocessorConfig
+    cfg = PreprocessorConfig(max_tokens=64)
+    pats = oracle.default_patterns()
+    pats[2].append(oracle.compile_pattern("aa"))
+    texts = ADVERSARIAL + _random_texts(500, seed=21)
+    g = TextPipeline(cfg, device=DEV).run(texts, pats, classify=False, keep_device=True)
+    c = CpuTextPipeline(cfg).run(texts, pats, prompt_cap=64)
+    assert (g.stats == c.stats).all()
+    gh = g.hashes.cpu().numpy().view(np.uint32)
+    for j in range(len(texts)):
+        n = int(g.stats[j, 5])
+        assert (gh[j, :n] == c.prompt_hashes[j, :n]).all(), repr(texts[j])
+
+
 def test_text_analyze_adversarial():
     _check_batch(ADVERSARIAL)
 
