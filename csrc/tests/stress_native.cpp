@@ -32,6 +32,7 @@
 #include "queue/mlq_core.h"
 #include "queue/shm_coll.h"
 #include "queue/shm_ring.h"
+#include "text/text_cpu.h"
 
 #define CHECK(c)                                                              \
   do {                                                                        \
@@ -259,6 +260,46 @@ static void stress_shm_coll() {
   std::printf("shm collective: %d ranks x %d exchanges OK, dead-peer timeout OK\n", W, OPS);
 }
 
+static void fuzz_text_cpu() {
+  // the CPU twin of the preprocess kernel reads untrusted request bodies:
+  // random bytes (invalid UTF-8, truncated sequences, fold-special bytes,
+  // Unicode spaces at the very end) of random lengths, with a pattern table
+  // that includes bordered and case-insensitive patterns -- every message is
+  // analysed in an exactly-sized heap buffer so ASan sees any overread
+  using llmq::textcpu::Analyzer;
+  using llmq::textcpu::PatternTable;
+  PatternTable pt{};
+  const char* pats[] = {"urgent", "aa", "\xc5\xbf", "now", "zz"};
+  pt.npat = 5;
+  for (int j = 0; j < pt.npat; ++j) {
+    const std::string p = j == 2 ? std::string("\xe2\x80", 2) : std::string(pats[j]);
+    std::memset(pt.text[j], 0, 16);
+    std::memcpy(pt.text[j], p.data(), p.size());
+    std::memset(pt.mask[j], 0, 16);
+    std::memset(pt.mask[j], 0xFF, p.size());
+    pt.len[j] = (int)p.size();
+    pt.slot[j] = j % 8;
+    pt.flags[j] = (j == 0 ? 1 : 0) | (j == 1 || j == 4 ? 2 : 0);
+  }
+  const Analyzer an(pt, 64);
+  std::mt19937 rng(7);
+  const uint8_t alphabet[] = {' ', 'a', 'A', 'z', 'u', '?', 0xC2, 0x85, 0xA0, 0xE2, 0x80, 0x81, 0x9F, 0xE3,
+                              0xC5, 0xBF, 0xC4, 0xB0, 0x84, 0xAA, 0xF0, 0x9F, 0x98, 0x80, 0xFF, 0x00, '\t'};
+  int32_t st[16];
+  uint32_t h[64];
+  long words = 0;
+  for (int it = 0; it < 20000; ++it) {
+    const int len = (int)(rng() % 300);
+    std::unique_ptr<uint8_t[]> buf(new uint8_t[len > 0 ? len : 1]);
+    for (int i = 0; i < len; ++i)
+      buf[i] = (rng() & 3) ? alphabet[rng() % sizeof(alphabet)] : (uint8_t)rng();
+    an.analyze(buf.get(), len, st, h);
+    CHECK(st[5] >= 0 && st[5] <= 64 && st[5] <= st[0] && st[0] <= len);
+    words += st[0];
+  }
+  std::printf("text cpu fuzz: 20000 random messages, %ld words, no fault\n", words);
+}
+
 static void stress_guard() {
   // 8 threads hammer one global bucket + per-user buckets with a fixed clock
   // window: admitted count must equal the token budget exactly.
@@ -330,6 +371,7 @@ int main() {
   stress_delayed();
   stress_ring();
   stress_shm_coll();
+  fuzz_text_cpu();
   stress_guard();
   fuzz_guard_parser();
   std::printf("ALL OK\n");
