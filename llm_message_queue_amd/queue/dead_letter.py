@@ -48,6 +48,15 @@ class DeadLetterQueue:
         self._notify: List[_pyqueue.Queue] = []
         self.logger = logger or get_logger("dead_letter_queue")
         self.dropped_notifications = 0
+        # handlers run asynchronously (the reference's `go handler(item)`) on
+        # ONE worker thread fed by a queue -- a thread per item per handler
+        # would spawn thousands of threads a second when overload shedding
+        # moves whole batches here
+        self._work: _pyqueue.SimpleQueue = _pyqueue.SimpleQueue()
+        self._worker: Optional[threading.Thread] = None
+        # bulk moves log at most once per LOG_EVERY_S with the count since the last line
+        self._log_next = 0.0
+        self._log_pending = 0
 
     def add_handler(self, handler: DeadLetterHandler) -> None:
         with self._lock:
@@ -69,7 +78,7 @@ class DeadLetterQueue:
         self.logger.warning("Message moved to dead letter queue", message_id=message.id,
                             reason=str(fail_reason), source=source_queue)
         for h in handlers:
-            threading.Thread(target=self._run_handler, args=(h, item), daemon=True).start()
+            self._submit(h, item)
         for ch in chans:
             try:
                 ch.put_nowait(item)
@@ -88,11 +97,17 @@ class DeadLetterQueue:
             handlers = list(self._handlers)
             chans = list(self._notify)
         if items:
-            self.logger.warning("Messages moved to dead letter queue", count=len(items), reason=str(fail_reason),
-                                source=source_queue, dropped=len(messages) - len(items))
+            self._log_pending += len(items)
+            t = time.monotonic()
+            if t >= self._log_next:
+                self.logger.warning("Messages moved to dead letter queue", count=self._log_pending,
+                                    reason=str(fail_reason), source=source_queue,
+                                    dropped=len(messages) - len(items))
+                self._log_pending = 0
+                self._log_next = t + self.LOG_EVERY_S
         for item in items:
             for h in handlers:
-                threading.Thread(target=self._run_handler, args=(h, item), daemon=True).start()
+                self._submit(h, item)
             for ch in chans:
                 try:
                     ch.put_nowait(item)
@@ -104,6 +119,21 @@ class DeadLetterQueue:
         """Re-insert an item from a snapshot (no handlers/notifications fire)."""
         with self._lock:
             self._items.append(item)
+
+    LOG_EVERY_S = 1.0
+
+    def _submit(self, h: DeadLetterHandler, item: DeadLetterItem) -> None:
+        self._work.put((h, item))
+        if self._worker is None or not self._worker.is_alive():
+            with self._lock:
+                if self._worker is None or not self._worker.is_alive():
+                    self._worker = threading.Thread(target=self._drain, name="dlq-handlers", daemon=True)
+                    self._worker.start()
+
+    def _drain(self) -> None:
+        while True:
+            h, item = self._work.get()
+            self._run_handler(h, item)
 
     def _run_handler(self, h: DeadLetterHandler, item: DeadLetterItem) -> None:
         try:

@@ -363,3 +363,21 @@ def test_dlq_batch_requeue_handlers_and_notify():
         small = DeadLetterQueue(1)
         small.push(new_message("c", "u", "a", 3), "r", "q")
         small.push(new_message("c", "u", "b", 3), "r", "q")
+
+
+def test_dlq_bulk_handlers_run_on_one_worker_thread():
+    """Overload shedding moves thousands of messages at once: every handler
+    call still runs (asynchronously, in order) but on one worker thread, not a
+    thread per item."""
+    import threading
+    d = DeadLetterQueue(0)
+    seen = []
+    d.add_handler(lambda it: seen.append(it.message.id))
+    before = threading.active_count()
+    msgs = [new_message("c", "u", str(i), 3) for i in range(5000)]
+    assert d.push_many(msgs, "timeout", "low") == 5000
+    assert threading.active_count() <= before + 1
+    t0 = time.time()
+    while len(seen) < 5000 and time.time() - t0 < 10:
+        time.sleep(0.01)
+    assert seen == [m.id for m in msgs]
