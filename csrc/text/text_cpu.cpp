@@ -4,9 +4,12 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "text/text_cpu.h"
 
@@ -38,9 +41,23 @@ static void analyze(py::array_t<uint8_t, py::array::c_style> bytes, py::array_t<
   uint32_t* h = hashes.mutable_data();
   py::gil_scoped_release nogil;
   const Analyzer an(pt, L);
-  for (int i = 0; i < B; ++i)
-    an.analyze(src + off[i], (int)(off[i + 1] - off[i]), st + (int64_t)i * llmq::textcpu::STAT_COLS,
-               h + (int64_t)i * L);
+  auto run = [&](int i0, int i1) {
+    for (int i = i0; i < i1; ++i)
+      an.analyze(src + off[i], (int)(off[i + 1] - off[i]), st + (int64_t)i * llmq::textcpu::STAT_COLS,
+                 h + (int64_t)i * L);
+  };
+  // large batches (an ingest backlog) split over a few threads; messages are
+  // independent and each writes only its own rows
+  const int nt = B >= 2048 ? (int)std::min<unsigned>(std::max(1u, std::thread::hardware_concurrency()), 8u) : 1;
+  if (nt <= 1) {
+    run(0, B);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int per = (B + nt - 1) / nt;
+  for (int t = 1; t < nt; ++t) th.emplace_back(run, std::min(B, t * per), std::min(B, (t + 1) * per));
+  run(0, std::min(B, per));
+  for (auto& x : th) x.join();
 }
 
 PYBIND11_MODULE(_textcpu, m) {

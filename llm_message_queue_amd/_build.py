@@ -71,7 +71,7 @@ def _targets() -> Dict[str, dict]:
             compiler="g++",
             sources=[os.path.join(CSRC, "text", "text_cpu.cpp")],
             deps=[os.path.join(CSRC, "text", "text_cpu.h")],
-            flags=["-O3", "-std=c++17", "-fvisibility=hidden"],
+            flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
             libs=[],
         ),
         "_telemetry": dict(
