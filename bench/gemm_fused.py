@@ -123,6 +123,8 @@ def main():
                   flush=True)
             fns = {"hipblaslt+rope_kv": lambda: ops.rope_kv(F.linear(x, wqkv), pos, slot, cos_t, sin_t, Hq, Hkv, kc1, vc1),
                    "fused": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2),
+                   "fused_g4": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2, group_m=4),
+                   "fused_g16": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2, group_m=16),
                    "fused_nosplit": lambda: G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc2, vc2,
                                                        split=False)}
             if T <= 1024:   # split every tile: the cost of a K-half + the handoff vs a whole tile

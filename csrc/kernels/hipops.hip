@@ -237,7 +237,8 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
 static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr_t pos, uintptr_t slot,
                           uintptr_t cos_t, uintptr_t sin_t, int Hq, int Hkv, int max_ctx, int n_slots,
                           uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t stream, uintptr_t rs,
-                          int split_full, uintptr_t split_ws, uintptr_t split_cnt) {
+                          int split_full, uintptr_t split_ws, uintptr_t split_cnt, int group_m) {
+  require(group_m >= 1 && group_m <= 64, "gemm_qkv_rope: group_m");
   require(M > 0 && K > 0, "gemm_qkv_rope: empty operand");
   require(Hq % 2 == 0 && Hkv % 2 == 0 && Hkv >= 2, "gemm_qkv_rope: head counts must be even");
   require(N == (Hq + 2 * Hkv) * 128, "gemm_qkv_rope: N must be (Hq + 2 Hkv) * 128");
@@ -256,7 +257,7 @@ static void gemm_qkv_rope(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr
     require(split_cnt != 0 && split_ws % 16 == 0, "gemm_qkv_rope: split workspace");
     sp = GmSplit{split_full, P<float>(split_ws), P<int>(split_cnt)};
   }
-  launch_gemm<GM_EPI_ROPE>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M,
+  launch_gemm<GM_EPI_ROPE>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), group_m,
                            rs ? P<const float>(rs) : nullptr, rp, sp);
   check_launch();
 }
@@ -444,7 +445,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("gemm_qkv_rope", &gemm_qkv_rope, py::arg("a"), py::arg("w"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("pos"), py::arg("slot"), py::arg("cos_t"), py::arg("sin_t"), py::arg("Hq"), py::arg("Hkv"),
         py::arg("max_ctx"), py::arg("n_slots"), py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("stream"),
-        py::arg("rs") = 0, py::arg("split_full") = 0, py::arg("split_ws") = 0, py::arg("split_cnt") = 0);
+        py::arg("rs") = 0, py::arg("split_full") = 0, py::arg("split_ws") = 0, py::arg("split_cnt") = 0,
+        py::arg("group_m") = GM_GROUP_M);
   m.def("gemm_argmax", &gemm_argmax);
   m.def("row_rms", &row_rms);
   m.attr("GEMM_EPI_STORE") = (int)GM_EPI_STORE;

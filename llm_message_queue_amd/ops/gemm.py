@@ -179,7 +179,7 @@ def _cu_count(device) -> int:
 def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
              cos_t: torch.Tensor, sin_t: torch.Tensor, Hq: int, Hkv: int,
              kc: torch.Tensor, vc: torch.Tensor, q_out: torch.Tensor = None, row_scale=None,
-             split: bool = True, split_full: int = None) -> torch.Tensor:
+             split: bool = True, split_full: int = None, group_m: int = 8) -> torch.Tensor:
     """The qkv projection with RoPE + the K/V cache write as its epilogue:
     returns q [T][Hq*128] (rotated) and writes this step's K/V rows into
     ``kc`` / ``vc`` [slots][Hkv][max_ctx][128] -- the same result as
@@ -216,7 +216,7 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
             full, ws, cnt = f, w_t.data_ptr(), c_t.data_ptr()
     k.gemm_qkv_rope(x.data_ptr(), wqkv.data_ptr(), T, N, K, pos.data_ptr(), slot.data_ptr(),
                     cos_t.data_ptr(), sin_t.data_ptr(), Hq, Hkv, max_ctx, S, q.data_ptr(), kc.data_ptr(),
-                    vc.data_ptr(), stream, _row_scale_ptr(row_scale, T), full, ws, cnt)
+                    vc.data_ptr(), stream, _row_scale_ptr(row_scale, T), full, ws, cnt, group_m)
     return q
 
 
