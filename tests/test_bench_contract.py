@@ -40,6 +40,11 @@ def test_bench_single_rank_dry_run():
     # offered rate ran first (the driver's 20-step window used to
     # start from the empty system the calibration drain left)
     assert d["steady_ticks"] >= 60
+    # value = min(dispatched, arrived) per second in the window: never above
+    # the rate the offered load actually arrived at
+    assert d["value"] <= d["dispatch_rate_in_window"] + 1e-6
+    assert d["value"] <= d["arrival_rate_in_window"] + 1e-6
+    assert abs(d["value"] - min(d["dispatch_rate_in_window"], d["arrival_rate_in_window"])) < 0.02
 
 
 def test_bench_four_ranks_torchrun_dry_run():
