@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--rope", action="store_true", help="also A/B the qkv GEMM with the RoPE/KV epilogue")
     ap.add_argument("--head", action="store_true", help="also A/B the LM head: hipBLASLt + argmax vs argmax epilogue")
     ap.add_argument("--groups", default="", help="e.g. 4,8,16: also time gemm_swiglu per block-order group size")
+    ap.add_argument("--prio", action="store_true",
+                    help="also time gemm_swiglu with s_setprio flips per MFMA cluster / a static priority on wave row 0 / none")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -85,6 +87,12 @@ def main():
             F.linear(x, w_gu)
 
         fns = {"hipblaslt+silu_mul": unfused, "fused": fused, "hipblaslt_gemm_only": blas_only}
+        if a.prio:
+            ref_out = G.gemm_swiglu(x, w_perm).clone()
+            for name, code in (("fused_prio_flips", 48), ("fused_prio_row0", 64), ("fused_noprio", 80)):
+                fns[name] = (lambda code=code: G._launch(x, w_perm, out, G.EPI_SWIGLU + code))
+                fns[name]()
+                print(json.dumps({"check": name, "T": T, "bit_equal": bool(torch.equal(out, ref_out))}), flush=True)
         for gm in [int(v) for v in a.groups.split(",") if v]:
             fns[f"fused_g{gm}"] = (lambda gm=gm: G._launch(x, w_perm, out, G.EPI_SWIGLU, group_m=gm))
         for f in fns.values():

@@ -142,7 +142,7 @@ __device__ __forceinline__ void gm_stage(__amdgpu_buffer_rsrc_t rs, uint32_t v0,
     GM_FENCE();                       \
   } while (0)
 
-template <int EPI, bool STAGGER = true, int SCHED = 1>
+template <int EPI, bool STAGGER = true, int SCHED = 2>
 __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
     int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp,
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 
   gm_bf16x8 af[4][2];                              // one m-half: [m][kk]
   gm_bf16x8 bfr[2][2][2];                          // both n-halves: [nh][n][kk]
-  gm_bf16x8 b0y[2][2];                             // SCHED 1: buffer-1 B0 fragments
+  gm_bf16x8 b0y[2][2];                             // SCHED >= 1: buffer-1 B0 fragments
 
 #define GM_STAGE(BUF, HALF, KT)                                                               \
   do {                                                                                        \
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     __builtin_amdgcn_s_setprio(0);                                                             \
   } while (0)
 
-// SCHED 1 helpers: B0 fragments into an explicit register set, MFMA with it
+// SCHED >= 1 helpers: B0 fragments into an explicit register set, MFMA with it
 #define GM_READ_B0_INTO(BUF, DST)                                                              \
   do {                                                                                         \
     _Pragma("unroll") for (int n = 0; n < 2; ++n)                                              \
@@ -267,13 +267,13 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 
 #define GM_MFMA_WITH(MH, NH, BREG)                                                             \
   do {                                                                                         \
-    __builtin_amdgcn_s_setprio(1);                                                             \
+    if constexpr (SCHED == 1) __builtin_amdgcn_s_setprio(1);                                   \
     _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                           \
       _Pragma("unroll") for (int m = 0; m < 4; ++m)                                            \
         _Pragma("unroll") for (int n = 0; n < 2; ++n)                                          \
           acc[MH][m][NH][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], BREG[n][kk],  \
                                                                       acc[MH][m][NH][n], 0, 0, 0); \
-    __builtin_amdgcn_s_setprio(0);                                                             \
+    if constexpr (SCHED == 1) __builtin_amdgcn_s_setprio(0);                                   \
   } while (0)
 
 #define GM_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
@@ -283,7 +283,15 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   const int nt = khalf < 0 ? K / GM_BK : K / GM_BK / 2;
   const int kt0 = khalf > 0 ? nt : 0;
 
-  if constexpr (SCHED == 1) {
+  if constexpr (SCHED >= 1) {
+    // Wave priority.  SCHED 2 (default): one static s_setprio 1 for wave row
+    // 1 (the later-dispatched half, cdna_hip_programming.md T5 static form),
+    // no per-cluster flips -- 1.7 % faster than SCHED 1 (s_setprio 1 around
+    // every MFMA cluster) at T = 4041 (profiles/r2_gemm_prio_ab.jsonl).
+    // SCHED 3 / 4 (A/B only): the static priority on wave row 0 / none.
+    if constexpr (SCHED == 2 || SCHED == 3) {
+      if (wr == (SCHED == 2 ? 1 : 0)) __builtin_amdgcn_s_setprio(1);
+    }
     // Balanced schedule: every phase retires the half-tile staged 3 phases
     // earlier (vmcnt(6) each phase), so the NEXT buffer's B0 fragments can be
     // read one phase early (phases 4 and 8, which otherwise read nothing):
@@ -333,6 +341,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         GM_READ_A(1, 1); GM_PHASE_END(1, 1, bfr[1]);
         GM_PHASE_END(1, 0, b0y);
     }
+    if constexpr (SCHED == 2 || SCHED == 3) __builtin_amdgcn_s_setprio(0);
 #undef GM_PHASE_END
   } else {
     // prologue: tile 0 -> buffer 0 (all halves), tile 1 -> buffer 1 (B0, A0, B1)

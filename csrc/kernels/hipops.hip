@@ -188,7 +188,7 @@ static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T,
 
 // C = A · Wᵀ (epi 0, C [M][N]) or H = silu(A·Wgᵀ) * (A·Wuᵀ) over a
 // swiglu-permuted W (epi 2, C [M][N/2]); A [M][K], W [N][K], bf16.
-template <int EPI, bool STAGGER = true, int SCHED = 1>
+template <int EPI, bool STAGGER = true, int SCHED = 2>
 static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st,
                         int group_m, const float* rs = nullptr, const GmRope& rp = GmRope{},
                         const GmSplit& sp = GmSplit{0, nullptr, nullptr},
@@ -206,7 +206,9 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
 }
 
 // epi: 0 / 2 = store / SwiGLU; 16 / 32 = store with the round-1 phase
-// schedule / without the wave-row stagger (A/B measurements only).
+// schedule / without the wave-row stagger; 50 / 66 / 82 = SwiGLU with
+// s_setprio around every MFMA cluster / the static priority on wave row 0 /
+// no priority (A/B only; the default is a static priority on wave row 1).
 static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t stream,
                       int group_m, uintptr_t rs) {
   require(group_m >= 1 && group_m <= 64, "gemm: group_m out of range");
@@ -225,7 +227,16 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
   else if (epi == GM_EPI_STORE + 16)
     launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_STORE + 32)
-    launch_gemm<GM_EPI_STORE, false, 1>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
+    launch_gemm<GM_EPI_STORE, false, 2>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
+  else if (epi == GM_EPI_SWIGLU + 48)
+    launch_gemm<GM_EPI_SWIGLU, true, 1>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
+                                        group_m, rsp);
+  else if (epi == GM_EPI_SWIGLU + 64)
+    launch_gemm<GM_EPI_SWIGLU, true, 3>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
+                                        group_m, rsp);
+  else if (epi == GM_EPI_SWIGLU + 80)
+    launch_gemm<GM_EPI_SWIGLU, true, 4>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
+                                        group_m, rsp);
   else
     throw std::invalid_argument("gemm: unknown epilogue");
   check_launch();
