@@ -71,6 +71,8 @@ def parse(argv=None):
                     help="fused GEMMs read rmsnorm'd rows instead of raw rows + a per-row scale (A/B)")
     ap.add_argument("--no-fused-head", action="store_true",
                     help="LM head on hipBLASLt + torch.argmax instead of the GEMM with the argmax epilogue")
+    ap.add_argument("--fused-resid", action="store_true",
+                    help="A/B: o / down projections on the hand-written residual-add GEMM epilogue (default hipBLASLt beta = 1)")
     ap.add_argument("--no-fused-qkv", action="store_true",
                     help="qkv on hipBLASLt + rope_kv instead of the GEMM with the RoPE/KV epilogue (A/B)")
     ap.add_argument("--no-fused-mlp", action="store_true",
@@ -161,7 +163,8 @@ def main(argv=None) -> int:
                            residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv,
                            fused_mlp=False if a.no_fused_mlp else None,
                            fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
-                           fused_head=False if a.no_fused_head else None)
+                           fused_head=False if a.no_fused_head else None,
+                           fused_resid=True if a.fused_resid else None)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -383,7 +386,8 @@ def main(argv=None) -> int:
                    "split_qkv": a.split_qkv, "fused_mlp": bool(engine.model.fused_mlp),
                    "fused_qkv": bool(engine.model.fused_qkv),
                    "row_scale_norm": bool(engine.model.row_scale_norm),
-                   "fused_head": bool(engine.model.fused_head)},
+                   "fused_head": bool(engine.model.fused_head),
+                   "fused_resid": bool(engine.model.fused_resid)},
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),
         "p99_enqueue_to_dispatch_ms": round(lat["p99_enq_ms"], 3),

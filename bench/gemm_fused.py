@@ -172,6 +172,8 @@ def main():
                 x = torch.randn(T, K, device=dev).to(torch.bfloat16)
                 y = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
                 fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "hip": lambda: G.gemm(x, w, out=y),
+                       "hipblaslt_resid": lambda: y.addmm_(x, w.t()),
+                       "hip_resid": lambda: G.gemm_residual(x, w, y),
                        "hip_r1sched": lambda: G._launch(x, w, y, G.EPI_STORE + 16),
                        "hip_nostagger": lambda: G._launch(x, w, y, G.EPI_STORE + 32)}
                 for f in fns.values():

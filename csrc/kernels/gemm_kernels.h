@@ -5,6 +5,9 @@
 //
 //   GM_EPI_STORE   C[M][N] = A·Wᵀ                         (bf16)
 //   GM_EPI_SWIGLU  H[M][N/2] = silu(A·Wgᵀ) * (A·Wuᵀ)       (Llama gate/up)
+//   GM_EPI_RESID   C[M][N] += A·Wᵀ   (bf16 C read + written; one rounding of
+//                  the fp32 sum, as hipBLASLt's beta = 1: the o / down
+//                  projections into the residual stream)
 //
 // The SwiGLU form removes the separate silu_mul pass and the HBM round trip
 // of the [M][2F] gate/up product (profiles/r1_gemm_experiments.md): W rows are
@@ -54,7 +57,7 @@ constexpr int GM_BUF_BYTES = 4 * GM_HALF_BYTES;    // A0 A1 B0 B1
 constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
 constexpr int GM_GROUP_M = 8;                    // default M-tiles per block-order group
 
-enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4 };
+enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4, GM_EPI_RESID = 5 };
 
 // GM_EPI_ARGMAX: the LM head's greedy sampling as the epilogue -- no [M][N]
 // logits tensor.  Each tile writes, per row, the max over its 256 columns and
@@ -543,6 +546,61 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         am.pi[(int64_t)grow * tiles_n + tn] = tn * GM_BN + c;
       }
     }
+  } else if (EPI == GM_EPI_RESID) {
+    // fp32 through LDS in four passes of 32 rows (8.5 KiB per wave, row
+    // stride 68 floats: the four fq row groups of a write land on distinct
+    // banks), then coalesced: 16 B of fp32 + 8 B of the bf16 residual per
+    // lane, one rounding of the sum
+    float* o = reinterpret_cast<float*>(smem + w * (32 * 68 * 4));
+    const int col0 = tn * GM_BN + wc * 64;
+    // every residual chunk of this lane loaded up front (64 VGPRs): after the
+    // first store the compiler cannot move a load of C above a store to C, so
+    // loads interleaved with the passes would wait out one round trip each
+    uint2 cres[2][2][8];
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int mp = 0; mp < 2; ++mp)
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int qd = it * 64 + lane;
+          const int grow = row0 + mh * 64 + mp * 32 + (qd >> 4);
+          cres[mh][mp][it] = grow < M ? *reinterpret_cast<const uint2*>(C + (int64_t)grow * N + col0 + (qd & 15) * 4)
+                                      : make_uint2(0u, 0u);
+        }
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int mp = 0; mp < 2; ++mp) {
+#pragma unroll
+        for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                o[(mm * 16 + fq * 4 + j) * 68 + nh * 32 + n * 16 + fr] = acc[mh][mp * 2 + mm][nh][n][j];
+        GM_LGKM(0);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int qd = it * 64 + lane;           // row qd/16, 4-float chunk qd%16
+          const int r = qd >> 4, c4 = qd & 15;
+          const int grow = row0 + mh * 64 + mp * 32 + r;
+          const gm_f32x4 v = *reinterpret_cast<const gm_f32x4*>(o + r * 68 + c4 * 4);
+          if (grow < M) {
+            uint2* cp = reinterpret_cast<uint2*>(C + (int64_t)grow * N + col0 + c4 * 4);
+            const uint2 cr = cres[mh][mp][it];
+            const float r0 = __uint_as_float(cr.x << 16) + v[0], r1 = __uint_as_float(cr.x & 0xffff0000u) + v[1];
+            const float r2 = __uint_as_float(cr.y << 16) + v[2], r3 = __uint_as_float(cr.y & 0xffff0000u) + v[3];
+            *cp = make_uint2((uint32_t)gm_f2bf(r0) | ((uint32_t)gm_f2bf(r1) << 16),
+                             (uint32_t)gm_f2bf(r2) | ((uint32_t)gm_f2bf(r3) << 16));
+          }
+        }
+        GM_LGKM(0);
+        __builtin_amdgcn_wave_barrier();
+      }
   } else if (EPI == GM_EPI_SWIGLU) {
     // wave w: 128 rows x 32 features bf16 = 8 KiB at w * 8 KiB
     uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 8192);

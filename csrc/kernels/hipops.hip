@@ -205,7 +205,7 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
                      M, N, K, group_m, rs, rp, sp, am);
 }
 
-// epi: 0 / 2 = store / SwiGLU; 16 / 32 = store with the round-1 phase
+// epi: 0 / 2 / 5 = store / SwiGLU / residual add (C += A·Wᵀ); 16 / 32 = store with the round-1 phase
 // schedule / without the wave-row stagger; 50 / 66 / 82 = SwiGLU with
 // s_setprio around every MFMA cluster / the static priority on wave row 0 /
 // no priority (A/B only; the default is a static priority on wave row 1).
@@ -224,6 +224,8 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
   else if (epi == GM_EPI_SWIGLU)
     launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m,
                                rsp);
+  else if (epi == GM_EPI_RESID)                    // C += A·Wᵀ in place (no row scales)
+    launch_gemm<GM_EPI_RESID>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_STORE + 16)
     launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_STORE + 32)

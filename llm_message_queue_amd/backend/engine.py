@@ -84,7 +84,7 @@ class BackendEngine:
                  token_budget: int = 2048, device="cuda", impl: str = "hip", seed: int = 0,
                  page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True,
                  split_qkv: bool = False, fused_mlp=None, fused_qkv=None, row_scale_norm: bool = True,
-                 fused_head=None):
+                 fused_head=None, fused_resid=None):
         self.cfg = model_cfg
         self.slots = slots
         self.max_ctx = max_ctx
@@ -95,7 +95,8 @@ class BackendEngine:
         self.cuda = self.device.type == "cuda"
         self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
-                               fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head)
+                               fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
+                               fused_resid=fused_resid)
         self.impl = impl
         self.active: Dict[int, Request] = {}            # slot -> request
         self.free: List[int] = list(range(slots - 1, -1, -1))

@@ -71,7 +71,7 @@ class LlamaStub:
                  seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False,
                  fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512,
                  fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048, row_scale_norm: bool = True,
-                 fused_head: Optional[bool] = None):
+                 fused_head: Optional[bool] = None, fused_resid: Optional[bool] = None):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -107,6 +107,16 @@ class LlamaStub:
         # LM head + greedy argmax in one hand-written GEMM (argmax epilogue, no
         # [rows][vocab] logits) when the step samples >= 256 rows
         self.fused_head = (impl == "hip") if fused_head is None else bool(fused_head)
+        # o / down projections into the residual on the hand-written kernel
+        # (GM_EPI_RESID) when its 256x256 tiles fill whole waves of the chip
+        # (the saturated serving step: T ~ 4,040 -> 256 tiles); hipBLASLt's
+        # beta = 1 stream-K kernel otherwise (ops.gemm.residual_tiles_ok).
+        # Off by default: at parity with hipBLASLt (down 0.306 vs 0.305 ms,
+        # o 0.0997 vs 0.0980 ms at T = 4041, profiles/r2_gemm_resid_ab.jsonl)
+        # -- with one wave of tiles every block reads and writes its residual
+        # tile at the same moment, so the 66 MB round trip is exposed in both.
+        self.fused_resid = False if fused_resid is None else bool(fused_resid)
+        self._cus = G._cu_count(self.device) if (self.fused_resid and self.device.type == "cuda") else 0
         # fused paths take the raw residual rows + a per-row RMSNorm scale
         # (True) or an rmsnorm'd copy of the rows (False, A/B)
         self.row_scale_norm = bool(row_scale_norm)
@@ -198,6 +208,14 @@ class LlamaStub:
         T = res.shape[0]
         rows_qkv = self.fused_qkv and T >= self.min_fused_qkv_tokens
         rows_mlp = self.fused_mlp and T >= self.min_fused_tokens
+        resid_o = self._cus > 0 and G.residual_tiles_ok(T, cfg.dim, self._cus)
+
+        def into_res(a, wt):                             # res += a · wtᵀ
+            if resid_o:
+                G.gemm_residual(a, wt, res)
+            else:
+                res.addmm_(a, wt.t())
+
         for i, L in enumerate(self.layers):
             if rows_qkv and self.row_scale_norm:
                 q = ops.qkv_rope_rows(res, L["wqkv"], ops.row_rms(res, cfg.eps), pos, slot, self.cos, self.sin,
@@ -207,7 +225,7 @@ class LlamaStub:
                                self.sin, cfg.heads, cfg.kv_heads, self.kcache[i], self.vcache[i])
             else:
                 q = self._qkv(ops.rmsnorm(res, L["attn_norm"], cfg.eps), L, i, pos, slot)
-            res.addmm_(self._attend(q, i, pos, slot, tiles, n_dec), L["wo"].t())
+            into_res(self._attend(q, i, pos, slot, tiles, n_dec), L["wo"])
             if rows_mlp and self.row_scale_norm:
                 act = ops.swiglu_rows(res, L["w_gu"], ops.row_rms(res, cfg.eps))
             elif rows_mlp:
@@ -215,7 +233,7 @@ class LlamaStub:
             else:
                 act = ops.mlp_up(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"], self.fused_mlp,
                                  self.min_fused_tokens)
-            res.addmm_(act, L["w_down"].t())
+            into_res(act, L["w_down"])
         return ops.rmsnorm(res, self.final_norm, cfg.eps)
 
     def _qkv(self, x, L, i, pos, slot):

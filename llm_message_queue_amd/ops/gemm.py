@@ -23,6 +23,7 @@ from .. import _native
 
 EPI_STORE = 0
 EPI_SWIGLU = 2
+EPI_RESID = 5
 TILE_N = 256
 SWIGLU_HALF = 32   # per-wave gate/up split (a wave owns 64 output columns)
 
@@ -130,6 +131,30 @@ def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None,
     if y.shape != (x.shape[0], F):
         raise ValueError("gemm_swiglu: out shape mismatch")
     return _launch(x, w_perm, y, EPI_SWIGLU, row_scale=row_scale)
+
+
+def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+    """``res += x · wᵀ`` in place (bf16 ``res`` [M][N]; the fp32 sum is
+    rounded once, as hipBLASLt's beta = 1 epilogue) -- the o / down
+    projections accumulating into the residual stream."""
+    _check(x, "x")
+    _check(w, "w")
+    _check(res, "res")
+    if res.shape != (x.shape[0], w.shape[0]):
+        raise ValueError("gemm_residual: res shape mismatch")
+    return _launch(x, w, res, EPI_RESID)
+
+
+def residual_tiles_ok(M: int, N: int, cus: int, min_fill: float = 0.97) -> bool:
+    """Whether the 256x256-tile kernel fills the chip for ``res += x·wᵀ``:
+    the last wave of tiles at least ``min_fill`` busy.  On a partial wave
+    (e.g. 128 tiles on 256 CUs) hipBLASLt's stream-K kernel splits K across
+    the idle CUs and stays ahead (profiles/r2_gemm_resid_ab.jsonl)."""
+    if not supported(M, N, 128) or N % TILE_N:
+        return False
+    tiles = -(-M // TILE_M) * (N // TILE_N)
+    waves = -(-tiles // cus)
+    return tiles / (waves * cus) >= min_fill
 
 
 TILE_M = 256

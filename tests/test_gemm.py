@@ -232,6 +232,68 @@ def test_serving_shapes_match_fp32():
     assert (vc1.float() - vc2.float()).abs().max().item() <= tol
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K", [(1, 512), (37, 4096), (300, 1024), (4041, 4096), (4041, 14336)])
+def test_gemm_residual_matches_fp32(T, K):
+    """res += x·wᵀ in place (GM_EPI_RESID, the o / down projections): against
+    the fp32 sum rounded once; rows past M of a larger buffer untouched."""
+    N = 4096 if T == 4041 else 1024
+    x, w = _rand(T, K, N, seed=300 + T)
+    g = torch.Generator(device=DEV).manual_seed(T)
+    big = torch.full((T + 19, N), 3.0, dtype=torch.bfloat16, device=DEV)
+    big[:T] = torch.randn(T, N, generator=g, device=DEV).to(torch.bfloat16)
+    res0 = big[:T].float().clone()
+    ref = res0 + x.float() @ w.float().t()
+    G.gemm_residual(x, w, big[:T])
+    err = (big[:T].float() - ref).abs().max().item()
+    assert err <= 0.01 * ref.abs().max().item() + 1e-3, err
+    assert (big[T:] == 3.0).all()
+    if T == 4041 and K == 4096:                      # same single rounding as hipBLASLt's beta = 1
+        r2 = res0.to(torch.bfloat16)
+        r2.addmm_(x, w.t())
+        d = (big[:T].float() - r2.float()).abs()
+        assert d.max().item() <= 0.01 * ref.abs().max().item() + 1e-3
+        assert (d == 0).float().mean().item() > 0.9, "residual epilogue should round like beta = 1"
+
+
+@pytest.mark.gpu
+def test_8b_model_residual_gemm_matches_hipblaslt_path():
+    """At a full-chip step (T = 4041 -> 256 tiles of o / down) the model's
+    o / down projections run on GM_EPI_RESID; hidden states equal the
+    hipBLASLt beta = 1 path to bf16 noise (2 layers, 8B dims)."""
+    cfg = LlamaConfig(layers=2)
+    a = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=5, fused_resid=True)
+    b = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=5)
+    T = 4041
+    assert a.fused_resid and a._cus > 0 and not b.fused_resid
+    if not G.residual_tiles_ok(T, cfg.dim, a._cus):
+        pytest.skip(f"{a._cus} CUs: T = {T} is not a whole wave of tiles here")
+    called = []
+    orig = G.gemm_residual
+    G.gemm_residual = lambda *x: (called.append(1), orig(*x))[1]
+    try:
+        tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
+        pos = (torch.arange(T, device=DEV, dtype=torch.int32) % 64)
+        slot = (torch.arange(T, device=DEV, dtype=torch.int32) // 64)
+        ha = a.hidden(tok, pos, slot).float()
+        hb = b.hidden(tok, pos, slot).float()
+    finally:
+        G.gemm_residual = orig
+    assert len(called) == 2 * cfg.layers
+    rel = ((ha - hb).norm() / hb.norm()).item()
+    assert rel < 1e-2, rel
+
+
+def test_residual_tiles_ok_wants_whole_waves():
+    assert G.residual_tiles_ok(4041, 4096, 256)                 # 16 x 16 = 256 tiles: one full wave
+    assert G.residual_tiles_ok(3841, 4096, 256)                 # 16 x 16 tiles (the last M-tile holds 1 row)
+    assert not G.residual_tiles_ok(3840, 4096, 256)             # 15 x 16 = 240 tiles: 94 % of the chip
+    assert not G.residual_tiles_ok(2048, 4096, 256)             # 128 tiles: half the chip
+    assert G.residual_tiles_ok(8192, 4096, 256)                 # two full waves
+    assert not G.residual_tiles_ok(4041, 4000, 256)             # N not a multiple of 256
+    assert not G.residual_tiles_ok(0, 4096, 256)
+
+
 def test_split_plan_only_splits_a_half_empty_last_wave():
     assert G.split_plan(4041, 6144, 4096, 256) == 256          # 384 tiles: 256 whole + 128 split
     assert G.split_plan(2600, 6144, 4096, 256) == 256          # 264 tiles: 8 split
