@@ -541,30 +541,47 @@ __device__ __forceinline__ void attention_dec_block(int bid, float (*__restrict_
   const int kh = lane >> 5, dp = lane & 31;            // P.V layout: key parity x 4-dim slices
   for (int k0 = 0; k0 < ctx; k0 += 64) {
     const int nk = min(64, ctx - k0);
-    // ---- scores of keys k0 .. k0+nk-1 (pre-scaled by scale*log2e) -> ps
-    for (int kb = 0; kb < nk; kb += 8) {
-      const int key = kb + ksub;
-      float d[4] = {0.f, 0.f, 0.f, 0.f};
-      if (key < nk) {
-        const uint4* kr = reinterpret_cast<const uint4*>(kc + kvbase + (int64_t)(k0 + key) * 128 + part * 16);
-        const uint4 a = kr[0], b = kr[1];
-        const uint32_t kw[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    // ---- scores of keys k0 .. k0+nk-1 (pre-scaled by scale*log2e) -> ps.
+    // The K rows of 32 keys (4 passes) are loaded before any is used: one
+    // memory round trip per 32 keys instead of one per 8
+    for (int kb0 = 0; kb0 < nk; kb0 += 32) {
+      uint4 ka[4], kb[4];
 #pragma unroll
-        for (int h = 0; h < 4; ++h)
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            d[h] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qv[h][i]),
-                                                   __builtin_bit_cast(bf16x2_t, kw[i]), d[h], false);
+      for (int u = 0; u < 4; ++u) {
+        const int key = kb0 + u * 8 + ksub;
+        if (key < nk) {
+          const uint4* kr = reinterpret_cast<const uint4*>(kc + kvbase + (int64_t)(k0 + key) * 128 + part * 16);
+          ka[u] = kr[0];
+          kb[u] = kr[1];
+        } else {
+          ka[u] = make_uint4(0u, 0u, 0u, 0u);
+          kb[u] = ka[u];
+        }
       }
 #pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        d[h] += __shfl_xor(d[h], 1, 64);
-        d[h] += __shfl_xor(d[h], 2, 64);
-        d[h] += __shfl_xor(d[h], 4, 64);
-      }
-      if (part == 0 && key < nk) {
+      for (int u = 0; u < 4; ++u) {
+        if (kb0 + u * 8 >= nk) break;                // wave-uniform
+        const int key = kb0 + u * 8 + ksub;
+        float d[4] = {0.f, 0.f, 0.f, 0.f};
+        if (key < nk) {
+          const uint32_t kw[8] = {ka[u].x, ka[u].y, ka[u].z, ka[u].w, kb[u].x, kb[u].y, kb[u].z, kb[u].w};
 #pragma unroll
-        for (int h = 0; h < 4; ++h) ps[wv][h][key] = d[h] * scale_log2;
+          for (int h = 0; h < 4; ++h)
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              d[h] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, qv[h][i]),
+                                                     __builtin_bit_cast(bf16x2_t, kw[i]), d[h], false);
+        }
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          d[h] += __shfl_xor(d[h], 1, 64);
+          d[h] += __shfl_xor(d[h], 2, 64);
+          d[h] += __shfl_xor(d[h], 4, 64);
+        }
+        if (part == 0 && key < nk) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h) ps[wv][h][key] = d[h] * scale_log2;
+        }
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -585,20 +602,31 @@ __device__ __forceinline__ void attention_dec_block(int bid, float (*__restrict_
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
-    // ---- O += P V (half-wave kh takes keys of parity kh)
+    // ---- O += P V (half-wave kh takes keys of parity kh); the V rows of 16
+    // keys are loaded before the first is used (same key order per lane)
     const uint16_t* vr = vc + kvbase + (int64_t)k0 * 128 + dp * 4;
-#pragma unroll 4
-    for (int j = kh; j < nk; j += 2) {
-      const uint2 v2 = *reinterpret_cast<const uint2*>(vr + (int64_t)j * 128);
-      const float v0 = bf((uint16_t)(v2.x & 0xFFFFu)), v1 = bf((uint16_t)(v2.x >> 16));
-      const float v2f = bf((uint16_t)(v2.y & 0xFFFFu)), v3 = bf((uint16_t)(v2.y >> 16));
+    for (int j0 = 0; j0 < nk; j0 += 16) {
+      uint2 vv[8];
 #pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        const float p = ps[wv][h][j];
-        acc[h][0] += p * v0;
-        acc[h][1] += p * v1;
-        acc[h][2] += p * v2f;
-        acc[h][3] += p * v3;
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + kh + 2 * u;
+        vv[u] = j < nk ? *reinterpret_cast<const uint2*>(vr + (int64_t)j * 128) : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + kh + 2 * u;
+        if (j >= nk) break;
+        const uint2 v2 = vv[u];
+        const float v0 = bf((uint16_t)(v2.x & 0xFFFFu)), v1 = bf((uint16_t)(v2.x >> 16));
+        const float v2f = bf((uint16_t)(v2.y & 0xFFFFu)), v3 = bf((uint16_t)(v2.y >> 16));
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const float p = ps[wv][h][j];
+          acc[h][0] += p * v0;
+          acc[h][1] += p * v1;
+          acc[h][2] += p * v2f;
+          acc[h][3] += p * v3;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();          // ps is rewritten by the next block
