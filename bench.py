@@ -100,8 +100,114 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def comm_evidence(comm, dev, world: int, dry: bool) -> dict:
+    """Proof of what the job ran on, gathered from every rank: data-plane
+    backend, per-rank HIP device index and PCI address (distinct unless the
+    ranks were wrapped onto fewer GPUs), and one timed all_reduce on the data
+    plane (64 MiB on RCCL; 8 MiB on the CPU rehearsal's gloo)."""
+    import torch
+    from llm_message_queue_amd.parallel.comm import gpus_oversubscribed
+    ev = {"world": world, "control_plane": "solo" if world == 1 else str(getattr(comm, "backend", "?")),
+          "data_backend": "none", "oversubscribed": False}
+    if dev.type == "cuda":
+        p = torch.cuda.get_device_properties(dev)
+        mine = [int(dev.index), int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)]
+    else:
+        mine = [-1, -1, -1, -1]
+    rows = comm.all_gather_i64(np.array(mine, dtype=np.int64))
+    ev["devices"] = [{"rank": r, "hip_device": int(x[0]),
+                      "pci": "%04x:%02x:%02x" % (x[1], x[2], x[3]) if x[0] >= 0 else "cpu"}
+                     for r, x in enumerate(rows.tolist())]
+    if dev.type == "cuda":
+        ev["device_name"] = torch.cuda.get_device_name(dev)
+        ev["distinct_devices"] = len({tuple(x[1:]) for x in rows.tolist()})
+    if world == 1:
+        return ev
+    import torch.distributed as dist
+    ev["data_backend"] = dist.get_backend()
+    ev["oversubscribed"] = bool(gpus_oversubscribed()) if not dry else False
+    if dev.type == "cuda":
+        ev["one_gpu_per_rank"] = ev["distinct_devices"] == world
+        if not ev["oversubscribed"] and not ev["one_gpu_per_rank"]:
+            print(f"bench: WARNING ranks share GPUs without oversubscription: {ev['devices']}", file=sys.stderr)
+    nbytes = (64 << 20) if ev["data_backend"] == "nccl" else (8 << 20)
+    tdev = dev if ev["data_backend"] == "nccl" else torch.device("cpu")
+    x = torch.ones(nbytes // 4, dtype=torch.float32, device=tdev)
+    for _ in range(2):
+        dist.all_reduce(x)
+    iters = 5
+    if tdev.type == "cuda":
+        torch.cuda.synchronize(tdev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(x)
+    if tdev.type == "cuda":
+        torch.cuda.synchronize(tdev)
+    dt = comm.max_f64((time.perf_counter() - t0) / iters)
+    alg = nbytes / dt / 1e9
+    ev["allreduce"] = {"bytes": nbytes, "backend": ev["data_backend"], "ms": round(dt * 1e3, 3),
+                       "algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * 2 * (world - 1) / world, 2)}
+    del x
+    return ev
+
+
+def lockstep_report(gw, engine, comm, elapsed: float) -> dict:
+    """Where a multi-rank tick's time goes, per rank: control-plane wait
+    (collectives: the exchange plus waiting for the slowest peer) and GPU
+    execution time of the forward steps (timing events)."""
+    ls = gw.lockstep_stats(reset=True)
+    gms = engine.gpu_step_ms
+    nst = max(1, engine.gpu_steps)
+    mine = np.array([int(ls["p50_ms"] * 1e4), int(ls["max_ms"] * 1e4), int(ls["mean_ms"] * 1e4),
+                     int(gms / nst * 1e4), int(engine.gpu_step_max_ms * 1e4), int(gms * 1e4), engine.gpu_steps],
+                    dtype=np.int64)
+    g = comm.all_gather_i64(mine).astype(np.float64)
+    step_mean = g[:, 3] / 1e4
+    busy = g[:, 5] / 1e4 / max(1e-9, elapsed * 1e3)
+    return {"collective_wait_ms_p50_by_rank": [round(v, 3) for v in (g[:, 0] / 1e4).tolist()],
+            "collective_wait_ms_max_by_rank": [round(v, 3) for v in (g[:, 1] / 1e4).tolist()],
+            "collective_wait_ms_mean_by_rank": [round(v, 3) for v in (g[:, 2] / 1e4).tolist()],
+            "gpu_step_ms_mean_by_rank": [round(v, 3) for v in step_mean.tolist()],
+            "gpu_step_ms_max_by_rank": [round(v, 3) for v in (g[:, 4] / 1e4).tolist()],
+            "gpu_busy_frac_by_rank": [round(v, 4) for v in busy.tolist()],
+            "gpu_steps_by_rank": [int(v) for v in g[:, 6].tolist()],
+            "slowest_over_mean_gpu_step": round(float(step_mean.max() / max(1e-9, step_mean.mean())), 4)}
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def self_launch(a, argv) -> int:
+    """``bench.py --gpus N`` (N > 1) started without a launcher: run the
+    same command under ``torch.distributed.run`` (one rank per GPU, N ranks)
+    as a CHILD process and return its exit code.  Nothing here touches the
+    GPU (no HIP call before the child starts; never exec).  Rank 0's JSON
+    line reaches our stdout because the child inherits it."""
+    import subprocess
+    args = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + args
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"bench: --gpus {a.gpus} without a launcher; starting {a.gpus} ranks under torch.distributed.run",
+          file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None) -> int:
     a = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return self_launch(a, argv)
+    if env_world is not None and int(env_world) != a.gpus:
+        print(f"bench: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} ranks; refusing to "
+              "report a number for a different GPU count", file=sys.stderr, flush=True)
+        return 3
     import torch
 
     from llm_message_queue_amd.backend.engine import BackendEngine
@@ -117,8 +223,6 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        print(f"warning: --gpus {a.gpus} != WORLD_SIZE {world}", file=sys.stderr)
     dry = a.cpu_dry_run
     if dry:
         # CPU rehearsal of the exact control flow (collectives, tick counts,
@@ -135,6 +239,7 @@ def main(argv=None) -> int:
         dev = torch.device("cuda", local)
         comm = init_from_env(control=a.control_plane)
     comm_kind = "solo" if world == 1 else str(getattr(comm, "backend", a.control_plane))
+    evidence = comm_evidence(comm, dev, world, dry)
 
     def dsync():
         if not dry:
@@ -310,7 +415,11 @@ def main(argv=None) -> int:
     # synchronise itself finds an idle GPU
     gw.quiesce(pump)
     d0 = gw.counters["dispatched"]
+    r0 = gw.counters["remote_sent"]
     tok0 = engine.total_tokens
+    gw.lockstep_stats(reset=True)
+    engine.gpu_step_ms, engine.gpu_steps, engine.gpu_step_max_ms = 0.0, 0, 0.0
+    engine.time_steps = True
     sync_all()
     sub0 = gw.counters["submitted"]
     t0 = time.perf_counter()
@@ -321,7 +430,9 @@ def main(argv=None) -> int:
     gw.quiesce(pump)
     sync_all()
     t1 = time.perf_counter()
+    engine.time_steps = False
     arrived_local = gw.counters["submitted"] - sub0
+    remote_local = gw.counters["remote_sent"] - r0
     gc.enable()
     if tracer is not None:
         gw.tracer = engine.tracer = None
@@ -346,6 +457,8 @@ def main(argv=None) -> int:
     agg = comm.all_gather_i64(np.array([int(elapsed_local * 1e9), dispatched_local, tokens_local, arrived_local],
                                        dtype=np.int64))
     elapsed = agg[:, 0].max() / 1e9
+    lockstep = lockstep_report(gw, engine, comm, elapsed)
+    remote_in_window = int(comm.all_gather_i64(np.array([remote_local], dtype=np.int64)).sum())
     dispatched = int(agg[:, 1].sum())
     tokens = int(agg[:, 2].sum())
     arrived = int(agg[:, 3].sum())
@@ -408,6 +521,9 @@ def main(argv=None) -> int:
         "dispatch_rate_in_window": round(dispatched / elapsed, 2) if elapsed > 0 else 0.0,
         "arrival_rate_in_window": round(arrived / elapsed, 2) if elapsed > 0 else 0.0,
         "remote_dispatched": int(comm.all_gather_i64(np.array([gw.counters["remote_sent"]], dtype=np.int64)).sum()),
+        "remote_dispatched_in_window": remote_in_window,
+        "comm": evidence,
+        "lockstep": lockstep,
         "steady_ticks": steady,
         "requests_accounted": {"offered": int(acct[0]), "completed": int(acct[1]), "rejected": int(acct[2]),
                                "shed": int(acct[3]), "lost": int(acct[0] - acct[1] - acct[2] - acct[3])},

@@ -77,6 +77,7 @@ class _Inflight:
     t0: float
     out: object                   # device tensor of sampled tokens (kept alive for the next gather)
     t0_ns: int = 0                # monotonic launch time (tracing)
+    ev_start: object = None       # timing event before the forward (``time_steps``)
 
 
 class BackendEngine:
@@ -155,6 +156,14 @@ class BackendEngine:
         # {"drop_heartbeat": True} stops the load-page census
         self.fault: Dict[str, float] = {}
         self.tracer = None          # utils.tracing.RequestTracer (backend step spans)
+        # GPU execution time of every forward step (timing events around it;
+        # the start event's timestamp is when the GPU reached the step, so the
+        # difference is device time, not queueing): bench.py's lock-step
+        # attribution (slowest vs mean GPU of a multi-rank job)
+        self.time_steps = False
+        self.gpu_step_ms = 0.0
+        self.gpu_steps = 0
+        self.gpu_step_max_ms = 0.0
         if self.cuda and page is not None and page.dev_ptr is None:
             page.register_device()
         if page is not None:
@@ -502,11 +511,15 @@ class BackendEngine:
             src = d[o_dec + D:o_til].long()
             tok_d.index_copy_(0, rows, self._prev_out.index_select(0, src).long())
         til = d[o_til:].view(NT, 4) if self.use_tiles else None
+        ev0 = None
+        if self.cuda and self.time_steps:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til, n_dec=D)
         self._census(T)
         ev = None
         if self.cuda:
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=ev0 is not None)
             ev.record()
         # deterministic bookkeeping: every sampled slot gets one token
         ss = samp_slots
@@ -535,7 +548,7 @@ class BackendEngine:
                 self.free.append(x)
         self.s_active[done] = False
         self._prev_out = out
-        self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out, t_mono))
+        self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out, t_mono, ev0))
         self.step_id += 1
         self.total_tokens += T
         self.completed_total += len(completed)
@@ -552,6 +565,11 @@ class BackendEngine:
                 return None
         self._q.popleft()
         now = time.monotonic_ns()
+        if f.ev_start is not None:
+            ms = f.ev_start.elapsed_time(f.event)
+            self.gpu_step_ms += ms
+            self.gpu_steps += 1
+            self.gpu_step_max_ms = max(self.gpu_step_max_ms, ms)
         if self.tracer is not None:
             self.tracer.step(f.step, f.t0_ns, now, f.T)
         for r in f.firsts:

@@ -22,6 +22,7 @@ MI355X design:
 """
 from __future__ import annotations
 
+import collections
 import threading
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -242,6 +243,10 @@ class Gateway:
         self.ingest_ns = np.zeros(3, dtype=np.int64)  # [preprocess ns, queue push ns, messages]
         self._ticks0 = 0
         self._next_req = 1 << 40
+        # lock-step attribution: host time each multi-rank tick spends inside
+        # its control-plane collectives (load all_gather + descriptor
+        # all_to_all) -- the wait for the slowest rank plus the exchange
+        self.coll_wait_ns: "collections.deque[int]" = collections.deque(maxlen=1 << 16)
 
     # ------------------------------------------------------------------ ingress
     def submit(self, msgs: Sequence[Message]) -> None:
@@ -643,7 +648,10 @@ class Gateway:
 
     def _dispatch_global(self) -> int:
         W, me = self.world, self.rank
-        loads = self.comm.all_gather_i64(self._my_load())
+        my_load = self._my_load()
+        tc0 = time.perf_counter_ns()
+        loads = self.comm.all_gather_i64(my_load)
+        t_wait = time.perf_counter_ns() - tc0
         orders_prev, self._mig_out = self._mig_out, []   # decided last tick: sent / executed now
         held_prev, self._await_kv = self._await_kv, {}   # turns flagged last tick
         self._observe_loads(loads)
@@ -717,7 +725,9 @@ class Gateway:
         recv_counts = [int(quota[i, me].sum()) + int(loads[i, planner.L_DONE + me])
                        + int(loads[i, planner.L_MIGC + me]) if i != me else 0 for i in range(W)]
         send[me] = np.zeros((0, width), dtype=np.int32)
+        tc0 = time.perf_counter_ns()
         got = self.comm.all_to_all_rows(send, recv_counts, width)
+        self.coll_wait_ns.append(t_wait + time.perf_counter_ns() - tc0)
         # orders where I am the home GPU: K_MIGRATE rows from the routers, plus
         # my own router's orders for my own KV
         src_orders = [(c, me, d) for c, h, d in orders_prev if h == me]
@@ -1203,6 +1213,19 @@ class Gateway:
             self.host_ns[:] = 0
             self.ingest_ns[:] = 0
             self._ticks0 = self.counters["ticks"]
+        return out
+
+    def lockstep_stats(self, reset: bool = False) -> Dict[str, float]:
+        """Per-tick control-plane collective time of this rank (ms): the
+        wait for the slowest peer plus the exchange itself."""
+        w = np.asarray(self.coll_wait_ns, dtype=np.float64) / 1e6
+        out = {"ticks": int(w.size),
+               "p50_ms": round(float(np.percentile(w, 50)), 4) if w.size else 0.0,
+               "p99_ms": round(float(np.percentile(w, 99)), 4) if w.size else 0.0,
+               "max_ms": round(float(w.max()), 4) if w.size else 0.0,
+               "mean_ms": round(float(w.mean()), 4) if w.size else 0.0}
+        if reset:
+            self.coll_wait_ns.clear()
         return out
 
     def request_stop(self) -> None:
