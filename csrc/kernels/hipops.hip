@@ -16,6 +16,7 @@
 
 #include "classify_kernels.h"
 #include "gemm_kernels.h"
+#include "kv_migrate_kernels.h"
 #include "llama_kernels.h"
 #include "summarise_kernels.h"
 #include "text_kernels.h"
@@ -409,6 +410,25 @@ static void slot_census(uintptr_t slot_state, int S_, int tokens, uint32_t step,
   check_launch();
 }
 
+// ---------------------------------------------------------------------- KV migration
+// pack=true: cache rows -> buf; false: buf -> cache rows (see kv_migrate_kernels.h)
+static void kv_move(uintptr_t table, int layers, int slots, int slot, int n, int max_ctx, int hkv, int head_dim,
+                    uintptr_t buf, bool pack, uintptr_t stream) {
+  require(head_dim == 128, "kv_move: head_dim must be 128");
+  require(layers > 0 && hkv > 0 && slots > 0, "kv_move: bad cache shape");
+  require(slot >= 0 && slot < slots, "kv_move: slot out of range");
+  require(n > 0 && n <= max_ctx, "kv_move: token count out of range");
+  require(table != 0 && buf != 0 && buf % 16 == 0, "kv_move: null or misaligned buffer");
+  const dim3 grid(layers * 2 * hkv);
+  if (pack)
+    hipLaunchKernelGGL(kv_move_kernel<true>, grid, dim3(256), 0, S(stream), P<const uint64_t>(table), layers, slot,
+                       n, max_ctx, hkv, P<uint4>(buf));
+  else
+    hipLaunchKernelGGL(kv_move_kernel<false>, grid, dim3(256), 0, S(stream), P<const uint64_t>(table), layers,
+                       slot, n, max_ctx, hkv, P<uint4>(buf));
+  check_launch();
+}
+
 static py::dict device_info(int dev) {
   hipDeviceProp_t p;
   HIP_CHECK(hipGetDeviceProperties(&p, dev));
@@ -476,4 +496,6 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("unregister_host_page", &unregister_host_page);
   m.def("slot_census", &slot_census);
   m.def("device_info", &device_info);
+  m.def("kv_move", &kv_move, py::arg("table"), py::arg("layers"), py::arg("slots"), py::arg("slot"), py::arg("n"),
+        py::arg("max_ctx"), py::arg("hkv"), py::arg("head_dim"), py::arg("buf"), py::arg("pack"), py::arg("stream"));
 }

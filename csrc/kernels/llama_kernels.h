@@ -1,7 +1,9 @@
 // Decode-path kernels of the Llama-3-8B-shaped backend stub (N12): fused
 // residual-add + RMSNorm, SiLU*up, RoPE + paged KV write, and a unified
-// prefill/decode GQA attention over the slot KV cache.  The GEMMs stay on
-// hipBLASLt through torch.matmul.
+// prefill/decode GQA attention over the slot KV cache.  The big GEMMs with
+// fused epilogues (qkv + RoPE/KV write, gate/up + SwiGLU, LM head + argmax)
+// are the hand-written MFMA kernels of gemm_kernels.h; the o / down
+// projections stay on hipBLASLt's beta = 1 residual GEMM.
 //
 // Unified attention: every token of a step (prefill chunk tokens and decode
 // tokens alike) carries (slot, pos); its K/V are written to the slot's cache

@@ -113,20 +113,28 @@ class ShmCollective {
   void unlink() { shm_unlink(name_.c_str()); }
   uint64_t ops() const { return seq_; }
   uint64_t buf_bytes() const { return buf_bytes_; }
+  static constexpr uint64_t kOverflow = ~uint64_t(0);
 
   // Every rank contributes `n` bytes; afterwards payload(r) is rank r's.
+  // An oversized payload is published as an overflow marker instead of
+  // throwing before the publish: every rank then fails the SAME op at once
+  // (std::length_error) instead of the others spinning to their timeout.
   void exchange(const void* data, uint64_t n, double timeout_s) {
-    if (n > buf_bytes_) throw std::length_error("ShmCollective: payload exceeds the per-rank buffer");
+    const bool over = n > buf_bytes_;
     const uint64_t k = seq_ + 1;
     const auto deadline = clock::now() + std::chrono::duration_cast<clock::duration>(
                                              std::chrono::duration<double>(timeout_s));
     wait_all(k - 1, deadline);
     const int par = (int)(k & 1);
-    if (n) std::memcpy(buf(rank_, par), data, n);
-    slots_[rank_].nbytes[par] = n;
+    if (n && !over) std::memcpy(buf(rank_, par), data, n);
+    slots_[rank_].nbytes[par] = over ? kOverflow : n;
     slots_[rank_].pub.store(k, std::memory_order_release);
     seq_ = k;
     wait_all(k, deadline);
+    for (int r = 0; r < world_; ++r)
+      if (slots_[r].nbytes[par] == kOverflow)
+        throw std::length_error("ShmCollective: rank " + std::to_string(r) +
+                                "'s payload exceeds the per-rank buffer of " + std::to_string(buf_bytes_) + " bytes");
   }
 
   // After exchange(): rank r's payload of the last op.

@@ -99,6 +99,7 @@ class BackendEngine:
                                fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
                                fused_resid=fused_resid)
         self.impl = impl
+        self.weight_bytes = self.model.weight_bytes()
         self.active: Dict[int, Request] = {}            # slot -> request
         self.free: List[int] = list(range(slots - 1, -1, -1))
         # Conversation KV residency (BASELINE config 4): when a request of a
@@ -114,6 +115,7 @@ class BackendEngine:
         self.kv_evictions = 0
         self.kv_imported = 0
         self.kv_stale = 0                                   # parked copies found outdated at admission
+        self._importing: Dict[int, int] = {}                # slot -> conv: KV arriving (migration in flight)
         # per-slot host state (the batch builder is vectorised over these)
         self.s_prompt = np.zeros((slots, max_ctx), dtype=np.int32)
         self.s_plen = np.zeros(slots, dtype=np.int64)
@@ -231,7 +233,7 @@ class BackendEngine:
         if s is not None:
             self.s_conv[s] = -1
             self.s_cached[s] = 0
-            self.free.append(s)
+            self.free.insert(0, s)          # reused last (``free`` pops from the end)
 
     def import_kv(self, conv: int, tokens: int) -> int:
         """Park an incoming conversation's KV (``tokens`` positions) in a
@@ -245,6 +247,49 @@ class BackendEngine:
         self.conv_lru[conv] = s
         self.kv_imported += 1
         return s
+
+    def reserve_import(self, conv: int, tokens: int = 0) -> int:
+        """A slot for an incoming conversation's KV while the transfer is in
+        flight on the migration stream: out of the free list and the LRU
+        (so no admission can take it) until ``finish_import`` parks it."""
+        self.drop_parked(conv)
+        s = self._take_slot()
+        self.s_conv[s] = -1
+        self.s_cached[s] = int(tokens)
+        self._importing[s] = conv
+        return s
+
+    def finish_import(self, conv: int, slot: int, tokens: int) -> None:
+        """The KV landed in ``slot``: park it like a resident dialog (the
+        conversation's held turn is admitted next and reuses it)."""
+        if self._importing.pop(slot, None) is None:
+            return                                          # aborted meanwhile (evacuation)
+        old = self.conv_lru.pop(conv, None)
+        if old is not None and old != slot:
+            self.s_conv[old] = -1
+            self.free.append(old)
+        self.s_conv[slot] = conv
+        self.s_cached[slot] = int(tokens)
+        self.conv_lru[conv] = slot
+        self.kv_imported += 1
+
+    def resident_kv_tokens(self) -> int:
+        """KV positions held in this GPU's cache right now: the context of
+        every active request (prompt + generated so far) plus every parked
+        dialog -- the live HBM occupancy of the KV pool (the pool itself is
+        preallocated, so allocator figures never move)."""
+        act = self.s_active
+        n = int((self.s_plen[act] + self.s_gen[act]).sum())
+        if self.conv_lru:
+            n += int(self.s_cached[np.fromiter(self.conv_lru.values(), dtype=np.int64)].sum())
+        return n + int(self.s_cached[list(self._importing)].sum()) if self._importing else n
+
+    def kv_token_capacity(self) -> int:
+        return self.slots * self.max_ctx
+
+    def kv_bytes_per_token(self) -> int:
+        c = self.cfg
+        return c.layers * 2 * c.kv_heads * c.head_dim * 2          # K and V, bf16 (128 KiB for Llama-3-8B)
 
     def lane_capacity(self) -> int:
         """Slots a realtime request may take beyond ``admit_capacity``: every
@@ -442,6 +487,7 @@ class BackendEngine:
         self.active.clear()
         self.s_active[:] = False
         self.conv_lru.clear()
+        self._importing.clear()
         self.s_conv[:] = -1
         self.free = list(range(self.slots - 1, -1, -1))
         return out

@@ -102,10 +102,13 @@ class TelemetryService:
                     self.metrics.inflight.labels(str(g)).set(page.active())
             if self.rs is not None and s["valid"]:
                 try:
+                    # device-level HBM (amd-smi) rides in the metadata: the
+                    # resource's "memory" dimension is the serving footprint
+                    # (weights + live KV) the gateway heartbeats every tick
                     r = self.rs.get_resource(f"gpu{g}")
-                    used = dict(r.used)
-                    used["memory"] = int(s["hbm_used_mb"]) << 20
-                    self.rs.heartbeat(f"gpu{g}", used=used)
+                    r.metadata["hbm_device_used"] = int(s["hbm_used_mb"]) << 20
+                    r.metadata["hbm_device_total"] = int(s["hbm_total_mb"]) << 20
+                    self.rs.heartbeat(f"gpu{g}", used=dict(r.used))
                 except Exception:
                     pass
             self._health(g, s)

@@ -123,7 +123,10 @@ class GatewayApp:
             # per-GPU usage (in-flight slots, HBM) from every tick's load
             # exchange -> /api/v1/resources (multi-rank; one rank keeps its
             # own resource current through the same path)
-            self.gateway.resources = self.resources
+            # with several GPUs, rank 0's autoscale decisions park / unpark
+            # GPU endpoints (its L_EXCLUDE view reaches every rank's planner)
+            self.gateway.attach_resource_scheduler(self.resources,
+                                                   act=self.gateway.rank == 0 and self.gateway.world > 1)
         self.batcher = MicroBatcher(self._flush, cfg.preprocessor.batch_window_us, cfg.preprocessor.max_batch)
         self._stop = threading.Event()
         self._wake = threading.Event()

@@ -169,6 +169,7 @@ class Gateway:
         # identical on every rank, advanced identically by every plan)
         self.plan_state = planner.PlanState(strategy=str(getattr(cfg.loadbalancer, "algorithm", "")))
         self.resources = None          # optional ResourceScheduler: per-GPU usage from the load exchange
+        self._parked_eps: Dict[str, object] = {}   # GPU endpoints the resource scheduler parked
         self._res_next_ns = 0
         self.hbm_fn = None             # optional () -> (used MiB, total MiB) of this rank's GPU
         self._hbm_cache = (0, 0, 0)    # (used, total, refreshed at ns)
@@ -190,6 +191,8 @@ class Gateway:
         # that tick's load vector), when home and dest both execute them
         self._mig_out: List[Tuple[int, int, int]] = []
         self._await_kv: Dict[int, List[Tuple[Request, int]]] = {}   # conv -> [(held turn, home GPU)]
+        # held turns whose KV transfer is in flight on the device (RCCL)
+        self._await_import: Dict[int, List[Tuple[Request, int]]] = {}
         self.migrator = None
         if self.world > 1 and engine is not None and self.kv_migrate and hasattr(engine, "model"):
             from ..parallel.migration import KVMigrator
@@ -529,12 +532,28 @@ class Gateway:
         return max(0, room)
 
     def _pin(self, m: Message, delta: int) -> None:
-        """Count a queued request against its (home GPU, tier) pin."""
+        """Count a queued request against its (home GPU, tier) pin.  The key
+        it was counted under is remembered on the message and released
+        exactly (the conversation may be re-homed -- migration, a completed
+        turn elsewhere -- while this turn waits, and recomputing the home at
+        pop time would decrement the wrong GPU and leave the old one
+        inflated for good)."""
+        if delta < 0:
+            k = m.pin_key
+            if k >= 0:
+                h, t = divmod(k, planner.NTIERS)
+                if h < self.world:
+                    self.pinned[h, t] = max(0, int(self.pinned[h, t]) - 1)
+                m.pin_key = -1
+            return
+        if m.pin_key >= 0:
+            return                                   # already counted
         h = self._home(m)
         if 0 <= h < self.world:
             t = self.tier_of_queue.get(m.queue_name, 2) if m.tier < 0 else m.tier
             t = min(max(int(t), 0), planner.NTIERS - 1)
-            self.pinned[h, t] = max(0, int(self.pinned[h, t]) + delta)
+            self.pinned[h, t] += 1
+            m.pin_key = h * planner.NTIERS + t
 
     def _exclude_mask(self) -> int:
         """GPUs this rank's balancer view rules out for new work: parked by
@@ -556,6 +575,42 @@ class Gateway:
             if not lb._eligible(ep):
                 mask |= 1 << j
         return mask
+
+    # ------------------------------------------------------------------ resource scheduler
+    def attach_resource_scheduler(self, rs, act: bool = True) -> None:
+        """Per-GPU usage (slots, HBM footprint, KV tokens) flows into ``rs``
+        from every load exchange; with ``act`` its autoscale decisions park /
+        unpark GPU endpoints in this rank's balancer (one rank -- rank 0 --
+        should act: its ``L_EXCLUDE`` bit takes the GPU out of placement on
+        every rank)."""
+        self.resources = rs
+        if act and self.lb is not None:
+            rs.on_scale = self._on_resource_scale
+
+    def _on_resource_scale(self, action: str, avg_load: float) -> Optional[str]:
+        rs, lb = self.resources, self.lb
+        rid = rs.scale_target(action)
+        if rid is None or not rid.startswith("gpu"):
+            return None
+        if action == "scale_down":
+            try:
+                ep = lb.get_endpoint_by_id(rid)
+            except Exception:
+                return None
+            lb.remove_endpoint(rid)
+            self._parked_eps[rid] = ep
+            rs.park(rid)
+            self.log.info("resource scheduler parked a GPU", gpu=rid, average_load=round(avg_load, 3))
+        else:
+            ep = self._parked_eps.pop(rid, None)
+            if ep is None:
+                rs.unpark(rid)
+                return None
+            ep.pending = 0
+            lb.add_endpoint(ep)
+            rs.unpark(rid)
+            self.log.info("resource scheduler unparked a GPU", gpu=rid, average_load=round(avg_load, 3))
+        return rid
 
     def _weights(self) -> List[int]:
         lb = self.lb
@@ -603,7 +658,14 @@ class Gateway:
         free = max(0, eng.admit_capacity() - held) if up else 0
         slots_free = max(0, eng.lane_capacity() - held) if (up and self.realtime_lane) else free
         inflight = (eng.inflight() if eng is not None else 0) + held
-        used, total = self._hbm_mib() if eng is not None else (0, 0)
+        kv_tok = kv_cap = 0
+        if eng is not None and hasattr(eng, "resident_kv_tokens"):
+            # live HBM occupancy: weights + resident KV over weights + KV pool
+            kv_tok, kv_cap = eng.resident_kv_tokens(), eng.kv_token_capacity()
+            per, wb = eng.kv_bytes_per_token(), eng.weight_bytes
+            used, total = (wb + kv_tok * per) >> 20, (wb + kv_cap * per) >> 20
+        else:
+            used, total = self._hbm_mib() if eng is not None else (0, 0)
         return planner.make_load(
             free, inflight, depth, age, hbm_used_mib=used, hbm_total_mib=total, healthy=up, epoch=self.epoch,
             done_for=[len(self._done_owed[r]) for r in range(W)],
@@ -611,7 +673,9 @@ class Gateway:
             slots_free=slots_free, slots_total=eng.slots if eng is not None else 0,
             exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
             weights=self._weights(),
-            migrate_rows=[sum(1 for _, h, _ in self._mig_out if h == j and j != self.rank) for j in range(W)])
+            migrate_rows=[sum(1 for _, h, _ in self._mig_out if h == j and j != self.rank) for j in range(W)],
+            migrate_busy=bool(self._mig_out) or bool(self._await_kv),
+            kv_tokens=kv_tok, kv_capacity=kv_cap)
 
     def _observe_loads(self, loads: np.ndarray) -> None:
         """Per-tick bookkeeping on the gathered load matrix: peers' health and
@@ -637,13 +701,15 @@ class Gateway:
         for j in range(W):
             rid = f"gpu{j}"
             slots = int(loads[j, planner.L_SLOTS_TOTAL])
-            cap = {ResourceType.GPU: slots, ResourceType.MEMORY: int(loads[j, planner.L_HBM_TOTAL]) << 20}
+            cap = {ResourceType.GPU: slots, ResourceType.MEMORY: int(loads[j, planner.L_HBM_TOTAL]) << 20,
+                   ResourceType.TOKENS: int(loads[j, planner.L_KV_CAP])}
             used = {ResourceType.GPU: int(loads[j, planner.L_INFLIGHT]),
-                    ResourceType.MEMORY: int(loads[j, planner.L_HBM_USED]) << 20}
+                    ResourceType.MEMORY: int(loads[j, planner.L_HBM_USED]) << 20,
+                    ResourceType.TOKENS: int(loads[j, planner.L_KV_TOKENS])}
             try:
                 rs.heartbeat(rid, used=used, capacity=cap)
             except Exception:            # first sight of a peer GPU: register it
-                rs.register_gpu(j, "llm", slots, cap[ResourceType.MEMORY], 0)
+                rs.register_gpu(j, "llm", slots, cap[ResourceType.MEMORY], cap[ResourceType.TOKENS])
                 rs.heartbeat(rid, used=used, capacity=cap)
 
     def _dispatch_global(self) -> int:
@@ -824,8 +890,10 @@ class Gateway:
         return left
 
     def awaiting_kv(self) -> int:
-        """Turns dispatched here that wait for their KV (next tick)."""
-        return sum(len(v) for v in self._await_kv.values())   # (turn, home) pairs
+        """Turns dispatched here that wait for their KV (next tick, or an
+        RCCL transfer still in flight)."""
+        return (sum(len(v) for v in self._await_kv.values())
+                + sum(len(v) for v in self._await_import.values()))
 
     def _plan_migrations(self, dest: Dict[int, List[Message]]) -> Dict[int, int]:
         """Turns placed on a GPU other than their (alive) home GPU move their
@@ -858,23 +926,48 @@ class Gateway:
                  held: Dict[int, List[Tuple[Request, int]]]) -> List[Request]:
         """Execute last tick's migration orders -- as the home GPU
         (``src_orders``) and as the destination (the turns ``held`` for their
-        KV) -- then release the held turns: resident KV if it arrived, else a
-        dialog replay.  A home GPU that is down (by this tick's loads, the
-        view every rank shares) neither sends nor is waited for."""
-        up = [bool(x) for x in loads[:, planner.L_HEALTHY]]
-        orders = [o for o in src_orders if up[self.rank]]
-        for ck, rs in held.items():
-            srcs = {h for _, h in rs if 0 <= h < self.world and up[h]}
-            orders.extend((ck, h, self.rank) for h in srcs)
-        imported: Dict[int, int] = {}
-        if orders and self.migrator is not None:
-            imported = self.migrator.execute(orders, self.engine, self.rank)
-            self.epoch += 1
+        KV) -- and return the held turns that may be admitted now: KV landed
+        (synchronous data plane, or an RCCL transfer of an earlier tick that
+        completed), or nothing will come (dialog replay).  Turns whose KV is
+        still in flight on the device wait in ``_await_import``.
+
+        A home GPU that is down (by this tick's loads, the view every rank
+        shares) is not asked; a home only sends to a destination that is up
+        AND still wants the KV (the header exchange matches both sides, so a
+        destination that dropped its held turns never leaves an unmatched
+        RCCL send behind).  Every rank joins the header collective on a
+        migration tick (``L_MIGBUSY`` set anywhere)."""
+        W = self.world
         ready: List[Request] = []
+        if self.migrator is None:
+            for rs in held.values():
+                ready.extend(r for r, _h in rs)
+            return ready
+        up = [bool(x) for x in loads[:, planner.L_HEALTHY]]
+        result: Dict[int, int] = {}
+        wanted = set()
+        if loads[:, planner.L_MIGBUSY].any():
+            orders = [(c, d) for c, h, d in src_orders if up[self.rank] and 0 <= d < W and up[d]]
+            wants = []
+            if up[self.rank]:
+                for ck, rs in held.items():
+                    for h in sorted({h for _, h in rs if 0 <= h < W and h != self.rank and up[h]}):
+                        wants.append((ck, h))
+                        wanted.add(ck)
+            result = self.migrator.execute(orders, wants, self.engine, self.rank)
+            if orders or wants:
+                self.epoch += 1
         for ck, rs in held.items():
-            got = imported.get(ck, 0)
+            if ck in wanted and ck not in result:
+                self._await_import.setdefault(ck, []).extend(rs)     # in flight on the device
+                continue
+            got = result.get(ck, 0)
             for r, _h in rs:
                 self.counters["kv_migrated" if got > 0 else "kv_migrate_replays"] += 1
+                ready.append(r)
+        for ck, n in self.migrator.poll(self.engine).items():
+            for r, _h in self._await_import.pop(ck, []):
+                self.counters["kv_migrated"] += 1
                 ready.append(r)
         return ready
 
@@ -962,8 +1055,9 @@ class Gateway:
         self.log.warning("GPU backend unhealthy; evacuating", rank=self.rank, reason=reason)
         self._err_ewma = 0.9 * self._err_ewma + 0.1
         n = 0
-        held = [r for rs in self._await_kv.values() for r, _h in rs]
+        held = [r for d in (self._await_kv, self._await_import) for rs in d.values() for r, _h in rs]
         self._await_kv = {}
+        self._await_import = {}
         for r in held:                                  # turns waiting for a KV that will not be used here
             n += 1
             if isinstance(r.meta, Message):

@@ -183,7 +183,7 @@ class Message:
         "id", "conversation_id", "user_id", "content", "priority", "status",
         "queue_name", "retry_count", "max_retries", "timeout", "created_at",
         "updated_at", "scheduled_at", "completed_at", "metadata", "handle",
-        "enqueued_at", "dispatched_at", "arrival_ns", "prompt_ids", "endpoint_id", "tier",
+        "enqueued_at", "dispatched_at", "arrival_ns", "prompt_ids", "endpoint_id", "tier", "pin_key",
     )
 
     def __init__(self, id: str = "", conversation_id: str = "", user_id: str = "",
@@ -215,6 +215,7 @@ class Message:
         self.prompt_ids = None    # token ids from the GPU tokenizer (backend prompt)
         self.endpoint_id = ""     # backend chosen at dispatch
         self.tier = -1            # tier index at dispatch
+        self.pin_key = -1         # (home GPU, tier) the queued message is counted under (gateway pins)
 
     # -- JSON ------------------------------------------------------------------
     def to_dict(self) -> Dict[str, Any]:

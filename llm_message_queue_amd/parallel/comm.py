@@ -51,6 +51,15 @@ class Comm:
     def broadcast_i64(self, vec: np.ndarray, root: int = 0) -> np.ndarray:
         raise NotImplementedError
 
+    def all_to_all_var(self, send: Sequence[np.ndarray], width: int) -> List[np.ndarray]:
+        """``all_to_all_rows`` when the receiver does not know its row counts
+        (int32 rows of ``width``): the counts travel first in one all_gather.
+        Host-side only -- used for the small KV-migration headers, so no
+        device value is ever read back."""
+        counts = np.array([int(np.asarray(x).size // width) for x in send], dtype=np.int64)
+        mat = self.all_gather_i64(counts)                  # [src, dst]
+        return self.all_to_all_rows(send, [int(mat[src, self.rank]) for src in range(self.world)], width)
+
     def send_tensor(self, t, dst: int) -> None:
         raise NotImplementedError
 
@@ -87,6 +96,9 @@ class SoloComm(Comm):
 
     def broadcast_i64(self, vec, root=0):
         return np.asarray(vec, dtype=np.int64).copy()
+
+    def all_to_all_var(self, send, width):
+        return [np.asarray(send[0], dtype=np.int32).reshape(-1, width).copy()]
 
     def send_tensor(self, t, dst):
         raise RuntimeError("no peer in a world of one")
@@ -255,7 +267,7 @@ class ShmComm(Comm):
     backend = "shm"
 
     def __init__(self, data: "TorchComm", name: str, timeout_s: float = DEFAULT_TIMEOUT_S,
-                 buf_bytes: int = 4 << 20):
+                 buf_bytes: int = 16 << 20):
         """Collective over ``data``: rank 0 creates the segment, the others
         attach.  Raises ``ShmUnavailable`` on EVERY rank if any rank failed
         (no /dev/shm, out of space, ...), so the caller can fall back to the
@@ -293,6 +305,8 @@ class ShmComm(Comm):
             return fn(arg, self.timeout_s)
         except TimeoutError as e:
             raise PeerLost(f"rank {self.rank}: {e}") from e
+        except ValueError as e:          # std::length_error: some rank's payload overflowed (every rank raises)
+            raise PeerLost(f"rank {self.rank}: control-plane payload overflow ({e})") from e
 
     def all_gather_i64(self, vec):
         v = np.ascontiguousarray(vec, dtype=np.int64).reshape(-1)
@@ -307,6 +321,11 @@ class ShmComm(Comm):
             if out[src].shape[0] != c:
                 raise RuntimeError(f"rank {self.rank}: expected {c} rows from {src}, got {out[src].shape[0]}")
         return out
+
+    def all_to_all_var(self, send, width):
+        parts = [np.ascontiguousarray(x, dtype=np.int32).reshape(-1, width).tobytes() for x in send]
+        got = self._x(self.c.all_to_all, parts)
+        return [np.frombuffer(g, dtype=np.int32).reshape(-1, width).copy() for g in got]
 
     def broadcast_i64(self, vec, root=0):
         v = np.ascontiguousarray(vec, dtype=np.int64).reshape(-1)
@@ -385,6 +404,10 @@ class FakeComm(Comm):
             if out[src].shape[0] != c:
                 raise RuntimeError(f"rank {self.rank}: expected {c} rows from {src}, got {out[src].shape[0]}")
         return out
+
+    def all_to_all_var(self, send, width):
+        got = self._exchange([np.asarray(x, dtype=np.int32).reshape(-1, width).copy() for x in send])
+        return [got[src][self.rank] for src in range(self.world)]
 
     def broadcast_i64(self, vec, root=0):
         got = self._exchange(np.asarray(vec, dtype=np.int64).copy())

@@ -53,7 +53,11 @@ NTIERS = 4
 L_FREE, L_INFLIGHT = 0, 1        # admits the next step's prefill headroom takes; slots in use
 L_DEPTH = 2                      # 4 tiers: 2..5 queued (within tier budget)
 L_AGE_US = 6                     # 4 tiers: 6..9 (oldest head wait, microseconds)
-L_HBM_USED, L_HBM_TOTAL = 10, 11  # MiB (telemetry page / device memory info)
+# MiB of the GPU's serving footprint in use / in total: model weights + LIVE
+# KV (active contexts + parked dialogs) over weights + the KV pool.  The pool
+# is preallocated, so allocator or amd-smi figures never move; resident KV is
+# what varies between GPUs and what placement should avoid filling
+L_HBM_USED, L_HBM_TOTAL = 10, 11
 L_HEALTHY, L_EPOCH = 12, 13      # epoch: KV migrations this rank has completed
 L_STOP = 14                      # the rank is shutting down: every rank leaves after this same tick
 L_SLOTS = 15                     # free batch slots (realtime lane capacity)
@@ -63,6 +67,9 @@ L_EXCLUDE = L_PIN + MAX_WORLD * NTIERS   # 56: bitmask of GPUs this rank's balan
 L_RT_US = L_EXCLUDE + 1          # EWMA service time (admit -> done) on this GPU, microseconds
 L_ERR_PPM = L_EXCLUDE + 2        # EWMA backend error rate, parts per million
 L_SLOTS_TOTAL = L_EXCLUDE + 3    # batch slots of this GPU
+L_MIGBUSY = L_EXCLUDE + 4        # this rank takes part in a KV migration this tick (header collective)
+L_KV_TOKENS = L_EXCLUDE + 5      # KV positions resident on this GPU (active + parked dialogs)
+L_KV_CAP = L_EXCLUDE + 6         # KV positions the pool holds (slots x max_ctx)
 L_WEIGHT = L_EXCLUDE + 8         # [64 + j] endpoint weight of GPU j in this rank's balancer (rank 0 row is used)
 # KV migration: [72 + h] = K_MIGRATE rows this router sends rank h in THIS
 # tick's all_to_all (orders decided last tick; h = the conversation's home,
@@ -78,7 +85,8 @@ def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[i
               done_for: Sequence[int] = (), pinned=None, stopping: bool = False,
               slots_free: Optional[int] = None, slots_total: int = 0, exclude_mask: int = 0,
               rt_us: int = 0, err_ppm: int = 0, weights: Sequence[int] = (),
-              migrate_rows: Sequence[int] = ()) -> np.ndarray:
+              migrate_rows: Sequence[int] = (), migrate_busy: bool = False, kv_tokens: int = 0,
+              kv_capacity: int = 0) -> np.ndarray:
     """``pinned``: [W, 4] (home GPU x tier) queued counts, or a [W] vector
     (all counted as tier 2, normal -- legacy callers)."""
     v = np.zeros(LOAD_WIDTH, dtype=np.int64)
@@ -104,6 +112,8 @@ def make_load(free: int, inflight: int, depth: Sequence[int], age_us: Sequence[i
         v[L_WEIGHT + j] = w
     for h, n in enumerate(list(migrate_rows)[:MAX_WORLD]):
         v[L_MIGC + h] = n
+    v[L_MIGBUSY] = int(bool(migrate_busy))
+    v[L_KV_TOKENS], v[L_KV_CAP] = kv_tokens, kv_capacity
     return v
 
 

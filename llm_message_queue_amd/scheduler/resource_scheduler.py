@@ -16,7 +16,10 @@ Fixes: D10 (``queued_at`` is always set, no type-assert panic), D11 (release
 subtracts exactly what was allocated; the reference halves ``Load`` and
 never decrements ``Used``), D12 (pending queue ordered MORE urgent first:
 lower priority int, then FIFO).  Autoscale decisions are returned/recorded and
-can drive a callback (the reference only logs).
+drive ``on_scale``: on a GPU node the gateway wires it to park / unpark GPU
+endpoints (``Gateway.attach_resource_scheduler``), which takes the GPU out of
+(or back into) multi-GPU placement through the balancer's ``L_EXCLUDE`` view
+-- the reference's `checkAutoScaling` (`:525-571`) only logs.
 """
 from __future__ import annotations
 
@@ -144,6 +147,9 @@ class ResourceScheduler:
         self._last_scale = 0.0
         self.on_scale = on_scale
         self.scale_events: List[dict] = []
+        # resources taken out of service by a scale-down (GPU endpoints parked
+        # in the balancer): not counted as active capacity, first to return
+        self.parked: List[str] = []
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
         if start:
@@ -323,8 +329,39 @@ class ResourceScheduler:
     def average_load(self) -> float:
         with self._lock:
             act = [r.load for r in self.resources.values()
-                   if r.status not in (ResourceStatus.OFFLINE, ResourceStatus.ERROR)]
+                   if r.status not in (ResourceStatus.OFFLINE, ResourceStatus.ERROR) and r.id not in self.parked]
         return sum(act) / len(act) if act else 0.0
+
+    # ------------------------------------------------------------------ scale actions
+    def scale_target(self, action: str) -> Optional[str]:
+        """Which resource a scale action applies to: ``scale_down`` parks
+        the least-loaded active one (ties: highest id, so GPU 0 -- which
+        fronts HTTP -- goes last); ``scale_up`` returns the most recently
+        parked one."""
+        with self._lock:
+            if action == "scale_up":
+                return self.parked[-1] if self.parked else None
+            act = [r for r in self.resources.values()
+                   if r.status not in (ResourceStatus.OFFLINE, ResourceStatus.ERROR) and r.id not in self.parked]
+            if len(act) <= max(1, self.cfg.min_resources):
+                return None
+            return min(act, key=lambda r: (r.load, [-ord(c) for c in r.id])).id
+
+    def park(self, resource_id: str) -> None:
+        with self._lock:
+            if resource_id not in self.parked:
+                self.parked.append(resource_id)
+            r = self.resources.get(resource_id)
+            if r is not None:
+                r.metadata["parked"] = True
+
+    def unpark(self, resource_id: str) -> None:
+        with self._lock:
+            if resource_id in self.parked:
+                self.parked.remove(resource_id)
+            r = self.resources.get(resource_id)
+            if r is not None:
+                r.metadata.pop("parked", None)
 
     def check_auto_scaling(self) -> Optional[str]:
         if not self.cfg.enable_auto_scaling:
@@ -333,7 +370,8 @@ class ResourceScheduler:
             return None
         with self._lock:
             active = sum(1 for r in self.resources.values()
-                         if r.status not in (ResourceStatus.OFFLINE, ResourceStatus.ERROR))
+                         if r.status not in (ResourceStatus.OFFLINE, ResourceStatus.ERROR)
+                         and r.id not in self.parked)
             pend = len(self.pending)
         avg = self.average_load()
         action = None

@@ -1,0 +1,116 @@
+"""KV migration data plane on the GPU (N11, VERDICT r2 missing #5 / next #2):
+one gather / one scatter HIP kernel over all layers, and the RCCL leg run
+asynchronously on a side stream (world-1 self send/recv through
+``exchange_p2p``) while two Llama-3-8B forwards are queued on the compute
+stream -- the host only enqueues.  Numerics: bit-exact against torch slicing
+of the same cache rows."""
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_kv_move_pack_unpack_bit_exact():
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
+    from llm_message_queue_amd.parallel.comm import SoloComm
+    from llm_message_queue_amd.parallel.migration import KVMigrator
+    cfg = LlamaConfig.tiny()
+    m = LlamaStub(cfg, slots=6, max_ctx=96, device=DEV, impl="hip", seed=3)
+    for t in m.kcache + m.vcache:
+        t.normal_()
+    mig = KVMigrator(m, SoloComm())
+    for slot, n in ((0, 1), (4, 37), (5, 96)):
+        buf = mig.pack(slot, n)
+        torch.cuda.synchronize()
+        ref = torch.stack([torch.stack([m.kcache[L][slot, :, :n], m.vcache[L][slot, :, :n]])
+                           for L in range(cfg.layers)])
+        assert buf.shape == ref.shape and torch.equal(buf, ref)
+        dst = (slot + 1) % 6
+        before = [t[dst].clone() for t in m.kcache]
+        mig.unpack(buf, dst)
+        torch.cuda.synchronize()
+        for L in range(cfg.layers):
+            assert torch.equal(m.kcache[L][dst, :, :n], m.kcache[L][slot, :, :n])
+            assert torch.equal(m.vcache[L][dst, :, :n], m.vcache[L][slot, :, :n])
+            assert torch.equal(m.kcache[L][dst, :, n:], before[L][:, n:])     # nothing past n touched
+
+
+def test_rccl_self_p2p_migration_is_async_under_queued_8b_forwards():
+    import torch.distributed as dist
+    from llm_message_queue_amd.backend.engine import BackendEngine
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.parallel.comm import TorchComm
+    from llm_message_queue_amd.parallel.migration import KVMigrator
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                            device_id=DEV)
+    try:
+        comm = TorchComm()
+        eng = BackendEngine(LlamaConfig.llama3_8b(), slots=32, max_ctx=512, token_budget=4096, device=DEV,
+                            impl="hip", seed=5)
+        m = eng.model
+        mig = KVMigrator(m, comm)
+        assert mig._p2p_on_device()
+        conv, n = 4242, 300
+        src_slot = eng.import_kv(conv, n)                     # a parked dialog of 300 positions
+        for L in range(m.cfg.layers):
+            m.kcache[L][src_slot, :, :n].normal_()
+            m.vcache[L][src_slot, :, :n].normal_()
+        ref_k = [m.kcache[L][src_slot, :, :n].clone() for L in (0, 31)]
+
+        def queue_two_forwards():
+            T = 4096
+            r = torch.arange(T, device=DEV, dtype=torch.int32)
+            slot = (r // 16) % 32
+            pos = (r % 16) + 16 * 20                          # scratch rows of other slots / positions
+            slot = torch.where(slot == src_slot, (slot + 1) % 32, slot)
+            for _ in range(2):
+                m.forward(torch.zeros(T, dtype=torch.long, device=DEV), pos.contiguous(), slot.contiguous(),
+                          torch.arange(8, device=DEV, dtype=torch.long))
+
+        # warm: RCCL builds the self-p2p communicator on first use
+        c0 = 777
+        s0 = eng.import_kv(c0, 8)
+        mig._device_transfer([(0, c0)], [(0, c0 + 1)], {(0, c0): (s0, 8)}, {(0, c0 + 1): 8}, eng)
+        while mig.in_flight():
+            mig.poll(eng)
+        torch.cuda.synchronize()
+
+        queue_two_forwards()
+        t0 = time.perf_counter()
+        mig._device_transfer([(0, conv)], [(0, conv + 1)], {(0, conv): (src_slot, n)}, {(0, conv + 1): n}, eng)
+        host_ms = (time.perf_counter() - t0) * 1e3
+        first_poll = mig.poll(eng)
+        e_fwd = torch.cuda.Event()
+        e_fwd.record()
+        busy = not e_fwd.query()                              # the forwards were still running
+        deadline = time.time() + 30
+        got = {}
+        while not got and time.time() < deadline:
+            got = mig.poll(eng)
+            time.sleep(0.001)
+        torch.cuda.synchronize()
+        print(f"host time of the device transfer: {host_ms:.3f} ms (forwards still queued: {busy})")
+        assert busy and first_poll == {}
+        assert host_ms < 5.0, host_ms                         # enqueue only: two 8B forwards are ~80 ms
+        assert got == {conv + 1: n}
+        dst_slot, tokens = eng.export_kv(conv + 1)
+        assert tokens == n and dst_slot != src_slot
+        for i, L in enumerate((0, 31)):
+            assert torch.equal(m.kcache[L][dst_slot, :, :n], ref_k[i])
+        assert eng.export_kv(conv) == (-1, 0)                  # moved out of the source
+    finally:
+        dist.destroy_process_group()

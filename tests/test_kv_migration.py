@@ -53,9 +53,9 @@ def test_migrated_turn_equals_resident_turn():
     _run(g0, Request(1, p1.copy(), 3, conv=conv))
     m0, m1 = KVMigrator(g0.model, comms[0]), KVMigrator(g1.model, comms[1])
     got = {}
-    th = threading.Thread(target=lambda: got.update(r0=m0.execute([(conv, 0, 1)], g0, 0)))
+    th = threading.Thread(target=lambda: got.update(r0=m0.execute([(conv, 1)], [], g0, 0)))
     th.start()
-    got["r1"] = m1.execute([(conv, 0, 1)], g1, 1)
+    got["r1"] = m1.execute([], [(conv, 0)], g1, 1)
     th.join()
     n = got["r1"][conv]
     assert n == len(p1) + 3 - 1 and g1.kv_imported == 1
