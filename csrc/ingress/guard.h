@@ -77,6 +77,15 @@ class RateLimiter {
     return false;
   }
 
+  // Give back a token taken by allow() for a request a later check refused.
+  void refund(const std::string& key) {
+    if (!enabled()) return;
+    Shard& sh = shards_[std::hash<std::string>{}(key) & (kShards - 1)];
+    std::lock_guard<std::mutex> g(sh.mu);
+    auto it = sh.b.find(key);
+    if (it != sh.b.end()) it->second.tokens = std::min(burst_, it->second.tokens + 1.0);
+  }
+
   size_t keys() {
     size_t n = 0;
     for (auto& sh : shards_) {
@@ -360,18 +369,27 @@ class Guard {
       }
       if (!role_allows(r.role, perm)) return fail(r, G_FORBIDDEN, "role '" + r.role + "' lacks " + perm);
     }
-    // Most specific bucket first: a request one IP's or one user's limit
-    // refuses must not have drained the shared global bucket on its way
-    // (one abusive client could otherwise exhaust global capacity for all).
-    // The per-user bucket is keyed on the AUTHENTICATED subject only; an
-    // anonymous caller is limited by its address (per-IP bucket) -- a body's
-    // user_id is a claim anyone can make, so keying on it would let a
-    // client spend another user's quota.
+    // A refused request drains NO bucket: buckets are taken most specific
+    // first, and a token already taken is refunded when a later bucket
+    // refuses (a client held back by the per-user or global limit keeps its
+    // per-IP budget; one abusive client cannot exhaust the global bucket
+    // through requests its own limit refuses).  The per-user bucket is keyed
+    // on the AUTHENTICATED subject only; an anonymous caller is limited by
+    // its address (per-IP bucket) -- a body's user_id is a claim anyone can
+    // make, so keying on it would let a client spend another user's quota.
     (void)user_hint;
     double ra = 0;
-    if (!ip.empty() && !per_ip_.allow(ip, now_ns, &ra)) return limited(r, "per_ip", ra);
-    if (!r.subject.empty() && !per_user_.allow(r.subject, now_ns, &ra)) return limited(r, "per_user", ra);
-    if (!global_.allow("*", now_ns, &ra)) return limited(r, "global", ra);
+    const bool by_ip = !ip.empty(), by_user = !r.subject.empty();
+    if (by_ip && !per_ip_.allow(ip, now_ns, &ra)) return limited(r, "per_ip", ra);
+    if (by_user && !per_user_.allow(r.subject, now_ns, &ra)) {
+      if (by_ip) per_ip_.refund(ip);
+      return limited(r, "per_user", ra);
+    }
+    if (!global_.allow("*", now_ns, &ra)) {
+      if (by_ip) per_ip_.refund(ip);
+      if (by_user) per_user_.refund(r.subject);
+      return limited(r, "global", ra);
+    }
     return r;
   }
 

@@ -10,7 +10,12 @@
 // and a push into the process-shared request ring (shm_ring.h) as a RAW
 // record.  The GPU dispatcher drains the ring in large batches, so
 // preprocessing (text_analyze + MFMA classifier) sees big batches too.
-// Other routes (status, conversations, admin) stay on the Python API server.
+// Other routes (status, conversations, admin) stay on the Python API server;
+// with an upstream set (``set_upstream``, the multi-GPU `cli serve` front
+// door) they are reverse-proxied to it, so one public port serves the whole
+// REST surface.  Messages with a conversation_id can be routed to a separate
+// ring (``set_conv_ring``) drained by the process that owns conversation
+// state; the rest go to the shared ring every GPU rank drains.
 //
 // Response: 202 {"message_id", "priority", "queue_time", "estimated_wait"}
 // where priority is the requested one (0 = to be decided by the
@@ -35,6 +40,7 @@
 #include <cstdio>
 #include <cstring>
 #include <ctime>
+#include <memory>
 #include <random>
 #include <string>
 #include <thread>
@@ -58,6 +64,7 @@ constexpr size_t kMaxHeader = 64u << 10; // request line + headers cap (431 beyo
 // ------------------------------------------------------------------ JSON scan
 struct Scan {
   bool ok = false;
+  bool has_conv = false;   // a non-empty conversation_id (routed to the conversation owner's ring)
   std::string id, user_id;
   int priority = 0;
   std::string error;   // why the body was refused (400 text)
@@ -367,6 +374,7 @@ Scan scan_message(const char* b, size_t n) {
     if (key == "id" || key == "user_id") {
       std::string v;
       if (c0 == '"') {
+        js.lone_surrogate = false;                    // (set by an earlier field's escapes)
         if (!js.str(&v)) return r;
         if (js.lone_surrogate || !plain_token(v)) {
           r.error = key + " must be printable ASCII without quotes or backslashes";
@@ -398,6 +406,12 @@ Scan scan_message(const char* b, size_t n) {
         }
         r.priority = (int)d;
       }
+    } else if (key == "conversation_id") {             // Message.from_dict: str(v or "")
+      const char* v0 = js.p;
+      if (!js.value()) return r;
+      const std::string raw(v0, js.p - v0);
+      r.has_conv = !(raw == "null" || raw == "false" || raw == "\"\"" || raw == "0" || raw == "[]" ||
+                     raw == "{}" || raw == "0.0" || raw == "-0");
     } else if (key == "metadata") {                    // Message.from_dict: object (or null)
       if (c0 != '{' && c0 != 'n') {
         r.error = "metadata must be an object";
@@ -531,10 +545,23 @@ class HttpIngress {
     d["rate_limited"] = limited_.load();
     d["refused_no_fd"] = refused_fd_.load();
     d["idle_closed"] = idle_closed_.load();
+    d["proxied"] = proxied_.load();
+    d["proxy_errors"] = proxy_errors_.load();
     return d;
   }
 
   void set_guard(std::shared_ptr<llmq::Guard> g) { guard_ = std::move(g); }
+  // Messages that carry a conversation_id go to this ring instead (the
+  // process that owns conversation state drains it); others to the shared one.
+  void set_conv_ring(const std::string& name) {
+    conv_ring_ = name.empty() ? nullptr : std::make_unique<llmq::ShmRing>(name, 1 << 26, "open");
+  }
+  // Every route but the hot submit path (and /health) is forwarded to the
+  // API server at host:port -- one public port for the whole REST surface.
+  void set_upstream(const std::string& host, int port) {
+    upstream_host_ = host;
+    upstream_port_ = port;
+  }
   void set_envelope(bool on) { envelope_ = on; }
   void set_idle_timeout(double seconds) { idle_ns_.store(seconds > 0 ? (int64_t)(seconds * 1e9) : 0); }
 
@@ -850,7 +877,8 @@ class HttpIngress {
           const uint32_t bl = (uint32_t)clen;
           memcpy(&rec[44], &bl, 4);
           memcpy(&rec[48], body, clen);
-          if (id.size() > 36 || !ring_.push(rec, TAG_RAW)) {
+          llmq::ShmRing& dst = (s.has_conv && conv_ring_) ? *conv_ring_ : ring_;
+          if (id.size() > 36 || !dst.push(rec, TAG_RAW)) {
             if (id.size() > 36) {
               bad_++;
               respond(cn, 400, "Bad Request", "{\"error\":\"id longer than 36 bytes\"}", keep);
@@ -867,6 +895,9 @@ class HttpIngress {
         }
       } else if (method == "GET" && (path == "/health" || path == "/api/v1/health")) {
         respond(cn, 200, "OK", "{\"status\":\"ok\",\"version\":\"1.0.0\",\"time\":\"" + rfc3339_now() + "\"}", keep);
+      } else if (upstream_port_ > 0) {
+        proxied_++;
+        proxy(cn, h, hl, body, clen, keep);
       } else {
         respond(cn, 404, "Not Found", "{\"error\":\"route served by the API server\"}", keep);
       }
@@ -875,9 +906,101 @@ class HttpIngress {
     if (pos) cn.in.erase(0, pos);
   }
 
+  // Blocking reverse proxy of one request to the API server (status,
+  // conversation and admin routes: low rate, so the epoll thread may wait for
+  // the answer; the submit path never comes here).  Connection: close
+  // upstream; the client's keep-alive is kept when the answer is framed by
+  // Content-Length.
+  void proxy(Conn& cn, const char* h, size_t hl, const char* body, size_t clen, bool keep) {
+    std::string req;
+    req.reserve(hl + clen + 128);
+    const char* line_end = (const char*)memchr(h, '\n', hl);
+    const char* cur = line_end ? line_end + 1 : h + hl;
+    req.append(h, cur - h);                                      // request line (with its CRLF)
+    while (cur < h + hl) {
+      const char* eol = (const char*)memchr(cur, '\n', h + hl - cur);
+      const char* le = eol ? eol + 1 : h + hl;
+      const char* colon = (const char*)memchr(cur, ':', le - cur);
+      std::string name = colon ? std::string(cur, colon - cur) : std::string();
+      for (auto& c : name) c = (char)tolower((unsigned char)c);
+      if (name != "connection" && name != "expect" && name != "keep-alive" && name != "x-forwarded-for") {
+        req.append(cur, le - cur);
+        if (req.back() != '\n') req.append("\r\n");
+      }
+      cur = le;
+    }
+    req.append("Connection: close\r\nX-Forwarded-For: " + cn.ip + "\r\n\r\n");
+    req.append(body, clen);
+    std::string resp;
+    bool ok = false;
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (fd >= 0) {
+      timeval tv{30, 0};
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+      setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+      sockaddr_in a{};
+      a.sin_family = AF_INET;
+      a.sin_port = htons((uint16_t)upstream_port_);
+      inet_pton(AF_INET, upstream_host_.c_str(), &a.sin_addr);
+      if (connect(fd, (sockaddr*)&a, sizeof a) == 0) {
+        size_t off = 0;
+        while (off < req.size()) {
+          ssize_t w = ::send(fd, req.data() + off, req.size() - off, MSG_NOSIGNAL);
+          if (w <= 0) break;
+          off += (size_t)w;
+        }
+        if (off == req.size()) {
+          char b[65536];
+          for (;;) {
+            ssize_t r = ::recv(fd, b, sizeof b, 0);
+            if (r <= 0) {
+              ok = r == 0;
+              break;
+            }
+            resp.append(b, (size_t)r);
+            if (resp.size() > (64u << 20)) break;
+          }
+        }
+      }
+      ::close(fd);
+    }
+    const size_t he = resp.find("\r\n\r\n");
+    if (!ok || he == std::string::npos || resp.compare(0, 5, "HTTP/") != 0) {
+      proxy_errors_++;
+      respond(cn, 502, "Bad Gateway", "{\"error\":\"API server unreachable\"}", keep);
+      return;
+    }
+    // drop the upstream's Connection header; keep the client connection open
+    // only when the body length is explicit
+    std::string head;
+    bool has_len = false, chunked = false;
+    size_t p = 0;
+    while (p < he) {
+      size_t e = resp.find("\r\n", p);
+      if (e == std::string::npos || e > he) e = he;
+      std::string ln = resp.substr(p, e - p);
+      std::string low = ln;
+      for (auto& c : low) c = (char)tolower((unsigned char)c);
+      if (low.compare(0, 15, "content-length:") == 0) has_len = true;
+      if (low.compare(0, 18, "transfer-encoding:") == 0) chunked = true;
+      if (p == 0 || low.compare(0, 11, "connection:") != 0) head += ln + "\r\n";
+      p = e + 2;
+    }
+    const bool k = keep && has_len && !chunked;
+    if (!k) head += "Connection: close\r\n";
+    cn.out.append(head);
+    cn.out.append("\r\n");
+    cn.out.append(resp, he + 4, std::string::npos);
+    if (!k) cn.close_after = true;
+  }
+
   int port_;
   std::string host_;
   llmq::ShmRing ring_;
+  std::unique_ptr<llmq::ShmRing> conv_ring_;
+  std::string upstream_host_ = "127.0.0.1";
+  int upstream_port_ = 0;
+  std::atomic<int64_t> proxied_{0}, proxy_errors_{0};
   int nthreads_;
   std::atomic<bool> running_{false};
   std::vector<std::thread> th_;
@@ -901,6 +1024,8 @@ PYBIND11_MODULE(_ingress, m) {
       .def("stop", &HttpIngress::stop, py::call_guard<py::gil_scoped_release>())
       .def("stats", &HttpIngress::stats)
       .def("set_guard", &HttpIngress::set_guard)
+      .def("set_conv_ring", &HttpIngress::set_conv_ring, py::arg("name"))
+      .def("set_upstream", &HttpIngress::set_upstream, py::arg("host"), py::arg("port"))
       .def("set_envelope", &HttpIngress::set_envelope)
       .def("set_idle_timeout", &HttpIngress::set_idle_timeout, py::arg("seconds"));
   py::class_<llmq::Guard, std::shared_ptr<llmq::Guard>>(m, "Guard")
@@ -943,6 +1068,6 @@ PYBIND11_MODULE(_ingress, m) {
   m.def("scan_message", [](py::bytes b) {
     std::string s = b;
     Scan r = scan_message(s.data(), s.size());
-    return py::make_tuple(r.ok, r.id, r.priority, r.user_id, r.error);
+    return py::make_tuple(r.ok, r.id, r.priority, r.user_id, r.error, r.has_conv);
   });
 }

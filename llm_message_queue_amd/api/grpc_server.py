@@ -318,7 +318,11 @@ class _Service:
         self._admit(context, "GetMessage")
         m = self.G.messages.get(req.message_id)
         if m is None:
-            context.abort(grpc.StatusCode.NOT_FOUND, "Message not found")
+            d = self.G.find_message(req.message_id) if getattr(self.G, "peers", None) is not None else None
+            if d is None:
+                context.abort(grpc.StatusCode.NOT_FOUND, "Message not found")
+            m = Message.from_dict(d)          # held by another GPU rank (multi-GPU front door)
+            m.status = d.get("status", m.status)
         return self._info(m)
 
     def WatchMessage(self, req, context):

@@ -242,16 +242,17 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
 
     @app.get("/api/v1/messages/{mid}")
     def get_message(mid: str):
-        m = G.messages.get(mid)
-        if m is None:
+        # this process's store, else the GPU rank that popped it (multi-GPU front door)
+        d = G.find_message(mid)
+        if d is None:
             return _err(404, "Message not found")
-        return m.to_dict()
+        return d
 
     @app.get("/api/v1/messages")
     def list_messages(user_id: str = "", conversation_id: str = "", status: str = "", limit: int = 10,
                       offset: int = 0):
-        total, msgs = G.messages.query(user_id, conversation_id, status, max(0, limit), max(0, offset))
-        return {"messages": [m.to_dict() for m in msgs], "total": total, "limit": limit, "offset": offset}
+        total, msgs = G.query_messages(user_id, conversation_id, status, max(0, limit), max(0, offset))
+        return {"messages": msgs, "total": total, "limit": limit, "offset": offset}
 
     @app.put("/api/v1/messages/{mid}/status")
     async def update_message_status(mid: str, request: Request):
@@ -264,6 +265,8 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             return _err(400, f"invalid status {status!r}")
         m = G.messages.get(mid)
         if m is None:
+            if G.peers is not None and G.peers.first("set_status", [mid, status]):
+                return {"status": "updated", "message_id": mid}
             return _err(404, "Message not found")
         m.status = status
         m.updated_at = time.time_ns()
@@ -273,6 +276,9 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
     def delete_message(mid: str):
         m = G.messages.get(mid)
         if m is None:
+            res = G.peers.first("remove", [mid]) if G.peers is not None else None
+            if isinstance(res, dict):
+                return {"status": "deleted", "message_id": mid, "dequeued": bool(res.get("dequeued"))}
             return _err(404, "Message not found")
         removed = m.queue_name and G.standard.has_queue(m.queue_name) and G.standard.mlq.remove(m.queue_name, m)
         G.messages.remove(mid)

@@ -8,10 +8,17 @@ of one entry point.
     python -m llm_message_queue_amd.cli validate-config [--config DIR]
     python -m llm_message_queue_amd.cli bench [bench.py args]
 
-Multi-GPU: launch under ``torch.distributed.run`` (one rank per GPU, RCCL).
-Rank 0 hosts HTTP; every rank runs the gateway tick loop and the ranks share
-work through the RCCL planner (all_gather of load vectors + all_to_all of
-request descriptors).  Split deployment: any number of ``api-gateway``
+Multi-GPU: launch under ``torch.distributed.run`` (one rank per GPU).  Rank
+0 hosts the public port: the C++ front door (``server.front_door: native``)
+takes ``POST /api/v1/messages`` into a shared-memory ring that EVERY rank
+drains (so ingest and GPU preprocessing spread over the GPUs), routes
+conversation turns to rank 0 (owner of conversation state) and
+reverse-proxies every other route to rank 0's API server; status queries for
+messages another rank popped are answered through ``gateway.peers``.  Every
+rank runs the gateway tick loop; per tick the ranks exchange load vectors
+and request descriptors over the node-local shared-memory control plane
+(``parallel.comm.ShmComm``) and compute the same placement plan, and KV
+migrations move over RCCL / xGMI.  Split deployment: any number of ``api-gateway``
 processes (HTTP + preprocess) push into a shared-memory request ring that the
 ``queue-manager`` process (dispatcher + GPU backend) drains, with status
 events flowing back -- the reference's microservices never shared their
@@ -43,17 +50,49 @@ def _build_engine(cfg, model: str, device):
                          token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank), page
 
 
+def _build_cpu_engine(cfg):
+    """``--cpu-ranks``: a tiny Llama-shaped engine on the CPU reference ops
+    (the multi-rank control flow without a GPU; never a measurement)."""
+    from ..backend.engine import BackendEngine
+    from ..backend.slot_page import SlotPage
+    from ..models.llama_stub import LlamaConfig
+    rank = int(os.environ.get("RANK", "0"))
+    page = SlotPage(f"serve{os.environ.get('TORCHELASTIC_RUN_ID', os.getpid())}", rank)
+    return BackendEngine(LlamaConfig.tiny(), slots=min(cfg.gpu.slots_per_gpu, 16), max_ctx=64, token_budget=128,
+                         device="cpu", impl="ref", seed=1000 + rank, page=page, gpu_index=rank), page
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def _wait_port(host: str, port: int, thread, timeout_s: float = 30.0) -> None:
+    import socket
+    deadline = time.monotonic() + timeout_s
+    while time.monotonic() < deadline and thread.is_alive():
+        try:
+            with socket.create_connection((host, port), timeout=0.5):
+                return
+        except OSError:
+            time.sleep(0.05)
+    raise RuntimeError(f"API server did not come up on {host}:{port}")
+
+
 def cmd_native_ingress(a) -> int:
     """``api-gateway --native``: the C++ HTTP ingress for POST /api/v1/messages
     feeding the shared request ring (no Python request handling at all)."""
     from ..gateway.native_ingress import NativeIngress
     cfg = _load_cfg(a.config)
     port = a.port or cfg.server.port
-    ing = NativeIngress(port, a.ring or cfg.server.shared_ring, a.ingress_threads, a.host or cfg.server.host,
+    threads = a.ingress_threads or cfg.server.ingress_threads
+    ing = NativeIngress(port, a.ring or cfg.server.shared_ring, threads, a.host or cfg.server.host,
                         cfg=cfg)
     port = ing.start()
     print(json.dumps({"event": "listening", "host": a.host or cfg.server.host, "port": port, "role": "native-ingress",
-                      "ring": ing.ring, "threads": a.ingress_threads}), flush=True)
+                      "ring": ing.ring, "threads": threads}), flush=True)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
@@ -80,21 +119,51 @@ def cmd_serve(a, role: str = "serve") -> int:
         cfg.server.host = a.host
     ulog.configure(cfg.logging.level, cfg.logging.format, cfg.logging.output)
     rank = int(os.environ.get("RANK", "0"))
-    use_gpu = torch.cuda.is_available() and not a.no_gpu
-    comm = init_from_env(control=cfg.gpu.control_plane) if use_gpu else None
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    cpu_ranks = bool(getattr(a, "cpu_ranks", False))
+    if getattr(a, "front_door", ""):
+        cfg.server.front_door = a.front_door
+    use_gpu = torch.cuda.is_available() and not a.no_gpu and not cpu_ranks
+    comm = None
+    if use_gpu:
+        comm = init_from_env(control=cfg.gpu.control_plane)
+    elif cpu_ranks and world > 1:
+        # CPU rehearsal of the multi-GPU job: gloo data plane, the same
+        # control plane, tiny reference-op engines (tests / CI)
+        comm = init_from_env(backend="gloo", control=cfg.gpu.control_plane)
     engine = page = None
     if use_gpu and role in ("serve", "queue-manager"):
         local = local_device_index()
         torch.cuda.set_device(local)
         engine, page = _build_engine(cfg, a.model, torch.device("cuda", local))
         engine.warm_shapes()      # cold-start GEMM shapes before the first request (idle -> busy)
+    elif cpu_ranks and role == "serve":
+        engine, page = _build_cpu_engine(cfg)
     ring, app_role = None, "serve"
-    if role in ("api-gateway", "queue-manager") and not a.no_ring:
+    front = world > 1 and role == "serve" and engine is not None and cfg.server.front_door == "native"
+    job = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
+    conv_ring = None
+    if front:
+        # multi-GPU front door: ONE shared request ring every rank drains
+        # (MPMC), plus rank 0's ring for conversation turns (rank 0 owns
+        # conversation state); the C++ ingress on rank 0 feeds both
+        from ..gateway.shm_bridge import RingPair
+        shared = f"{a.ring or cfg.server.shared_ring}-{job}"
+        ring = RingPair(shared, cfg.server.shared_ring_bytes, "open")
+        if rank == 0:
+            conv_ring = RingPair(f"{shared}-conv", cfg.server.shared_ring_bytes, "open")
+        app_role = "rank"
+    elif role in ("api-gateway", "queue-manager") and not a.no_ring:
         # the split deployment shares ONE request queue through shared memory (D14)
         from ..gateway.shm_bridge import RingPair
         ring = RingPair(a.ring or cfg.server.shared_ring, cfg.server.shared_ring_bytes, "open")
         app_role = "ingress" if role == "api-gateway" else "dispatcher"
     gapp = GatewayApp(cfg, use_gpu=use_gpu, engine=engine, comm=comm, start=False, role=app_role, ring=ring)
+    if front:
+        from ..gateway.peers import PeerDirectory
+        if conv_ring is not None:
+            gapp.extra_rings.append(conv_ring)
+        gapp.peers = PeerDirectory(ring.name, rank, world, handler=gapp.peer_op)
     if engine is not None:
         # every rank's balancer lists EVERY GPU of the job (its own bound to
         # the zero-copy load page): the multi-GPU planner reads the view of
@@ -104,9 +173,9 @@ def cmd_serve(a, role: str = "serve") -> int:
         for j in range(world):
             gapp.lb.add_endpoint(Endpoint(id=f"gpu{j}", type="llm", gpu_index=j, page=page if j == rank else None,
                                           max_connections=cfg.gpu.slots_per_gpu))
-        gapp.resources.register_gpu(rank, a.model, cfg.gpu.slots_per_gpu,
-                                    torch.cuda.get_device_properties(engine.device).total_memory,
-                                    cfg.gpu.slots_per_gpu * cfg.backend.max_ctx)
+        hbm = (torch.cuda.get_device_properties(engine.device).total_memory if engine.cuda
+               else engine.weight_bytes + engine.kv_token_capacity() * engine.kv_bytes_per_token())
+        gapp.resources.register_gpu(rank, a.model, engine.slots, hbm, engine.kv_token_capacity())
     if page is not None:
         gapp.start_telemetry({rank: page})
     gapp.start()
@@ -120,17 +189,32 @@ def cmd_serve(a, role: str = "serve") -> int:
                 stop.set()
             stop.wait(0.2)
     threading.Thread(target=_watch_fatal, daemon=True).start()
+    ingress = None
     if rank == 0 and role in ("serve", "api-gateway", "queue-manager"):
         # queue-manager serves the full API too: with a native ingress in
         # front, status / conversation / admin routes live with the dispatcher
         import uvicorn
         from ..api.server import create_app
         app = create_app(gapp)
-        server = uvicorn.Server(uvicorn.Config(app, host=cfg.server.host, port=cfg.server.port, log_level="warning"))
+        api_host, api_port = cfg.server.host, cfg.server.port
+        if front:
+            # the public port belongs to the C++ front door; the API server
+            # listens on loopback behind it (reverse-proxied routes)
+            api_host, api_port = "127.0.0.1", _free_port()
+        server = uvicorn.Server(uvicorn.Config(app, host=api_host, port=api_port, log_level="warning"))
         t = threading.Thread(target=server.run, daemon=True)
         t.start()
-        print(json.dumps({"event": "listening", "host": cfg.server.host, "port": cfg.server.port,
-                          "gpu": use_gpu, "role": role}), flush=True)
+        port = api_port
+        if front:
+            from ..gateway.native_ingress import NativeIngress
+            _wait_port(api_host, api_port, t)
+            ingress = NativeIngress(cfg.server.port, ring.name, getattr(a, "ingress_threads", 0)
+                                    or cfg.server.ingress_threads, cfg.server.host, cfg=cfg,
+                                    conv_ring=f"{ring.name}-conv", upstream=(api_host, api_port))
+            port = ingress.start()
+        print(json.dumps({"event": "listening", "host": cfg.server.host, "port": port,
+                          "gpu": use_gpu, "role": role, "world": world,
+                          "front_door": "native" if front else "python", "api_port": api_port}), flush=True)
         grpc_srv = None
         if cfg.server.grpc_port:
             from ..api.grpc_server import GrpcServer
@@ -142,6 +226,8 @@ def cmd_serve(a, role: str = "serve") -> int:
             stop.wait(0.5)
         if grpc_srv is not None:
             grpc_srv.stop()
+        if ingress is not None:
+            ingress.stop()
         server.should_exit = True
         t.join(timeout=5)
     else:
@@ -150,6 +236,12 @@ def cmd_serve(a, role: str = "serve") -> int:
     gapp.stop()
     if page is not None:
         page.close(unlink=True)
+    if front:
+        if gapp.peers is not None:
+            gapp.peers.close(unlink=rank == 0)
+        for r in (ring, conv_ring):
+            if r is not None:
+                r.close(unlink=rank == 0)
     if gapp.fatal is not None:
         print(json.dumps({"event": "fatal", "error": str(gapp.fatal)}), flush=True)
         return 3
@@ -250,7 +342,13 @@ def main(argv=None) -> int:
         p.add_argument("--ring", default="", help="shared request ring name (api-gateway/queue-manager)")
         p.add_argument("--no-ring", action="store_true", help="api-gateway/queue-manager without the shared ring")
         p.add_argument("--native", action="store_true", help="api-gateway: C++ HTTP ingress for POST /messages")
-        p.add_argument("--ingress-threads", type=int, default=4)
+        p.add_argument("--ingress-threads", type=int, default=0,
+                       help="native ingress epoll threads (default: server.ingress_threads)")
+        p.add_argument("--front-door", default="", choices=["", "native", "python"],
+                       help="multi-GPU serve: C++ front door feeding a ring every rank drains (native, "
+                            "default) or every route on rank 0's ASGI server (python)")
+        p.add_argument("--cpu-ranks", action="store_true",
+                       help="serve: tiny CPU engines per rank over gloo (multi-rank rehearsal without a GPU)")
     p = sub.add_parser("scheduler")
     p.add_argument("--config", default=None)
     p.add_argument("--gateway", default="http://127.0.0.1:8080")

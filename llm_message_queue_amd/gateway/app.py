@@ -77,16 +77,22 @@ class GatewayApp:
                  simulate_ms: Sequence[float] = (5, 10, 20, 30), start: bool = True,
                  role: str = "serve", ring=None):
         """``role``: "serve" (monolith), "ingress" (HTTP + preprocess, pushes
-        into the shared request ring ``ring``), or "dispatcher" (pops the ring
+        into the shared request ring ``ring``), "dispatcher" (pops the ring
         into its queue and runs the backend; reports status via the event
-        ring).  See ``shm_bridge``."""
+        ring), or "rank" (one GPU rank of the multi-GPU front door: drains
+        ``ring`` -- the shared ring every rank pops -- plus ``extra_rings``
+        into its gateway inbox, so ingest and preprocessing spread over the
+        GPUs; status queries for its messages come through ``peers``).  See
+        ``shm_bridge`` and ``peers``."""
         import torch
-        if role not in ("serve", "ingress", "dispatcher"):
+        if role not in ("serve", "ingress", "dispatcher", "rank"):
             raise ValueError(f"unknown gateway role {role!r}")
         if role != "serve" and ring is None:
             raise ValueError(f"role {role!r} needs a shared ring")
         self.role = role
         self.ring = ring
+        self.extra_rings: List[object] = []       # role "rank": e.g. rank 0's conversation ring
+        self.peers = None                          # gateway.peers.PeerDirectory (multi-rank front door)
         self._ring_thread: Optional[threading.Thread] = None
         self._snap_thread: Optional[threading.Thread] = None
         self.telemetry = None
@@ -162,6 +168,9 @@ class GatewayApp:
         if self.role == "dispatcher":
             self._ring_thread = threading.Thread(target=self._ring_loop, name="ring-ingest", daemon=True)
             self._ring_thread.start()
+        elif self.role == "rank":
+            self._ring_thread = threading.Thread(target=self._rank_ring_loop, name="ring-ingest", daemon=True)
+            self._ring_thread.start()
         if self.engine is not None:
             self._loop_thread = threading.Thread(target=self._serve_loop, name="gateway-loop", daemon=True)
             self._loop_thread.start()
@@ -179,6 +188,8 @@ class GatewayApp:
             self.ring.wake_all()
         if self.telemetry is not None:
             self.telemetry.stop()
+        if self.peers is not None:
+            self.peers.stop()
         for t in (self._loop_thread, self._ring_thread, self._snap_thread):
             if t is not None:
                 t.join(timeout=10)
@@ -337,6 +348,116 @@ class GatewayApp:
                     self.messages.put(m)
                 self.ring.put_events(undecodable, error="undecodable request body")
             self._wake.set()
+
+    def _rank_ring_loop(self) -> None:
+        """Role "rank": pop raw requests from the shared ring (and this
+        rank's extra rings) into the gateway inbox.  Preprocessing runs in the
+        serve loop's ingest (one overlapped GPU batch per tick on THIS rank's
+        GPU), and queueing goes through the gateway, so conversation pins and
+        the per-tick planner see every message -- the same path bench.py
+        measures.  Messages with a conversation_id arrive on rank 0's ring
+        (the native front door routes them there): rank 0 owns conversation
+        state and records the turn like ``POST /api/v1/messages`` does."""
+        from .shm_bridge import TAG_RAW, decode_message, decode_raw
+        rings = [self.ring] + list(self.extra_rings)
+        k = 0
+        while not self._stop.is_set():
+            got = []
+            for i in range(len(rings)):
+                r = rings[(k + i) % len(rings)]
+                got.extend(r.get_records(self.cfg.preprocessor.max_batch, timeout_ms=0))
+            k += 1
+            if not got:                              # block briefly on one ring (short when several)
+                got = rings[k % len(rings)].get_records(self.cfg.preprocessor.max_batch,
+                                                        timeout_ms=20 if len(rings) == 1 else 2)
+                if not got:
+                    continue
+            now = time.time_ns()
+            msgs, undecodable = [], []
+            for tag, b in got:
+                try:
+                    m = decode_raw(b) if tag == TAG_RAW else decode_message(b)
+                except Exception as e:               # noqa: BLE001 -- accounted for below
+                    undecodable.append(self._undecodable(b, e))
+                    continue
+                if tag == TAG_RAW:
+                    m.created_at = m.updated_at = now
+                m.metadata["ingest_rank"] = self.gateway.rank
+                if m.conversation_id:
+                    self._record_turn(m)
+                msgs.append(m)
+                self.messages.put(m)
+            if undecodable:
+                self.factory.dead_letter_queue.push_many(undecodable, "undecodable request body", "ingress")
+                self.metrics.requests_rejected.labels("undecodable").inc(len(undecodable))
+                for m in undecodable:
+                    self.messages.put(m)
+            if msgs:
+                self._accepted += len(msgs)
+                self.gateway.submit(msgs)
+                self._wake.set()
+
+    def _record_turn(self, m: Message) -> None:
+        """Conversation bookkeeping of a submitted turn (``POST
+        /api/v1/messages`` with a conversation_id, `api/handlers.go:700`)."""
+        from ..conversation.state_manager import ConversationNotFound
+        cid = m.conversation_id
+        self.state.get_conversation(cid, m.user_id)
+        home = self.state.home_gpu(cid)
+        if home >= 0:
+            m.metadata.setdefault("home_gpu", home)
+        try:
+            self.state.add_message(cid, m)
+        except ConversationNotFound:
+            pass
+
+    # ------------------------------------------------------------------ cross-rank lookups
+    def peer_op(self, op: str, args: list):
+        """Answer a rank-0 query about messages this rank popped."""
+        if op == "get":
+            m = self.messages.get(str(args[0]))
+            return None if m is None else m.to_dict()
+        if op == "list":
+            user_id, conversation_id, status, limit = str(args[0]), str(args[1]), str(args[2]), int(args[3])
+            total, msgs = self.messages.query(user_id, conversation_id, status, limit, 0)
+            return [total, [m.to_dict() for m in msgs]]
+        if op == "set_status":
+            m = self.messages.get(str(args[0]))
+            if m is None:
+                return False
+            m.status = str(args[1])
+            m.updated_at = time.time_ns()
+            return True
+        if op == "remove":
+            m = self.messages.remove(str(args[0]))
+            if m is None:
+                return False
+            removed = bool(m.queue_name and self.standard.has_queue(m.queue_name)
+                           and self.standard.mlq.remove(m.queue_name, m))
+            return {"dequeued": removed}
+        raise ValueError(f"unknown op {op!r}")
+
+    def find_message(self, mid: str) -> Optional[dict]:
+        """A message by id from this process's store, else from the rank that
+        popped it (multi-GPU front door)."""
+        m = self.messages.get(mid)
+        if m is not None:
+            return m.to_dict()
+        if self.peers is not None:
+            return self.peers.first("get", [mid])
+        return None
+
+    def query_messages(self, user_id: str, conversation_id: str, status: str, limit: int,
+                       offset: int) -> Tuple[int, List[dict]]:
+        total, msgs = self.messages.query(user_id, conversation_id, status, limit + offset, 0)
+        out = [m.to_dict() for m in msgs]
+        if self.peers is not None:
+            for _r, res in sorted(self.peers.ask("list", [user_id, conversation_id, status,
+                                                          limit + offset]).items()):
+                if isinstance(res, list) and len(res) == 2:
+                    total += int(res[0])
+                    out.extend(res[1])
+        return total, out[offset:offset + limit]
 
     @staticmethod
     def _undecodable(b: bytes, err: BaseException) -> Message:

@@ -6,17 +6,27 @@ Other routes stay on the Python API server (``cli serve`` / ``api-gateway``).
 """
 from __future__ import annotations
 
+from typing import Optional, Tuple
+
 from .. import _native
 
 
 class NativeIngress:
     def __init__(self, port: int = 8080, ring: str = "default", threads: int = 4, host: str = "0.0.0.0",
-                 cfg=None):
+                 cfg=None, conv_ring: str = "", upstream: Optional[Tuple[str, int]] = None):
         """``cfg`` (optional): attach the config's guard (authentication, RBAC,
-        rate limits -- ``api/security.py``) and response envelope."""
+        rate limits -- ``api/security.py``) and response envelope.
+        ``conv_ring``: ring (name of a ``RingPair``) for messages that carry a
+        conversation_id -- drained by the process that owns conversation
+        state.  ``upstream``: (host, port) of the Python API server; every
+        other route is reverse-proxied to it (one public port)."""
         self.ring = ring
         self._k = _native.ingress().HttpIngress(int(port), f"llmq-{ring}-req", int(threads), host)
         self.port = int(port)
+        if conv_ring:
+            self._k.set_conv_ring(f"llmq-{conv_ring}-req")
+        if upstream is not None:
+            self._k.set_upstream(str(upstream[0]), int(upstream[1]))
         self.guard = None
         if cfg is not None:
             from ..api.security import guard_from_config

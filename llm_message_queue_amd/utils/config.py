@@ -38,6 +38,13 @@ class ServerConfig:
     # shared-memory request ring the two modes exchange messages through
     shared_ring: str = "default"
     shared_ring_bytes: int = 64 << 20
+    # multi-GPU `cli serve` (torchrun, one rank per GPU): "native" = the C++
+    # HTTP front door on rank 0 takes POST /api/v1/messages into a shared
+    # ring EVERY rank drains (ingest + preprocess spread over the GPUs) and
+    # reverse-proxies the other routes to rank 0's API server; "python" =
+    # every route on rank 0's ASGI server (the round-2 topology)
+    front_door: str = "native"
+    ingress_threads: int = 4
     # wrap JSON bodies in {"code","message","data","timestamp"} (docs/api.md:12-20);
     # off by default: the reference's handlers return bare objects
     response_envelope: bool = False
@@ -458,6 +465,8 @@ def validate(cfg: Config) -> Config:
         seen.add(lv.priority)
     if cfg.gpu.slots_per_gpu <= 0:
         raise ConfigError("gpu.slots_per_gpu must be > 0")
+    if cfg.server.front_door not in ("native", "python"):
+        raise ConfigError("server.front_door must be native or python")
     auth = cfg.security.authentication
     if auth.method not in ("none", "api_key", "jwt"):
         raise ConfigError("security.authentication.method must be none, api_key or jwt")
