@@ -97,15 +97,15 @@ def _wait_up(url, timeout=120.0):
     return False
 
 
-def _bench_config_file() -> str:
+def _bench_config_file(slots: int = 1536) -> str:
     """configs/config.yaml plus the serving settings bench.py measures."""
     import yaml
     with open(os.path.join(ROOT, "configs", "config.yaml")) as fh:
         c = yaml.safe_load(fh)
     for lv, ms in zip(sorted(c["queue"]["levels"], key=lambda x: x["priority"]), (50, 100, 150, 200)):
-        lv["max_concurrent"] = 1536
+        lv["max_concurrent"] = slots * 8
         lv["max_wait_time"] = f"{ms}ms"
-    c.setdefault("gpu", {})["slots_per_gpu"] = 1536
+    c.setdefault("gpu", {})["slots_per_gpu"] = slots
     c.setdefault("backend", {}).update({"token_budget": 4096, "max_ctx": 512, "prompt_tokens": 32, "gen_tokens": 4})
     c.setdefault("logging", {})["level"] = "warning"
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"llmq_bench_config_{os.getpid()}.yaml")
@@ -117,7 +117,11 @@ def _bench_config_file() -> str:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--url", default="")
-    ap.add_argument("--spawn", choices=["", "serve", "split", "native"], default="")
+    ap.add_argument("--spawn", choices=["", "serve", "split", "native", "multirank"], default="",
+                    help="multirank: torch.distributed.run --nproc-per-node RANKS cli serve (C++ front door on "
+                         "rank 0, every rank drains the shared ring; --gpu: ranks wrap onto the visible GPUs)")
+    ap.add_argument("--ranks", type=int, default=2, help="multirank: serving ranks")
+    ap.add_argument("--slots", type=int, default=1536, help="--bench-config: batch slots per rank")
     ap.add_argument("--threads", type=int, default=4, help="native ingress threads")
     ap.add_argument("--ingress", type=int, default=2, help="api-gateway processes (split)")
     ap.add_argument("--gpu", action="store_true", help="spawned server uses the GPU")
@@ -145,7 +149,7 @@ def main() -> None:
     gpu = [] if a.gpu else ["--no-gpu"]
     cfg_args = []
     if a.bench_config:
-        cfg_args = ["--config", _bench_config_file()]
+        cfg_args = ["--config", _bench_config_file(a.slots)]
     try:
         if a.spawn == "serve":
             port = _port()
@@ -184,6 +188,17 @@ def main() -> None:
                                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                           start_new_session=True))
             urls = [f"http://127.0.0.1:{port}"]
+        elif a.spawn == "multirank":
+            port = _port()
+            procs.append(subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                                           f"--nproc-per-node={a.ranks}", "--master-addr=127.0.0.1",
+                                           f"--master-port={_port()}", "-m", "llm_message_queue_amd.cli", "serve",
+                                           "--port", str(port), "--host", "127.0.0.1", "--ingress-threads",
+                                           str(a.threads)] + ([] if a.gpu else ["--cpu-ranks"]) + cfg_args,
+                                          cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                          start_new_session=True))
+            urls = [f"http://127.0.0.1:{port}"]
+            api_url = urls[0]                    # every other route is proxied by the front door
         else:
             urls = [a.url or "http://127.0.0.1:8080"]
         for u in urls + ([api_url] if api_url else []):
@@ -230,6 +245,10 @@ def main() -> None:
                 time.sleep(2.0)
                 with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
                     st = json.loads(rr.read())
+                if "job" in st:                  # multi-rank: every rank's counters and histograms
+                    st, st_end = st["job"], st_end["job"]
+                    out["ranks"] = st.get("ranks")
+                    out["accepted_by_rank"] = st.get("accepted_by_rank")
                 out["dispatcher"] = {"dispatch": st.get("dispatch"), "latency": st_end.get("latency"),
                                      "latency_e2e": st_end.get("latency_e2e"),
                                      "note": "latency: HTTP arrival (native ingress clock) -> GPU slot admission; "

@@ -568,7 +568,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
     def reset_stats():
         """Open a new latency window (arrival->dispatch and ->completion
         histograms); counters are cumulative and stay."""
-        gw_app.reset_latency()
+        gw_app.reset_latency_all()                  # (every GPU rank behind the front door)
         return {"status": "reset"}
 
     @app.get("/api/v1/admin/dead-letter")

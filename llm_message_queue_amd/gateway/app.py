@@ -435,7 +435,42 @@ class GatewayApp:
             removed = bool(m.queue_name and self.standard.has_queue(m.queue_name)
                            and self.standard.mlq.remove(m.queue_name, m))
             return {"dequeued": removed}
+        if op == "stats":
+            return self._rank_stats()
+        if op == "reset_latency":
+            self.reset_latency()
+            return True
         raise ValueError(f"unknown op {op!r}")
+
+    def _rank_stats(self) -> dict:
+        gw = self.gateway
+        gw.flush_latency()
+        return {"rank": gw.rank, "counters": dict(gw.counters), "accepted": self._accepted,
+                "arr": gw.rec.arr.tolist(), "enq": gw.rec.enq.tolist(), "done": gw.rec_done.arr.tolist()}
+
+    def job_stats(self) -> dict:
+        """Dispatch counters and latency summed over every rank of the job
+        (multi-GPU front door): this rank's plus each peer's answer."""
+        from .router import LatencyRecorder
+        parts = [self._rank_stats()]
+        if self.peers is not None:
+            parts += [r for _k, r in sorted(self.peers.ask("stats", []).items()) if isinstance(r, dict)]
+        cnt: Dict[str, int] = {}
+        for p in parts:
+            for k, v in p["counters"].items():
+                cnt[k] = cnt.get(k, 0) + int(v)
+        arr = sum(np.asarray(p["arr"], dtype=np.int64) for p in parts)
+        enq = sum(np.asarray(p["enq"], dtype=np.int64) for p in parts)
+        done = sum(np.asarray(p["done"], dtype=np.int64) for p in parts)
+        rec = LatencyRecorder(len(self.gateway.tiers))
+        return {"ranks": sorted(int(p["rank"]) for p in parts), "dispatch": cnt,
+                "accepted_by_rank": {int(p["rank"]): int(p["accepted"]) for p in parts},
+                "latency": rec.summary(arr, enq), "latency_e2e": rec.summary(done, done)}
+
+    def reset_latency_all(self) -> None:
+        self.reset_latency()
+        if self.peers is not None:
+            self.peers.ask("reset_latency", [])
 
     def find_message(self, mid: str) -> Optional[dict]:
         """A message by id from this process's store, else from the rank that
@@ -585,4 +620,6 @@ class GatewayApp:
         if self.ring is not None:
             out["rings"] = self.ring.stats()
         out["delayed"] = self.factory.delayed_queue.size()
+        if self.peers is not None:
+            out["job"] = self.job_stats()         # every GPU rank of the multi-GPU front door
         return out

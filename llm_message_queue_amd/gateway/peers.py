@@ -22,7 +22,7 @@ import msgpack
 
 from .. import _native
 
-OPS = ("get", "list", "set_status", "remove")
+OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency")
 
 
 class PeerDirectory:
