@@ -121,6 +121,7 @@ def main() -> None:
                     help="multirank: torch.distributed.run --nproc-per-node RANKS cli serve (C++ front door on "
                          "rank 0, every rank drains the shared ring; --gpu: ranks wrap onto the visible GPUs)")
     ap.add_argument("--ranks", type=int, default=2, help="multirank: serving ranks")
+    ap.add_argument("--server-log", default="", help="file for the spawned server's stdout+stderr")
     ap.add_argument("--slots", type=int, default=1536, help="--bench-config: batch slots per rank")
     ap.add_argument("--threads", type=int, default=4, help="native ingress threads")
     ap.add_argument("--ingress", type=int, default=2, help="api-gateway processes (split)")
@@ -142,6 +143,7 @@ def main() -> None:
                          "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
     a = ap.parse_args()
     procs, urls = [], []
+    slog = open(a.server_log, "w") if a.server_log else subprocess.DEVNULL
     api_url = ""
     env = dict(os.environ, PYTHONUNBUFFERED="1", LLMQ_LOGGING__LEVEL="warning",
                LLMQ_QUEUE__WORKER__MAX_CONCURRENT="512", LLMQ_QUEUE__WORKER__MAX_BATCH_SIZE="256",
@@ -195,7 +197,7 @@ def main() -> None:
                                            f"--master-port={_port()}", "-m", "llm_message_queue_amd.cli", "serve",
                                            "--port", str(port), "--host", "127.0.0.1", "--ingress-threads",
                                            str(a.threads)] + ([] if a.gpu else ["--cpu-ranks"]) + cfg_args,
-                                          cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                          cwd=ROOT, env=env, stdout=slog, stderr=subprocess.STDOUT,
                                           start_new_session=True))
             urls = [f"http://127.0.0.1:{port}"]
             api_url = urls[0]                    # every other route is proxied by the front door

@@ -100,6 +100,8 @@ class GatewayApp:
         self.fatal: Optional[BaseException] = None     # PeerLost from the serve loop
         self.cfg = cfg
         self.log = get_logger("app")
+        self._bound = threading.local()
+        self._main_device = torch.cuda.current_device() if torch.cuda.is_available() else None
         self.metrics: QueueMetrics = default_metrics()
         gpu = torch.cuda.is_available() if use_gpu is None else use_gpu
         self.gpu = gpu
@@ -201,8 +203,28 @@ class GatewayApp:
         self.resources.stop()
         self.lb.stop()
 
+    # ------------------------------------------------------------------ threads
+    def _bind_device(self) -> None:
+        """Make this thread's current HIP device the backend's GPU.  The
+        current device (and with it ``torch.cuda.Event()`` / current-stream
+        defaults) is per THREAD: a serve-loop thread of rank 3 would
+        otherwise record its step events on device 0's stream."""
+        if self._bound.__dict__.get("ok"):
+            return
+        self._bound.ok = True
+        dev = getattr(self.engine, "device", None) if self.engine is not None else None
+        if dev is not None and getattr(dev, "type", "") == "cuda":
+            import torch
+            torch.cuda.set_device(dev)
+        elif self.gpu:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.set_device(torch.cuda.current_device() if self._main_device is None
+                                      else self._main_device)
+
     # ------------------------------------------------------------------ ingest
     def _flush(self, msgs: Sequence[Message]) -> List[Optional[QueueError]]:
+        self._bind_device()
         self.preprocessor.process_batch(msgs, use_gpu=self.preprocessor.gpu_enabled(),
                                         prompt_cap=self.gateway.prompt_cap)
         for m in msgs:
@@ -301,6 +323,7 @@ class GatewayApp:
         from a Python ingress are already preprocessed; RAW records from the
         native HTTP ingress are preprocessed here in one batch per drain."""
         from .shm_bridge import TAG_RAW, decode_message, decode_raw
+        self._bind_device()
         while not self._stop.is_set():
             recs = self.ring.get_records(self.cfg.preprocessor.max_batch, timeout_ms=100)
             if not recs:
@@ -543,6 +566,7 @@ class GatewayApp:
         import gc
         from ..parallel.comm import PeerLost
         gw = self.gateway
+        self._bind_device()
         if self.cfg.server.gc_freeze_interval > 0:
             gc.collect()
             gc.freeze()

@@ -262,8 +262,11 @@ class TextPipeline:
     def _ensure_weights(self) -> ClassifierWeights:
         if self.weights is None:
             c = self.cfg
-            self.weights = ClassifierWeights(c.vocab_buckets, c.embed_dim, c.hidden_dim, c.seed,
-                                             device=self.device)
+            # initialised on the preprocess stream (ordered before the kernels
+            # that read them; see _workspace for the allocator's stream pools)
+            with self.torch.cuda.stream(self.stream):
+                self.weights = ClassifierWeights(c.vocab_buckets, c.embed_dim, c.hidden_dim, c.seed,
+                                                 device=self.device)
         return self.weights
 
     def _patterns(self, patterns, version) -> PackedPatterns:
@@ -346,7 +349,21 @@ class TextPipeline:
             n = max(B, 2 * ws["B"] if ws else 0, 256)
             h = max(H, ws["H"] if ws else 0)
             dev = self.device
-            ws = self._ws = {
+            # allocated in the PREPROCESS stream's pool: the kernels that use
+            # these buffers run there.  A block from the compute stream's pool
+            # may have been freed by a forward that is still running on the
+            # GPU (the caching allocator orders reuse on the allocating stream
+            # only), and preprocess kernels writing into it corrupted that
+            # forward's activations (token ids -> out-of-range embedding gather,
+            # seen under a 5k req/s multi-rank HTTP load whose growing batches
+            # re-grew this workspace mid-serving)
+            with torch.cuda.stream(self.stream):
+                ws = self._ws = self._alloc_ws(n, h, dev)
+        return ws
+
+    def _alloc_ws(self, n: int, h: int, dev):
+        torch = self.torch
+        return {
                 "B": n, "H": h,
                 "stats": torch.empty((n, STAT_COLS), dtype=torch.int32, device=dev),
                 "hashes": torch.empty((n, self.L), dtype=torch.int32, device=dev),
@@ -355,7 +372,6 @@ class TextPipeline:
                 "logits": torch.empty((n, 8), dtype=torch.float32, device=dev),
                 "pred": torch.empty(n, dtype=torch.int32, device=dev),
             }
-        return ws
 
     def _launch_one_call(self, t0, B, pk, lens, ob, total, classify, prompt_cap, stream, contents):
         """The serve loop's path: the whole chain is one native call
@@ -401,8 +417,9 @@ class TextPipeline:
         pnp[ob:ob + offsets.nbytes] = offsets.view(np.uint8)
         total = ob + offsets.nbytes
         if self._dev_bytes.numel() < total:
-            self._dev_bytes = torch.empty(max(total, 2 * self._dev_bytes.numel()), dtype=torch.uint8,
-                                          device=self.device)
+            with torch.cuda.stream(self.stream):          # (the preprocess stream's pool, see _workspace)
+                self._dev_bytes = torch.empty(max(total, 2 * self._dev_bytes.numel()), dtype=torch.uint8,
+                                              device=self.device)
         dev = self._dev_bytes
         # H2D with a copy kernel reading host-mapped pinned memory: the
         # runtime's async H2D path was measured to wait for the backend's
