@@ -24,6 +24,19 @@ def _post(port, body, raw=False):
         return e.code, json.loads(e.read())
 
 
+def test_lone_surrogate_in_another_field_does_not_poison_the_id():
+    """a lone-surrogate escape in content must not make a
+    later valid id fail (the flag was never reset); Python accepts this body."""
+    scan = _native.ingress().scan_message
+    r = scan(b'{"content":"bad \\ud800 escape","id":"abc-123","user_id":"u1"}')
+    assert r[0] and r[1] == "abc-123" and r[3] == "u1", r
+    assert not scan(b'{"id":"a\\ud800b"}')[0]          # the id itself still must be printable ASCII
+    # conversation_id presence (front door routing to the conversation owner's ring)
+    assert scan(b'{"content":"x","conversation_id":"c-1"}')[5]
+    for v in (b'null', b'""', b'0', b'false'):
+        assert not scan(b'{"content":"x","conversation_id":' + v + b'}')[5], v
+
+
 def test_json_scanner():
     scan = _native.ingress().scan_message
     assert scan(b'{"content":"hi","priority":"urgent","id":"abc"}')[:4] == (True, "abc", 2, "")

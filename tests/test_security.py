@@ -68,6 +68,28 @@ def test_specific_limits_checked_before_the_global_bucket():
     assert g.check("POST", "/api/v1/messages", ip="8.8.8.8", now_ns=t)[0] == 0
 
 
+def test_refused_request_drains_no_bucket():
+    """a request the per-user or the global limit refuses
+    keeps the caller's per-IP token (refunded), so a client held back by a
+    shared limit does not also lose its own address budget."""
+    g = _guard(method="api_key", api_keys=["k-a:alice:user"], ip_rps=0.001, ip_burst=2.0, user_rps=0.001,
+               user_burst=1.0, global_rps=0.001, global_burst=100.0)
+    t = 9_000_000_000
+    assert g.check("POST", "/api/v1/messages", ip="9.9.9.9", api_key="k-a", now_ns=t)[0] == 0
+    for _ in range(5):                                    # alice's user bucket is empty now
+        code, *_, reason, _ = g.check("POST", "/api/v1/messages", ip="9.9.9.9", api_key="k-a", now_ns=t)
+        assert code == 429 and "per_user" in reason
+    # the address still has its second token (refunded each time)
+    g2 = _guard(ip_rps=0.001, ip_burst=2.0, global_rps=0.001, global_burst=1.0)
+    assert g2.check("POST", "/api/v1/messages", ip="1.2.3.4", now_ns=t)[0] == 0     # takes the 1 global token
+    for _ in range(3):
+        code, *_, reason, _ = g2.check("POST", "/api/v1/messages", ip="1.2.3.4", now_ns=t)
+        assert code == 429 and "global" in reason
+    # global refill: one token after 1000 s; 1.2.3.4's per-IP bucket kept its second token
+    code, *_, reason, _ = g2.check("POST", "/api/v1/messages", ip="1.2.3.4", now_ns=t + 1_000_000_000_000)
+    assert code == 0, reason
+
+
 def test_api_key_auth_and_rbac():
     g = _guard(method="api_key", api_keys=["k-user", "k-ro:rita:readonly", "k-adm:ada:admin"], rbac=True,
                roles={"admin": ["*"], "user": ["message:*", "conversation:read"], "readonly": ["message:read"]})
