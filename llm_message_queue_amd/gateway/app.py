@@ -382,19 +382,24 @@ class GatewayApp:
         (the native front door routes them there): rank 0 owns conversation
         state and records the turn like ``POST /api/v1/messages`` does."""
         from .shm_bridge import TAG_RAW, decode_message, decode_raw
-        rings = [self.ring] + list(self.extra_rings)
-        k = 0
+        gw = self.gateway
+        # backpressure: a rank pops the shared ring only while its own backlog
+        # (inbox + queue) is below about one batch of its slots, so the ring's
+        # traffic spreads over the ranks by what each can absorb instead of
+        # going to whichever thread the futex wakes first
+        high = max(256, int(getattr(self.engine, "slots", 0) or self.cfg.gpu.slots_per_gpu))
+        mb = self.cfg.preprocessor.max_batch
         while not self._stop.is_set():
             got = []
-            for i in range(len(rings)):
-                r = rings[(k + i) % len(rings)]
-                got.extend(r.get_records(self.cfg.preprocessor.max_batch, timeout_ms=0))
-            k += 1
-            if not got:                              # block briefly on one ring (short when several)
-                got = rings[k % len(rings)].get_records(self.cfg.preprocessor.max_batch,
-                                                        timeout_ms=20 if len(rings) == 1 else 2)
-                if not got:
-                    continue
+            for r in self.extra_rings:               # rank 0's conversation ring: never held back
+                got.extend(r.get_records(mb, timeout_ms=0))
+            if gw.inbox_size() + gw.pending() < high:
+                got.extend(self.ring.get_records(mb, timeout_ms=0 if got else (5 if self.extra_rings else 20)))
+            elif not got:
+                time.sleep(0.001)
+                continue
+            if not got:
+                continue
             now = time.time_ns()
             msgs, undecodable = [], []
             for tag, b in got:
