@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--tokens", default="37,1024,2048,4041,4096")
     ap.add_argument("--plain", action="store_true", help="also time the plain GEMM shapes")
+    ap.add_argument("--resid", action="store_true", help="A/B the o / down residual GEMM variants")
     ap.add_argument("--rope", action="store_true", help="also A/B the qkv GEMM with the RoPE/KV epilogue")
     ap.add_argument("--head", action="store_true", help="also A/B the LM head: hipBLASLt + argmax vs argmax epilogue")
     ap.add_argument("--groups", default="", help="e.g. 4,8,16: also time gemm_swiglu per block-order group size")
@@ -163,6 +164,31 @@ def main():
                               "speedup": round(med["hipblaslt+argmax"] / med["fused"], 3),
                               "tflops_fused": round(2 * M * V * d / med["fused"] / 1e9, 1),
                               "token_agreement": round(agree, 4)}), flush=True)
+
+    if a.resid:
+        # o / down into the residual stream: hipBLASLt beta = 1 vs the
+        # hand-written residual epilogue and its L2-prefetch variants
+        shapes = {"o": (d, d), "down": (d, ffn)}
+        for name, (N, K) in shapes.items():
+            w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+            for T in (4041, 4096):
+                x = torch.randn(T, K, device=dev).to(torch.bfloat16)
+                y = torch.randn(T, N, device=dev).to(torch.bfloat16)
+                fns = {"hipblaslt_resid": lambda: y.addmm_(x, w.t()),
+                       "hip_resid": lambda: G.gemm_residual(x, w, y, epi=G.EPI_RESID),
+                       "hip_resid_pf5": lambda: G.gemm_residual(x, w, y, epi=G.EPI_RESID_PF5),
+                       "hip_resid_pf1": lambda: G.gemm_residual(x, w, y, epi=G.EPI_RESID_PF1)}
+                for f in fns.values():
+                    f()
+                res = {k: [] for k in fns}
+                for _ in range(a.rounds):
+                    for k, f in fns.items():
+                        res[k].append(timeit(f, a.iters))
+                med = {k: statistics.median(v) for k, v in res.items()}
+                flop = 2.0 * T * N * K
+                print(json.dumps({"bench": "resid", "gemm": name, "T": T,
+                                  **{k + "_ms": round(v, 4) for k, v in med.items()},
+                                  **{k + "_tflops": round(flop / v / 1e9, 1) for k, v in med.items()}}), flush=True)
 
     if a.plain:
         shapes = {"qkv": (6144, d), "o": (d, d), "gate_up": (2 * ffn, d), "down": (d, ffn)}
