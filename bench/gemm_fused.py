@@ -167,7 +167,7 @@ def main():
 
     if a.resid:
         # o / down into the residual stream: hipBLASLt beta = 1 vs the
-        # hand-written residual epilogue and its L2-prefetch variants
+        # hand-written residual epilogue
         shapes = {"o": (d, d), "down": (d, ffn)}
         for name, (N, K) in shapes.items():
             w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
@@ -175,9 +175,7 @@ def main():
                 x = torch.randn(T, K, device=dev).to(torch.bfloat16)
                 y = torch.randn(T, N, device=dev).to(torch.bfloat16)
                 fns = {"hipblaslt_resid": lambda: y.addmm_(x, w.t()),
-                       "hip_resid": lambda: G.gemm_residual(x, w, y, epi=G.EPI_RESID),
-                       "hip_resid_pf5": lambda: G.gemm_residual(x, w, y, epi=G.EPI_RESID_PF5),
-                       "hip_resid_pf1": lambda: G.gemm_residual(x, w, y, epi=G.EPI_RESID_PF1)}
+                       "hip_resid": lambda: G.gemm_residual(x, w, y)}
                 for f in fns.values():
                     f()
                 res = {k: [] for k in fns}

@@ -57,19 +57,7 @@ constexpr int GM_BUF_BYTES = 4 * GM_HALF_BYTES;    // A0 A1 B0 B1
 constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
 constexpr int GM_GROUP_M = 8;                    // default M-tiles per block-order group
 
-enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4, GM_EPI_RESID = 5,
-       GM_EPI_RESID_PF5 = 6, GM_EPI_RESID_PF1 = 7 };
-
-// GM_EPI_RESID_PF5 / _PF1: the residual epilogue with the C tile pulled into
-// L2 during the K-loop drain -- one 4-B buffer load per 128-B line of the
-// wave's 128 x 64 residual block (2 per lane), issued after the last staging
-// load (PF1: drain phase 1, 8 MFMA phases before the epilogue; the drain's
-// counted vmcnt waits are raised by those 2 loads) or after the drain's
-// vmcnt(0) (PF5: 4 phases before).  The epilogue's residual reads then hit
-// L2 instead of waiting one HBM round trip with the whole chip reading at once.
-__device__ __forceinline__ constexpr bool gm_resid(int e) {
-  return e == GM_EPI_RESID || e == GM_EPI_RESID_PF5 || e == GM_EPI_RESID_PF1;
-}
+enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4, GM_EPI_RESID = 5 };
 
 // GM_EPI_ARGMAX: the LM head's greedy sampling as the epilogue -- no [M][N]
 // logits tensor.  Each tile writes, per row, the max over its 256 columns and
@@ -233,22 +221,6 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
 #pragma unroll
         for (int d = 0; d < 2; ++d) acc[a][b][c][d] = gm_f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // residual L2 prefetch (GM_EPI_RESID_PF*): lines of rows row0 + lane and
-  // row0 + 64 + lane of this wave's 64 output columns
-  uint32_t pf0 = 0, pf1 = 0;
-  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, M * N * 2, 0x00020000);
-  uint32_t pfo0 = 0, pfo1 = 0;
-  if constexpr (EPI == GM_EPI_RESID_PF5 || EPI == GM_EPI_RESID_PF1) {
-    const uint32_t colb = (uint32_t)(tn * GM_BN + wc * 64) * 2u;
-    pfo0 = (uint32_t)(tm * GM_BM + wr * 128 + lane) * (uint32_t)N * 2u + colb;
-    pfo1 = pfo0 + 64u * (uint32_t)N * 2u;
-  }
-#define GM_RES_PREFETCH()                                                \
-  do {                                                                   \
-    pf0 = __builtin_amdgcn_raw_buffer_load_b32(rsc, pfo0, 0, 0);         \
-    pf1 = __builtin_amdgcn_raw_buffer_load_b32(rsc, pfo1, 0, 0);         \
-  } while (0)
-
   gm_bf16x8 af[4][2];                              // one m-half: [m][kk]
   gm_bf16x8 bfr[2][2][2];                          // both n-halves: [nh][n][kk]
   gm_bf16x8 b0y[2][2];                             // SCHED >= 1: buffer-1 B0 fragments
@@ -363,18 +335,10 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
       }
     }
     {                                              // last two K-tiles: drain
-      if constexpr (EPI == GM_EPI_RESID_PF1) {
-        GM_READ_A(0, 0); GM_STAGE(1, GM_A1, t + 1); GM_RES_PREFETCH(); GM_VMCNT(8); GM_PHASE_END(0, 0, bfr[0]);
-        GM_READ_B(0, 1); GM_VMCNT(6); GM_PHASE_END(0, 1, bfr[1]);
-        GM_READ_A(0, 1); GM_VMCNT(4); GM_PHASE_END(1, 1, bfr[1]);
-        GM_READ_B0_INTO(1, b0y); GM_VMCNT(2); GM_PHASE_END(1, 0, bfr[0]);
-      } else {
         GM_READ_A(0, 0); GM_STAGE(1, GM_A1, t + 1); GM_VMCNT(6); GM_PHASE_END(0, 0, bfr[0]);
         GM_READ_B(0, 1); GM_VMCNT(4); GM_PHASE_END(0, 1, bfr[1]);
         GM_READ_A(0, 1); GM_VMCNT(2); GM_PHASE_END(1, 1, bfr[1]);
         GM_READ_B0_INTO(1, b0y); GM_VMCNT(0); GM_PHASE_END(1, 0, bfr[0]);
-        if constexpr (EPI == GM_EPI_RESID_PF5) GM_RES_PREFETCH();
-      }
         GM_READ_A(1, 0); GM_PHASE_END(0, 0, b0y);
         GM_READ_B(1, 1); GM_PHASE_END(0, 1, bfr[1]);
         GM_READ_A(1, 1); GM_PHASE_END(1, 1, bfr[1]);
@@ -582,7 +546,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         am.pi[(int64_t)grow * tiles_n + tn] = tn * GM_BN + c;
       }
     }
-  } else if (gm_resid(EPI)) {
+  } else if (EPI == GM_EPI_RESID) {
     // fp32 through LDS in four passes of 32 rows (8.5 KiB per wave, row
     // stride 68 floats: the four fq row groups of a write land on distinct
     // banks), then coalesced: 16 B of fp32 + 8 B of the bf16 residual per
@@ -637,10 +601,6 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         GM_LGKM(0);
         __builtin_amdgcn_wave_barrier();
       }
-    if constexpr (EPI == GM_EPI_RESID_PF5 || EPI == GM_EPI_RESID_PF1) {
-      // the prefetch registers stay live until here (never true: M > 0)
-      if ((pf0 & pf1) == 0xFFFFFFFFu && M < 0) C[0] = 0;
-    }
   } else if (EPI == GM_EPI_SWIGLU) {
     // wave w: 128 rows x 32 features bf16 = 8 KiB at w * 8 KiB
     uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 8192);
@@ -814,6 +774,5 @@ __global__ __launch_bounds__(256) void gemm_argmax_reduce_kernel(const float* __
 #undef GM_VMCNT
 #undef GM_BARRIER
 #undef GM_FENCE
-#undef GM_RES_PREFETCH
 
 }  // namespace llmq

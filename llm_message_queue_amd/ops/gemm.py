@@ -24,10 +24,6 @@ from .. import _native
 EPI_STORE = 0
 EPI_SWIGLU = 2
 EPI_RESID = 5
-EPI_RESID_PF5 = 6      # + the residual tile pulled into L2 during the K-loop drain (4 phases ahead)
-EPI_RESID_PF1 = 7      # ... 8 phases ahead
-RESID_EPIS = (EPI_RESID, EPI_RESID_PF5, EPI_RESID_PF1)
-RESID_EPI = EPI_RESID  # the variant gemm_residual runs by default
 TILE_N = 256
 SWIGLU_HALF = 32   # per-wave gate/up split (a wave owns 64 output columns)
 
@@ -137,20 +133,20 @@ def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None,
     return _launch(x, w_perm, y, EPI_SWIGLU, row_scale=row_scale)
 
 
-def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor, epi: int = None) -> torch.Tensor:
+def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
     """``res += x · wᵀ`` in place (bf16 ``res`` [M][N]; the fp32 sum is
     rounded once, as hipBLASLt's beta = 1 epilogue) -- the o / down
-    projections accumulating into the residual stream.  ``epi``: one of
-    ``RESID_EPIS`` (default ``RESID_EPI``)."""
+    projections accumulating into the residual stream.  Pulling the residual
+    tile into L2 during the K-loop drain (4 or 8 MFMA phases ahead of the
+    epilogue) was measured at +0.0-0.1 % (no gain: the epilogue is not
+    waiting on the read; profiles/r3_gemm_resid_prefetch_ab.jsonl), so the
+    plain epilogue stays."""
     _check(x, "x")
     _check(w, "w")
     _check(res, "res")
     if res.shape != (x.shape[0], w.shape[0]):
         raise ValueError("gemm_residual: res shape mismatch")
-    epi = RESID_EPI if epi is None else int(epi)
-    if epi not in RESID_EPIS:
-        raise ValueError(f"gemm_residual: unknown epilogue {epi}")
-    return _launch(x, w, res, epi)
+    return _launch(x, w, res, EPI_RESID)
 
 
 def residual_tiles_ok(M: int, N: int, cus: int, min_fill: float = 0.97) -> bool:
