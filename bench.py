@@ -50,6 +50,9 @@ def parse(argv=None):
     ap.add_argument("--slots", type=int, default=1536)
     ap.add_argument("--max-ctx", type=int, default=512)
     ap.add_argument("--token-budget", type=int, default=4096)
+    ap.add_argument("--token-budget-by-rank", default="",
+                    help="lock-step experiments: per-rank token budget overrides, e.g. '1:2048' (rank 1 takes "
+                         "half-size steps)")
     ap.add_argument("--gen-tokens", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=2, help="forward steps queued ahead on the GPU")
     ap.add_argument("--aging-ms", default="50,100,150,200",
@@ -262,8 +265,13 @@ def main(argv=None) -> int:
         lv.max_wait_time = int(ms * 1e6)
     job = os.environ.get("TORCHELASTIC_RUN_ID", str(os.getpid() if world == 1 else "bench"))
     page = SlotPage(f"bench{job}", rank)
+    budget = a.token_budget
+    for item in filter(None, a.token_budget_by_rank.split(",")):
+        r_, b_ = item.split(":")
+        if int(r_) == rank:
+            budget = int(b_)
     engine = BackendEngine(LlamaConfig.by_name(a.model), slots=a.slots, max_ctx=a.max_ctx,
-                           token_budget=a.token_budget, device=dev, impl="ref" if dry else "hip", seed=1000 + rank,
+                           token_budget=budget, device=dev, impl="ref" if dry else "hip", seed=1000 + rank,
                            page=page, gpu_index=rank, max_inflight=a.inflight,
                            residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv,
                            fused_mlp=False if a.no_fused_mlp else None,
@@ -318,6 +326,7 @@ def main(argv=None) -> int:
     n_sat = warm - w0
     host_sat = dict(gw.host_profile(), engine_build=round(float(engine.host_ns[0] - sat_eng0[0]) / n_sat / 1e6, 3),
                     engine_sync=round(float(engine.host_ns[1] - sat_eng0[1]) / n_sat / 1e6, 3),
+                    engine_enqueue=round(float(engine.host_ns[2] - sat_eng0[2]) / n_sat / 1e6, 3),
                     tick_ms=round((t_c1 - t_c0) * 1e3 / n_sat, 3),
                     tokens_per_tick=round((engine.total_tokens - tok0) / n_sat, 1))
     tok_rate = (engine.total_tokens - tok0) / max(1e-9, t_c1 - t_c0)
@@ -430,6 +439,8 @@ def main(argv=None) -> int:
     gw.quiesce(pump)
     sync_all()
     t1 = time.perf_counter()
+    eng_host1 = engine.host_ns.copy()          # (the untimed drain below must not count)
+    host_timed = gw.host_profile()
     engine.time_steps = False
     arrived_local = gw.counters["submitted"] - sub0
     remote_local = gw.counters["remote_sent"] - r0
@@ -492,6 +503,7 @@ def main(argv=None) -> int:
         "config": {"model": f"{a.model}-stub (32L, random bf16)" if a.model == "llama3-8b" else a.model,
                    "global_batch": a.slots * world, "seq_len": a.max_ctx,
                    "parallelism": f"dp{world}", "ingress": a.ingress, "placement": a.lb,
+                   "token_budget_by_rank": a.token_budget_by_rank or None,
                    "control_plane": comm_kind, "token_budget": a.token_budget,
                    "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap, "inflight": a.inflight,
                    "aging_ms": a.aging_ms, "util": a.util,
@@ -532,9 +544,10 @@ def main(argv=None) -> int:
         "backend_tokens_per_s": round(tokens / elapsed, 1) if elapsed > 0 else 0.0,
         "dispatched": dispatched,
         "host_ms_per_tick_saturated": host_sat,
-        "host_ms_per_tick": dict(gw.host_profile(), engine_build=round(
-            float(engine.host_ns[0] - eng_host0[0]) / max(1, a.steps) / 1e6, 3), engine_sync=round(
-            float(engine.host_ns[1] - eng_host0[1]) / max(1, a.steps) / 1e6, 3)),
+        "host_ms_per_tick": dict(host_timed, engine_build=round(
+            float(eng_host1[0] - eng_host0[0]) / max(1, a.steps) / 1e6, 3), engine_sync=round(
+            float(eng_host1[1] - eng_host0[1]) / max(1, a.steps) / 1e6, 3), engine_enqueue=round(
+            float(eng_host1[2] - eng_host0[2]) / max(1, a.steps) / 1e6, 3)),
     }
     if a.gateway_only_s > 0:
         # Secondary, untimed-by-contract measurement: the gateway path alone

@@ -144,7 +144,7 @@ class BackendEngine:
         self._q: Deque[_Inflight] = collections.deque()
         self._reaped: List[_Inflight] = []               # reaped by launch(), not yet returned
         self._fence: List[object] = []                   # events of steps dropped by abort_all
-        self.host_ns = np.zeros(2, dtype=np.int64)       # [batch build, wait for GPU] host time
+        self.host_ns = np.zeros(3, dtype=np.int64)       # [batch build, wait for GPU, enqueue forward] host time
         self._prev_out = None                            # device int32 [n_samples] of the last launched step
         # double-buffered pinned staging (a buffer is reused only after the
         # step that read it has finished: <= 2 steps in flight)
@@ -561,7 +561,9 @@ class BackendEngine:
         if self.cuda and self.time_steps:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
+        te = time.perf_counter_ns()
         out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til, n_dec=D)
+        self.host_ns[2] += time.perf_counter_ns() - te
         self._census(T)
         ev = None
         if self.cuda:

@@ -17,6 +17,8 @@ import time
 import urllib.error
 import urllib.request
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -104,6 +106,62 @@ def test_two_rank_serve_native_front_door():
         st, lst = _req("GET", base + "/api/v1/messages?limit=200")
         assert st == 200 and lst["total"] >= len(ids) + 1
         assert _req("GET", base + "/api/v1/messages/does-not-exist")[0] == 404
+    finally:
+        try:
+            os.killpg(srv.pid, signal.SIGTERM)
+            srv.wait(timeout=60)
+        except Exception:
+            os.killpg(srv.pid, signal.SIGKILL)
+            srv.wait(timeout=10)
+
+
+@pytest.mark.gpu
+def test_two_rank_serve_front_door_on_gpu():
+    """The same topology with GPU engines (tiny Llama-shaped model on the HIP
+    kernels, both ranks on the one MI355X of the box -- gloo between them):
+    HTTP POSTs through the C++ front door complete on the GPU backends and
+    every message is addressable from rank 0's API."""
+    port, mport = _port(), _port()
+    env = dict(os.environ, LLMQ_LOGGING__LEVEL="warning", LLMQ_GPU__SLOTS_PER_GPU="64",
+               LLMQ_BACKEND__TOKEN_BUDGET="512")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={mport}", "-m", "llm_message_queue_amd.cli", "serve",
+           "--model", "tiny", "--port", str(port), "--host", "127.0.0.1"]
+    srv = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           start_new_session=True)
+    base = f"http://127.0.0.1:{port}"
+    try:
+        ev = None
+        t0 = time.time()
+        while time.time() - t0 < 240:
+            line = srv.stdout.readline()
+            if not line:
+                if srv.poll() is not None:
+                    break
+                continue
+            if line.startswith("{") and '"listening"' in line:
+                ev = json.loads(line)
+                break
+        assert ev is not None and ev["gpu"] and ev["front_door"] == "native", "server did not come up"
+        ids = []
+        for i in range(40):
+            st, r = _req("POST", base + "/api/v1/messages", {"content": f"urgent: check node {i} asap",
+                                                             "user_id": f"g{i % 5}"})
+            assert st == 202, r
+            ids.append(r["message_id"])
+        deadline = time.time() + 120
+        done = {}
+        while time.time() < deadline and len(done) < len(ids):
+            for mid in ids:
+                if mid not in done:
+                    st, m = _req("GET", base + f"/api/v1/messages/{mid}")
+                    if st == 200 and m["status"] == "completed":
+                        done[mid] = m
+            time.sleep(0.1)
+        assert len(done) == len(ids), f"{len(done)} of {len(ids)} completed"
+        st, stats = _req("GET", base + "/api/v1/queues/stats")
+        assert st == 200 and stats["job"]["ranks"] == [0, 1]
+        assert stats["job"]["dispatch"]["completed"] >= len(ids)
     finally:
         try:
             os.killpg(srv.pid, signal.SIGTERM)
