@@ -31,11 +31,15 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -477,7 +481,33 @@ struct Conn {
   bool close_after = false;
   bool continued = false;   // "100 Continue" already sent for the pending request
   bool out_armed = false;   // EPOLLOUT registered (a write hit EAGAIN)
+  bool proxying = false;    // a request is with the API server: later (pipelined) ones wait in `in`
+  uint64_t gen = 0;         // accept generation (a proxy answer for a reused fd is dropped)
+  int fd = -1;
   int64_t last_ns = 0;      // last byte received (idle / slow-client reaping)
+};
+
+// Per epoll thread: proxy answers handed back by the proxy workers.  All
+// socket writes stay on the epoll thread; the workers only do the blocking
+// upstream round trip.
+struct ProxyDone {
+  int fd;
+  uint64_t gen;
+  std::string resp;
+  bool close;
+};
+struct LoopCtx {
+  int efd = -1;                  // eventfd: "answers waiting"
+  std::mutex mu;
+  std::vector<ProxyDone> done;
+  uint64_t next_gen = 0;
+};
+struct ProxyTask {
+  LoopCtx* lp;
+  int fd;
+  uint64_t gen;
+  std::string req;
+  bool keep;
 };
 
 int64_t mono_ns() {
@@ -505,6 +535,15 @@ class HttpIngress {
 
   int start() {
     if (running_.exchange(true)) return port_;
+    {
+      std::lock_guard<std::mutex> g(pq_mu_);
+      pq_stop_ = false;
+    }
+    for (int i = 0; i < kProxyWorkers; ++i) pw_.emplace_back([this] { proxy_worker(); });
+    for (int i = 0; i < nthreads_; ++i) {
+      ctx_.push_back(std::make_unique<LoopCtx>());
+      ctx_.back()->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    }
     for (int i = 0; i < nthreads_; ++i) {
       int fd = listen_socket();
       if (fd < 0) {
@@ -518,7 +557,8 @@ class HttpIngress {
         port_ = ntohs(a.sin_port);
       }
       lfds_.push_back(fd);
-      th_.emplace_back([this, fd, i] { loop(fd, i); });
+      LoopCtx* lp = ctx_[i].get();
+      th_.emplace_back([this, fd, i, lp] { loop(fd, i, lp); });
     }
     return port_;
   }
@@ -528,6 +568,18 @@ class HttpIngress {
     for (auto& t : th_)
       if (t.joinable()) t.join();
     th_.clear();
+    {
+      std::lock_guard<std::mutex> g(pq_mu_);
+      pq_stop_ = true;
+      pq_.clear();
+    }
+    pq_cv_.notify_all();
+    for (auto& t : pw_)
+      if (t.joinable()) t.join();
+    pw_.clear();
+    for (auto& c : ctx_)
+      if (c->efd >= 0) ::close(c->efd);
+    ctx_.clear();
     for (int fd : lfds_) ::close(fd);
     lfds_.clear();
   }
@@ -583,12 +635,16 @@ class HttpIngress {
     return fd;
   }
 
-  void loop(int lfd, int tid) {
+  void loop(int lfd, int tid, LoopCtx* lp) {
     int ep = epoll_create1(0);
     epoll_event ev{};
     ev.events = EPOLLIN;
     ev.data.fd = lfd;
     epoll_ctl(ep, EPOLL_CTL_ADD, lfd, &ev);
+    epoll_event eev{};
+    eev.events = EPOLLIN;
+    eev.data.fd = lp->efd;
+    epoll_ctl(ep, EPOLL_CTL_ADD, lp->efd, &eev);
     std::unordered_map<int, Conn> conns;
     std::mt19937_64 rng((uint64_t)mono_ns() ^ ((uint64_t)tid << 40) ^ (uint64_t)(uintptr_t)this);
     std::vector<epoll_event> evs(256);
@@ -606,7 +662,8 @@ class HttpIngress {
         const int64_t now = mono_ns();
         next_sweep = now + std::min<int64_t>(idle / 4 + 1, 1'000'000'000);
         for (auto it = conns.begin(); it != conns.end();) {
-          if (now - it->second.last_ns > idle && it->second.out_off >= it->second.out.size()) {
+          if (now - it->second.last_ns > idle && it->second.out_off >= it->second.out.size() &&
+              !it->second.proxying) {
             epoll_ctl(ep, EPOLL_CTL_DEL, it->first, nullptr);
             ::close(it->first);
             it = conns.erase(it);
@@ -619,6 +676,33 @@ class HttpIngress {
       }
       for (int k = 0; k < n; ++k) {
         int fd = evs[k].data.fd;
+        if (fd == lp->efd) {                         // proxy answers are back
+          uint64_t cnt;
+          while (::read(lp->efd, &cnt, sizeof cnt) > 0) {
+          }
+          std::vector<ProxyDone> done;
+          {
+            std::lock_guard<std::mutex> g(lp->mu);
+            done.swap(lp->done);
+          }
+          for (auto& d : done) {
+            auto it = conns.find(d.fd);
+            if (it == conns.end() || it->second.gen != d.gen) continue;   // closed meanwhile
+            Conn& cn = it->second;
+            cn.proxying = false;
+            cn.out.append(d.resp);
+            if (d.close) cn.close_after = true;
+            if (!cn.close_after) process(cn, rng, lp);  // requests pipelined behind it
+            bool dead = !cn.out.empty() && !flush(d.fd, cn, ep);
+            if (dead || (cn.close_after && cn.out.empty() && !cn.proxying)) {
+              epoll_ctl(ep, EPOLL_CTL_DEL, d.fd, nullptr);
+              ::close(d.fd);
+              conns.erase(it);
+              conns_--;
+            }
+          }
+          continue;
+        }
         if (fd == lfd) {
           for (;;) {
             sockaddr_in pa{};
@@ -645,8 +729,11 @@ class HttpIngress {
             epoll_ctl(ep, EPOLL_CTL_ADD, c, &ce);
             char ipb[INET_ADDRSTRLEN] = {0};
             inet_ntop(AF_INET, &pa.sin_addr, ipb, sizeof ipb);
+            conns[c] = Conn();
             conns[c].ip = ipb;
             conns[c].last_ns = mono_ns();
+            conns[c].gen = ++lp->next_gen;
+            conns[c].fd = c;
             conns_++;
           }
           continue;
@@ -667,7 +754,7 @@ class HttpIngress {
             if (r == 0) eof = true;   // peer half-closed: answer what it sent, then close
             break;
           }
-          if (!dead) process(cn, rng);
+          if (!dead && !cn.proxying) process(cn, rng, lp);
           if (eof) cn.close_after = true;
         }
         if (!dead && !cn.out.empty()) dead = !flush(fd, cn, ep);
@@ -680,7 +767,7 @@ class HttpIngress {
           epoll_ctl(ep, EPOLL_CTL_MOD, fd, &ce);
           cn.out_armed = false;
         }
-        if (dead || (cn.close_after && cn.out.empty())) {
+        if (dead || (cn.close_after && cn.out.empty() && !cn.proxying)) {
           epoll_ctl(ep, EPOLL_CTL_DEL, fd, nullptr);
           ::close(fd);
           conns.erase(it);
@@ -778,9 +865,9 @@ class HttpIngress {
     return s;
   }
 
-  void process(Conn& cn, std::mt19937_64& rng) {
+  void process(Conn& cn, std::mt19937_64& rng, LoopCtx* lp) {
     size_t pos = 0;
-    while (!cn.close_after) {
+    while (!cn.close_after && !cn.proxying) {
       size_t he = cn.in.find("\r\n\r\n", pos);
       if (he == std::string::npos) {
         if (cn.in.size() - pos > kMaxHeader)
@@ -896,8 +983,10 @@ class HttpIngress {
       } else if (method == "GET" && (path == "/health" || path == "/api/v1/health")) {
         respond(cn, 200, "OK", "{\"status\":\"ok\",\"version\":\"1.0.0\",\"time\":\"" + rfc3339_now() + "\"}", keep);
       } else if (upstream_port_ > 0) {
+        // handed to a proxy worker; the connection's later requests wait in
+        // `in` until the answer is back (responses stay in request order)
         proxied_++;
-        proxy(cn, h, hl, body, clen, keep);
+        start_proxy(cn, lp, h, hl, body, clen, keep);
       } else {
         respond(cn, 404, "Not Found", "{\"error\":\"route served by the API server\"}", keep);
       }
@@ -906,12 +995,14 @@ class HttpIngress {
     if (pos) cn.in.erase(0, pos);
   }
 
-  // Blocking reverse proxy of one request to the API server (status,
-  // conversation and admin routes: low rate, so the epoll thread may wait for
-  // the answer; the submit path never comes here).  Connection: close
-  // upstream; the client's keep-alive is kept when the answer is framed by
-  // Content-Length.
-  void proxy(Conn& cn, const char* h, size_t hl, const char* body, size_t clen, bool keep) {
+  // Reverse proxy of one request to the API server (status, conversation
+  // and admin routes).  The epoll thread only builds the upstream request and
+  // queues it; one of kProxyWorkers threads does the blocking round trip
+  // (Connection: close upstream) and hands the framed answer back through the
+  // loop's eventfd -- a slow admin query never stalls the other connections of
+  // that epoll thread, and every socket write stays on it.  The client's
+  // keep-alive is kept when the answer is framed by Content-Length.
+  void start_proxy(Conn& cn, LoopCtx* lp, const char* h, size_t hl, const char* body, size_t clen, bool keep) {
     std::string req;
     req.reserve(hl + clen + 128);
     const char* line_end = (const char*)memchr(h, '\n', hl);
@@ -931,9 +1022,42 @@ class HttpIngress {
     }
     req.append("Connection: close\r\nX-Forwarded-For: " + cn.ip + "\r\n\r\n");
     req.append(body, clen);
+    cn.proxying = true;
+    {
+      std::lock_guard<std::mutex> g(pq_mu_);
+      pq_.push_back(ProxyTask{lp, cn.fd, cn.gen, std::move(req), keep});
+    }
+    pq_cv_.notify_one();
+  }
+
+  void proxy_worker() {
+    for (;;) {
+      ProxyTask t;
+      {
+        std::unique_lock<std::mutex> g(pq_mu_);
+        pq_cv_.wait(g, [&] { return pq_stop_ || !pq_.empty(); });
+        if (pq_stop_) return;
+        t = std::move(pq_.front());
+        pq_.pop_front();
+      }
+      bool close = false;
+      std::string resp = proxy_fetch(t.req, t.keep, &close);
+      {
+        std::lock_guard<std::mutex> g(t.lp->mu);
+        t.lp->done.push_back(ProxyDone{t.fd, t.gen, std::move(resp), close});
+      }
+      const uint64_t one = 1;
+      if (::write(t.lp->efd, &one, sizeof one) < 0) {
+      }
+    }
+  }
+
+  // The upstream round trip; returns the bytes for the client (502 when the
+  // API server is unreachable or answers garbage).
+  std::string proxy_fetch(const std::string& req, bool keep, bool* close) {
     std::string resp;
     bool ok = false;
-    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
     if (fd >= 0) {
       timeval tv{30, 0};
       setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
@@ -967,8 +1091,10 @@ class HttpIngress {
     const size_t he = resp.find("\r\n\r\n");
     if (!ok || he == std::string::npos || resp.compare(0, 5, "HTTP/") != 0) {
       proxy_errors_++;
-      respond(cn, 502, "Bad Gateway", "{\"error\":\"API server unreachable\"}", keep);
-      return;
+      Conn tmp;
+      respond(tmp, 502, "Bad Gateway", "{\"error\":\"API server unreachable\"}", keep);
+      *close = tmp.close_after;
+      return tmp.out;
     }
     // drop the upstream's Connection header; keep the client connection open
     // only when the body length is explicit
@@ -988,10 +1114,10 @@ class HttpIngress {
     }
     const bool k = keep && has_len && !chunked;
     if (!k) head += "Connection: close\r\n";
-    cn.out.append(head);
-    cn.out.append("\r\n");
-    cn.out.append(resp, he + 4, std::string::npos);
-    if (!k) cn.close_after = true;
+    std::string out = head + "\r\n";
+    out.append(resp, he + 4, std::string::npos);
+    *close = !k;
+    return out;
   }
 
   int port_;
@@ -1001,6 +1127,13 @@ class HttpIngress {
   std::string upstream_host_ = "127.0.0.1";
   int upstream_port_ = 0;
   std::atomic<int64_t> proxied_{0}, proxy_errors_{0};
+  static constexpr int kProxyWorkers = 4;
+  std::vector<std::unique_ptr<LoopCtx>> ctx_;
+  std::vector<std::thread> pw_;
+  std::mutex pq_mu_;
+  std::condition_variable pq_cv_;
+  std::deque<ProxyTask> pq_;
+  bool pq_stop_ = false;
   int nthreads_;
   std::atomic<bool> running_{false};
   std::vector<std::thread> th_;

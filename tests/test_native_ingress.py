@@ -461,3 +461,91 @@ def test_slow_reader_does_not_spin_ingress_thread():
     finally:
         ing.stop()
         ring.close(unlink=True)
+
+
+def test_front_door_proxy_is_async_ordered_and_reports_502():
+    """The multi-GPU front door reverse-proxies every non-submit route to the
+    API server.  The upstream round trip runs on a proxy worker, so a slow
+    admin request does not stall other connections of the same epoll thread;
+    pipelined requests on one connection are answered in order; an
+    unreachable API server is a 502."""
+    import http.server
+    import socket
+    import threading
+    import time
+
+    class Slow(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            if "slow" in self.path:
+                time.sleep(1.0)
+            body = json.dumps({"path": self.path, "xff": self.headers.get("X-Forwarded-For", "")}).encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    up = http.server.ThreadingHTTPServer(("127.0.0.1", 0), Slow)
+    threading.Thread(target=up.serve_forever, daemon=True).start()
+    from llm_message_queue_amd.gateway.native_ingress import NativeIngress
+    name = f"pytest-proxy-{os.getpid()}"
+    ing = NativeIngress(0, name, threads=1, host="127.0.0.1", upstream=("127.0.0.1", up.server_address[1]))
+    port = ing.start()
+    try:
+        res = {}
+
+        def slow():
+            t0 = time.time()
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}/api/v1/queues/slow", timeout=10) as r:
+                res["slow"] = (r.status, json.loads(r.read()), time.time() - t0)
+
+        th = threading.Thread(target=slow)
+        th.start()
+        time.sleep(0.2)                               # the slow request is with the API server now
+        t0 = time.time()
+        st, body = _post(port, {"content": "hello", "id": "fast-1"})
+        fast_s = time.time() - t0
+        th.join()
+        assert st == 202 and body["message_id"] == "fast-1"
+        assert fast_s < 0.5, fast_s                   # not stuck behind the 1 s upstream answer
+        assert res["slow"][0] == 200 and res["slow"][1]["path"] == "/api/v1/queues/slow"
+        assert res["slow"][1]["xff"] == "127.0.0.1" and res["slow"][2] >= 0.9
+        # pipelining: a proxied request then a native one on ONE connection -> answers in order
+        s = socket.create_connection(("127.0.0.1", port), timeout=10)
+        body = b'{"content":"x","id":"pipe-2"}'
+        s.sendall(b"GET /slow-first HTTP/1.1\r\nHost: x\r\n\r\n"
+                  b"POST /api/v1/messages HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                  b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
+        data = b""
+        t0 = time.time()
+        while data.count(b"HTTP/1.") < 2 and time.time() - t0 < 10:
+            data += s.recv(65536)
+        s.close()
+        first, second = data.index(b"/slow-first"), data.index(b"pipe-2")
+        assert first < second and data.count(b" 200 OK") == 1 and data.count(b"HTTP/1.1 202") == 1
+        st_ = ing.stats()
+        assert st_["proxied"] == 2 and st_["proxy_errors"] == 0
+    finally:
+        ing.stop()
+        up.shutdown()
+    # an API server that is gone: 502
+    dead = socket.socket()
+    dead.bind(("127.0.0.1", 0))
+    dead_port = dead.getsockname()[1]
+    dead.close()
+    ing = NativeIngress(0, name, threads=1, host="127.0.0.1", upstream=("127.0.0.1", dead_port))
+    port = ing.start()
+    try:
+        try:
+            urllib.request.urlopen(f"http://127.0.0.1:{port}/api/v1/queues/stats", timeout=10)
+            assert False, "expected 502"
+        except urllib.error.HTTPError as e:
+            assert e.code == 502
+        assert ing.stats()["proxy_errors"] == 1
+    finally:
+        ing.stop()
+        from llm_message_queue_amd import _native
+        _native.shmring().ShmRing(f"llmq-{name}-req", 1 << 20, "open").unlink()
