@@ -46,7 +46,7 @@ def _targets() -> Dict[str, dict]:
         "_shmring": dict(
             compiler="g++",
             sources=[os.path.join(CSRC, "queue", "shm_ring.cpp")],
-            deps=[os.path.join(CSRC, "queue", "shm_ring.h")],
+            deps=[os.path.join(CSRC, "queue", "shm_ring.h"), os.path.join(CSRC, "queue", "shm_coll.h")],
             flags=["-O3", "-std=c++17", "-fvisibility=hidden", "-pthread"],
             libs=["-lrt"],
         ),
@@ -89,12 +89,36 @@ def _out(name: str) -> str:
     return os.path.join(LIB, name + EXT)
 
 
+def _includes(path: str, seen: set) -> None:
+    """Every in-tree header ``path`` includes, transitively (``#include "x"``
+    resolved against the file's directory and ``csrc/``): the staleness check
+    must not miss a header nobody listed (a stale ``_shmring`` once survived
+    an edit of ``shm_coll.h``)."""
+    import re
+    try:
+        with open(path, encoding="utf-8", errors="replace") as fh:
+            text = fh.read()
+    except OSError:
+        return
+    for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+        for base in (os.path.dirname(path), CSRC):
+            cand = os.path.normpath(os.path.join(base, inc))
+            if os.path.exists(cand):
+                if cand not in seen:
+                    seen.add(cand)
+                    _includes(cand, seen)
+                break
+
+
 def _stale(name: str, t: dict) -> bool:
     out = _out(name)
     if not os.path.exists(out):
         return True
     mt = os.path.getmtime(out)
-    return any(os.path.exists(s) and os.path.getmtime(s) > mt for s in t["sources"] + t["deps"])
+    deps = set(t["deps"])
+    for src in t["sources"]:
+        _includes(src, deps)
+    return any(os.path.exists(s) and os.path.getmtime(s) > mt for s in list(t["sources"]) + sorted(deps))
 
 
 def build_one(name: str, t: dict, verbose: bool = False) -> str:

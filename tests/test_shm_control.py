@@ -44,6 +44,10 @@ def _coll_worker(rank, world, port, out):
         for s, rows in enumerate(got):
             ok &= rows.shape == (counts[s], 4)
             ok &= bool((rows[:, 0] == s).all() and (rows[:, 1] == rank).all() and (rows[:, 2] == it).all())
+        # the variable form (receivers do not know the counts: KV-migration headers)
+        var = comm.all_to_all_var(send, 4)
+        for s, rows in enumerate(var):
+            ok &= rows.shape == (counts[s], 4) and bool((rows[:, 0] == s).all() if len(rows) else True)
         root = it % world
         b = comm.broadcast_i64(np.array([root * 100 + it], dtype=np.int64), root=root)
         ok &= int(b[0]) == root * 100 + it
@@ -97,6 +101,32 @@ def _dead_peer_worker(rank, world, port, out):
         out.put((rank, "no error", 0.0))
     except PeerLost:
         out.put((rank, "PeerLost", time.time() - t0))
+
+
+def _overflow_worker(rank, world, port, out):
+    _env(rank, world, port)
+    from llm_message_queue_amd.parallel.comm import PeerLost, ShmComm, init_from_env
+    comm = init_from_env(backend="gloo", control="shm", timeout_s=30)
+    assert isinstance(comm, ShmComm)
+    cap = comm.c.buf_bytes
+    t0 = time.monotonic()
+    try:                                   # rank 1's payload does not fit its buffer
+        comm.all_gather_i64(np.zeros(cap // 8 + 16 if rank == 1 else 4, dtype=np.int64))
+        res = "no error"
+    except PeerLost as e:
+        res = "overflow" if "overflow" in str(e) else f"other: {e}"
+    out.put((rank, res, time.monotonic() - t0))
+
+
+def test_shm_payload_overflow_fails_every_rank_at_once():
+    """an oversized control payload used to raise on the
+    sending rank only, while every other rank spun to its 60 s timeout; now
+    the overflow is published and every rank raises PeerLost immediately."""
+    res, codes = _run(_overflow_worker, 3, timeout=120)
+    assert len(res) == 3, codes
+    for rank, what, dt in res:
+        assert what == "overflow", (rank, what)
+        assert dt < 10.0, (rank, dt)
 
 
 def test_shm_dead_peer_raises_peer_lost_within_timeout():
