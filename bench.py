@@ -88,10 +88,12 @@ def parse(argv=None):
     ap.add_argument("--trace-sample", type=int, default=20, help="trace every Nth completed request")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="rehearse the multi-rank control flow on CPU (gloo, tiny model); not a measurement")
-    ap.add_argument("--ingress", default="per-rank", choices=["per-rank", "rank0"],
+    ap.add_argument("--ingress", default="per-rank", choices=["per-rank", "rank0", "rank0-funnel"],
                     help="per-rank: every GPU process fronts its own Poisson stream (weak scaling, one ingress "
-                         "per GPU); rank0: rank 0 alone receives N x the per-GPU rate and the planner spreads it "
-                         "over all GPUs with all_to_all (the `cli serve` topology: HTTP on rank 0)")
+                         "per GPU); rank0: rank 0 alone receives N x the per-GPU rate (the `cli serve` topology: "
+                         "one front door) and ships the RAW records round-robin through node-shared rings, so "
+                         "every rank decodes and GPU-preprocesses its share; rank0-funnel: the r2 form, rank 0 "
+                         "preprocesses the whole job's traffic on GPU 0 and the planner spreads it (A/B)")
     ap.add_argument("--lb", default="least_connections",
                     choices=["round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first"],
                     help="multi-GPU placement strategy (loadbalancer.algorithm)")
@@ -176,6 +178,68 @@ def lockstep_report(gw, engine, comm, elapsed: float) -> dict:
             "gpu_busy_frac_by_rank": [round(v, 4) for v in busy.tolist()],
             "gpu_steps_by_rank": [int(v) for v in g[:, 6].tolist()],
             "slowest_over_mean_gpu_step": round(float(step_mean.max() / max(1e-9, step_mean.mean())), 4)}
+
+
+class FrontDoorRings:
+    """``--ingress rank0``: rank 0 is the job's one front door.  It ships each
+    arrival as the RAW record the native HTTP ingress writes (TAG_RAW:
+    arrival ns, id, JSON body -- `csrc/ingress/http_ingress.cpp`) into the
+    node-shared ring of a destination rank, round-robin; every rank decodes
+    the records it receives and GPU-preprocesses them on its own GPU, so GPU
+    0 does not carry the job's preprocessing.  The
+    bodies come from a pool drawn from the bench workload once, untimed, so
+    the front door's per-request cost is a record header, as in C++."""
+
+    POOL = 16384
+
+    def __init__(self, world: int, rank: int, job: str, wl):
+        from llm_message_queue_amd import _native
+        self.world, self.rank = world, rank
+        self.prefix = f"llmq-benchdoor-{job}-{os.environ.get('MASTER_PORT', '0')}"
+        self._R = _native.shmring().ShmRing
+        self.inbox = self._R(f"{self.prefix}-r{rank}", 64 << 20, "open")
+        self.out = []
+        self.serial = 0
+        self.pool = []
+        if rank == 0:
+            for m in wl.make(self.POOL):
+                body = {"content": m.content, "user_id": m.user_id}
+                if m.priority:
+                    body["priority"] = int(m.priority)
+                self.pool.append(json.dumps(body).encode())
+
+    def attach_outboxes(self) -> None:
+        if self.rank == 0:
+            self.out = [self.inbox if r == 0 else self._R(f"{self.prefix}-r{r}", 64 << 20, "open")
+                        for r in range(self.world)]
+
+    def ship(self, due) -> None:
+        from llm_message_queue_amd.gateway.shm_bridge import TAG_RAW
+        per = [[] for _ in range(self.world)]
+        s, pool, P = self.serial, self.pool, self.POOL
+        for ts in due:
+            body = pool[s % P]
+            per[s % self.world].append(int(ts * 1e9).to_bytes(8, "little", signed=True)
+                                       + (b"door-%x" % s).ljust(36, b"\0")
+                                       + len(body).to_bytes(4, "little") + body)
+            s += 1
+        self.serial = s
+        for r, recs in enumerate(per):
+            if recs and self.out[r].push_many(recs, TAG_RAW) != len(recs):
+                raise RuntimeError(f"front-door ring of rank {r} full")
+
+    def receive(self):
+        from llm_message_queue_amd.gateway.shm_bridge import decode_raw
+        return [decode_raw(b) for _, b in self.inbox.pop(1 << 16, 0)]
+
+    def backlog(self) -> int:
+        return int(self.inbox.size())
+
+    def close(self) -> None:
+        self.inbox.unlink()
+        self.inbox.close()
+        for r in self.out[1:]:
+            r.close()
 
 
 def _free_port() -> int:
@@ -340,7 +404,12 @@ def main(argv=None) -> int:
     capacity = float(np.mean(caps))
     rate = a.rate if a.rate > 0 else a.util * capacity
     # rank0 ingress: one front door takes the whole job's traffic
-    my_rate = (rate * world if rank == 0 else 0.0) if a.ingress == "rank0" else rate
+    front_door = a.ingress in ("rank0", "rank0-funnel")
+    my_rate = (rate * world if rank == 0 else 0.0) if front_door else rate
+    door = FrontDoorRings(world, rank, job, wl) if a.ingress == "rank0" and world > 1 else None
+    if door is not None:
+        comm.barrier()                   # every rank's ring exists before rank 0 attaches to it
+        door.attach_outboxes()
     # drain the calibration backlog (untimed)
     gw.drop_pending()
 
@@ -350,7 +419,8 @@ def main(argv=None) -> int:
         return (engine.inflight() + engine.queued_steps() + len(gw.remote_out)
                 + sum(len(v) for v in gw._done_owed.values()) + gw.pending() + gw.inbox_size()
                 + gw.preprocessing()
-                + gw.awaiting_kv())
+                + gw.awaiting_kv()
+                + (door.backlog() if door is not None else 0))
 
     busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
     while busy.max() > 0:
@@ -365,6 +435,13 @@ def main(argv=None) -> int:
 
     def pump():
         due = arrivals.due(time.monotonic())
+        if door is not None:
+            if due:
+                door.ship(due)
+            msgs = door.receive()
+            if msgs:
+                gw.submit(msgs)
+            return
         if due:
             msgs = wl.make(len(due))
             for m, ts in zip(msgs, due):
@@ -456,6 +533,7 @@ def main(argv=None) -> int:
     busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
     n_drain = 0
     while busy.max() > 0 and n_drain < 2000:
+        pump()                  # no new arrivals (rate 0); takes what the front door's rings still hold
         gw.tick()
         n_drain += 1
         busy = comm.all_gather_i64(np.array([busy_local()], dtype=np.int64))
@@ -469,6 +547,10 @@ def main(argv=None) -> int:
                                        dtype=np.int64))
     elapsed = agg[:, 0].max() / 1e9
     lockstep = lockstep_report(gw, engine, comm, elapsed)
+    lockstep["ingested_by_rank"] = [int(v) for v in agg[:, 3].tolist()]   # requests each rank preprocessed
+    if door is not None:
+        comm.barrier()
+        door.close()
     remote_in_window = int(comm.all_gather_i64(np.array([remote_local], dtype=np.int64)).sum())
     dispatched = int(agg[:, 1].sum())
     tokens = int(agg[:, 2].sum())
