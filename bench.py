@@ -88,6 +88,14 @@ def parse(argv=None):
     ap.add_argument("--trace-sample", type=int, default=20, help="trace every Nth completed request")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="rehearse the multi-rank control flow on CPU (gloo, tiny model); not a measurement")
+    ap.add_argument("--sim-gpu", default="",
+                    help="with --cpu-dry-run: per-rank relative GPU speeds, e.g. '1,0.97,1.02' (cycled over "
+                         "ranks); each rank's backend is a SimEngine (the engine's host side for real, the 8B "
+                         "forward as a simulated device clock) at the serving config's slots / token budget -- "
+                         "for studying multi-GPU dynamics (lock-step vs GPU speed spread) without the GPUs")
+    ap.add_argument("--no-extra-steps", action="store_true",
+                    help="multi-rank A/B: never launch an extra local forward while the peers are still "
+                         "behind at the per-tick exchange (pure lock-step)")
     ap.add_argument("--ingress", default="per-rank", choices=["per-rank", "rank0", "rank0-funnel"],
                     help="per-rank: every GPU process fronts its own Poisson stream (weak scaling, one ingress "
                          "per GPU); rank0: rank 0 alone receives N x the per-GPU rate (the `cli serve` topology: "
@@ -296,7 +304,8 @@ def main(argv=None) -> int:
         # reductions) with a tiny model and gloo -- never a measurement
         dev = torch.device("cpu")
         comm = init_from_env(backend="gloo", control="gloo" if a.control_plane == "nccl" else a.control_plane)
-        a.model, a.slots, a.max_ctx, a.token_budget, a.prompt_cap = "tiny", 16, 64, 128, 16
+        if not a.sim_gpu:
+            a.model, a.slots, a.max_ctx, a.token_budget, a.prompt_cap = "tiny", 16, 64, 128, 16
     else:
         if not torch.cuda.is_available():
             print("bench.py needs a GPU (MI355X)", file=sys.stderr)
@@ -334,14 +343,22 @@ def main(argv=None) -> int:
         r_, b_ = item.split(":")
         if int(r_) == rank:
             budget = int(b_)
-    engine = BackendEngine(LlamaConfig.by_name(a.model), slots=a.slots, max_ctx=a.max_ctx,
-                           token_budget=budget, device=dev, impl="ref" if dry else "hip", seed=1000 + rank,
-                           page=page, gpu_index=rank, max_inflight=a.inflight,
-                           residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv,
-                           fused_mlp=False if a.no_fused_mlp else None,
-                           fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
-                           fused_head=False if a.no_fused_head else None,
-                           fused_resid=True if a.fused_resid else None)
+    sim_speed = None
+    if dry and a.sim_gpu:
+        from llm_message_queue_amd.backend.sim_engine import SimEngine
+        speeds = [float(x) for x in a.sim_gpu.split(",")]
+        sim_speed = speeds[rank % len(speeds)]
+        engine = SimEngine(speed=sim_speed, slots=a.slots, max_ctx=a.max_ctx, token_budget=budget,
+                           max_inflight=a.inflight, page=page, gpu_index=rank, seed=1000 + rank)
+    else:
+        engine = BackendEngine(LlamaConfig.by_name(a.model), slots=a.slots, max_ctx=a.max_ctx,
+                               token_budget=budget, device=dev, impl="ref" if dry else "hip", seed=1000 + rank,
+                               page=page, gpu_index=rank, max_inflight=a.inflight,
+                               residual_in_gemm=not a.no_residual_gemm, split_qkv=a.split_qkv,
+                               fused_mlp=False if a.no_fused_mlp else None,
+                               fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
+                               fused_head=False if a.no_fused_head else None,
+                               fused_resid=True if a.fused_resid else None)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -350,6 +367,7 @@ def main(argv=None) -> int:
     for j in range(world):          # every rank's balancer lists every GPU (cli serve does the same)
         lb.add_endpoint(Endpoint(id=f"gpu{j}", type="llm", gpu_index=j, page=page if j == rank else None,
                                  max_connections=a.slots))
+    cfg.gpu.extra_steps = not a.no_extra_steps
     gw = Gateway(cfg, preprocessor=pre, engine=engine, comm=comm, load_balancer=lb,
                  use_gpu_preprocess=not dry, prompt_cap=a.prompt_cap, gen_tokens=a.gen_tokens)
     wl = Workload(seed=a.seed * 1000 + rank)
@@ -502,6 +520,7 @@ def main(argv=None) -> int:
     gw.quiesce(pump)
     d0 = gw.counters["dispatched"]
     r0 = gw.counters["remote_sent"]
+    x0 = gw.counters["extra_steps"]
     tok0 = engine.total_tokens
     gw.lockstep_stats(reset=True)
     engine.gpu_step_ms, engine.gpu_steps, engine.gpu_step_max_ms = 0.0, 0, 0.0
@@ -521,6 +540,7 @@ def main(argv=None) -> int:
     engine.time_steps = False
     arrived_local = gw.counters["submitted"] - sub0
     remote_local = gw.counters["remote_sent"] - r0
+    extra_local = gw.counters["extra_steps"] - x0
     gc.enable()
     if tracer is not None:
         gw.tracer = engine.tracer = None
@@ -548,6 +568,9 @@ def main(argv=None) -> int:
     elapsed = agg[:, 0].max() / 1e9
     lockstep = lockstep_report(gw, engine, comm, elapsed)
     lockstep["ingested_by_rank"] = [int(v) for v in agg[:, 3].tolist()]   # requests each rank preprocessed
+    # extra forwards a rank launched while its peers were behind (Gateway._extra_local_step)
+    lockstep["extra_steps_by_rank"] = [int(v) for v in
+                                       comm.all_gather_i64(np.array([extra_local], dtype=np.int64))[:, 0].tolist()]
     if door is not None:
         comm.barrier()
         door.close()
@@ -586,6 +609,7 @@ def main(argv=None) -> int:
                    "global_batch": a.slots * world, "seq_len": a.max_ctx,
                    "parallelism": f"dp{world}", "ingress": a.ingress, "placement": a.lb,
                    "token_budget_by_rank": a.token_budget_by_rank or None,
+                   "sim_gpu": a.sim_gpu or None, "extra_steps": not a.no_extra_steps,
                    "control_plane": comm_kind, "token_budget": a.token_budget,
                    "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap, "inflight": a.inflight,
                    "aging_ms": a.aging_ms, "util": a.util,

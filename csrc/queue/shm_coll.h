@@ -137,6 +137,16 @@ class ShmCollective {
                                 "'s payload exceeds the per-rank buffer of " + std::to_string(buf_bytes_) + " bytes");
   }
 
+  // Non-blocking: how many OTHER ranks have already published the next op
+  // (are waiting in it).  world - 1 means joining now completes it at once.
+  int arrived_next() const {
+    const uint64_t k = seq_ + 1;
+    int n = 0;
+    for (int r = 0; r < world_; ++r)
+      if (r != rank_ && slots_[r].pub.load(std::memory_order_acquire) >= k) ++n;
+    return n;
+  }
+
   // After exchange(): rank r's payload of the last op.
   const uint8_t* payload(int r, uint64_t* n) const {
     const int par = (int)(seq_ & 1);

@@ -114,6 +114,7 @@ PYBIND11_MODULE(_shmring, m) {
            },
            py::arg("parts"), py::arg("timeout_s") = 60.0)
       .def("attached", &ShmCollective::attached)
+      .def("arrived_next", &ShmCollective::arrived_next)
       .def("unlink", &ShmCollective::unlink)
       .def_property_readonly("ops", &ShmCollective::ops)
       .def_property_readonly("world", &ShmCollective::world)

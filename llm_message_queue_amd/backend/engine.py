@@ -94,6 +94,7 @@ class BackendEngine:
         self.token_budget = max(token_budget, slots)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
+        self.async_device = self.cuda          # forwards run asynchronously (a GPU stream)
         self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
                                fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
@@ -290,6 +291,15 @@ class BackendEngine:
     def kv_bytes_per_token(self) -> int:
         c = self.cfg
         return c.layers * 2 * c.kv_heads * c.head_dim * 2          # K and V, bf16 (128 KiB for Llama-3-8B)
+
+    def ready_tokens(self) -> int:
+        """Tokens the next launch would run right now: one per decoding slot
+        plus the pending prefill, capped at the token budget."""
+        act = self.s_active
+        if not act.any():
+            return 0
+        plen, pref = self.s_plen[act], self.s_pref[act]
+        return min(self.token_budget, int((pref >= plen).sum()) + int((plen - pref).clip(min=0).sum()))
 
     def lane_capacity(self) -> int:
         """Slots a realtime request may take beyond ``admit_capacity``: every
@@ -557,18 +567,12 @@ class BackendEngine:
             src = d[o_dec + D:o_til].long()
             tok_d.index_copy_(0, rows, self._prev_out.index_select(0, src).long())
         til = d[o_til:].view(NT, 4) if self.use_tiles else None
-        ev0 = None
-        if self.cuda and self.time_steps:
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev0.record()
+        ev0 = self._start_event()
         te = time.perf_counter_ns()
         out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til, n_dec=D)
         self.host_ns[2] += time.perf_counter_ns() - te
         self._census(T)
-        ev = None
-        if self.cuda:
-            ev = torch.cuda.Event(enable_timing=ev0 is not None)
-            ev.record()
+        ev = self._end_event(T, ev0 is not None)
         # deterministic bookkeeping: every sampled slot gets one token
         ss = samp_slots
         self.s_gen[ss] += 1
@@ -601,6 +605,23 @@ class BackendEngine:
         self.total_tokens += T
         self.completed_total += len(completed)
         self.completed_tokens += sum(len(r.prompt) + r.gen_tokens - 1 for r in completed)
+
+    def _start_event(self):
+        """Timing event before a forward (``time_steps``), or None."""
+        if self.cuda and self.time_steps:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            return ev0
+        return None
+
+    def _end_event(self, T: int, timing: bool):
+        """Completion event of the forward just enqueued (None: the step ran
+        synchronously on the host)."""
+        if not self.cuda:
+            return None
+        ev = torch.cuda.Event(enable_timing=timing)
+        ev.record()
+        return ev
 
     def _reap(self, block: bool) -> Optional[_Inflight]:
         if not self._q:

@@ -205,12 +205,14 @@ class Gateway:
         self.rec = LatencyRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
-                         "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0, "realtime_local": 0}
+                         "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0, "realtime_local": 0,
+                         "extra_steps": 0, "extra_admitted": 0}
         # overload shedding (expire_queued) -> dead-letter queue
         self.shed_expired = bool(getattr(q, "shed_expired", True))
         # realtime lane (tier 0 admitted past the step's prefill headroom and
         # prefilled first): queue.realtime_lane, default on
         self.realtime_lane = bool(getattr(q, "realtime_lane", True))
+        self.extra_steps = bool(getattr(cfg.gpu, "extra_steps", True))
         self.dead_letter = dead_letter
         self.on_expire = None       # optional callback(msg)
         # failure detection: a backend error (HIP error / OOM), the telemetry
@@ -714,6 +716,7 @@ class Gateway:
 
     def _dispatch_global(self) -> int:
         W, me = self.world, self.rank
+        self._extra_local_step()
         my_load = self._my_load()
         tc0 = time.perf_counter_ns()
         loads = self.comm.all_gather_i64(my_load)
@@ -1210,13 +1213,21 @@ class Gateway:
         budgets = [0] * len(self.tiers)
         budgets[0] = room
         msgs, _t, _e = self.qm.pop_tiers(self.tiers, room, [0] * len(self.tiers), budgets, None)
+        n = self._admit_own(msgs, [0] * len(msgs))
+        self.counters["realtime_local"] += n
+        return n
+
+    def _admit_own(self, msgs: Sequence[Message], tiers: Sequence[int]) -> int:
+        """Admit popped queued requests into this rank's OWN GPU (no
+        cross-rank decision: the next load vector reports the slots taken)."""
         if not msgs:
             return 0
+        eng = self.engine
         reqs = []
-        for m in msgs:
+        for m, t in zip(msgs, tiers):
             self._pin(m, -1)
-            m.tier = 0
-            reqs.append(self._make_request(m, 0))
+            m.tier = int(t)
+            reqs.append(self._make_request(m, int(t)))
         admitted = eng.admit(reqs)
         now = time.monotonic_ns()
         for r in admitted:
@@ -1225,14 +1236,65 @@ class Gateway:
             m.status = MessageStatus.PROCESSING
             m.endpoint_id = f"gpu{self.rank}"
             self.local[m.handle] = m
-            self.inflight_by_tier[0] += 1
+            self.inflight_by_tier[r.tier] += 1
         for r in reqs[len(admitted):]:             # cannot happen (room was counted); requeue defensively
             self._requeue(r.meta)
-        self._record([0] * len(admitted), [r.meta.arrival_ns for r in admitted],
+        self._record([r.tier for r in admitted], [r.meta.arrival_ns for r in admitted],
                      [r.meta.enqueued_at for r in admitted], now)
         self.counters["dispatched"] += len(admitted)
-        self.counters["realtime_local"] += len(admitted)
         return len(admitted)
+
+    # An extra step must carry at least this fraction of the token budget: a
+    # forward's GEMM cost is quantised in 256-row tiles, so many small steps
+    # would cost more GPU time than the idle they fill.
+    EXTRA_STEP_MIN_FRAC = 0.5
+    ROTATING_STRATEGIES = ("round_robin", "weighted_random")
+
+    def _extra_local_step(self) -> bool:
+        """Multi-rank, before the tick's exchange: if the engine's run-ahead
+        queue has room (this GPU finishes its steps faster than the job's
+        tick cadence -- a faster GPU than the slowest peer) and a peer has not
+        reached the exchange yet (so joining now means waiting), admit this
+        rank's own queued requests into its free slots and launch one more
+        forward.  Lock-step would otherwise leave the faster GPU idle for the
+        speed difference every tick (``lockstep.gpu_busy_frac_by_rank``);
+        with it the job serves the SUM of its GPUs' capacities, and the
+        planner, seeing the faster GPU's free slots, moves the slower GPUs'
+        excess there.  At most one per tick, so a rank always joins the
+        exchange promptly; placement of own requests onto the own GPU is what
+        least-connections would choose for a GPU with free slots, and is
+        skipped for tiers holding turns homed on another GPU and while this
+        GPU is parked; under round robin / weighted random the step runs only
+        work already admitted.  Engines without an asynchronous device (the
+        CPU reference engine runs its forward on the host) never idle, so
+        never take one."""
+        eng = self.engine
+        if (not self.extra_steps or eng is None or not getattr(eng, "async_device", False) or not self.healthy
+                or self.stopping or not self.tiers or eng.queued_steps() >= eng.max_inflight):
+            return False
+        behind = getattr(self.comm, "peers_behind", None)
+        if behind is None or not behind():
+            return False
+        if (self._exclude_mask() >> self.rank) & 1:
+            return False
+        room = eng.admit_capacity() - self.awaiting_kv()
+        # own-GPU admission is what a load-aware strategy picks for a GPU with
+        # free slots; round robin / weighted random keep their rotation (the
+        # extra step then runs only the work already admitted)
+        if room > 0 and self.plan_state.strategy not in self.ROTATING_STRATEGIES:
+            b = self._budgets()
+            elsewhere = self.pinned.sum(axis=0) - self.pinned[self.rank]
+            budgets = [0 if (t < planner.NTIERS and elsewhere[t] > 0) else (room if b[t] < 0 else min(room, b[t]))
+                       for t in range(len(self.tiers))]
+            if any(budgets):
+                msgs, tier_idx, _e = self.qm.pop_tiers(self.tiers, room, self.aging_ns, budgets, self.lifo_ns)
+                self.counters["extra_admitted"] += self._admit_own(msgs, [int(t) for t in tier_idx])
+        if eng.ready_tokens() < self.EXTRA_STEP_MIN_FRAC * eng.token_budget:
+            return False
+        eng.launch()
+        self.finish_backend()
+        self.counters["extra_steps"] += 1
+        return True
 
     def quiesce(self, pump=None, poll_s: float = 0.0002) -> None:
         """Wait until no forward step is queued on the GPU, ingesting (and on

@@ -308,6 +308,11 @@ class ShmComm(Comm):
         except ValueError as e:          # std::length_error: some rank's payload overflowed (every rank raises)
             raise PeerLost(f"rank {self.rank}: control-plane payload overflow ({e})") from e
 
+    def peers_behind(self) -> bool:
+        """Non-blocking: some other rank has not reached the next collective
+        yet (joining it now means waiting)."""
+        return self.c.arrived_next() < self.world - 1
+
     def all_gather_i64(self, vec):
         v = np.ascontiguousarray(vec, dtype=np.int64).reshape(-1)
         parts = self._x(self.c.all_gather, v.tobytes())
@@ -376,6 +381,11 @@ class FakeComm(Comm):
     def make(world: int, timeout_s: Optional[float] = None) -> List["FakeComm"]:
         hub = _Hub(world, timeout_s)
         return [FakeComm(hub, r) for r in range(world)]
+
+    def peers_behind(self) -> bool:
+        """Some other rank has not reached the barrier of the next collective
+        (every FakeComm collective starts with one)."""
+        return self.hub.bar.n_waiting < self.world - 1
 
     def _wait(self):
         try:

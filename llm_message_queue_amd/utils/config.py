@@ -248,6 +248,11 @@ class GPUConfig:
     # move a conversation's KV to the GPU its next turn is placed on (RCCL
     # send/recv over xGMI) instead of replaying the dialog there
     kv_migration: bool = True
+    # multi-rank: a GPU whose run-ahead queue has room at the per-tick
+    # exchange while a peer is still behind launches one extra forward from
+    # its own queue (lock-step would leave a faster GPU idle for the speed
+    # difference every tick; Gateway._extra_local_step)
+    extra_steps: bool = True
     rebalance_interval_ms: int = 100
 
 

@@ -1,0 +1,114 @@
+"""Multi-rank ticks with GPUs of different speed (SimEngine: the engine's host
+side for real, the forward as a simulated device clock; FakeComm ranks in
+threads).
+
+Every tick is one collective, so under pure lock-step a faster GPU idles for
+the speed difference every tick and the job serves N x its SLOWEST GPU.  With
+``gpu.extra_steps`` a rank whose run-ahead queue has room while a peer is
+still behind launches one extra forward from its own queue
+(``Gateway._extra_local_step``), so the job approaches the SUM of its GPUs'
+capacities (bench.py ``--sim-gpu`` measures it at 8 ranks)."""
+import threading
+import time
+
+import numpy as np
+
+from llm_message_queue_amd.backend.engine import Request
+from llm_message_queue_amd.backend.sim_engine import SimEngine
+from llm_message_queue_amd.gateway.router import Gateway
+from llm_message_queue_amd.gateway.workload import Workload
+from llm_message_queue_amd.parallel.comm import FakeComm
+from llm_message_queue_amd.utils.config import default_config
+
+
+def test_sim_engine_clock():
+    """Steps run back to back on the simulated device at step_ms(T) / speed
+    (tile-quantised), completion events fire at their end time, the run-ahead
+    queue bounds the host like a real GPU's."""
+    e = SimEngine(speed=2.0, tile_ms=4.0, base_ms=2.0, slots=64, token_budget=512)
+    assert e.step_ms(1) == 3.0 and e.step_ms(256) == 3.0 and e.step_ms(257) == 5.0
+    e.time_steps = True
+    e.admit([Request(req_id=i, prompt=np.arange(20, dtype=np.int32), gen_tokens=3) for i in range(40)])
+    assert e.ready_tokens() == 512                     # 800 prompt tokens pending, capped at the budget
+    t0 = time.monotonic()
+    e.launch()
+    e.launch()
+    assert e.queued_steps() == 2                       # asynchronous: nothing finished yet
+    e.launch()                                         # queue full: waits for the oldest step
+    e.finish(block=True)
+    wall = (time.monotonic() - t0) * 1e3
+    # T = 512 (prefill), 313 (25 decodes + the last 288 prompt tokens), 40
+    # decodes: 2, 2 and 1 tiles -> 5 + 5 + 3 ms at speed 2
+    assert e.gpu_steps == 3 and abs(e.gpu_step_ms - 13.0) < 1e-6
+    assert wall >= 12.5                                # the three steps ran back to back
+    assert e.completed_total == 25 and e.step_id == 3   # completions count at launch (the last token's step)
+
+
+def _cfg(extra: bool):
+    c = default_config()
+    c.queue.enable_metrics = False
+    c.loadbalancer.algorithm = "least_connections"
+    c.loadbalancer.health_check_interval = 0
+    c.gpu.extra_steps = extra
+    for lv in c.queue.levels:
+        lv.max_concurrent = 4096
+    return c
+
+
+def _run(extra: bool, ticks: int = 40):
+    W = 2
+    comms = FakeComm.make(W, timeout_s=60)
+    speeds = [1.0, 0.6]
+    gws = [Gateway(_cfg(extra), engine=SimEngine(speed=speeds[r], tile_ms=2.0, base_ms=1.0, slots=256,
+                                                 token_budget=1024),
+                   comm=comms[r], use_gpu_preprocess=False, prompt_cap=16, gen_tokens=2) for r in range(W)]
+    wls = [Workload(seed=r) for r in range(W)]
+
+    def loop(r):
+        g = gws[r]
+        for _ in range(ticks):
+            need = 512 - g.pending() - g.engine.inflight()
+            if need > 0:
+                g.submit(wls[r].make(need))      # saturated: every rank keeps a local backlog
+            g.tick()
+
+    ths = [threading.Thread(target=loop, args=(r,)) for r in range(W)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return gws
+
+
+def test_faster_gpu_takes_extra_steps_and_job_serves_more():
+    on = _run(True)
+    off = _run(False)
+    # pure lock-step: one forward per tick on every rank
+    assert all(g.engine.step_id <= g.counters["ticks"] for g in off)   # (the first tick has nothing yet)
+    assert all(g.counters["extra_steps"] == 0 for g in off)
+    # the fast rank (speed 1.0 vs 0.6) fills its idle time with extra forwards;
+    # the slow one is ahead of its peer only in transients
+    fast, slow = on
+    assert fast.counters["extra_steps"] >= 8, fast.counters
+    assert fast.engine.step_id > fast.counters["ticks"]
+    assert slow.counters["extra_steps"] * 2 < fast.counters["extra_steps"], (slow.counters, fast.counters)
+    # more tokens through the job in the same number of ticks
+    assert sum(g.engine.total_tokens for g in on) > 1.15 * sum(g.engine.total_tokens for g in off)
+
+
+def test_extra_steps_skip_a_parked_gpu():
+    """A GPU the autoscaler parked takes no new local work in extra steps."""
+    c = _cfg(True)
+    comms = FakeComm.make(2, timeout_s=30)
+    g = Gateway(c, engine=SimEngine(slots=64, token_budget=256), comm=comms[0], use_gpu_preprocess=False,
+                prompt_cap=16, gen_tokens=2)
+    g._exclude_mask = lambda: 1                            # rank 0's own GPU excluded
+    g.submit(Workload(seed=1).make(64))
+    g.ingest()
+    assert g.pending() > 0
+    assert comms[0].peers_behind()                         # rank 1 has not reached the exchange
+    assert g._extra_local_step() is False
+    assert g.counters["extra_admitted"] == 0 and g.engine.step_id == 0
+    g._exclude_mask = lambda: 0                            # back in placement: the extra step runs
+    assert g._extra_local_step() is True
+    assert g.counters["extra_admitted"] > 0 and g.engine.step_id == 1
