@@ -1291,8 +1291,12 @@ class Gateway:
                 self.counters["extra_admitted"] += self._admit_own(msgs, [int(t) for t in tier_idx])
         if eng.ready_tokens() < self.EXTRA_STEP_MIN_FRAC * eng.token_budget:
             return False
-        eng.launch()
-        self.finish_backend()
+        try:
+            eng.launch()
+            self.finish_backend()
+        except RuntimeError as e:                   # HIP error / OOM: as in _tick, this GPU leaves placement
+            self._set_healthy(False, f"backend error: {e}")
+            return False
         self.counters["extra_steps"] += 1
         return True
 

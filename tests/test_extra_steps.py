@@ -112,3 +112,20 @@ def test_extra_steps_skip_a_parked_gpu():
     g._exclude_mask = lambda: 0                            # back in placement: the extra step runs
     assert g._extra_local_step() is True
     assert g.counters["extra_admitted"] > 0 and g.engine.step_id == 1
+
+
+def test_extra_step_backend_error_evacuates_instead_of_raising():
+    """A HIP error in the extra forward takes the GPU out of placement (its
+    admitted requests go back to the queue) like an error in the tick's own
+    launch -- the tick does not raise."""
+    comms = FakeComm.make(2, timeout_s=30)
+    g = Gateway(_cfg(True), engine=SimEngine(slots=64, token_budget=256), comm=comms[0], use_gpu_preprocess=False,
+                prompt_cap=16, gen_tokens=2)
+    g.submit(Workload(seed=2).make(64))
+    g.ingest()
+    queued = g.pending()
+    g.engine.inject(fail_launch=1)
+    assert g._extra_local_step() is False
+    assert not g.healthy and "injected" in g.health_reason
+    assert g.counters["extra_admitted"] > 0 and g.counters["evacuated"] == g.counters["extra_admitted"]
+    assert g.pending() == queued                          # every admitted request is queued again
