@@ -121,3 +121,20 @@ def test_bench_refuses_world_mismatch():
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_sim_gpu_two_ranks_extra_steps():
+    """``--sim-gpu``: each rank's backend is a SimEngine at the serving config
+    (1536 slots, 4096-token steps, 8B step clock).  With rank 1 simulated 30 %
+    slower, rank 0 takes extra local steps instead of idling for rank 1's
+    pace, and every request is accounted for."""
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+              "--cpu-dry-run", "--sim-gpu", "1,0.7", "--steps", "40", "--warmup", "2", "--gateway-only-s", "0"],
+             timeout=420)
+    assert d["config"]["sim_gpu"] == "1,0.7" and d["config"]["extra_steps"]
+    assert d["config"]["global_batch"] == 2 * 1536 and d["config"]["token_budget"] == 4096
+    ls = d["lockstep"]
+    assert ls["extra_steps_by_rank"][0] > ls["extra_steps_by_rank"][1]
+    assert ls["gpu_steps_by_rank"][0] > ls["gpu_steps_by_rank"][1]
+    assert d["requests_accounted"]["lost"] == 0 and d["value"] > 0
