@@ -539,6 +539,10 @@ def main(argv=None) -> int:
     host_timed = gw.host_profile()
     engine.time_steps = False
     arrived_local = gw.counters["submitted"] - sub0
+    # dispatches and backend tokens of the WINDOW (the untimed drain below
+    # dispatches the requests still queued at t1; those must not count)
+    dispatched_local = gw.counters["dispatched"] - d0
+    tokens_local = engine.total_tokens - tok0
     remote_local = gw.counters["remote_sent"] - r0
     extra_local = gw.counters["extra_steps"] - x0
     gc.enable()
@@ -560,8 +564,6 @@ def main(argv=None) -> int:
     arrivals.rate = pump_stop
     acct = comm.all_gather_i64(np.array([gw.counters[k] - c0[k] for k in ("submitted", "completed", "rejected",
                                                                           "expired")], dtype=np.int64)).sum(axis=0)
-    dispatched_local = gw.counters["dispatched"] - d0
-    tokens_local = engine.total_tokens - tok0
 
     agg = comm.all_gather_i64(np.array([int(elapsed_local * 1e9), dispatched_local, tokens_local, arrived_local],
                                        dtype=np.int64))
@@ -584,12 +586,15 @@ def main(argv=None) -> int:
     gw.flush_latency()
     arr_d = comm.all_gather_i64(gw.rec_done.arr.reshape(-1)).sum(axis=0).reshape(gw.rec_done.arr.shape)
     lat_done = LatencyRecorder(len(gw.tiers)).summary(arr_d, arr_d)
-    # Sustained throughput: requests dispatched in the window, capped by the
-    # requests that arrived in it.  A finite window also dispatches part of
-    # the queue it started with (the window edges drain the GPU while
-    # admitting), which would read as more than the offered rate; the cap
-    # removes that bias, and under overload (dispatches < arrivals) the
-    # dispatch rate is what counts.
+    # Sustained throughput: requests dispatched inside the window (counted at
+    # t1, before the untimed drain), capped by the requests that arrived in
+    # it -- a window that starts with a queue must not read above the offered
+    # rate, and under overload (dispatches < arrivals) the dispatch rate is
+    # what counts.  (Until round 3 the dispatch count was read after the
+    # drain, so it included the requests still queued at t1 and the min()
+    # always returned the arrival rate; profiles/r3_bench_window_counts.jsonl.)
+    # Latency histograms cover every dispatch from t0 through the drain:
+    # requests that arrived in the window and were dispatched after t1 count.
     value = min(dispatched, arrived) / elapsed if elapsed > 0 else 0.0
     out = {
         "metric": METRIC,
