@@ -140,11 +140,14 @@ def cmd_serve(a, role: str = "serve") -> int:
     elif cpu_ranks and role == "serve":
         engine, page = _build_cpu_engine(cfg)
     ring, app_role = None, "serve"
-    front = world > 1 and role == "serve" and engine is not None and cfg.server.front_door == "native"
-    job = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
+    # the C++ front door fronts every `serve` with a backend -- one GPU or a
+    # whole node (the Python ASGI stack tops out at ~2k req/s for POST
+    # /api/v1/messages); `server.front_door: python` keeps uvicorn on the port
+    front = role == "serve" and engine is not None and cfg.server.front_door == "native"
+    job = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT") or str(os.getpid())
     conv_ring = None
     if front:
-        # multi-GPU front door: ONE shared request ring every rank drains
+        # the front door: ONE shared request ring every rank drains
         # (MPMC), plus rank 0's ring for conversation turns (rank 0 owns
         # conversation state); the C++ ingress on rank 0 feeds both
         from ..gateway.shm_bridge import RingPair

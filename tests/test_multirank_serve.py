@@ -169,3 +169,62 @@ def test_two_rank_serve_front_door_on_gpu():
         except Exception:
             os.killpg(srv.pid, signal.SIGKILL)
             srv.wait(timeout=10)
+
+
+def test_single_rank_serve_native_front_door():
+    """``cli serve`` without a launcher (one backend) is fronted by the C++
+    ingress too: POST /api/v1/messages never touches the Python ASGI stack
+    (~2k req/s), every other route is proxied to the API server behind it."""
+    port = _port()
+    env = dict(os.environ, LLMQ_LOGGING__LEVEL="warning", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    cmd = [sys.executable, "-m", "llm_message_queue_amd.cli", "serve", "--cpu-ranks", "--port", str(port),
+           "--host", "127.0.0.1"]
+    srv = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                           start_new_session=True)
+    base = f"http://127.0.0.1:{port}"
+    try:
+        ev = None
+        t0 = time.time()
+        while time.time() - t0 < 120:
+            line = srv.stdout.readline()
+            if not line:
+                if srv.poll() is not None:
+                    break
+                continue
+            if line.startswith("{") and '"listening"' in line:
+                ev = json.loads(line)
+                break
+        assert ev is not None, srv.stderr.read()[-3000:] if srv.poll() is not None else "no listening line"
+        assert ev["front_door"] == "native" and ev["world"] == 1 and ev["port"] == port and ev["api_port"] != port
+        st, conv = _req("POST", base + "/api/v1/conversations", {"user_id": "solo"})
+        assert st == 201
+        ids = []
+        for i in range(30):
+            st, r = _req("POST", base + "/api/v1/messages", {"content": f"urgent: ping {i}", "user_id": f"u{i % 3}"})
+            assert st == 202, r
+            ids.append(r["message_id"])
+        st, r = _req("POST", base + "/api/v1/messages", {"content": "and then?", "user_id": "solo",
+                                                         "conversation_id": conv["conversation_id"]})
+        assert st == 202
+        ids.append(r["message_id"])
+        deadline = time.time() + 60
+        done = set()
+        while time.time() < deadline and len(done) < len(ids):
+            for mid in ids:
+                if mid not in done:
+                    st, m = _req("GET", base + f"/api/v1/messages/{mid}")
+                    if st == 200 and m["status"] == "completed":
+                        done.add(mid)
+            time.sleep(0.1)
+        assert len(done) == len(ids)
+        st, c = _req("GET", base + f"/api/v1/conversations/{conv['conversation_id']}")
+        assert st == 200 and any(m["id"] == ids[-1] for m in c.get("messages", []))
+    finally:
+        try:
+            os.killpg(srv.pid, signal.SIGTERM)
+            srv.wait(timeout=60)
+        except Exception:
+            os.killpg(srv.pid, signal.SIGKILL)
+            srv.wait(timeout=10)
