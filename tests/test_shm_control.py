@@ -195,3 +195,33 @@ def test_shm_setup_failure_falls_back_to_torch_group_on_every_rank():
     assert len(res) == 2, codes
     assert {kind for _, kind, _ in res} == {"TorchComm"}
     assert all(g == [0, 1] for _, _, g in res)
+
+
+def _behind_worker(rank, world, port, out):
+    _env(rank, world, port)
+    from llm_message_queue_amd.parallel.comm import ShmComm, init_from_env
+    comm = init_from_env(backend="gloo", control="shm", timeout_s=30)
+    assert isinstance(comm, ShmComm)
+    comm.all_gather_i64(np.array([rank]))
+    if rank == 0:
+        behind_before = comm.peers_behind()         # rank 1 sleeps before the next collective
+        t0 = time.monotonic()
+        while comm.peers_behind() and time.monotonic() - t0 < 20:
+            time.sleep(0.005)
+        waited = time.monotonic() - t0
+        behind_after = comm.peers_behind()         # rank 1 now waits inside the collective
+        comm.all_gather_i64(np.array([rank]))
+        out.put((rank, behind_before, behind_after, waited))
+    else:
+        time.sleep(1.0)
+        comm.all_gather_i64(np.array([rank]))
+        out.put((rank, comm.peers_behind(), None, 0.0))
+
+
+def test_shm_peers_behind_is_a_non_blocking_arrival_probe():
+    """``ShmComm.peers_behind`` (the extra-local-step trigger) reports, without
+    joining, whether some peer has not reached the next collective yet."""
+    res, codes = _run(_behind_worker, 2, timeout=90)
+    assert len(res) == 2, codes
+    r0 = [r for r in res if r[0] == 0][0]
+    assert r0[1] is True and r0[2] is False and 0.5 < r0[3] < 20, r0
