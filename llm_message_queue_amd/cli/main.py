@@ -137,7 +137,7 @@ def cmd_serve(a, role: str = "serve") -> int:
         torch.cuda.set_device(local)
         engine, page = _build_engine(cfg, a.model, torch.device("cuda", local))
         engine.warm_shapes()      # cold-start GEMM shapes before the first request (idle -> busy)
-    elif cpu_ranks and role == "serve":
+    elif cpu_ranks and role in ("serve", "queue-manager"):
         engine, page = _build_cpu_engine(cfg)
     ring, app_role = None, "serve"
     # the C++ front door fronts every `serve` with a backend -- one GPU or a
@@ -208,9 +208,9 @@ def cmd_serve(a, role: str = "serve") -> int:
         t = threading.Thread(target=server.run, daemon=True)
         t.start()
         port = api_port
+        _wait_port(api_host, api_port, t)          # "listening" means accepting connections
         if front:
             from ..gateway.native_ingress import NativeIngress
-            _wait_port(api_host, api_port, t)
             ingress = NativeIngress(cfg.server.port, ring.name, getattr(a, "ingress_threads", 0)
                                     or cfg.server.ingress_threads, cfg.server.host, cfg=cfg,
                                     conv_ring=f"{ring.name}-conv", upstream=(api_host, api_port))
@@ -351,7 +351,8 @@ def main(argv=None) -> int:
                        help="multi-GPU serve: C++ front door feeding a ring every rank drains (native, "
                             "default) or every route on rank 0's ASGI server (python)")
         p.add_argument("--cpu-ranks", action="store_true",
-                       help="serve: tiny CPU engines per rank over gloo (multi-rank rehearsal without a GPU)")
+                       help="serve / queue-manager: tiny CPU engines per rank over gloo (multi-rank rehearsal "
+                            "without a GPU)")
     p = sub.add_parser("scheduler")
     p.add_argument("--config", default=None)
     p.add_argument("--gateway", default="http://127.0.0.1:8080")

@@ -228,3 +228,68 @@ def test_single_rank_serve_native_front_door():
         except Exception:
             os.killpg(srv.pid, signal.SIGKILL)
             srv.wait(timeout=10)
+
+
+def _wait_listening(proc, timeout=180):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        line = proc.stdout.readline()
+        if not line:
+            if proc.poll() is not None:
+                return None
+            continue
+        if line.startswith("{") and '"listening"' in line:
+            return json.loads(line)
+    return None
+
+
+def test_split_deployment_two_queue_manager_ranks():
+    """The documented split deployment (docs/deployment.md): ``queue-manager``
+    under torchrun (here 2 CPU ranks) drains ONE shared request ring that an
+    ``api-gateway`` process fills; every rank pushes status events back
+    through the event ring, so the gateway that accepted a message reports it
+    completed whichever rank served it."""
+    ring = f"splittest{os.getpid()}"
+    qport, gport, mport = _port(), _port(), _port()
+    env = dict(os.environ, LLMQ_LOGGING__LEVEL="warning", OMP_NUM_THREADS="1")
+    qm = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                           "--master-addr=127.0.0.1", f"--master-port={mport}", "-m", "llm_message_queue_amd.cli",
+                           "queue-manager", "--cpu-ranks", "--ring", ring, "--port", str(qport), "--host",
+                           "127.0.0.1"], cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                          text=True, start_new_session=True)
+    gw = None
+    try:
+        ev = _wait_listening(qm)
+        assert ev is not None and ev["world"] == 2, qm.stderr.read()[-3000:] if qm.poll() is not None else ev
+        gw = subprocess.Popen([sys.executable, "-m", "llm_message_queue_amd.cli", "api-gateway", "--no-gpu",
+                               "--ring", ring, "--port", str(gport), "--host", "127.0.0.1"], cwd=ROOT, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+        assert _wait_listening(gw) is not None, gw.stderr.read()[-3000:] if gw.poll() is not None else "no gw"
+        base = f"http://127.0.0.1:{gport}"
+        ids = []
+        for i in range(40):
+            st, r = _req("POST", base + "/api/v1/messages", {"content": f"please check item {i}", "user_id": f"s{i}"})
+            assert st == 202, r
+            ids.append(r["message_id"])
+        deadline = time.time() + 90
+        done = set()
+        while time.time() < deadline and len(done) < len(ids):
+            for mid in ids:
+                if mid not in done:
+                    st, m = _req("GET", base + f"/api/v1/messages/{mid}")
+                    if st == 200 and m["status"] == "completed":
+                        done.add(mid)
+            time.sleep(0.2)
+        assert len(done) == len(ids), f"{len(done)} of {len(ids)} completed"
+        st, stats = _req("GET", f"http://127.0.0.1:{qport}/api/v1/queues/stats")
+        assert st == 200 and stats["dispatch"]["completed"] > 0       # rank 0's own share
+    finally:
+        for p in (gw, qm):
+            if p is None:
+                continue
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+                p.wait(timeout=60)
+            except Exception:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait(timeout=10)
