@@ -12,7 +12,6 @@ which is also HIP's default order; a process restricted with
 from __future__ import annotations
 
 import threading
-import time
 from typing import Callable, Dict, List, Optional
 
 from .. import _native
