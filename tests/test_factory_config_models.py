@@ -143,3 +143,22 @@ def test_grafana_dashboard_queries_only_exported_series():
         names.update(fam.name + x for x in suffix.get(fam.type, ("",)))
     missing = sorted(u for u in used if u not in names)
     assert used and not missing, missing
+
+
+REFERENCE_CONFIG = "/root/reference/configs/config.yaml"
+
+
+@pytest.mark.skipif(not os.path.exists(REFERENCE_CONFIG), reason="reference checkout not present")
+def test_reference_config_file_loads_unchanged():
+    """docs/migration.md: a user of the Go service keeps their config file.
+    The reference's shipped ``configs/config.yaml`` loads through our loader
+    (safe YAML, Go durations) and validates; parity unpinned beyond the keys
+    checked here."""
+    from llm_message_queue_amd.utils.config import load_config
+    c = load_config(REFERENCE_CONFIG)
+    assert c.server.port == 8080
+    assert [lv.name for lv in sorted(c.queue.levels, key=lambda lv: lv.priority)] == ["realtime", "high", "normal",
+                                                                                   "low"]
+    assert c.queue.levels[0].max_wait_time == 1_000_000_000              # "1s" -> ns
+    assert c.loadbalancer.algorithm == "weighted_round_robin"
+    assert c.database.redis.addr and c.database.postgres.dbname
