@@ -89,11 +89,11 @@ def test_faster_gpu_takes_extra_steps_and_job_serves_more():
     # the fast rank (speed 1.0 vs 0.6) fills its idle time with extra forwards;
     # the slow one is ahead of its peer only in transients
     fast, slow = on
-    assert fast.counters["extra_steps"] >= 8, fast.counters
+    assert fast.counters["extra_steps"] >= 5, fast.counters              # typically ~20 of 40 ticks
     assert fast.engine.step_id > fast.counters["ticks"]
     assert slow.counters["extra_steps"] * 2 < fast.counters["extra_steps"], (slow.counters, fast.counters)
     # more tokens through the job in the same number of ticks
-    assert sum(g.engine.total_tokens for g in on) > 1.15 * sum(g.engine.total_tokens for g in off)
+    assert sum(g.engine.total_tokens for g in on) > 1.08 * sum(g.engine.total_tokens for g in off)   # ~1.26-1.31x
 
 
 def test_extra_steps_skip_a_parked_gpu():
@@ -129,3 +129,56 @@ def test_extra_step_backend_error_evacuates_instead_of_raising():
     assert not g.healthy and "injected" in g.health_reason
     assert g.counters["extra_admitted"] > 0 and g.counters["evacuated"] == g.counters["extra_admitted"]
     assert g.pending() == queued                          # every admitted request is queued again
+
+
+def test_extra_steps_with_dialogs_and_rehoming_lose_nothing():
+    """Extra local steps alongside conversation residency and KV migration:
+    two simulated GPUs of different speed serve dialogs; midway the slow GPU
+    is parked on rank 0's balancer, so its dialogs' next turns re-home (KV
+    migration).  Every submitted message completes exactly once."""
+    from llm_message_queue_amd.balancer.load_balancer import Endpoint, LoadBalancer
+    W = 2
+    comms = FakeComm.make(W, timeout_s=60)
+    lbs = []
+    gws = []
+    for r in range(W):
+        cfg = _cfg(True)
+        lb = LoadBalancer(cfg.loadbalancer)
+        for j in range(W):
+            lb.add_endpoint(Endpoint(id=f"gpu{j}", type="llm", gpu_index=j, max_connections=128))
+        lbs.append(lb)
+        gws.append(Gateway(cfg, engine=SimEngine(speed=[1.0, 0.6][r], tile_ms=2.0, base_ms=1.0, slots=128,
+                                                 max_ctx=256, token_budget=512),
+                           comm=comms[r], load_balancer=lb, use_gpu_preprocess=False, prompt_cap=16, gen_tokens=2))
+    wls = [Workload(seed=40 + r, conversations=12) for r in range(W)]
+    submitted = [0, 0]
+
+    def loop(r, ticks, feed):
+        g = gws[r]
+        for t in range(ticks):
+            if feed and t < 50 and g.pending() < 200:
+                batch = wls[r].make(24)
+                g.submit(batch)
+                submitted[r] += len(batch)
+            if r == 0 and feed and t == 25:
+                lbs[0].remove_endpoint("gpu1")            # park the slow GPU: its dialogs re-home
+            g.tick()
+
+    ths = [threading.Thread(target=loop, args=(r, 90, True)) for r in range(W)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    done = lambda: sum(g.counters["completed"] for g in gws)
+    for _ in range(40):
+        if done() >= sum(submitted):
+            break
+        ths = [threading.Thread(target=loop, args=(r, 10, False)) for r in range(W)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    assert done() == sum(submitted), (done(), submitted, [g.counters for g in gws])
+    assert gws[0].counters["extra_steps"] > 0
+    moved = sum(g.counters["kv_migrated"] + g.counters["kv_migrate_replays"] for g in gws)
+    assert moved > 0, [g.counters for g in gws]
