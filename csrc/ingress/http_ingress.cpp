@@ -268,14 +268,30 @@ struct JsonScanner {
   }
 };
 
+// The same rule as models/message.py:parse_priority (the Python front door and
+// the rank's decode): ASCII-trimmed, case-insensitive level name ("urgent" is
+// realtime, "medium" normal) or a decimal integer 0..4; anything else -> -1.
 int priority_from_string(const std::string& s) {
+  size_t a = 0, b = s.size();
+  auto ws = [](char c) { return c == ' ' || (c >= '\t' && c <= '\r'); };
+  while (a < b && ws(s[a])) ++a;
+  while (b > a && ws(s[b - 1])) --b;
   std::string l;
-  for (char c : s) l.push_back((char)tolower((unsigned char)c));
-  if (l == "realtime" || l == "1") return 1;
-  if (l == "high" || l == "urgent" || l == "2") return 2;
-  if (l == "normal" || l == "3") return 3;
-  if (l == "low" || l == "4") return 4;
-  return -1;
+  for (size_t i = a; i < b; ++i) l.push_back((char)tolower((unsigned char)s[i]));
+  if (l == "realtime" || l == "urgent") return 1;
+  if (l == "high") return 2;
+  if (l == "normal" || l == "medium") return 3;
+  if (l == "low") return 4;
+  const bool neg = !l.empty() && l[0] == '-';
+  size_t i = (!l.empty() && (l[0] == '+' || neg)) ? 1 : 0;
+  if (i == l.size()) return -1;
+  int v = 0;
+  for (; i < l.size(); ++i) {
+    if (l[i] < '0' || l[i] > '9') return -1;
+    v = v * 10 + (l[i] - '0');
+    if (v > 4) return -1;
+  }
+  return (neg && v != 0) ? -1 : v;                   // "-0" is 0
 }
 
 // Go duration text as utils/duration.parse_duration_ns accepts it:
@@ -404,7 +420,7 @@ Scan scan_message(const char* b, size_t n) {
         if (!js.lit("null")) return r;
       } else {
         double d = 0;
-        if (!js.num(&d) || d != (double)(int64_t)d || d < 0 || d > 4) {
+        if (!js.num(&d) || !(d >= 0 && d <= 4) || d != (double)(int)d) {   // range first: no out-of-range cast
           r.error = "invalid priority";
           return r;
         }

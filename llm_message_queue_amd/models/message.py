@@ -16,6 +16,8 @@ from __future__ import annotations
 
 import datetime as _dt
 import itertools
+import math
+import re
 import time
 import uuid
 from typing import Any, Dict, List, Optional
@@ -63,26 +65,35 @@ class PriorityParseError(ValueError):
     pass
 
 
+_ASCII_WS = " \t\n\r\x0b\x0c"
+_INT_TEXT = re.compile(r"[+-]?[0-9]+\Z")
+
+
 def parse_priority(value: Any, default: int = 0) -> int:
-    """Accept an int, a numeric string, or a level name (case-insensitive)."""
+    """Accept an integral number 0..4 (0 = let the preprocessor decide), a
+    decimal string of one, or a level name (case-insensitive, ASCII-trimmed;
+    ``urgent`` = realtime, ``medium`` = normal).  Anything else raises.  The
+    C++ front door applies the same rule (``csrc/ingress/http_ingress.cpp:
+    priority_from_string``), so both front doors accept and assign alike."""
     if value is None:
         return default
     if isinstance(value, bool):
         raise PriorityParseError(f"invalid priority {value!r}")
-    if isinstance(value, int):
-        return int(value)
     if isinstance(value, float):
-        if value != int(value):
+        if not math.isfinite(value) or value != int(value):
+            raise PriorityParseError(f"invalid priority {value!r}")
+        value = int(value)
+    if isinstance(value, int):
+        if not 0 <= value <= PRIORITY_LOW:
             raise PriorityParseError(f"invalid priority {value!r}")
         return int(value)
     if isinstance(value, str):
-        s = value.strip().lower()
+        s = value.strip(_ASCII_WS).lower()
         if s in _PRIO_BY_NAME:
             return _PRIO_BY_NAME[s]
-        try:
-            return int(s)
-        except ValueError:
-            raise PriorityParseError(f"invalid priority {value!r}") from None
+        if _INT_TEXT.match(s) and len(s.lstrip("+-").lstrip("0")) <= 1:
+            return parse_priority(int(s))
+        raise PriorityParseError(f"invalid priority {value!r}")
     raise PriorityParseError(f"invalid priority {value!r}")
 
 

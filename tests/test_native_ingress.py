@@ -39,11 +39,46 @@ def test_lone_surrogate_in_another_field_does_not_poison_the_id():
 
 def test_json_scanner():
     scan = _native.ingress().scan_message
-    assert scan(b'{"content":"hi","priority":"urgent","id":"abc"}')[:4] == (True, "abc", 2, "")
+    assert scan(b'{"content":"hi","priority":"urgent","id":"abc"}')[:4] == (True, "abc", 1, "")
     assert scan(b'{"content":"a\\"b","metadata":{"x":[1,{"y":null}]},"priority":4,"user_id":"u"}')[0:3:2] == (True, 4)
     assert scan(b'{}')[:4] == (True, "", 0, "")
-    for bad in (b'', b'[1]', b'{"content":}', b'{"priority":"bogus"}', b'{"a":1,}', b'{"a":1} x', b'{"priority":9}'):
+    for bad in (b'', b'[1]', b'{"content":}', b'{"priority":"bogus"}', b'{"a":1,}', b'{"a":1} x', b'{"priority":9}',
+                b'{"priority":-1}', b'{"priority":"5"}', b'{"priority":"-2"}', b'{"priority":" "}'):
         assert not scan(bad)[0], bad
+
+
+def test_priority_rule_matches_python_front_door():
+    """Both front doors accept the same priorities and assign the same tier:
+    the native scanner's value equals ``parse_priority`` (what the Python
+    front door and the rank's decode use) and it rejects exactly what
+    ``parse_priority`` rejects."""
+    from hypothesis import given, settings, strategies as st
+    from llm_message_queue_amd.models.message import PriorityParseError, parse_priority
+    scan = _native.ingress().scan_message
+    names = ["realtime", "urgent", "high", "normal", "medium", "low", "URGENT", " High\t", "\nlow ", "Medium",
+             "0", "1", "4", "5", "-0", "-1", "+2", "+", "-", "", " ", "002", "0004", "00005", "1_0", "2.0", "1e0",
+             " high", "high ", "٣", "Kow", "hi gh", "realtime!"]
+    nums = [0, 1, 2, 3, 4, 5, -1, 9, 2.0, 2.5, -0.0, 1e300, 4.000001]
+
+    def check(v):
+        body = json.dumps({"content": "x", "priority": v}).encode()
+        ok, _id, prio = scan(body)[:3]
+        try:
+            want = parse_priority(v, 0)
+        except PriorityParseError:
+            assert not ok, (v, prio)
+            return
+        assert ok and prio == want, (v, ok, prio, want)
+
+    for v in names + nums:
+        check(v)
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.text(alphabet=st.sampled_from(list("0123456789+- \t\nLOWHIGHlowhighmediumurgent ")), max_size=9)
+           | st.integers(-10, 10))
+    def prop(v):
+        check(v)
+    prop()
 
 
 @pytest.fixture
