@@ -477,6 +477,17 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         return G.lb.get_endpoint_stats()
 
     # ------------------------------------------------------------------ admin
+    async def _sync_preprocessor() -> Optional[JSONResponse]:
+        """Multi-GPU front door: every rank preprocesses the requests it
+        pops, so an admin change on this rank is copied to all of them
+        before the reply (a 500 names ranks that did not confirm; the next
+        change, which carries the whole state, repairs them)."""
+        sync = getattr(G, "sync_preprocessor", None)
+        missing = await asyncio.get_running_loop().run_in_executor(None, sync) if sync is not None else None
+        if missing:
+            return _err(500, f"preprocessor change not confirmed by GPU ranks {missing}")
+        return None
+
     @app.post("/api/v1/admin/preprocessor/rules")
     async def add_priority_rule(request: Request):
         try:
@@ -493,6 +504,9 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             G.preprocessor.add_keyword_pattern(prio, pattern)
         except Exception as e:
             return _err(400, f"Invalid pattern: {e}")
+        bad = await _sync_preprocessor()
+        if bad is not None:
+            return bad
         return JSONResponse({"status": "rule added"}, status_code=201)
 
     @app.get("/api/v1/admin/preprocessor/rules")
@@ -508,7 +522,10 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             ok = G.preprocessor.remove_keyword_pattern(parse_priority(body.get("priority")), str(body["pattern"]))
         except Exception as e:
             return _err(400, f"Invalid rule format: {e}")
-        return {"status": "rule removed"} if ok else _err(404, "rule not found")
+        if not ok:
+            return _err(404, "rule not found")
+        bad = await _sync_preprocessor()
+        return bad if bad is not None else {"status": "rule removed"}
 
     @app.post("/api/v1/admin/preprocessor/user-priorities")
     async def set_user_priority(request: Request):
@@ -529,7 +546,8 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         if p not in (1, 2, 3, 4):
             p = 3
         G.preprocessor.set_user_priority(str(user_id), p)
-        return {"status": "user priority set"}
+        bad = await _sync_preprocessor()
+        return bad if bad is not None else {"status": "user priority set"}
 
     @app.delete("/api/v1/admin/queues/{queue_type}/{mid}")
     def remove_message(queue_type: str, mid: str):

@@ -162,11 +162,15 @@ def cmd_serve(a, role: str = "serve") -> int:
         ring = RingPair(a.ring or cfg.server.shared_ring, cfg.server.shared_ring_bytes, "open")
         app_role = "ingress" if role == "api-gateway" else "dispatcher"
     gapp = GatewayApp(cfg, use_gpu=use_gpu, engine=engine, comm=comm, start=False, role=app_role, ring=ring)
-    if front:
+    if conv_ring is not None:
+        gapp.extra_rings.append(conv_ring)
+    # every GPU rank that drains a ring answers rank 0's API through the peer
+    # directory: status queries for the messages it popped, and the
+    # preprocessor's admin state (it preprocesses what it pops)
+    peered = front or (role == "queue-manager" and ring is not None and comm is not None and comm.world > 1)
+    if peered:
         from ..gateway.peers import PeerDirectory
-        if conv_ring is not None:
-            gapp.extra_rings.append(conv_ring)
-        gapp.peers = PeerDirectory(ring.name, rank, world, handler=gapp.peer_op)
+        gapp.peers = PeerDirectory(ring.name, rank, comm.world if comm is not None else 1, handler=gapp.peer_op)
     if engine is not None:
         # every rank's balancer lists EVERY GPU of the job (its own bound to
         # the zero-copy load page): the multi-GPU planner reads the view of
@@ -239,9 +243,9 @@ def cmd_serve(a, role: str = "serve") -> int:
     gapp.stop()
     if page is not None:
         page.close(unlink=True)
+    if gapp.peers is not None:
+        gapp.peers.close(unlink=rank == 0)
     if front:
-        if gapp.peers is not None:
-            gapp.peers.close(unlink=rank == 0)
         for r in (ring, conv_ring):
             if r is not None:
                 r.close(unlink=rank == 0)

@@ -464,7 +464,22 @@ class GatewayApp:
         if op == "reset_latency":
             self.reset_latency()
             return True
+        if op == "pre_state":
+            self.preprocessor.load_state(args[0])
+            return True
         raise ValueError(f"unknown op {op!r}")
+
+    def sync_preprocessor(self) -> List[int]:
+        """Copy this rank's preprocessor admin state (keyword rules, user
+        priorities) to every peer rank, which preprocess the requests they
+        pop with their own preprocessor.  Returns the ranks that did NOT
+        confirm (empty: the whole job applies the same rules).  The full
+        state travels each time, so a later successful sync repairs a rank
+        that missed one."""
+        if self.peers is None or self.peers.world <= 1:
+            return []
+        got = self.peers.ask("pre_state", [self.preprocessor.export_state()])
+        return [r for r in range(1, self.peers.world) if got.get(r) is not True]
 
     def _rank_stats(self) -> dict:
         gw = self.gateway

@@ -7,6 +7,9 @@ hold is answered by a scatter-gather query over node-local shared-memory
 rings: rank 0 pushes ``[qid, op, args]`` into each peer's query ring, a
 responder thread on every peer answers from its own store into the shared
 reply ring.  Admin-rate traffic only (the hot submit path never queries).
+The same channel carries the preprocessor's admin state (``pre_state``):
+every rank preprocesses the requests it pops, so a keyword rule or user
+priority set through rank 0's API must reach every rank.
 
 The reference serves every route from one process and keeps no per-message
 state at all (`api/handlers.go:222-256` are stubs); this keeps the whole
@@ -22,7 +25,7 @@ import msgpack
 
 from .. import _native
 
-OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency")
+OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency", "pre_state")
 
 
 class PeerDirectory:

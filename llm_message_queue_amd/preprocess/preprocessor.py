@@ -93,6 +93,27 @@ class Preprocessor:
         with self._lock:
             return {k: list(v) for k, v in self._patterns.items()}, self._pattern_version
 
+    def export_state(self) -> Dict[str, Any]:
+        """The admin-settable state (keyword rules, per-user defaults, default
+        priority) as plain data: what a multi-rank job copies from the rank
+        that serves the admin API to every other rank (``load_state``)."""
+        with self._lock:
+            return {"patterns": [[int(k), [p.source for p in v]] for k, v in sorted(self._patterns.items())],
+                    "user_priorities": dict(self._user_priorities),
+                    "default_priority": int(self.default_priority)}
+
+    def load_state(self, state: Dict[str, Any]) -> None:
+        """Replace the admin-settable state with ``export_state()``'s output
+        (all patterns compiled before anything changes: a bad pattern raises
+        and leaves the current state in place)."""
+        pats = {int(k): [oracle.compile_pattern(s) for s in srcs] for k, srcs in state["patterns"]}
+        users = {str(u): int(p) for u, p in state["user_priorities"].items()}
+        with self._lock:
+            self._patterns = pats
+            self._user_priorities = users
+            self.default_priority = int(state["default_priority"])
+            self._pattern_version += 1
+
     # ------------------------------------------------------------------ single message (CPU)
     def _resolve_priority_head(self, msg: Message) -> Optional[bool]:
         """Steps 1-3 of ProcessMessage that need no content analysis.

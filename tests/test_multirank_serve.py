@@ -72,11 +72,17 @@ def test_two_rank_serve_native_front_door():
         st, conv = _req("POST", base + "/api/v1/conversations", {"user_id": "u1"})
         assert st == 201
         cid = conv["conversation_id"]
+        # admin changes on rank 0's API reach the preprocessor of EVERY rank
+        # (each preprocesses what it pops): a keyword rule and a user default
+        st, r = _req("POST", base + "/api/v1/admin/preprocessor/rules", {"pattern": "(?i)zebra", "priority": 1})
+        assert st == 201, r
+        st, r = _req("POST", base + "/api/v1/admin/preprocessor/user-priorities", {"user_id": "u3", "priority": "low"})
+        assert st == 200, r
         ids = []
         for burst in range(6):
             for i in range(10):
                 st, r = _req("POST", base + "/api/v1/messages",
-                             {"content": f"please summarise report {burst}-{i}", "user_id": f"u{i}"})
+                             {"content": f"please summarise the Zebra report {burst}-{i}", "user_id": f"u{i}"})
                 assert st == 202, r
                 ids.append(r["message_id"])
             time.sleep(0.05)
@@ -99,6 +105,10 @@ def test_two_rank_serve_native_front_door():
         assert len(done) == len(ids) + 1, f"{len(done)} of {len(ids) + 1} completed"
         ranks = {m["metadata"].get("ingest_rank") for m in done.values()}
         assert ranks == {0, 1}, ranks                        # ingest spread over both ranks
+        for mid in ids:                                      # ... and both applied the admin rules
+            m = done[mid]
+            want = (4, "user_default") if m["user_id"] == "u3" else (1, "content_keywords")
+            assert (m["priority"], m["metadata"].get("priority_reason")) == want, m
         assert done[turn]["metadata"]["ingest_rank"] == 0    # conversation turns go to rank 0
         st, c = _req("GET", base + f"/api/v1/conversations/{cid}")
         assert st == 200 and any(m["id"] == turn for m in c.get("messages", [])), c

@@ -156,3 +156,22 @@ def test_kernel_side_decisions_match_score_argmax(B):
                       ph).decide(2)
     for k in ("priority", "sentiment", "question", "word_count", "fallback", "ntok"):
         assert list(fast[k]) == list(slow[k]), k
+
+
+def test_export_load_state_round_trip():
+    """The admin state a multi-rank job copies from rank 0 to every rank
+    (gateway.app.sync_preprocessor): rules, user defaults, default priority."""
+    a, b = Preprocessor(use_gpu=False), Preprocessor(use_gpu=False)
+    a.add_keyword_pattern(1, "(?i)zebra")
+    a.remove_keyword_pattern(2, "(?i)soon")
+    a.set_user_priority("alice", 4)
+    a.set_default_priority(2)
+    b.load_state(a.export_state())
+    assert b.all_patterns() == a.all_patterns() and b.user_priorities() == {"alice": 4}
+    assert b.default_priority == 2
+    assert b.process_message(Message(content="a zebra", user_id="bob")).priority == 1
+    assert b.process_message(Message(content="a zebra", user_id="alice")).priority == 4
+    assert b.process_message(Message(content="soon", user_id="bob")).priority == 2     # rule gone -> default
+    with pytest.raises(Exception):
+        b.load_state({"patterns": [[1, ["(unclosed"]]], "user_priorities": {}, "default_priority": 3})
+    assert b.all_patterns() == a.all_patterns()                                          # unchanged on error
