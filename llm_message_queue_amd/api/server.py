@@ -394,8 +394,11 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
                           "avg_wait_ms": (st.total_wait_time / max(1, st.completed_count + st.processing_count
                                                                    + st.failed_count)) / 1e6})
         lat = G.gateway.rec.summary()
-        return {"queues": tiers, "total_pending": G.standard.total_pending(), "latency": lat,
-                "dead_letter": G.factory.dead_letter_queue.size(), "delayed": G.factory.delayed_queue.size()}
+        out = {"queues": tiers, "total_pending": G.standard.total_pending(), "latency": lat,
+               "dead_letter": G.factory.dead_letter_queue.size(), "delayed": G.factory.delayed_queue.size()}
+        if G.peers is not None:
+            out["job"] = G.job_stats()            # every GPU rank (the fields above are rank 0's)
+        return out
 
     @app.get("/api/v1/metrics")
     def metrics_json():
@@ -413,7 +416,8 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
                 "queue_lengths": {n: G.standard.size(n) for n in G.gateway.tiers},
                 "dead_letter": G.factory.dead_letter_queue.size(), "delayed": G.factory.delayed_queue.size(),
                 "gpu": {"healthy": G.gateway.healthy, "reason": G.gateway.health_reason,
-                        "inflight_slots": G.engine.inflight() if G.engine is not None else 0}}
+                        "inflight_slots": G.engine.inflight() if G.engine is not None else 0},
+                **({"job": G.job_stats()} if G.peers is not None else {})}
 
     # ------------------------------------------------------------------ resources
     @app.post("/api/v1/resources")
@@ -553,34 +557,29 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
     def remove_message(queue_type: str, mid: str):
         if queue_type not in ("standard", "delayed", "dead_letter", "priority"):
             return _err(400, "Invalid queue type")
+        # (multi-GPU: on whichever rank holds the message)
         if queue_type == "dead_letter":
-            dlq = G.factory.dead_letter_queue
-            i = dlq.index_of(mid)
-            if i < 0:
+            if G.dead_letters("remove", mid) is not True:
                 return _err(404, "Message not found")
-            dlq.remove(i)
             return {"status": "removed", "message_id": mid}
         if queue_type == "delayed":
             return _err(404, "Message not found")
-        mgr = G.factory.get_queue_manager(queue_type)
-        m = G.messages.get(mid)
-        if mgr is None or m is None or not m.queue_name or not mgr.has_queue(m.queue_name) \
-                or not mgr.mlq.remove(m.queue_name, m):
+        if not G.dequeue(queue_type, mid):
             return _err(404, "Message not found")
         return {"status": "removed", "message_id": mid}
 
     @app.post("/api/v1/admin/dead-letter/requeue/{mid}")
     def requeue_dead_letter(mid: str):
-        try:
-            G.factory.dead_letter_queue.requeue_by_id(mid, G.standard)
-        except QueueError as e:
-            return _err(404 if e.code == "INDEX_OUT_OF_RANGE" else 500, str(e))
+        res = G.dead_letters("requeue", mid)
+        if isinstance(res, dict):
+            return _err(500, str(res.get("error")))
+        if res is not True:
+            return _err(404, f"message {mid} not in dead letter queue")
         return {"status": "requeued", "message_id": mid}
 
     @app.post("/api/v1/admin/dead-letter/requeue-all")
     def requeue_all_dead_letter():
-        n = G.factory.dead_letter_queue.requeue_all(G.standard)
-        return {"status": "requeued", "count": n}
+        return {"status": "requeued", "count": G.dead_letters("requeue_all")}
 
     @app.post("/api/v1/admin/stats/reset")
     def reset_stats():
@@ -590,8 +589,9 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         return {"status": "reset"}
 
     @app.get("/api/v1/admin/dead-letter")
-    def list_dead_letter():
-        return {"items": [it.to_dict() for it in G.factory.dead_letter_queue.get_all()]}
+    def list_dead_letter(limit: int = 1000):
+        """The oldest ``limit`` dead letters of each GPU rank (``rank`` field)."""
+        return {"items": G.dead_letters("list", str(max(1, min(int(limit), 5000))))}
 
     @app.get("/api/v1/config")
     def get_config():

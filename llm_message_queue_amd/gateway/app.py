@@ -467,7 +467,67 @@ class GatewayApp:
         if op == "pre_state":
             self.preprocessor.load_state(args[0])
             return True
+        if op == "dlq":
+            return self._dlq_local(str(args[0]), str(args[1]) if len(args) > 1 else "")
+        if op == "dequeue":
+            return self._dequeue_local(str(args[0]), str(args[1]))
         raise ValueError(f"unknown op {op!r}")
+
+    # ------------------------------------------------------------------ job-wide admin
+    def _dlq_local(self, action: str, mid: str = ""):
+        from ..queue.core import QueueError
+        dlq = self.factory.dead_letter_queue
+        if action == "list":                       # mid = the item limit per rank
+            return [dict(it.to_dict(), rank=self.gateway.rank) for it in dlq.get_all()[:int(mid or 1000)]]
+        if action == "requeue_all":
+            return dlq.requeue_all(self.standard)
+        try:
+            if action == "requeue":
+                dlq.requeue_by_id(mid, self.standard)
+            elif action == "remove":
+                i = dlq.index_of(mid)
+                if i < 0:
+                    return False
+                dlq.remove(i)
+            else:
+                raise ValueError(f"unknown dead-letter action {action!r}")
+        except QueueError as e:
+            return False if e.code == "INDEX_OUT_OF_RANGE" else {"error": str(e)}
+        return True
+
+    def dead_letters(self, action: str, mid: str = ""):
+        """Dead-letter admin over the whole job: every GPU rank keeps the
+        dead letters of the requests it popped, so ``list`` and
+        ``requeue_all`` gather from all ranks and ``requeue`` / ``remove``
+        act on the rank that holds ``mid`` (True; False: nowhere; a dict
+        ``{"error"}``: the requeue push failed)."""
+        res = self._dlq_local(action, mid)
+        if self.peers is None:
+            return res
+        if action == "list":
+            for _r, part in sorted(self.peers.ask("dlq", [action, mid]).items()):
+                if isinstance(part, list):
+                    res.extend(part)
+            return res
+        if action == "requeue_all":
+            return res + sum(int(n) for n in self.peers.ask("dlq", [action]).values() if isinstance(n, int))
+        if res is False:
+            got = self.peers.first("dlq", [action, mid])
+            return got if got is not None else False
+        return res
+
+    def _dequeue_local(self, queue_type: str, mid: str) -> bool:
+        mgr = self.factory.get_queue_manager(queue_type)
+        m = self.messages.get(mid)
+        return bool(mgr is not None and m is not None and m.queue_name and mgr.has_queue(m.queue_name)
+                    and mgr.mlq.remove(m.queue_name, m))
+
+    def dequeue(self, queue_type: str, mid: str) -> bool:
+        """Remove a queued message from ``queue_type`` on whichever rank
+        queued it (``DELETE /api/v1/admin/queues/{type}/{id}``)."""
+        if self._dequeue_local(queue_type, mid):
+            return True
+        return bool(self.peers is not None and self.peers.first("dequeue", [queue_type, mid]))
 
     def sync_preprocessor(self) -> List[int]:
         """Copy this rank's preprocessor admin state (keyword rules, user
@@ -485,7 +545,9 @@ class GatewayApp:
         gw = self.gateway
         gw.flush_latency()
         return {"rank": gw.rank, "counters": dict(gw.counters), "accepted": self._accepted,
-                "arr": gw.rec.arr.tolist(), "enq": gw.rec.enq.tolist(), "done": gw.rec_done.arr.tolist()}
+                "arr": gw.rec.arr.tolist(), "enq": gw.rec.enq.tolist(), "done": gw.rec_done.arr.tolist(),
+                "pending": [self.standard.size(n) for n in gw.tiers],
+                "dead_letter": self.factory.dead_letter_queue.size(), "delayed": self.factory.delayed_queue.size()}
 
     def job_stats(self) -> dict:
         """Dispatch counters and latency summed over every rank of the job
@@ -502,8 +564,13 @@ class GatewayApp:
         enq = sum(np.asarray(p["enq"], dtype=np.int64) for p in parts)
         done = sum(np.asarray(p["done"], dtype=np.int64) for p in parts)
         rec = LatencyRecorder(len(self.gateway.tiers))
+        tiers = self.gateway.tiers
         return {"ranks": sorted(int(p["rank"]) for p in parts), "dispatch": cnt,
                 "accepted_by_rank": {int(p["rank"]): int(p["accepted"]) for p in parts},
+                "pending_by_tier": {n: sum(int(p.get("pending", [0] * len(tiers))[t]) for p in parts)
+                                    for t, n in enumerate(tiers)},
+                "dead_letter": sum(int(p.get("dead_letter", 0)) for p in parts),
+                "delayed": sum(int(p.get("delayed", 0)) for p in parts),
                 "latency": rec.summary(arr, enq), "latency_e2e": rec.summary(done, done)}
 
     def reset_latency_all(self) -> None:

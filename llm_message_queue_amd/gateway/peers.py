@@ -25,10 +25,12 @@ import msgpack
 
 from .. import _native
 
-OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency", "pre_state")
+OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency", "pre_state", "dlq", "dequeue")
 
 
 class PeerDirectory:
+    REPLY_MAX = 2 << 20              # bytes per answer (the reply ring holds 8 MiB for all peers)
+
     def __init__(self, name: str, rank: int, world: int, handler: Optional[Callable[[str, list], Any]] = None):
         """``handler(op, args)`` answers a query on ranks > 0 (the app's
         local store); rank 0 asks with ``ask``."""
@@ -93,7 +95,11 @@ class PeerDirectory:
                     res = self.handler(op, args) if self.handler is not None else None
                 except Exception as e:                # noqa: BLE001 -- answered, never fatal
                     res = {"error": str(e)}
-                self.reply.push(msgpack.packb([qid, self.rank, res], use_bin_type=True, default=str), 1)
+                rec = msgpack.packb([qid, self.rank, res], use_bin_type=True, default=str)
+                if len(rec) > self.REPLY_MAX:          # never wedge the shared reply ring
+                    rec = msgpack.packb([qid, self.rank, {"error": f"reply of {len(rec)} B too large"}],
+                                        use_bin_type=True)
+                self.reply.push(rec, 1)
                 self.answered += 1
 
     def stop(self) -> None:

@@ -116,6 +116,34 @@ def test_two_rank_serve_native_front_door():
         st, lst = _req("GET", base + "/api/v1/messages?limit=200")
         assert st == 200 and lst["total"] >= len(ids) + 1
         assert _req("GET", base + "/api/v1/messages/does-not-exist")[0] == 404
+        # dead letters live on the rank that popped the request: the admin
+        # routes on rank 0 list / remove / requeue them job-wide
+        exp = []
+        for burst in range(4):
+            for i in range(10):
+                st, r = _req("POST", base + "/api/v1/messages", {"content": f"late {burst}-{i}", "timeout": "1us"})
+                assert st == 202, r
+                exp.append(r["message_id"])
+            time.sleep(0.05)
+        deadline = time.time() + 60
+        items = []
+        while time.time() < deadline:
+            st, d = _req("GET", base + "/api/v1/admin/dead-letter")
+            items = [it for it in d["items"] if it["message"]["id"] in exp]
+            if len(items) == len(exp):
+                break
+            time.sleep(0.2)
+        assert len(items) == len(exp), f"{len(items)} of {len(exp)} dead-lettered"
+        assert {it["rank"] for it in items} == {0, 1}
+        on1 = [it["message"]["id"] for it in items if it["rank"] == 1]
+        st, qs = _req("GET", base + "/api/v1/queues/status")
+        assert st == 200 and qs["job"]["dead_letter"] >= len(exp)
+        assert _req("DELETE", base + f"/api/v1/admin/queues/dead_letter/{on1[0]}")[0] == 200
+        assert _req("DELETE", base + f"/api/v1/admin/queues/dead_letter/{on1[0]}")[0] == 404
+        assert _req("POST", base + f"/api/v1/admin/dead-letter/requeue/{on1[1]}")[0] == 200
+        assert _req("POST", base + "/api/v1/admin/dead-letter/requeue/nope")[0] == 404
+        st, r = _req("POST", base + "/api/v1/admin/dead-letter/requeue-all")
+        assert st == 200 and r["count"] >= len(exp) - 3, r
     finally:
         try:
             os.killpg(srv.pid, signal.SIGTERM)
