@@ -314,15 +314,22 @@ class _Service:
                                  updated_at=format_time(m.updated_at), completed_at=format_time(m.completed_at),
                                  metadata_json=json.dumps(m.metadata, default=str, separators=(",", ":")))
 
+    def _lookup(self, mid: str) -> Optional[Message]:
+        """This process's message, else a copy from the GPU rank that popped
+        it (multi-GPU front door)."""
+        m = self.G.messages.get(mid)
+        if m is None and getattr(self.G, "peers", None) is not None:
+            d = self.G.find_message(mid)
+            if d is not None:
+                m = Message.from_dict(d)
+                m.status = d.get("status", m.status)
+        return m
+
     def GetMessage(self, req, context):
         self._admit(context, "GetMessage")
-        m = self.G.messages.get(req.message_id)
+        m = self._lookup(req.message_id)
         if m is None:
-            d = self.G.find_message(req.message_id) if getattr(self.G, "peers", None) is not None else None
-            if d is None:
-                context.abort(grpc.StatusCode.NOT_FOUND, "Message not found")
-            m = Message.from_dict(d)          # held by another GPU rank (multi-GPU front door)
-            m.status = d.get("status", m.status)
+            context.abort(grpc.StatusCode.NOT_FOUND, "Message not found")
         return self._info(m)
 
     def WatchMessage(self, req, context):
@@ -335,7 +342,7 @@ class _Service:
         last = None
         nap = 0.002                                   # poll backoff 2 -> 50 ms, reset on change
         while context.is_active() and time.monotonic() < deadline:
-            m = self.G.messages.get(req.message_id)
+            m = self._lookup(req.message_id)
             if m is None:
                 if last is None:
                     context.abort(grpc.StatusCode.NOT_FOUND, "Message not found")
@@ -352,15 +359,16 @@ class _Service:
     def QueueStats(self, req, context):
         self._admit(context, "QueueStats")
         G = self.G
+        job = G.job_stats() if getattr(G, "peers", None) is not None else None    # every GPU rank
         tiers = []
         for t, name in enumerate(G.gateway.tiers):
-            st = G.standard.get_queue_stats(name)
-            tiers.append(pb["TierStats"](name=name, priority=int(G.gateway.tier_prio[t]), pending=st.pending_count,
-                                         processing=st.processing_count, completed=st.completed_count,
-                                         failed=st.failed_count))
-        return pb["QueueStatsReply"](tiers=tiers, total_pending=G.standard.total_pending(),
-                                     dead_letter=G.factory.dead_letter_queue.size(),
-                                     delayed=G.factory.delayed_queue.size())
+            c = job["tiers"][name] if job else dict(zip(("pending", "processing", "completed", "failed"),
+                                                        G._tier_counts(name)))
+            tiers.append(pb["TierStats"](name=name, priority=int(G.gateway.tier_prio[t]), pending=c["pending"],
+                                         processing=c["processing"], completed=c["completed"], failed=c["failed"]))
+        return pb["QueueStatsReply"](tiers=tiers, total_pending=sum(x.pending for x in tiers),
+                                     dead_letter=job["dead_letter"] if job else G.factory.dead_letter_queue.size(),
+                                     delayed=job["delayed"] if job else G.factory.delayed_queue.size())
 
     def Health(self, req, context):
         return pb["HealthReply"](status="ok", version=VERSION, time=format_time(time.time_ns()))

@@ -547,7 +547,12 @@ class GatewayApp:
         return {"rank": gw.rank, "counters": dict(gw.counters), "accepted": self._accepted,
                 "arr": gw.rec.arr.tolist(), "enq": gw.rec.enq.tolist(), "done": gw.rec_done.arr.tolist(),
                 "pending": [self.standard.size(n) for n in gw.tiers],
+                "tier_stats": [self._tier_counts(n) for n in gw.tiers],
                 "dead_letter": self.factory.dead_letter_queue.size(), "delayed": self.factory.delayed_queue.size()}
+
+    def _tier_counts(self, name: str) -> List[int]:
+        st = self.standard.get_queue_stats(name)
+        return [int(st.pending_count), int(st.processing_count), int(st.completed_count), int(st.failed_count)]
 
     def job_stats(self) -> dict:
         """Dispatch counters and latency summed over every rank of the job
@@ -569,6 +574,10 @@ class GatewayApp:
                 "accepted_by_rank": {int(p["rank"]): int(p["accepted"]) for p in parts},
                 "pending_by_tier": {n: sum(int(p.get("pending", [0] * len(tiers))[t]) for p in parts)
                                     for t, n in enumerate(tiers)},
+                "tiers": {n: dict(zip(("pending", "processing", "completed", "failed"),
+                                      (sum(int(p["tier_stats"][t][k]) for p in parts if "tier_stats" in p)
+                                       for k in range(4))))
+                          for t, n in enumerate(tiers)},
                 "dead_letter": sum(int(p.get("dead_letter", 0)) for p in parts),
                 "delayed": sum(int(p.get("delayed", 0)) for p in parts),
                 "latency": rec.summary(arr, enq), "latency_e2e": rec.summary(done, done)}

@@ -41,11 +41,11 @@ def _req(method, url, body=None, timeout=10):
 
 
 def test_two_rank_serve_native_front_door():
-    port, mport = _port(), _port()
+    port, mport, gport = _port(), _port(), _port()
     env = dict(os.environ, LLMQ_LOGGING__LEVEL="warning", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={mport}", "-m", "llm_message_queue_amd.cli", "serve",
-           "--cpu-ranks", "--port", str(port), "--host", "127.0.0.1"]
+           "--cpu-ranks", "--port", str(port), "--host", "127.0.0.1", "--grpc-port", str(gport)]
     srv = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                            start_new_session=True)
     base = f"http://127.0.0.1:{port}"
@@ -116,6 +116,18 @@ def test_two_rank_serve_native_front_door():
         st, lst = _req("GET", base + "/api/v1/messages?limit=200")
         assert st == 200 and lst["total"] >= len(ids) + 1
         assert _req("GET", base + "/api/v1/messages/does-not-exist")[0] == 404
+        # gRPC on rank 0 sees the whole job too: a message rank 1 popped, and
+        # tier counters summed over both ranks
+        from llm_message_queue_amd.api.grpc_server import GrpcClient
+        gcli = GrpcClient(f"127.0.0.1:{gport}")
+        try:
+            on_rank1 = next(mid for mid, m in done.items() if m["metadata"].get("ingest_rank") == 1)
+            info = gcli.get_message(on_rank1)
+            assert info.id == on_rank1 and info.status == "completed"
+            st_rep = gcli.queue_stats()
+            assert sum(t.completed for t in st_rep.tiers) >= len(ids)
+        finally:
+            gcli.close()
         # dead letters live on the rank that popped the request: the admin
         # routes on rank 0 list / remove / requeue them job-wide
         exp = []
