@@ -151,10 +151,14 @@ class GatewayApp:
         snap = self.cfg.queue.snapshot_path
         if snap and self.role != "ingress":
             from ..queue.snapshot import read_snapshot
-            counts = read_snapshot(self.factory, snap)
-            if counts is not None:
-                self.log.info("Resumed queue snapshot", path=snap, **counts)
-                os.replace(snap, snap + ".resumed")
+            resumed = 0
+            for path in self._snapshots_to_resume():
+                counts = read_snapshot(self.factory, path)
+                if counts is not None:
+                    self.log.info("Resumed queue snapshot", path=path, **counts)
+                    os.replace(path, path + ".resumed")
+                    resumed += 1
+            if resumed:
                 for mgr in self.factory.managers().values():
                     for q in mgr.queue_names():
                         for m in mgr.mlq.messages(q):
@@ -303,11 +307,33 @@ class GatewayApp:
         return self.telemetry
 
     # ------------------------------------------------------------------ checkpoint
+    def snapshot_file(self) -> str:
+        """This process's snapshot: ``queue.snapshot_path`` for one rank,
+        ``<path>.rank<r>`` for rank r of a multi-GPU job (every rank holds
+        the queues of the requests it popped; one shared file would be
+        overwritten by each rank in turn and replayed N times)."""
+        path, gw = self.cfg.queue.snapshot_path, self.gateway
+        return path if gw.world <= 1 else f"{path}.rank{gw.rank}"
+
+    def _snapshots_to_resume(self) -> List[str]:
+        """The snapshots this rank replays at start: its own, plus those of
+        ranks a previous job of a different size had (rank k's file goes to
+        rank k mod world; a single-rank file to rank 0)."""
+        import glob
+        import re
+        path, gw = self.cfg.queue.snapshot_path, self.gateway
+        out = [path] if gw.rank == 0 else []
+        for f in sorted(glob.glob(glob.escape(path) + ".rank*")):
+            m = re.fullmatch(re.escape(path) + r"\.rank(\d+)", f)
+            if m and int(m.group(1)) % max(1, gw.world) == gw.rank:
+                out.append(f)
+        return out
+
     def snapshot(self, path: str = "") -> Dict[str, int]:
         """Write queued + in-flight + delayed + dead-lettered messages (JSONL)."""
         from ..queue.snapshot import write_snapshot
         inflight = [m for m in self.messages.values() if m.status == MessageStatus.PROCESSING]
-        return write_snapshot(self.factory, path or self.cfg.queue.snapshot_path, inflight)
+        return write_snapshot(self.factory, path or self.snapshot_file(), inflight)
 
     def _snapshot_loop(self) -> None:
         period = self.cfg.queue.snapshot_interval / 1e9

@@ -89,3 +89,26 @@ def test_gateway_app_resumes_after_restart(tmp_path):
         assert [g.priority for g in got] == [x.priority for x in msgs]          # preprocessing kept
     finally:
         b.stop()
+
+
+def test_multi_rank_snapshot_files(tmp_path):
+    """Every rank of a multi-GPU job snapshots its own queues to
+    ``<path>.rank<r>``; at start rank r replays its file plus those of ranks
+    k = r mod world of a previous job of another size (and rank 0 a
+    single-rank file), so nothing is replayed twice or lost."""
+    from types import SimpleNamespace
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    base = str(tmp_path / "q.snap")
+
+    def app(rank, world):
+        return SimpleNamespace(cfg=SimpleNamespace(queue=SimpleNamespace(snapshot_path=base)),
+                               gateway=SimpleNamespace(rank=rank, world=world))
+
+    assert GatewayApp.snapshot_file(app(0, 1)) == base
+    assert GatewayApp.snapshot_file(app(3, 8)) == base + ".rank3"
+    for f in [base] + [f"{base}.rank{k}" for k in range(8)] + [base + ".rank1.resumed", base + ".rankx"]:
+        open(f, "w").close()
+    got = {r: GatewayApp._snapshots_to_resume(app(r, 4)) for r in range(4)}
+    assert got[0] == [base, base + ".rank0", base + ".rank4"]
+    assert got[1] == [base + ".rank1", base + ".rank5"]
+    assert sorted(sum(got.values(), [])) == sorted([base] + [f"{base}.rank{k}" for k in range(8)])
