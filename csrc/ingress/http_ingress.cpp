@@ -379,7 +379,9 @@ Scan scan_message(const char* b, size_t n) {
   js.ws();
   if (js.p < js.e && *js.p == '}') {
     ++js.p;
-    r.ok = true;
+    js.ws();
+    r.ok = js.p == js.e;                             // nothing may follow the object, as below
+    if (r.ok) r.error.clear();
     return r;
   }
   for (;;) {

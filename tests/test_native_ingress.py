@@ -43,7 +43,8 @@ def test_json_scanner():
     assert scan(b'{"content":"a\\"b","metadata":{"x":[1,{"y":null}]},"priority":4,"user_id":"u"}')[0:3:2] == (True, 4)
     assert scan(b'{}')[:4] == (True, "", 0, "")
     for bad in (b'', b'[1]', b'{"content":}', b'{"priority":"bogus"}', b'{"a":1,}', b'{"a":1} x', b'{"priority":9}',
-                b'{"priority":-1}', b'{"priority":"5"}', b'{"priority":"-2"}', b'{"priority":" "}'):
+                b'{"priority":-1}', b'{"priority":"5"}', b'{"priority":"-2"}', b'{"priority":" "}',
+                b'{}\x00', b'{}\x80', b'{} x', b'{ }}'):
         assert not scan(bad)[0], bad
 
 
