@@ -196,7 +196,8 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
 
     @app.get("/metrics")
     def metrics():
-        return Response(G.metrics.render(), media_type=CONTENT_TYPE_LATEST)
+        render = getattr(G, "metrics_exposition", None) or G.metrics.render
+        return Response(render(), media_type=CONTENT_TYPE_LATEST)
 
     # ------------------------------------------------------------------ messages
     def _bind_message(body: Any) -> Message:

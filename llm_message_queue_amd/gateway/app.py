@@ -497,6 +497,8 @@ class GatewayApp:
             return self._dlq_local(str(args[0]), str(args[1]) if len(args) > 1 else "")
         if op == "dequeue":
             return self._dequeue_local(str(args[0]), str(args[1]))
+        if op == "metrics":
+            return self.metrics.render().decode()
         raise ValueError(f"unknown op {op!r}")
 
     # ------------------------------------------------------------------ job-wide admin
@@ -575,6 +577,19 @@ class GatewayApp:
                 "pending": [self.standard.size(n) for n in gw.tiers],
                 "tier_stats": [self._tier_counts(n) for n in gw.tiers],
                 "dead_letter": self.factory.dead_letter_queue.size(), "delayed": self.factory.delayed_queue.size()}
+
+    def metrics_exposition(self) -> bytes:
+        """``/metrics``: this process's registry; in a multi-GPU job every
+        rank's, merged with a ``rank`` label (each rank counts the requests it
+        popped, so rank 0 alone is a partial view)."""
+        if self.peers is None or self.peers.world <= 1:
+            return self.metrics.render()
+        from ..utils.metrics import merge_expositions
+        parts = {self.gateway.rank: self.metrics.render().decode()}
+        for r, text in self.peers.ask("metrics", []).items():
+            if isinstance(text, str):
+                parts[int(r)] = text
+        return merge_expositions(parts)
 
     def _tier_counts(self, name: str) -> List[int]:
         st = self.standard.get_queue_stats(name)

@@ -25,7 +25,7 @@ import msgpack
 
 from .. import _native
 
-OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency", "pre_state", "dlq", "dequeue")
+OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency", "pre_state", "dlq", "dequeue", "metrics")
 
 
 class PeerDirectory:

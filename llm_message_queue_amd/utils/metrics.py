@@ -13,7 +13,7 @@ New series for the MI355X gateway: ``llm_queue_enqueue_to_dispatch_seconds``
 from __future__ import annotations
 
 import threading
-from typing import Optional
+from typing import Dict, List, Optional
 
 try:  # prometheus_client is in the image; degrade to no-ops if absent
     from prometheus_client import (CollectorRegistry, Counter, Gauge, Histogram,
@@ -120,3 +120,47 @@ def reset_default_metrics() -> QueueMetrics:
     with _LOCK:
         _DEFAULT = QueueMetrics()
         return _DEFAULT
+
+
+def _with_rank(line: str, rank: int) -> str:
+    """One exposition sample line with a ``rank`` label added."""
+    i = 0
+    while i < len(line) and line[i] not in "{ ":
+        i += 1
+    if i < len(line) and line[i] == "{":
+        sep = "" if line[i + 1:i + 2] == "}" else ","
+        return f'{line[:i + 1]}rank="{rank}"{sep}{line[i + 1:]}'
+    return f'{line[:i]}{{rank="{rank}"}}{line[i:]}'
+
+
+def merge_expositions(parts: Dict[int, str]) -> bytes:
+    """Prometheus text expositions of several ranks as one: every sample gets
+    a ``rank`` label and each metric family stays one contiguous block under
+    a single HELP / TYPE header (the multi-GPU front door's ``/metrics``: one
+    scrape target for the whole job)."""
+    blocks: Dict[str, List[List[str]]] = {}
+    order: List[str] = []
+    for rank, text in sorted(parts.items()):
+        fam = ""
+        for line in text.splitlines():
+            if not line:
+                continue
+            if line.startswith("# HELP ") or line.startswith("# TYPE "):
+                fam = line.split(" ", 3)[2]
+                if fam not in blocks:
+                    blocks[fam] = [[], []]
+                    order.append(fam)
+                if line not in blocks[fam][0]:
+                    blocks[fam][0].append(line)
+                continue
+            if line.startswith("#"):
+                continue
+            if fam not in blocks:
+                blocks[fam] = [[], []]
+                order.append(fam)
+            blocks[fam][1].append(_with_rank(line, rank))
+    out: List[str] = []
+    for fam in order:
+        out.extend(blocks[fam][0])
+        out.extend(blocks[fam][1])
+    return ("\n".join(out) + "\n").encode() if out else b""

@@ -116,6 +116,16 @@ def test_two_rank_serve_native_front_door():
         st, lst = _req("GET", base + "/api/v1/messages?limit=200")
         assert st == 200 and lst["total"] >= len(ids) + 1
         assert _req("GET", base + "/api/v1/messages/does-not-exist")[0] == 404
+        # one Prometheus scrape covers every rank (a `rank` label per sample)
+        with urllib.request.urlopen(base + "/metrics", timeout=10) as resp:
+            prom = resp.read().decode()
+        from prometheus_client.parser import text_string_to_metric_families
+        fams = {f.name: f for f in text_string_to_metric_families(prom)}
+        done_by_rank = {}
+        for smp in fams["llm_queue_messages_completed"].samples:
+            if smp.name.endswith("_total"):
+                done_by_rank[smp.labels["rank"]] = done_by_rank.get(smp.labels["rank"], 0) + smp.value
+        assert set(done_by_rank) == {"0", "1"} and sum(done_by_rank.values()) >= len(ids), done_by_rank
         # gRPC on rank 0 sees the whole job too: a message rank 1 popped, and
         # tier counters summed over both ranks
         from llm_message_queue_amd.api.grpc_server import GrpcClient
