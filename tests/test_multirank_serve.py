@@ -203,9 +203,13 @@ def test_two_rank_serve_front_door_on_gpu():
                 ev = json.loads(line)
                 break
         assert ev is not None and ev["gpu"] and ev["front_door"] == "native", "server did not come up"
+        # a keyword rule added at run time is re-packed into EVERY rank's GPU
+        # text-kernel pattern table (each rank preprocesses what it pops)
+        st, r = _req("POST", base + "/api/v1/admin/preprocessor/rules", {"pattern": "(?i)zebra", "priority": 4})
+        assert st == 201, r
         ids = []
         for i in range(40):
-            st, r = _req("POST", base + "/api/v1/messages", {"content": f"urgent: check node {i} asap",
+            st, r = _req("POST", base + "/api/v1/messages", {"content": f"zebra zebra: check node {i}",
                                                              "user_id": f"g{i % 5}"})
             assert st == 202, r
             ids.append(r["message_id"])
@@ -219,6 +223,8 @@ def test_two_rank_serve_front_door_on_gpu():
                         done[mid] = m
             time.sleep(0.1)
         assert len(done) == len(ids), f"{len(done)} of {len(ids)} completed"
+        assert all((m["priority"], m["metadata"].get("priority_reason")) == (4, "content_keywords")
+                   for m in done.values()), [m["priority"] for m in done.values()]
         st, stats = _req("GET", base + "/api/v1/queues/stats")
         assert st == 200 and stats["job"]["ranks"] == [0, 1]
         assert stats["job"]["dispatch"]["completed"] >= len(ids)
