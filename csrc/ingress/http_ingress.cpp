@@ -633,6 +633,10 @@ class HttpIngress {
     upstream_port_ = port;
   }
   void set_envelope(bool on) { envelope_ = on; }
+  // `cli api-gateway --native`: the submit reply also carries the reference
+  // api-gateway's fields ({"message": "Message accepted", "id"},
+  // cmd/api-gateway/main.go:113), so clients of either binary read it
+  void set_gateway_compat(bool on) { gateway_compat_ = on; }
   void set_idle_timeout(double seconds) { idle_ns_.store(seconds > 0 ? (int64_t)(seconds * 1e9) : 0); }
 
  private:
@@ -994,7 +998,9 @@ class HttpIngress {
           } else {
             accepted_++;
             std::string out = "{\"message_id\":\"" + id + "\",\"priority\":" + std::to_string(s.priority) +
-                              ",\"queue_time\":\"" + rfc3339_now() + "\",\"estimated_wait\":0}";
+                              ",\"queue_time\":\"" + rfc3339_now() + "\",\"estimated_wait\":0";
+            if (gateway_compat_) out += ",\"message\":\"Message accepted\",\"id\":\"" + id + "\"";
+            out += "}";
             respond(cn, 202, "Accepted", out, keep);
           }
         }
@@ -1161,6 +1167,7 @@ class HttpIngress {
   std::atomic<int64_t> idle_ns_{60'000'000'000};   // 60 s; 0 = never reap
   std::shared_ptr<llmq::Guard> guard_;
   bool envelope_ = false;
+  bool gateway_compat_ = false;
 };
 
 }  // namespace
@@ -1178,6 +1185,7 @@ PYBIND11_MODULE(_ingress, m) {
       .def("set_conv_ring", &HttpIngress::set_conv_ring, py::arg("name"))
       .def("set_upstream", &HttpIngress::set_upstream, py::arg("host"), py::arg("port"))
       .def("set_envelope", &HttpIngress::set_envelope)
+      .def("set_gateway_compat", &HttpIngress::set_gateway_compat)
       .def("set_idle_timeout", &HttpIngress::set_idle_timeout, py::arg("seconds"));
   py::class_<llmq::Guard, std::shared_ptr<llmq::Guard>>(m, "Guard")
       .def(py::init<std::string, std::string, std::vector<std::string>, std::string, std::string, int64_t, bool,

@@ -200,6 +200,11 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         return Response(render(), media_type=CONTENT_TYPE_LATEST)
 
     # ------------------------------------------------------------------ messages
+    # `cli api-gateway` (role "ingress"): replies also carry the reference
+    # api-gateway's fields (cmd/api-gateway/main.go:113, 177) so clients of
+    # either reference binary read them
+    gateway_compat = getattr(G, "role", "") == "ingress"
+
     def _bind_message(body: Any) -> Message:
         m = Message.from_dict(body)
         if not m.id:
@@ -237,9 +242,11 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
                 G.state.add_message(m.conversation_id, m)
             except ConversationNotFound:
                 pass
-        return JSONResponse({"message_id": m.id, "priority": int(m.priority),
-                             "queue_time": format_time(time.time_ns()),
-                             "estimated_wait": G.estimated_wait_ns(m)}, status_code=202)
+        out = {"message_id": m.id, "priority": int(m.priority), "queue_time": format_time(time.time_ns()),
+               "estimated_wait": G.estimated_wait_ns(m)}
+        if gateway_compat:
+            out.update(message="Message accepted", id=m.id)
+        return JSONResponse(out, status_code=202)
 
     @app.get("/api/v1/messages/{mid}")
     def get_message(mid: str):
@@ -354,9 +361,11 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
         bad = await _enqueue(m)
         if bad is not None:
             return bad
-        return JSONResponse({"message_id": m.id, "conversation_id": cid, "priority": int(m.priority),
-                             "queue_time": format_time(time.time_ns()),
-                             "estimated_wait": G.estimated_wait_ns(m)}, status_code=202)
+        out = {"message_id": m.id, "conversation_id": cid, "priority": int(m.priority),
+               "queue_time": format_time(time.time_ns()), "estimated_wait": G.estimated_wait_ns(m)}
+        if gateway_compat:
+            out["message"] = "Message added successfully"
+        return JSONResponse(out, status_code=202)
 
     @app.put("/api/v1/conversations/{cid}/state")
     async def update_conversation_state(cid: str, request: Request):

@@ -89,7 +89,7 @@ def cmd_native_ingress(a) -> int:
     port = a.port or cfg.server.port
     threads = a.ingress_threads or cfg.server.ingress_threads
     ing = NativeIngress(port, a.ring or cfg.server.shared_ring, threads, a.host or cfg.server.host,
-                        cfg=cfg)
+                        cfg=cfg, gateway_compat=True)
     port = ing.start()
     print(json.dumps({"event": "listening", "host": a.host or cfg.server.host, "port": port, "role": "native-ingress",
                       "ring": ing.ring, "threads": threads}), flush=True)

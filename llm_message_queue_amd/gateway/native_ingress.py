@@ -13,13 +13,16 @@ from .. import _native
 
 class NativeIngress:
     def __init__(self, port: int = 8080, ring: str = "default", threads: int = 4, host: str = "0.0.0.0",
-                 cfg=None, conv_ring: str = "", upstream: Optional[Tuple[str, int]] = None):
+                 cfg=None, conv_ring: str = "", upstream: Optional[Tuple[str, int]] = None,
+                 gateway_compat: bool = False):
         """``cfg`` (optional): attach the config's guard (authentication, RBAC,
         rate limits -- ``api/security.py``) and response envelope.
         ``conv_ring``: ring (name of a ``RingPair``) for messages that carry a
         conversation_id -- drained by the process that owns conversation
         state.  ``upstream``: (host, port) of the Python API server; every
-        other route is reverse-proxied to it (one public port)."""
+        other route is reverse-proxied to it (one public port).
+        ``gateway_compat``: the submit reply also carries the reference
+        api-gateway's ``message`` / ``id`` fields (``cli api-gateway``)."""
         self.ring = ring
         self._k = _native.ingress().HttpIngress(int(port), f"llmq-{ring}-req", int(threads), host)
         self.port = int(port)
@@ -27,6 +30,8 @@ class NativeIngress:
             self._k.set_conv_ring(f"llmq-{conv_ring}-req")
         if upstream is not None:
             self._k.set_upstream(str(upstream[0]), int(upstream[1]))
+        if gateway_compat:
+            self._k.set_gateway_compat(True)
         self.guard = None
         if cfg is not None:
             from ..api.security import guard_from_config

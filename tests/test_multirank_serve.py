@@ -336,6 +336,8 @@ def test_split_deployment_two_queue_manager_ranks():
         for i in range(40):
             st, r = _req("POST", base + "/api/v1/messages", {"content": f"please check item {i}", "user_id": f"s{i}"})
             assert st == 202, r
+            # the reference api-gateway's reply fields ride along (cmd/api-gateway/main.go:113)
+            assert r["message"] == "Message accepted" and r["id"] == r["message_id"], r
             ids.append(r["message_id"])
         deadline = time.time() + 90
         done = set()

@@ -82,6 +82,25 @@ def test_priority_rule_matches_python_front_door():
     prop()
 
 
+def test_gateway_compat_reply():
+    """``cli api-gateway --native``: the 202 also carries the reference
+    api-gateway's ``message`` / ``id`` (cmd/api-gateway/main.go:113); the
+    monolith front door's reply stays the reference server's shape."""
+    name = f"pyt-compat-{os.getpid()}"
+    ring = RingPair(name, 1 << 20, "create")
+    ings = [NativeIngress(0, name, threads=1, host="127.0.0.1", gateway_compat=c) for c in (True, False)]
+    try:
+        ports = [i.start() for i in ings]
+        code, r = _post(ports[0], {"content": "hi", "id": "cid-7"})
+        assert code == 202 and r["message"] == "Message accepted" and r["id"] == "cid-7" == r["message_id"], r
+        code, r = _post(ports[1], {"content": "hi"})
+        assert code == 202 and "id" not in r and "message" not in r and len(r["message_id"]) == 36, r
+    finally:
+        for i in ings:
+            i.stop()
+        ring.close(unlink=True)
+
+
 @pytest.fixture
 def stack():
     from llm_message_queue_amd.gateway.app import GatewayApp
