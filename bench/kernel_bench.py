@@ -34,6 +34,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
+    ap.add_argument("--text-batches", default="4096", help="preprocess batch sizes (messages), comma-separated")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -55,10 +56,11 @@ def main() -> None:
     # --- preprocess pipeline (text_analyze + scan + MFMA embed_pool + head), 4096 messages
     if not want or "text" in want:
         pipe = TextPipeline(device="cuda:0")
-        msgs = [m.content for m in Workload(seed=1).make(4096)]
         pats = default_patterns()
-        ms = timeit(lambda: pipe.run(msgs, pats, 0, classify=True, prompt_cap=32), max(5, a.reps // 5))
-        rec("preprocess_pipeline_4096msgs", ms, us_per_msg=round(ms * 1e3 / 4096, 3))
+        for nb in (int(x) for x in a.text_batches.split(",")):
+            msgs = [m.content for m in Workload(seed=1).make(nb)]
+            ms = timeit(lambda: pipe.run(msgs, pats, 0, classify=True, prompt_cap=32), max(5, a.reps // 5))
+            rec(f"preprocess_pipeline_{nb}msgs", ms, us_per_msg=round(ms * 1e3 / nb, 3))
 
     ops = HipOps()
     Hq, Hkv, S, C = 32, 8, 1024, 512

@@ -12,22 +12,28 @@
 // rows.  W1 is stored transposed, W1t[H][D], so a B fragment is 16 contiguous
 // bytes of one W1t row.
 //
-// Tiling (gfx950): one 256-thread workgroup (4 waves) per 64-row tile.
+// Tiling (gfx950): one 256-thread workgroup (4 waves) per (64-row tile,
+// 256-column chunk of H) -- H / 256 blocks per tile, so the few tiles of a
+// serving micro-batch still spread over many CUs (the kernel is latency-bound
+// there: 57 -> 18 us at 64 messages, profiles/r3_embed_pool_ab.md).
 //   * the 64 x 256 bf16 A tile (32 KiB) is gathered ONCE into LDS with 16-byte
 //     register-staged loads (for row gathers from a ~32 MiB table an LDS-DMA
 //     global_load_lds with per-lane source rows reads at the same rate, per
 //     the MI355X microarchitecture measurements, so the simpler form stays); its 16-byte chunks are XOR-swizzled (chunk ^ (row & 15)) so the
 //     v_mfma_f32_16x16x32_bf16 A-fragment reads (16 rows x one chunk per lane
 //     group) are bank-conflict free for every ds_read_b128 lane group;
-//   * the tile stays resident while the 4 waves sweep H in 256-column chunks
-//     (64 columns per wave = 4x4 16x16 accumulators, K = 256 = 8 MFMA k-steps);
-//   * B fragments stream from L2 (W1t is 512 KiB, resident);
-//   * epilogue: bias + tanh-GELU into a 64 x 256 f32 LDS slab, then one thread
-//     per column walks the 64 rows, sums runs of equal message id and writes
-//     sum/ntok -- a plain store when the message lies wholly inside the tile,
-//     an f32 atomic add otherwise (pooled is zeroed before the launch).
-// Grid: ceil(rows_upper / 64) tiles; tiles past the device-side row total
-// exit immediately (rows_upper is a host bound from byte lengths).
+//   * 64 columns per wave = 4x4 16x16 accumulators, K = 256 = 8 MFMA
+//     k-steps; the 32 B fragments of all 8 k-steps are loaded from L2 at once
+//     (W1t is 512 KiB, resident): one round trip per block, not one per k-step;
+//   * epilogue in registers: bias + tanh-GELU on the C fragments, then per
+//     message segment of the tile (starts found by one ballot) each lane sums
+//     its rows, two xor-shuffles join the four row-quads of a column, and the
+//     mean sum/ntok is written -- a plain store when the message lies wholly
+//     inside the tile, an f32 atomic add otherwise (pooled is zeroed before
+//     the launch).  No LDS slab: the 32 KiB A tile is the block's LDS.
+// Grid: ceil(rows_upper / 64) tiles x H / 256 chunks; tiles past the
+// device-side row total exit immediately (rows_upper is a host bound from
+// byte lengths).
 
 #pragma once
 #include <hip/hip_runtime.h>
@@ -41,10 +47,6 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int EP_TM = 64;      // rows per tile
 constexpr int EP_D = 256;      // embedding dim (K)
 constexpr int EP_NCHUNK = 256; // columns per sweep step
-// f32 epilogue slab row stride: +4 floats so the C-layout stores of the 4
-// row-quads (rows 4 apart) land 16 banks apart (measured 19% LDS bank
-// conflicts with a 256-float stride; rocprofv3 SQ_LDS_BANK_CONFLICT)
-constexpr int EP_HS_STRIDE = EP_NCHUNK + 4;
 constexpr int EP_CHUNKS_PER_ROW = EP_D / 8;  // 16-byte chunks per A row
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
@@ -94,9 +96,9 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
                   float* __restrict__ pooled, const int32_t* __restrict__ ntok_src, int ntok_stride) {
   extern __shared__ __align__(16) uint8_t smem[];
   uint16_t* At = reinterpret_cast<uint16_t*>(smem);                       // 64 x 256 bf16 (32 KiB)
-  float* Hs = reinterpret_cast<float*>(smem + EP_TM * EP_D * 2);          // 64 x 260 f32 (65 KiB)
-  int32_t* rmsg = reinterpret_cast<int32_t*>(smem + EP_TM * EP_D * 2 + EP_TM * EP_HS_STRIDE * 4);
-  int32_t* rinfo = rmsg + EP_TM;  // [0]=rows in tile
+  int32_t* rmsg = reinterpret_cast<int32_t*>(smem + EP_TM * EP_D * 2);
+  int32_t* rinfo = rmsg + EP_TM;  // [0]=rows in tile, [1]=segments, [2..]=segment starts (+ end)
+  int32_t* seg = rinfo + 2;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -107,7 +109,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   const int32_t* ro = row_off;
   if (ntok_src) {
     __shared__ int32_t wtot[4];
-    int32_t* roff = rinfo + EP_TM;                                          // [B + 1] ints
+    int32_t* roff = rinfo + 2 * EP_TM;                                      // [B + 1] ints
     int carry = 0;
     for (int base = 0; base < B; base += 256) {
       const int i = base + tid;
@@ -131,7 +133,12 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
     ro = roff;
   }
   const int total = ro[B];
-  const int tile0 = blockIdx.x * EP_TM;
+  // one block per (64-row tile, 256-column chunk of H): a small batch (a few
+  // tiles) still spreads over H / 256 times as many CUs -- the kernel is
+  // latency-bound there; each block gathers its tile's rows (L2-resident)
+  const int nchunk = H / EP_NCHUNK;
+  const int tile0 = (blockIdx.x / nchunk) * EP_TM;
+  const int chunk0 = (blockIdx.x % nchunk) * EP_NCHUNK;
   if (tile0 >= total) return;  // uniform across the block
   const int rows = min(EP_TM, total - tile0);
 
@@ -151,6 +158,16 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   }
   if (tid == 0) rinfo[0] = rows;
   __syncthreads();
+  // ---- message segments of the tile (rows are message-major): starts by ballot
+  if (tid < EP_TM) {
+    const bool start = tid < rows && (tid == 0 || rmsg[tid] != rmsg[tid - 1]);
+    const uint64_t mask = __ballot(start);
+    if (start) seg[__popcll(mask & ((1ull << tid) - 1ull))] = tid;
+    if (tid == 0) {
+      rinfo[1] = __popcll(mask);
+      seg[__popcll(mask)] = rows;
+    }
+  }
 
   // ---- gather the A tile: 64 rows x 32 chunks of 16 B, swizzled chunk ^ (row & 15)
   for (int c = tid; c < EP_TM * EP_CHUNKS_PER_ROW; c += 256) {
@@ -171,7 +188,8 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   const int fr = lane & 15;   // fragment row / col within a 16x16 tile
   const int fq = lane >> 4;   // k-quarter (A/B), row-quad (C)
 
-  for (int n0 = 0; n0 < H; n0 += EP_NCHUNK) {
+  {
+    const int n0 = chunk0;
     const int wc0 = n0 + wv * 64;  // this wave's 64 output columns
     f32x4 acc[4][4];
 #pragma unroll
@@ -179,14 +197,17 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll 2
-    for (int ks = 0; ks < EP_D / 32; ++ks) {
-      bf16x8 bfrag[4];
+    // all 8 k-steps' B fragments issued at once (128 VGPRs): one L2 round
+    // trip per block instead of one per k-step
+    bf16x8 bfall[EP_D / 32][4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = wc0 + j * 16 + fr;
-        bfrag[j] = *reinterpret_cast<const bf16x8*>(W1t + (int64_t)col * EP_D + ks * 32 + fq * 8);
-      }
+    for (int ks = 0; ks < EP_D / 32; ++ks)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfall[ks][j] = *reinterpret_cast<const bf16x8*>(W1t + (int64_t)(wc0 + j * 16 + fr) * EP_D + ks * 32 + fq * 8);
+#pragma unroll
+    for (int ks = 0; ks < EP_D / 32; ++ks) {
+      const bf16x8* bfrag = bfall[ks];
       bf16x8 afrag[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -201,47 +222,49 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag[i], bfrag[j], acc[i][j], 0, 0, 0);
     }
 
-    // ---- epilogue 1: bias + GELU into the f32 slab (C map: row = 4*fq + k, col = fr)
+    // ---- epilogue: bias + GELU in registers, then the segmented mean over
+    // rows straight from the C fragments (lane: rows i*16 + 4fq + k, column
+    // j*16 + fr): per message segment each lane sums its rows inside it, the
+    // four row-quads of a column meet by two xor-shuffles, and lanes fq == 0
+    // write -- no LDS slab (2 blocks per CU instead of 1)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int lc = wv * 64 + j * 16 + fr;          // column within the 256-wide chunk
-      const float bias = b1[n0 + lc];
+      const float bias = b1[wc0 + j * 16 + fr];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[i][j][k] = gelu_tanh(acc[i][j][k] + bias);
+    }
+    const int nseg = rinfo[1];
+    for (int sg = 0; sg < nseg; ++sg) {                 // uniform: every lane runs the shuffles
+      const int r0 = seg[sg], r1 = seg[sg + 1];
+      const int cur = rmsg[r0];
+      float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int r = i * 16 + fq * 4 + k;
-          Hs[r * EP_HS_STRIDE + lc] = gelu_tanh(acc[i][j][k] + bias);
+          const bool in = r >= r0 && r < r1;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sum[j] += in ? acc[i][j][k] : 0.f;
         }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sum[j] += __shfl_xor(sum[j], 16, 64);
+        sum[j] += __shfl_xor(sum[j], 32, 64);
       }
-    }
-    __syncthreads();
-
-    // ---- epilogue 2: segmented mean over rows (one thread per column)
-    {
-      const int col = tid;  // 256 threads == 256 columns
-      float run = 0.f;
-      int cur = rmsg[0];
-      for (int r = 0; r < rows; ++r) {
-        const int m = rmsg[r];
-        if (m != cur) {
-          const int a = ro[cur], b = ro[cur + 1];
-          const float v = run / (float)(b - a);
-          float* dst = pooled + (int64_t)cur * H + n0 + col;
-          if (a >= tile0 && b <= tile0 + rows) *dst = v; else atomicAdd(dst, v);
-          run = 0.f;
-          cur = m;
-        }
-        run += Hs[r * EP_HS_STRIDE + col];
-      }
-      if (cur >= 0) {
+      if (fq == 0) {
         const int a = ro[cur], b = ro[cur + 1];
-        const float v = run / (float)(b - a);
-        float* dst = pooled + (int64_t)cur * H + n0 + col;
-        if (a >= tile0 && b <= tile0 + rows) *dst = v; else atomicAdd(dst, v);
+        const float inv = 1.0f / (float)(b - a);
+        const bool whole = a >= tile0 && b <= tile0 + rows;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float* dst = pooled + (int64_t)cur * H + wc0 + j * 16 + fr;
+          if (whole) *dst = sum[j] * inv; else atomicAdd(dst, sum[j] * inv);
+        }
       }
     }
-    __syncthreads();
   }
 }
 

@@ -72,7 +72,7 @@ static void scan_rows(uintptr_t ntok, int stride, int B, uintptr_t row_off, uint
 }
 
 static bool g_embed_attr = false;
-static constexpr size_t EP_SMEM_BASE = EP_TM * EP_D * 2 + EP_TM * EP_HS_STRIDE * 4 + 2 * EP_TM * 4 + 16;
+static constexpr size_t EP_SMEM_BASE = EP_TM * EP_D * 2 + 3 * EP_TM * 4 + 16;
 static constexpr size_t EP_SMEM_MAX = 160 * 1024 - 256;   // static __shared__ of the kernel counts too
 // largest batch whose row offsets fit in LDS next to the tile (in-block scan)
 static constexpr int EP_MAX_LDS_SCAN = (int)((EP_SMEM_MAX - EP_SMEM_BASE) / 4) - 1;
@@ -97,7 +97,7 @@ static void embed_pool(uintptr_t hashes, int L, uintptr_t row_off, int B, int ro
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)EP_SMEM_MAX));
     g_embed_attr = true;
   }
-  const int grid = (rows_upper + EP_TM - 1) / EP_TM;
+  const int grid = (rows_upper + EP_TM - 1) / EP_TM * (H / EP_NCHUNK);   // (tile, H chunk) blocks
   hipLaunchKernelGGL(embed_pool_kernel, dim3(grid), dim3(256), smem, S(stream), P<const uint32_t>(hashes),
                      L, P<const int32_t>(row_off), B, P<const uint16_t>(E), (uint32_t)(V - 1),
                      P<const uint16_t>(W1t), P<const float>(b1), H, P<float>(pooled),
