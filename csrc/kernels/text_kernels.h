@@ -32,7 +32,10 @@ constexpr int TA_SLOTS = 8;
 constexpr int TA_STAT_COLS = 16;
 constexpr int TA_MAX_TOKEN_BYTES = 32;   // classifier tokenizer hashes <= 32 bytes/token
 constexpr int TA_WAVES = 4;
-constexpr int TA_WIN = 96;               // staged bytes per wave per chunk
+// staged bytes per wave per chunk: 4 look-behind + 64 + 36 look-ahead, so a
+// token starting at the chunk's last byte (<= 32 bytes + the 2-byte space
+// test after it) is hashed from LDS too
+constexpr int TA_WIN = 104;
 
 enum : int32_t { FLAG_FOLD = 1 };
 enum : int32_t { ST_WORDS = 0, ST_POS = 1, ST_NEG = 2, ST_QUESTION = 3, ST_FLAGS = 4,
@@ -163,7 +166,7 @@ text_analyze_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict
   for (int s = 0; s < TA_SLOTS; ++s) score[s] = 0;
 
   for (int base = 0; base < len; base += 64) {
-    // ---- stage bytes [base-4, base+92) into this wave's LDS window
+    // ---- stage bytes [base-4, base+100) into this wave's LDS window
     {
       const int i0 = base - 4 + lane;
       win8[lane] = (i0 >= 0 && i0 < len) ? src[i0] : (uint8_t)0;
@@ -281,15 +284,17 @@ text_analyze_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict
       for (int s2 = 0; s2 < TA_SLOTS; ++s2) score[s2] += (sl == s2) ? cnt : 0;
     }
 
-    // ---- token hashes: the word-start lane walks its token (<= 32 bytes)
+    // ---- token hashes: the word-start lane walks its token (<= 32 bytes) in
+    // the LDS window (bytes past len are staged as 0, as the bounds below read)
     if (wstart && tok_idx < L) {
       uint32_t h = 0x811C9DC5u;
       int q2 = p;
+      const uint8_t* wb = win8 + 4 - base;              // wb[i] = byte i of the message
       for (int n = 0; n < TA_MAX_TOKEN_BYTES && q2 < len; ++n, ++q2) {
-        const uint32_t c = src[q2];
+        const uint32_t c = wb[q2];
         if (n > 0) {
-          const uint32_t d1 = (q2 + 1 < len) ? src[q2 + 1] : 0u;
-          const uint32_t d2 = (q2 + 2 < len) ? src[q2 + 2] : 0u;
+          const uint32_t d1 = (q2 + 1 < len) ? wb[q2 + 1] : 0u;
+          const uint32_t d2 = (q2 + 2 < len) ? wb[q2 + 2] : 0u;
           if (space_width(c, d1, d2) > 0) break;
         }
         h ^= (c >= 0x41u && c <= 0x5Au) ? (c | 0x20u) : c;
