@@ -138,6 +138,10 @@ def main() -> None:
     ap.add_argument("--workload", action="store_true",
                     help="native client sends bench.py's synthetic 4-tier workload (gateway/workload.py) instead "
                          "of four fixed bodies")
+    ap.add_argument("--admin-churn", type=float, default=0.0,
+                    help="every this many seconds of the measured run: add + remove a keyword rule (copied to "
+                         "every rank), scrape /metrics, list dead letters, read /queues/status; reports their "
+                         "latencies and errors")
     ap.add_argument("--bench-config", action="store_true",
                     help="spawned GPU dispatcher runs bench.py's serving config (1536 slots, 4096-token steps, "
                          "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
@@ -235,8 +239,33 @@ def main() -> None:
                     req = urllib.request.Request(api_url + "/api/v1/admin/stats/reset", method="POST", data=b"")
                     urllib.request.urlopen(req, timeout=10).read()
                 threading.Thread(target=_reset, daemon=True).start()
+            churn = {"calls": 0, "errors": 0, "ms": []}
+            churn_stop = threading.Event()
+
+            def _churn():
+                k = 0
+                while not churn_stop.wait(a.admin_churn):
+                    k += 1
+                    calls = [("POST", "/api/v1/admin/preprocessor/rules", {"pattern": f"(?i)churn{k}", "priority": 2}),
+                             ("GET", "/metrics", None), ("GET", "/api/v1/admin/dead-letter?limit=10", None),
+                             ("GET", "/api/v1/queues/status", None),
+                             ("DELETE", "/api/v1/admin/preprocessor/rules", {"pattern": f"(?i)churn{k}", "priority": 2})]
+                    for method, path, body in calls:
+                        t0 = time.perf_counter()
+                        try:
+                            req = urllib.request.Request(api_url + path, method=method,
+                                                         data=json.dumps(body).encode() if body else None,
+                                                         headers={"Content-Type": "application/json"})
+                            urllib.request.urlopen(req, timeout=10).read()
+                        except Exception:                      # noqa: BLE001 -- counted
+                            churn["errors"] += 1
+                        churn["calls"] += 1
+                        churn["ms"].append((time.perf_counter() - t0) * 1e3)
+            if a.admin_churn > 0 and api_url:
+                threading.Thread(target=_churn, daemon=True).start()
             r = subprocess.run([exe, host, port, str(a.rate), str(a.duration), str(a.procs), str(a.conns)] + extra,
                                capture_output=True, text=True, timeout=a.duration + 60)
+            churn_stop.set()
             st_end = None
             if api_url:                         # latency window closes with the load (before the drain)
                 with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
@@ -256,6 +285,10 @@ def main() -> None:
                                      "note": "latency: HTTP arrival (native ingress clock) -> GPU slot admission; "
                                              "latency_e2e: -> last generated token; window = the measured run"}
             out["mode"] = a.spawn or "url"
+            if a.admin_churn > 0 and churn["ms"]:
+                ms = sorted(churn["ms"])
+                out["admin_churn"] = {"every_s": a.admin_churn, "calls": churn["calls"], "errors": churn["errors"],
+                                      "p50_ms": round(ms[len(ms) // 2], 2), "max_ms": round(ms[-1], 2)}
             print(json.dumps(out))
             return
         ctx = mp.get_context("spawn")
