@@ -279,45 +279,69 @@ struct ClassifyReadback {
 };
 
 // logits[b, 0:8] = pooled[b] . W2 + b2 ; pred[b] = 1 + argmax(logits[b, 0:4])
-// One wave per message; lane l covers 16 hidden units.
+// One wave per CH_MSGS messages; lane l covers hidden units l, l+64, ...: each
+// W2 row (8 floats) is loaded once per wave and used for all its messages
+// (W2 is 32 KiB: one read per message made the kernel L2-bound at large
+// batches).  Per message the summation order is the one-message-per-wave
+// order, so the results are unchanged.
+// CH_MSGS = 1 below ~1k messages: a serving micro-batch has few waves, and
+// the latency of one wave's chain, not L2 traffic, sets the time there
+// (profiles/r3_embed_pool_ab.md: 64 messages 9.5 us at 1 vs 14.4 us at 4).
+template <int CH_MSGS>
 __global__ void __launch_bounds__(256)
 classify_head_kernel(const float* __restrict__ pooled, int B, int H, const float* __restrict__ W2,
                      const float* __restrict__ b2, float* __restrict__ logits, int32_t* __restrict__ pred,
                      const ClassifyReadback rb) {
   const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  if (rb.dst) {         // the batch's readback rides along: stats row + prompt hashes of message b
-    if (lane < rb.stat_cols) rb.dst[(int64_t)b * rb.stat_cols + lane] = rb.stats[(int64_t)b * rb.stat_cols + lane];
-    for (int c = lane; c < rb.cap; c += 64)
-      rb.dst[rb.o_ph + (int64_t)b * rb.cap + c] = (int32_t)rb.hashes[(int64_t)b * rb.L + c];
+  const int b0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CH_MSGS;
+  if (b0 >= B) return;                                  // whole wave
+  const int nm = min(CH_MSGS, B - b0);
+  if (rb.dst) {         // the batch's readback rides along: stats rows + prompt hashes of these messages
+    for (int m = 0; m < nm; ++m) {
+      const int b = b0 + m;
+      if (lane < rb.stat_cols) rb.dst[(int64_t)b * rb.stat_cols + lane] = rb.stats[(int64_t)b * rb.stat_cols + lane];
+      for (int c = lane; c < rb.cap; c += 64)
+        rb.dst[rb.o_ph + (int64_t)b * rb.cap + c] = (int32_t)rb.hashes[(int64_t)b * rb.L + c];
+    }
   }
-  float part[8];
+  float part[CH_MSGS][8];
 #pragma unroll
-  for (int o = 0; o < 8; ++o) part[o] = 0.f;
+  for (int m = 0; m < CH_MSGS; ++m)
+#pragma unroll
+    for (int o = 0; o < 8; ++o) part[m][o] = 0.f;
   for (int h = lane; h < H; h += 64) {
-    const float x = pooled[(int64_t)b * H + h];
     const float4 wa = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8);
     const float4 wb = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8 + 4);
-    part[0] += x * wa.x; part[1] += x * wa.y; part[2] += x * wa.z; part[3] += x * wa.w;
-    part[4] += x * wb.x; part[5] += x * wb.y; part[6] += x * wb.z; part[7] += x * wb.w;
+#pragma unroll
+    for (int m = 0; m < CH_MSGS; ++m) {
+      const float x = m < nm ? pooled[(int64_t)(b0 + m) * H + h] : 0.f;
+      part[m][0] += x * wa.x; part[m][1] += x * wa.y; part[m][2] += x * wa.z; part[m][3] += x * wa.w;
+      part[m][4] += x * wb.x; part[m][5] += x * wb.y; part[m][6] += x * wb.z; part[m][7] += x * wb.w;
+    }
   }
 #pragma unroll
-  for (int o = 0; o < 8; ++o) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) part[o] += __shfl_xor(part[o], off, 64);
-  }
-  if (lane == 0) {
-    int best = 0;
-    float bv = -3.4e38f;
+  for (int m = 0; m < CH_MSGS; ++m)
 #pragma unroll
     for (int o = 0; o < 8; ++o) {
-      const float v = part[o] + b2[o];
-      logits[(int64_t)b * 8 + o] = v;
-      if (o < 4 && v > bv) { bv = v; best = o; }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) part[m][o] += __shfl_xor(part[m][o], off, 64);
     }
-    pred[b] = best + 1;
-    if (rb.dst) rb.dst[rb.o_pred + b] = best + 1;
+  if (lane < nm) {                                      // lane m writes message b0 + m
+#pragma unroll
+    for (int m = 0; m < CH_MSGS; ++m) {
+      if (m != lane) continue;
+      const int b = b0 + m;
+      int best = 0;
+      float bv = -3.4e38f;
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        const float v = part[m][o] + b2[o];
+        logits[(int64_t)b * 8 + o] = v;
+        if (o < 4 && v > bv) { bv = v; best = o; }
+      }
+      pred[b] = best + 1;
+      if (rb.dst) rb.dst[rb.o_pred + b] = best + 1;
+    }
   }
   if (rb.dst) __threadfence_system();   // host-mapped: visible once the stream's event completes
 }

@@ -146,6 +146,11 @@ def test_embed_pool_large_batch_spans_tiles():
         Hd = w.E.float()[idx] @ w.W1t.float().t() + w.b1
         Hd = 0.5 * Hd * (1 + torch.tanh(0.7978845608028654 * (Hd + 0.044715 * Hd ** 3)))
         assert torch.allclose(res.pooled[j], Hd.mean(0), atol=2e-2, rtol=2e-2)
+    # the classifier head at > 1024 messages runs 4 messages per wave: same
+    # logits as an fp32 product of the kernel's own pooled rows, every message
+    logits_ref = res.pooled.float() @ w.W2 + w.b2
+    pred_ref = logits_ref[:, :4].argmax(1).cpu().numpy() + 1
+    assert (pred_ref == res.pred).mean() > 0.999
 
 
 @pytest.mark.parametrize("n", [1, 37, 1500, 3000])
