@@ -351,6 +351,8 @@ def test_split_deployment_two_queue_manager_ranks():
         assert len(done) == len(ids), f"{len(done)} of {len(ids)} completed"
         st, stats = _req("GET", f"http://127.0.0.1:{qport}/api/v1/queues/stats")
         assert st == 200 and stats["dispatch"]["completed"] > 0       # rank 0's own share
+        # ... and rank 0's API sees the whole queue-manager job through the peer channel
+        assert stats["job"]["ranks"] == [0, 1] and stats["job"]["dispatch"]["completed"] >= len(ids), stats["job"]
     finally:
         for p in (gw, qm):
             if p is None:
