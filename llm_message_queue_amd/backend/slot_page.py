@@ -40,6 +40,10 @@ class SlotPage:
         finally:
             os.close(fd)
         self.words = np.frombuffer(self._mm, dtype=np.uint32, count=PAGE_BYTES // 4)
+        if create:
+            # a page left by a crashed job of the same name (torchrun's default
+            # run id is the same for every launch) must not be read as live load
+            self.words[:] = 0
         self.dev_ptr: Optional[int] = None
         self._registered_ptr: Optional[int] = None
         self.owner = create
