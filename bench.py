@@ -206,6 +206,8 @@ class FrontDoorRings:
         self.prefix = f"llmq-benchdoor-{job}-{os.environ.get('MASTER_PORT', '0')}"
         self._R = _native.shmring().ShmRing
         self.inbox = self._R(f"{self.prefix}-r{rank}", 64 << 20, "open")
+        while self.inbox.pop(4096, 0):            # records a crashed run of the same name left behind
+            pass                                  # (rank 0 ships only after the next barrier)
         self.out = []
         self.serial = 0
         self.pool = []
