@@ -199,3 +199,24 @@ def test_json_metrics_summary(client):
     assert d["requests_total"] >= 3 and "requests_per_second" in d and 0.0 <= d["error_rate"] <= 1.0
     assert set(d["queue_lengths"]) == {"realtime", "high", "normal", "low"}
     assert "dispatch" in d["latency"] and "end_to_end" in d["latency"]
+
+
+def test_merge_expositions_adds_rank_and_groups_families():
+    """The multi-GPU front door's /metrics (gateway/app.py:metrics_exposition):
+    every sample gets a ``rank`` label, each family is one block under one
+    HELP/TYPE header, and the result parses as Prometheus text."""
+    from prometheus_client.parser import text_string_to_metric_families
+    from llm_message_queue_amd.utils.metrics import _with_rank, merge_expositions
+    assert _with_rank("up 1", 3) == 'up{rank="3"} 1'
+    assert _with_rank("up{} 1", 3) == 'up{rank="3"} 1'
+    assert _with_rank('x_total{a="b"} 2.0', 0) == 'x_total{rank="0",a="b"} 2.0'
+    a = "# HELP x_total X\n# TYPE x_total counter\nx_total{q=\"hi\"} 1.0\n# HELP g G\n# TYPE g gauge\ng 4\n"
+    b = "# HELP x_total X\n# TYPE x_total counter\nx_total{q=\"hi\"} 2.0\n# HELP g G\n# TYPE g gauge\ng 5\n"
+    txt = merge_expositions({1: b, 0: a}).decode()
+    assert txt.count("# TYPE x_total counter") == 1 and txt.count("# TYPE g gauge") == 1
+    fams = {f.name: f for f in text_string_to_metric_families(txt)}
+    assert sorted((s.labels["rank"], s.value) for s in fams["x"].samples) == [("0", 1.0), ("1", 2.0)]
+    assert sorted((s.labels["rank"], s.value) for s in fams["g"].samples) == [("0", 4.0), ("1", 5.0)]
+    lines = txt.splitlines()
+    assert lines.index("# TYPE g gauge") > max(i for i, l in enumerate(lines) if l.startswith("x_total"))
+    assert merge_expositions({}) == b""
