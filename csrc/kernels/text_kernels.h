@@ -284,19 +284,40 @@ text_analyze_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict
       for (int s2 = 0; s2 < TA_SLOTS; ++s2) score[s2] += (sl == s2) ? cnt : 0;
     }
 
-    // ---- token hashes: the word-start lane walks its token (<= 32 bytes) in
+    // ---- token hashes: the word-start lane walks its token (<= 32 bytes).
+    // Bytes p .. p+15 are already in registers (w): the first 14 steps read
+    // them there (the space test looks 2 bytes ahead), longer tokens go on in
     // the LDS window (bytes past len are staged as 0, as the bounds below read)
     if (wstart && tok_idx < L) {
       uint32_t h = 0x811C9DC5u;
-      int q2 = p;
-      const uint8_t* wb = win8 + 4 - base;              // wb[i] = byte i of the message
-      for (int n = 0; n < TA_MAX_TOKEN_BYTES && q2 < len; ++n, ++q2) {
-        const uint32_t c = wb[q2];
-        if (n > 0) {
-          const uint32_t d1 = (q2 + 1 < len) ? wb[q2 + 1] : 0u;
-          const uint32_t d2 = (q2 + 2 < len) ? wb[q2 + 2] : 0u;
-          if (space_width(c, d1, d2) > 0) break;
+      int n = 0;
+      bool done = false;
+#pragma unroll
+      for (int i = 0; i < 14; ++i) {
+        if (!done) {
+          if (p + i >= len) {
+            done = true;
+          } else {
+            const uint32_t c = byte_of(w, i);
+            if (i > 0) {
+              const uint32_t d1 = (p + i + 1 < len) ? byte_of(w, i + 1) : 0u;
+              const uint32_t d2 = (p + i + 2 < len) ? byte_of(w, i + 2) : 0u;
+              done = space_width(c, d1, d2) > 0;
+            }
+            if (!done) {
+              h ^= (c >= 0x41u && c <= 0x5Au) ? (c | 0x20u) : c;
+              h *= 0x01000193u;
+              ++n;
+            }
+          }
         }
+      }
+      const uint8_t* wb = win8 + 4 - base;              // wb[i] = byte i of the message
+      for (int q2 = p + n; !done && n < TA_MAX_TOKEN_BYTES && q2 < len; ++n, ++q2) {
+        const uint32_t c = wb[q2];
+        const uint32_t d1 = (q2 + 1 < len) ? wb[q2 + 1] : 0u;
+        const uint32_t d2 = (q2 + 2 < len) ? wb[q2 + 2] : 0u;
+        if (space_width(c, d1, d2) > 0) break;
         h ^= (c >= 0x41u && c <= 0x5Au) ? (c | 0x20u) : c;
         h *= 0x01000193u;
       }
