@@ -215,8 +215,8 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
 
     async def _enqueue(m: Message) -> Optional[JSONResponse]:
         if G.cfg.queue.enable_metrics:
-            m.metadata["analysis"] = json.dumps(G.preprocessor.analyze_message_content(m.content),
-                                                separators=(",", ":"))
+            a = G.preprocessor.analyze_message_content(m.content)
+            m.metadata["analysis"] = G.preprocessor.analysis_json(a["word_count"], a["sentiment"], a["is_question"])
         try:
             # await the micro-batch (GPU preprocess + queue push) without
             # blocking the event loop: concurrent requests share one batch

@@ -106,6 +106,9 @@ class GatewayApp:
         gpu = torch.cuda.is_available() if use_gpu is None else use_gpu
         self.gpu = gpu
         self.preprocessor = Preprocessor(cfg.preprocessor, use_gpu=gpu and cfg.preprocessor.use_gpu)
+        # raw requests (C++ ingress) are preprocessed here, not in the API
+        # handler that records metadata["analysis"] for the other paths
+        self.preprocessor.record_analysis = bool(cfg.queue.enable_metrics) and role in ("rank", "dispatcher")
         self.factory = QueueFactory(cfg.queue, metrics=self.metrics)
         self.standard = self.factory.create_queue_manager("standard", QueueType.STANDARD)
         self.factory.create_queue_manager("delayed", QueueType.DELAYED)

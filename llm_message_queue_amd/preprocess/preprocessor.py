@@ -20,6 +20,7 @@ reference's map writes are unguarded).
 """
 from __future__ import annotations
 
+import json
 import threading
 import time
 from typing import Any, Dict, List, Optional, Sequence
@@ -48,6 +49,11 @@ class Preprocessor:
         self._gpu = None           # lazily-built ops.text.TextPipeline
         self._cpu = None           # lazily-built ops.text.CpuTextPipeline (False: unavailable)
         self._pattern_version = 0
+        # metadata["analysis"] (AnalyzeMessageContent as JSON, `api/handlers.go:
+        # 181-191`) for every message of a batch: set where raw requests are
+        # preprocessed away from the API handler that adds it otherwise (the
+        # GPU ranks behind the C++ front door, when queue.enable_metrics)
+        self.record_analysis = False
         self.stats = {"gpu_batches": 0, "gpu_messages": 0, "oracle_fallbacks": 0,
                       "cpu_messages": 0, "last_gpu_ms": 0.0}
 
@@ -211,6 +217,13 @@ class Preprocessor:
         wc, sent, q = oracle.content_analysis(content)
         return {"word_count": wc, "sentiment": sent, "is_question": q}
 
+    @staticmethod
+    def analysis_json(word_count: int, sentiment: str, is_question: bool) -> str:
+        """``json.Marshal`` of AnalyzeMessageContent's map (keys sorted, as Go
+        emits a map)."""
+        return json.dumps({"is_question": bool(is_question), "sentiment": sentiment, "word_count": int(word_count)},
+                          separators=(",", ":"))
+
     # ------------------------------------------------------------------ batch (GPU)
     def gpu_pipeline(self):
         """The HIP text pipeline, built on first use.  Raises if the HIP
@@ -258,6 +271,9 @@ class Preprocessor:
                 self.process_message(m)
                 if prompt_cap:
                     m.prompt_ids = oracle.token_hashes(m.content, prompt_cap)
+                if self.record_analysis:
+                    a = self.analyze_message_content(m.content)
+                    m.metadata["analysis"] = self.analysis_json(a["word_count"], a["sentiment"], a["is_question"])
             return msgs
         # Per-message Python is the ingest ceiling at tens of thousands of
         # requests/s, so everything the kernels return is decided for the
@@ -354,6 +370,20 @@ class Preprocessor:
                     m.created_at = now
                 m.updated_at = now
                 heads[i] = None                     # finished
+        if self.record_analysis:
+            seen = {}
+            if work:
+                for j, i in enumerate(work):
+                    if not fb[j]:
+                        seen[i] = (wc[j], sent[j], qs[j] == "true")
+            for i, m in enumerate(msgs):
+                a = seen.get(i)
+                if a is None:
+                    w, se, q = oracle.content_analysis(m.content) if m.content else (0, "neutral", False)
+                    a = (w, se, q)
+                if m.metadata is None:
+                    m.metadata = {}
+                m.metadata["analysis"] = self.analysis_json(*a)
         # messages the kernels never saw: empty content (the oracle's
         # metadata-priority / default rule) and user-decided heads
         for i, h in enumerate(heads):

@@ -98,6 +98,17 @@ def test_preprocessor_gpu_matches_cpu():
         ma = {k: v for k, v in a.metadata.items() if k != "ml_priority"}
         assert ma == b.metadata, (a.content, ma, b.metadata)
         assert a.queue_name == b.queue_name
+    # metadata["analysis"] from the kernel's stats equals the oracle's
+    # AnalyzeMessageContent for every message (explicit priority, empty, fold-special)
+    import json as _json
+    msgs_c = [m.copy() for m in msgs_b]
+    for m in msgs_c:
+        m.metadata = {}
+        m.priority = 4 if m.id == "e" and m.content == "help" else 0
+    pre.record_analysis = True
+    pre.process_batch(msgs_c, use_gpu=True, classify=True, prompt_cap=32)
+    for m in msgs_c:
+        assert _json.loads(m.metadata["analysis"]) == pre2.analyze_message_content(m.content), m.content
 
 
 # ----------------------------------------------------------------------------- classifier

@@ -138,6 +138,9 @@ def test_native_ingress_end_to_end(stack):
     got = [disp.messages.get(i) for i in ids]
     assert all(g is not None and g.status == "completed" for g in got)
     assert got[5].priority == 1 and got[5].metadata.get("analyzed")        # preprocessed in the dispatcher
+    # the dispatcher records AnalyzeMessageContent like the API handler does (queue.enable_metrics)
+    assert all(json.loads(g.metadata["analysis"]) == disp.preprocessor.analyze_message_content(g.content)
+               for g in got)
     assert got[7].priority == 4 and got[0].arrival_ns > 0
     assert ing.stats()["accepted"] == 31
 

@@ -175,3 +175,29 @@ def test_export_load_state_round_trip():
     with pytest.raises(Exception):
         b.load_state({"patterns": [[1, ["(unclosed"]]], "user_priorities": {}, "default_priority": 3})
     assert b.all_patterns() == a.all_patterns()                                          # unchanged on error
+
+
+def test_record_analysis_matches_analyze_message_content():
+    """Behind the C++ front door the ranks preprocess raw requests, so they
+    record metadata["analysis"] (AnalyzeMessageContent as Go's json.Marshal
+    emits it, `api/handlers.go:181-191`) for every message -- explicit
+    priority and empty content included -- on the batch paths too."""
+    import json as _json
+    texts = ["Is this a good question?", "urgent: bad bad service", "", "KELVIN K what now", "plain words",
+             "happy", "terrible?"]
+    for native in (True, False):
+        pre = Preprocessor(use_gpu=False)
+        pre.record_analysis = True
+        if not native:
+            pre.cfg.native_cpu = False
+        msgs = [Message(content=t, priority=(4 if i % 3 == 1 else 0)) for i, t in enumerate(texts)]
+        pre.process_batch(msgs, use_gpu=False, prompt_cap=8)
+        for m in msgs:
+            want = pre.analyze_message_content(m.content)
+            got = m.metadata["analysis"]
+            assert _json.loads(got) == want, (native, m.content, got)
+            assert list(_json.loads(got)) == ["is_question", "sentiment", "word_count"]   # Go map order
+    off = Preprocessor(use_gpu=False)
+    ms = [Message(content="hello")]
+    off.process_batch(ms, use_gpu=False)
+    assert "analysis" not in ms[0].metadata
