@@ -288,8 +288,11 @@ def cmd_scheduler(a) -> int:
             send("DELETE", f"/api/v1/endpoints/{eid}")
 
     def stats():
-        st = get("/api/v1/queues/stats").get("standard", {})
-        return {q: v.get("PendingCount", 0) for q, v in st.items()}
+        st = get("/api/v1/queues/stats")
+        job = st.get("job")
+        if job and "pending_by_tier" in job:      # multi-GPU gateway: every rank's queues
+            return {q: int(n) for q, n in job["pending_by_tier"].items()}
+        return {q: v.get("PendingCount", 0) for q, v in st.get("standard", {}).items()}
 
     sc = cfg.scheduler
     s = Scheduler(SchedulerConfig(strategy=sc.strategy, monitor_interval=sc.check_interval,
