@@ -11,9 +11,12 @@ metric/config.
 One "step" = one gateway tick on every rank: ingest the requests that
 arrived (Poisson clock), GPU-preprocess them (text_analyze + MFMA
 classifier), push into the native 4-tier queue, dispatch into free backend
-batch slots (multi-GPU: RCCL all_gather of load vectors + all_to_all of
-request descriptors), and run one full 32-layer continuous-batching forward
-(chunked prefill + decode) on the backend.
+batch slots (multi-GPU: all_gather of load vectors + all_to_all of request
+descriptors through the node-local shared-memory control plane, KV
+migration on the RCCL data group; a GPU that is ahead of its peers may run
+one extra local forward instead of idling at the exchange), and run one full
+32-layer continuous-batching forward (chunked prefill + decode) on the
+backend.
 
 Calibration (untimed, inside the warmup phase): the backend is driven in
 saturation to measure its service capacity C (req/s); the timed phase then

@@ -10,8 +10,9 @@ conversation state + persistence), re-designed around one MI355X node:
     pipeline (tokenize/hash, keyword scoring, sentiment/question, MFMA
     embedding classifier) and context summarisation, plus the backend
     stub's decode kernels;
-  * GPU backends (one process per GPU) coordinated with RCCL collectives
-    over xGMI (``parallel/``), load signals from amd-smi + device-resident
+  * GPU backends (one process per GPU) coordinated per tick through a
+    node-local shared-memory control plane, KV migration over RCCL / xGMI
+    (``parallel/``), load signals from amd-smi + device-resident
     in-flight counters (``backend/``).
 """
 __version__ = "0.1.0"

@@ -2,7 +2,8 @@
   * the four level queues exist before the first request (D1);
   * a dispatcher always runs (D2): with a GPU, the gateway tick loop feeds
     the local Llama-stub backend (and, under torchrun, the other ranks' GPUs
-    via the RCCL planner); without a GPU, QueueFactory workers drain the level
+    through the per-tick planner on the shared-memory control plane); without
+    a GPU, QueueFactory workers drain the level
     queues with a simulated LLM call that goes through the LoadBalancer's
     GetEndpoint/ReleaseEndpoint (what `cmd/queue-manager/main.go:141-166`
     simulates);

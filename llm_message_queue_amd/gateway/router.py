@@ -16,7 +16,9 @@ MI355X design:
     slot is free for it (no unbounded backend-side queue), so
     enqueue->dispatch latency is the honest gateway metric;
   * with >1 GPU, each process is router + backend; per tick the ranks
-    all_gather their load vectors over RCCL, compute the same plan
+    all_gather their load vectors over the node-local shared-memory control
+    plane (``parallel.comm.ShmComm``; KV migration rides the RCCL data group),
+    compute the same plan
     (``parallel.planner``), and move request descriptors / completion records
     with one all_to_all (``parallel.comm``).
 """

@@ -1,8 +1,9 @@
 """Control-plane communication between GPU backend processes (N10, N11).
 
 One process per GPU, ``torch.distributed``: the data plane on the ``nccl``
-backend (= RCCL on ROCm, over xGMI), the tiny control messages on a gloo
-group by default (see ``TorchComm`` for why they stay off the GPU streams).  The reference has no inter-service transport at all
+backend (= RCCL on ROCm, over xGMI), the tiny control messages through a
+node-local shared-memory segment by default (``ShmComm``; gloo when the
+ranks span nodes; see ``TorchComm`` for why they stay off the GPU streams).  The reference has no inter-service transport at all
 (its three microservices each own a private queue); here
 every scheduler tick does
   * ``all_gather`` of a fixed-size int64 load vector per rank (latency-bound,
