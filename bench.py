@@ -148,23 +148,33 @@ def comm_evidence(comm, dev, world: int, dry: bool) -> dict:
             print(f"bench: WARNING ranks share GPUs without oversubscription: {ev['devices']}", file=sys.stderr)
     nbytes = (64 << 20) if ev["data_backend"] == "nccl" else (8 << 20)
     tdev = dev if ev["data_backend"] == "nccl" else torch.device("cpu")
-    x = torch.ones(nbytes // 4, dtype=torch.float32, device=tdev)
-    for _ in range(2):
-        dist.all_reduce(x)
-    iters = 5
-    if tdev.type == "cuda":
-        torch.cuda.synchronize(tdev)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        dist.all_reduce(x)
-    if tdev.type == "cuda":
-        torch.cuda.synchronize(tdev)
-    dt = comm.max_f64((time.perf_counter() - t0) / iters)
+    try:
+        x = torch.ones(nbytes // 4, dtype=torch.float32, device=tdev)
+        for _ in range(2):
+            dist.all_reduce(x)
+        iters = 5
+        if tdev.type == "cuda":
+            torch.cuda.synchronize(tdev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        if tdev.type == "cuda":
+            torch.cuda.synchronize(tdev)
+        dt = (time.perf_counter() - t0) / iters
+        err = 0.0
+    except Exception as e:      # noqa: BLE001 -- the serving path's control plane does not use this group
+        print(f"bench: data-plane all_reduce failed: {e!r}", file=sys.stderr)
+        dt, err = 0.0, 1.0
+    # every rank reaches this gather (on the control plane), so a rank whose
+    # collective raised cannot leave the others waiting on a later one
+    dt, failed = comm.max_f64(dt), comm.max_f64(err) > 0
+    if failed:
+        ev["allreduce"] = {"bytes": nbytes, "backend": ev["data_backend"], "error": "all_reduce failed (see stderr)"}
+        return ev
     alg = nbytes / dt / 1e9
     ev["allreduce"] = {"bytes": nbytes, "backend": ev["data_backend"], "ms": round(dt * 1e3, 3),
                        "algbw_GBps": round(alg, 2), "busbw_GBps": round(alg * 2 * (world - 1) / world, 2)}
-    del x
     return ev
 
 
