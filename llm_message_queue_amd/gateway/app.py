@@ -605,7 +605,8 @@ class GatewayApp:
         from .router import LatencyRecorder
         parts = [self._rank_stats()]
         if self.peers is not None:
-            parts += [r for _k, r in sorted(self.peers.ask("stats", []).items()) if isinstance(r, dict)]
+            parts += [r for _k, r in sorted(self.peers.ask("stats", []).items())
+                      if isinstance(r, dict) and "counters" in r]      # (not a peer's {"error": ...})
         cnt: Dict[str, int] = {}
         for p in parts:
             for k, v in p["counters"].items():

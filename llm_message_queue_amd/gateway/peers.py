@@ -28,6 +28,10 @@ from .. import _native
 OPS = ("get", "list", "set_status", "remove", "stats", "reset_latency", "pre_state", "dlq", "dequeue", "metrics")
 
 
+def _is_error(res: Any) -> bool:
+    return isinstance(res, dict) and set(res) == {"error"}
+
+
 class PeerDirectory:
     REPLY_MAX = 2 << 20              # bytes per answer (the reply ring holds 8 MiB for all peers)
 
@@ -79,10 +83,12 @@ class PeerDirectory:
             return out
 
     def first(self, op: str, args: list, timeout_s: float = 2.0) -> Any:
-        """The first non-None answer (a message lives on one rank)."""
+        """The first non-None answer (a message lives on one rank).  A peer
+        whose handler raised answers ``{"error": ...}``: that is no answer."""
         for _r, res in sorted(self.ask(op, args, timeout_s).items()):
-            if res is not None and res is not False:
-                return res
+            if res is None or res is False or _is_error(res):
+                continue
+            return res
         return None
 
     # ------------------------------------------------------------------ ranks > 0
