@@ -83,6 +83,8 @@ def parse(argv=None):
                     help="qkv on hipBLASLt + rope_kv instead of the GEMM with the RoPE/KV epilogue (A/B)")
     ap.add_argument("--no-fused-mlp", action="store_true",
                     help="gate/up on hipBLASLt + silu_mul instead of the hand-written SwiGLU GEMM (A/B)")
+    ap.add_argument("--no-prune-last", action="store_true",
+                    help="run the last layer's o projection and MLP on every row (A/B; default: sampled rows only)")
     ap.add_argument("--split-qkv", action="store_true",
                     help="q and kv as two GEMMs into one buffer (bench/qkv_split.py; default: one fused QKV GEMM)")
     ap.add_argument("--seed", type=int, default=0)
@@ -373,7 +375,8 @@ def main(argv=None) -> int:
                                fused_mlp=False if a.no_fused_mlp else None,
                                fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
                                fused_head=False if a.no_fused_head else None,
-                               fused_resid=True if a.fused_resid else None)
+                               fused_resid=True if a.fused_resid else None,
+                               prune_last=not a.no_prune_last)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -638,7 +641,8 @@ def main(argv=None) -> int:
                    "fused_qkv": bool(engine.model.fused_qkv),
                    "row_scale_norm": bool(engine.model.row_scale_norm),
                    "fused_head": bool(engine.model.fused_head),
-                   "fused_resid": bool(engine.model.fused_resid)},
+                   "fused_resid": bool(engine.model.fused_resid),
+                   "prune_last": bool(getattr(engine.model, "prune_last", False))},
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),
         "p99_enqueue_to_dispatch_ms": round(lat["p99_enq_ms"], 3),

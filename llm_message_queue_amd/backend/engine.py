@@ -85,7 +85,7 @@ class BackendEngine:
                  token_budget: int = 2048, device="cuda", impl: str = "hip", seed: int = 0,
                  page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True,
                  split_qkv: bool = False, fused_mlp=None, fused_qkv=None, row_scale_norm: bool = True,
-                 fused_head=None, fused_resid=None):
+                 fused_head=None, fused_resid=None, prune_last: bool = True):
         self.cfg = model_cfg
         self.slots = slots
         self.max_ctx = max_ctx
@@ -98,7 +98,7 @@ class BackendEngine:
         self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
                                fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
-                               fused_resid=fused_resid)
+                               fused_resid=fused_resid, prune_last=prune_last)
         self.impl = impl
         self.weight_bytes = self.model.weight_bytes()
         self.active: Dict[int, Request] = {}            # slot -> request
@@ -463,6 +463,13 @@ class BackendEngine:
             self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(), slot.contiguous(),
                                samp, tiles=tiles, n_dec=0)
             n += 1
+        if getattr(self.model, "prune_last", False) and hasattr(self.model, "warm_tail"):
+            # the pruned last layer runs at the sampled-row count: a finer ladder
+            tail, t = list(range(1, 33)), 32
+            while t < self.token_budget:
+                t = max(t + 1, t * 9 // 8)
+                tail.append(min(t, self.token_budget))
+            n += self.model.warm_tail(tail)
         torch.cuda.synchronize(dev)
         self.warmed_shapes = n
         return n

@@ -71,7 +71,8 @@ class LlamaStub:
                  seed: int = 0, dtype=torch.bfloat16, residual_in_gemm: bool = True, split_qkv: bool = False,
                  fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512,
                  fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048, row_scale_norm: bool = True,
-                 fused_head: Optional[bool] = None, fused_resid: Optional[bool] = None):
+                 fused_head: Optional[bool] = None, fused_resid: Optional[bool] = None,
+                 prune_last: bool = True):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -86,6 +87,9 @@ class LlamaStub:
         # (profiles/r1_gemm_experiments.md).  False: F.linear + fused
         # residual-add RMSNorm.
         self.residual_in_gemm = residual_in_gemm
+        # the last layer's o projection and MLP only for the step's sampled
+        # rows (see ``hidden``); False: every row, then select (A/B)
+        self.prune_last = bool(prune_last)
         # QKV as two GEMMs (q: d x d, kv: 2*kv_heads*hd x d) written into
         # column slices of one qkv buffer: the fused 6144-wide GEMM at
         # T = 4096 is 384 256x256 tiles = 1.5 rounds over 256 CUs; the split
@@ -186,13 +190,16 @@ class LlamaStub:
         tokens into per-slot segments for the MFMA attention kernel (its first
         ``n_dec`` rows are 1-token decode tiles); without it attention runs
         per token."""
-        xf = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec)
-        sel = xf.index_select(0, sample_idx)
+        if self.prune_last and self.residual_in_gemm:
+            sel = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec, rows=sample_idx)
+        else:
+            sel = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec).index_select(0, sample_idx)
         return self.ops.greedy_head(sel, self.lm_head, self.fused_head)
 
     @torch.no_grad()
     def hidden(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
-               tiles: Optional[torch.Tensor] = None, n_dec: int = 0) -> torch.Tensor:
+               tiles: Optional[torch.Tensor] = None, n_dec: int = 0,
+               rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """The 32-layer trunk: final-normed hidden states [T, d] (writes the
         step's K/V into the cache).
 
@@ -200,21 +207,23 @@ class LlamaStub:
         On steps large enough for the hand-written GEMMs, the RMSNorms before
         the qkv and gate/up projections are never materialised: ``row_rms``
         computes each row's scale, the norm weight is folded into W at init,
-        and the GEMM epilogue applies the scale to its accumulator rows."""
+        and the GEMM epilogue applies the scale to its accumulator rows.
+
+        ``rows`` (the step's sampled rows): the last layer writes every
+        token's K/V and attends for every token as usual, then keeps only
+        these rows for its o projection and MLP -- the other rows' outputs of
+        that layer feed nothing (no later layer reads them, and the LM head
+        reads only the sampled rows), so the result for ``rows`` is the same
+        computation.  Returns [len(rows), d] then, else [T, d]."""
         cfg, ops = self.cfg, self.ops
         if not self.residual_in_gemm:
             return self._hidden_residual_norm(tokens, pos, slot, tiles, n_dec)
         res = F.embedding(tokens, self.embed)            # [T, d], updated in place
         T = res.shape[0]
         rows_qkv = self.fused_qkv and T >= self.min_fused_qkv_tokens
-        rows_mlp = self.fused_mlp and T >= self.min_fused_tokens
-        resid_o = self._cus > 0 and G.residual_tiles_ok(T, cfg.dim, self._cus)
-
-        def into_res(a, wt):                             # res += a · wtᵀ
-            if resid_o:
-                G.gemm_residual(a, wt, res)
-            else:
-                res.addmm_(a, wt.t())
+        last = len(self.layers) - 1
+        if rows is not None and rows.numel() == T:
+            rows = None                                  # every row sampled: nothing to drop
 
         for i, L in enumerate(self.layers):
             if rows_qkv and self.row_scale_norm:
@@ -225,16 +234,53 @@ class LlamaStub:
                                self.sin, cfg.heads, cfg.kv_heads, self.kcache[i], self.vcache[i])
             else:
                 q = self._qkv(ops.rmsnorm(res, L["attn_norm"], cfg.eps), L, i, pos, slot)
-            into_res(self._attend(q, i, pos, slot, tiles, n_dec), L["wo"])
-            if rows_mlp and self.row_scale_norm:
-                act = ops.swiglu_rows(res, L["w_gu"], ops.row_rms(res, cfg.eps))
-            elif rows_mlp:
-                act = G.gemm_swiglu(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"])
-            else:
-                act = ops.mlp_up(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"], self.fused_mlp,
-                                 self.min_fused_tokens)
-            into_res(act, L["w_down"])
+            a = self._attend(q, i, pos, slot, tiles, n_dec)
+            if i == last and rows is not None:
+                res, a = res.index_select(0, rows), a.index_select(0, rows)
+            self._mlp_block(res, a, L)
         return ops.rmsnorm(res, self.final_norm, cfg.eps)
+
+    @torch.no_grad()
+    def warm_tail(self, sizes) -> int:
+        """Run the last layer's o + MLP block (``_mlp_block``) once per row
+        count in ``sizes`` on scratch rows: with ``prune_last`` that block
+        sees the step's sampled-row count, not its token count, so its GEMM
+        shapes get their own warm-up (a first use of a library kernel loads
+        its code object)."""
+        cfg = self.cfg
+        L = self.layers[-1]
+        n = 0
+        for M in sizes:
+            M = int(M)
+            res = torch.zeros((M, cfg.dim), dtype=self.embed.dtype, device=self.device)
+            a = torch.zeros((M, cfg.heads * cfg.head_dim), dtype=self.embed.dtype, device=self.device)
+            self._mlp_block(res, a, L)
+            n += 1
+        return n
+
+    def _mlp_block(self, res: torch.Tensor, a: torch.Tensor, L: dict) -> None:
+        """res += o(a); res += down(swiglu(norm(res))) -- in place, with the
+        fused-path choices made for this block's row count."""
+        cfg, ops = self.cfg, self.ops
+        M = res.shape[0]
+        rows_mlp = self.fused_mlp and M >= self.min_fused_tokens
+        resid_o = self._cus > 0 and G.residual_tiles_ok(M, cfg.dim, self._cus)
+
+        def into_res(x, wt):                             # res += x · wtᵀ
+            if resid_o:
+                G.gemm_residual(x, wt, res)
+            else:
+                res.addmm_(x, wt.t())
+
+        into_res(a, L["wo"])
+        if rows_mlp and self.row_scale_norm:
+            act = ops.swiglu_rows(res, L["w_gu"], ops.row_rms(res, cfg.eps))
+        elif rows_mlp:
+            act = G.gemm_swiglu(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"])
+        else:
+            act = ops.mlp_up(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"], self.fused_mlp,
+                             self.min_fused_tokens)
+        into_res(act, L["w_down"])
 
     def _qkv(self, x, L, i, pos, slot):
         """qkv projection (hipBLASLt) + RoPE / KV-cache write of normalised rows."""
