@@ -17,7 +17,8 @@ def _engine(impl):
     from llm_message_queue_amd.models.llama_stub import LlamaConfig
     cfg = LlamaConfig(layers=2)                       # 8B dims, 2 layers
     eng = BackendEngine(cfg, slots=16, max_ctx=128, token_budget=96, device="cuda:0", impl=impl, seed=11,
-                        residual_in_gemm=(impl == "hip"))
+                        residual_in_gemm=(impl == "hip"), prune_last=False)   # every row's hidden state
+    # (last-layer row pruning has its own test: tests/test_prune_last.py)
     cap = []
     orig = eng.model.hidden
 
