@@ -236,6 +236,8 @@ class LlamaStub:
                 q = self._qkv(ops.rmsnorm(res, L["attn_norm"], cfg.eps), L, i, pos, slot)
             a = self._attend(q, i, pos, slot, tiles, n_dec)
             if i == last and rows is not None:
+                if rows.numel() == 0:                    # nothing sampled (a step of unfinished prefill
+                    return res[:0]                       # chunks): K/V written, no row kernel gets 0 rows
                 res, a = res.index_select(0, rows), a.index_select(0, rows)
             self._mlp_block(res, a, L)
         return ops.rmsnorm(res, self.final_norm, cfg.eps)
