@@ -16,14 +16,14 @@ def _step(model, T, slots):
     return tokens, pos, slot
 
 
-@pytest.mark.parametrize("sampled", [[7, 15, 23], [0, 5, 9, 31], list(range(32)), []])
+@pytest.mark.parametrize("sampled", [[7, 15, 23], [0, 5, 9, 31], list(range(32)), []])   # []: only unfinished prefill chunks
 def test_pruned_rows_match_full_forward(sampled):
     cfg = LlamaConfig(vocab=512, dim=256, layers=2, heads=2, kv_heads=1, ffn=512)
     full = LlamaStub(cfg, slots=4, max_ctx=16, device="cpu", impl="ref", prune_last=False)
     pruned = LlamaStub(cfg, slots=4, max_ctx=16, device="cpu", impl="ref", prune_last=True)
     tokens, pos, slot = _step(full, 32, 4)
     idx = torch.tensor(sampled, dtype=torch.long)
-    h_full = full.hidden(tokens, pos, slot).index_select(0, idx)   # (no sampled row: a step of unfinished prefill chunks)
+    h_full = full.hidden(tokens, pos, slot).index_select(0, idx)
     h_pruned = pruned.hidden(tokens, pos, slot, rows=idx)
     assert h_pruned.shape == (len(sampled), cfg.dim)
     torch.testing.assert_close(h_pruned, h_full, rtol=2e-2, atol=2e-2)
@@ -57,7 +57,7 @@ def test_pruned_rows_match_full_forward_hip(T, n_samp):
         for i in range(cfg.layers):
             assert torch.equal(full.kcache[i], pruned.kcache[i])
         return
-    h_full = full.hidden(tokens, pos, slot).index_select(0, idx)   # (no sampled row: a step of unfinished prefill chunks).float()
+    h_full = full.hidden(tokens, pos, slot).index_select(0, idx).float()
     h_pruned = pruned.hidden(tokens, pos, slot, rows=idx).float()
     err = (h_pruned - h_full).abs().max().item()
     assert err <= 0.05 * h_full.abs().max().item(), err
