@@ -107,6 +107,10 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   // exclusive scan of the B token counts in LDS -- every block redoes the
   // few-hundred-element scan instead of a separate single-block launch
   const int32_t* ro = row_off;
+  // row offsets of messages mlo .. mlo + wn in LDS: the whole scan (in-block
+  // path) or a 65-entry window from the tile's first message (global path)
+  int32_t* win = rinfo + 2 * EP_TM;
+  int mlo = 0, wn = B;
   if (ntok_src) {
     __shared__ int32_t wtot[4];
     int32_t* roff = rinfo + 2 * EP_TM;                                      // [B + 1] ints
@@ -142,17 +146,56 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   if (tile0 >= total) return;  // uniform across the block
   const int rows = min(EP_TM, total - tile0);
 
+  if (!ntok_src) {
+    // global row_off (large batches): wave 0 finds the tile's first message
+    // mlo (largest m with row_off[m] <= tile0) by a 64-ary search -- ceil(log64
+    // B) dependent L2 round trips instead of log2 B per row -- and the block
+    // keeps row_off[mlo .. mlo + 64] in LDS for the per-row searches and the
+    // gather / pooling offsets
+    __shared__ int s_mlo;
+    if (wv == 0) {
+      int lo = 0, hi = B - 1;                          // answer in [lo, hi]; row_off[lo] <= tile0
+      while (lo < hi) {
+        const int step = (hi - lo + 63) >> 6;          // 64 probes lo + step .. lo + 64 step
+        const int c = lo + (lane + 1) * step;
+        const bool ok = c <= hi && ro[c] <= tile0;     // a prefix of the lanes (row_off is sorted)
+        lo += __popcll(__ballot(ok)) * step;
+        hi = min(hi, lo + step - 1);
+      }
+      if (lane == 0) s_mlo = lo;
+    }
+    __syncthreads();
+    mlo = s_mlo;
+    wn = min(EP_TM, B - mlo);
+    if (tid <= wn) win[tid] = ro[mlo + tid];           // mlo + wn <= B: row_off has B + 1 entries
+    __syncthreads();
+  }
+  // row_off[m]: from the LDS window when m is inside it
+  auto rofs = [&](int m) -> int {
+    const int k = m - mlo;
+    return (k >= 0 && k <= wn) ? win[k] : ro[m];
+  };
+
   // ---- row -> (message, token) by binary search over row_off
   if (tid < EP_TM) {
     int m = -1;
     const int g = tile0 + tid;
     if (tid < rows) {
-      int lo = 0, hi = B - 1;
-      while (lo < hi) {  // largest m with row_off[m] <= g
-        const int mid = (lo + hi + 1) >> 1;
-        if (ro[mid] <= g) lo = mid; else hi = mid - 1;
+      if (mlo + wn == B || win[wn] > g) {              // inside the window
+        int lo = 0, hi = wn - 1;
+        while (lo < hi) {  // largest k with row_off[mlo + k] <= g
+          const int mid = (lo + hi + 1) >> 1;
+          if (win[mid] <= g) lo = mid; else hi = mid - 1;
+        }
+        m = mlo + lo;
+      } else {                                         // past it (zero-token messages): global search
+        int lo = mlo + wn, hi = B - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (ro[mid] <= g) lo = mid; else hi = mid - 1;
+        }
+        m = lo;
       }
-      m = lo;
     }
     rmsg[tid] = m;
   }
@@ -176,7 +219,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     const int m = rmsg[r];
     if (m >= 0) {
-      const int tok = tile0 + r - ro[m];
+      const int tok = tile0 + r - rofs(m);
       const uint32_t bucket = hashes[(int64_t)m * L + tok] & vmask;
       v = *reinterpret_cast<const uint4*>(E + (int64_t)bucket * EP_D + ch * 8);
     }
@@ -255,7 +298,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
         sum[j] += __shfl_xor(sum[j], 32, 64);
       }
       if (fq == 0) {
-        const int a = ro[cur], b = ro[cur + 1];
+        const int a = rofs(cur), b = rofs(cur + 1);
         const float inv = 1.0f / (float)(b - a);
         const bool whole = a >= tile0 && b <= tile0 + rows;
 #pragma unroll

@@ -91,7 +91,8 @@ static void embed_pool(uintptr_t hashes, int L, uintptr_t row_off, int B, int ro
   require(ntok_src == 0 || (ntok_stride >= 1 && B <= EP_MAX_LDS_SCAN), "embed_pool: in-block scan bounds");
   require(ntok_src != 0 || row_off != 0, "embed_pool: row_off or ntok_src");
   if (B == 0 || rows_upper == 0) return;
-  const size_t smem = EP_SMEM_BASE + (ntok_src ? 4 * ((size_t)B + 1) : 0);
+  // + the in-block scan's B + 1 offsets, or the global path's 65-entry window
+  const size_t smem = EP_SMEM_BASE + 4 * ((ntok_src ? (size_t)B : (size_t)EP_TM) + 1);
   if (!g_embed_attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)embed_pool_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)EP_SMEM_MAX));

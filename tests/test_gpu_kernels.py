@@ -216,6 +216,54 @@ def test_embed_pool_in_block_scan_matches_row_off():
     assert torch.allclose(out[0], res.pooled, atol=1e-5, rtol=1e-5)
 
 
+def test_embed_pool_global_window_with_zero_token_runs():
+    """Global row_off path (large batches): the tile's first message by the
+    64-ary search, row offsets from the 65-entry LDS window, and the global
+    fallback for rows past it -- reachable only when a tile's 64 rows span
+    more than 64 messages, i.e. runs of zero-token messages.  Against the
+    in-block scan path and an fp32 torch reference."""
+    from llm_message_queue_amd.ops.text import TextPipeline
+    from llm_message_queue_amd.utils.config import PreprocessorConfig
+    B, L = 2600, 64
+    texts = [" ".join(f"z{i}_{k}" for k in range(1 + (i * 11) % 40)) for i in range(B)]
+    pipe = TextPipeline(PreprocessorConfig(max_tokens=L), device=DEV)
+    res = pipe.run(texts, oracle.default_patterns(), classify=True, keep_device=True)
+    w, k = pipe.weights, pipe.ops
+    ntok = res.stats[:, 5].astype(np.int64).copy()
+    i = np.arange(B)
+    ntok[(i % 2 == 1) & (i < 600)] = 0           # alternate 0 / n tokens
+    ntok[700:1100] = 0                           # a long zero run
+    ntok[1100:1400] = np.minimum(ntok[1100:1400], 1)   # 1-token messages: > 64 messages per tile
+    ntok[B - 70:] = 0                            # trailing zero run (window clamped at B)
+    st = np.zeros((B, 16), dtype=np.int32)
+    st[:, 5] = ntok
+    st_d = torch.as_tensor(st, device=DEV)
+    row_off = torch.zeros(B + 1, dtype=torch.int32, device=DEV)
+    row_off[1:] = torch.as_tensor(np.cumsum(ntok), device=DEV).to(torch.int32)
+    rows_upper = int(ntok.sum())
+    s = torch.cuda.current_stream().cuda_stream
+    out = []
+    assert res.hashes.shape == (B, L) and res.hashes.is_contiguous()
+    for mode in ("global", "lds"):
+        pooled = torch.zeros(B, w.hidden, dtype=torch.float32, device=DEV)
+        k.embed_pool(res.hashes.data_ptr(), L, row_off.data_ptr() if mode == "global" else 0, B, rows_upper,
+                     w.E.data_ptr(), w.vocab, w.W1t.data_ptr(), w.b1.data_ptr(), w.hidden, pooled.data_ptr(), s,
+                     st_d.data_ptr() + 4 * 5 if mode == "lds" else 0, 16 if mode == "lds" else 0)
+        out.append(pooled)
+    torch.cuda.synchronize()
+    assert torch.allclose(out[0], out[1], atol=1e-5, rtol=1e-5)
+    assert (out[0][torch.as_tensor(ntok == 0, device=DEV)] == 0).all()
+    hashes = res.hashes.cpu().numpy().view(np.uint32)
+    for j in (0, 1, 598, 599, 650, 1099, 1100, 1250, 1399, 2000, B - 71):
+        n = int(ntok[j])
+        if n == 0:
+            continue
+        idx = torch.as_tensor((hashes[j, :n] & (w.vocab - 1)).astype(np.int64), device=DEV)
+        Hd = w.E.float()[idx] @ w.W1t.float().t() + w.b1
+        Hd = 0.5 * Hd * (1 + torch.tanh(0.7978845608028654 * (Hd + 0.044715 * Hd ** 3)))
+        assert torch.allclose(out[0][j], Hd.mean(0), atol=2e-2, rtol=2e-2), j
+
+
 # ----------------------------------------------------------------------------- llama ops
 @pytest.fixture(scope="module")
 def ops():
