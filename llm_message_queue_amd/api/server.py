@@ -29,7 +29,7 @@ import json
 import math
 import time
 import uuid
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Sequence
 
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, Response
@@ -98,8 +98,16 @@ async def _json(request: Request) -> Any:
     return json.loads(raw)
 
 
-def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
-    """``gw_app`` is a ``gateway.app.GatewayApp``."""
+def create_app(gw_app, allowed_origins: Optional[List[str]] = None,
+               trusted_proxies: Sequence[str] = ()) -> FastAPI:
+    """``gw_app`` is a ``gateway.app.GatewayApp``.
+
+    ``trusted_proxies``: peer addresses whose ``X-Forwarded-For`` names the
+    real client (the C++ front door on loopback, which drops any
+    client-sent XFF and appends the connection's own address,
+    `csrc/ingress/http_ingress.cpp` start_proxy).  Behind it every request's
+    peer is 127.0.0.1, so without this the per-IP rate limit would put every
+    proxied client into one bucket."""
     app = FastAPI(title="llm_message_queue_amd", version=VERSION)
     origins = allowed_origins if allowed_origins is not None else ["*"]
     G = gw_app
@@ -109,6 +117,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
     # Middleware order, outermost first: CORS -> envelope -> guard -> route.
     guard = guard_from_config(G.cfg)
     app.state.guard = guard
+    trusted = frozenset(trusted_proxies)
     if guard is not None:
         @app.middleware("http")
         async def guard_mw(request: Request, call_next):
@@ -122,8 +131,13 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
                     user = str(body.get("user_id", "") or "") if isinstance(body, dict) else ""
                 except ValueError:
                     user = ""
+            ip = request.client.host if request.client else ""
+            if ip in trusted:
+                fwd = request.headers.get("x-forwarded-for", "")
+                if fwd:
+                    ip = fwd.rsplit(",", 1)[-1].strip() or ip
             code, subject, role, reason, retry = guard.check(
-                request.method, path, request.client.host if request.client else "",
+                request.method, path, ip,
                 request.headers.get(guard.key_header, ""), request.headers.get("authorization", ""), user)
             if code == 401:
                 return JSONResponse({"error": reason}, status_code=401, headers={"WWW-Authenticate": "Bearer"})
@@ -288,7 +302,7 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None) -> FastAPI:
             if isinstance(res, dict):
                 return {"status": "deleted", "message_id": mid, "dequeued": bool(res.get("dequeued"))}
             return _err(404, "Message not found")
-        removed = m.queue_name and G.standard.has_queue(m.queue_name) and G.standard.mlq.remove(m.queue_name, m)
+        removed = m.queue_name and G.standard.has_queue(m.queue_name) and G.standard.remove_message(m.queue_name, m)
         G.messages.remove(mid)
         return {"status": "deleted", "message_id": mid, "dequeued": bool(removed)}
 

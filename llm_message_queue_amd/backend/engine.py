@@ -485,6 +485,12 @@ class BackendEngine:
             else:
                 self.fault.pop(k, None)
 
+    def fence(self, events) -> None:
+        """Device events the next launch waits for (work that may still write
+        slots this engine is about to reuse: evacuated steps, abandoned KV
+        imports)."""
+        self._fence.extend(e for e in events if e is not None)
+
     def abort_all(self) -> List[Request]:
         """Evacuate: drop every queued step and active request (slots are
         freed) and return the unfinished requests so the caller can re-route

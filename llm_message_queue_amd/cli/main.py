@@ -202,7 +202,8 @@ def cmd_serve(a, role: str = "serve") -> int:
         # front, status / conversation / admin routes live with the dispatcher
         import uvicorn
         from ..api.server import create_app
-        app = create_app(gapp)
+        # behind the C++ front door every proxied request arrives from loopback
+        app = create_app(gapp, trusted_proxies=("127.0.0.1", "::1") if front else ())
         api_host, api_port = cfg.server.host, cfg.server.port
         if front:
             # the public port belongs to the C++ front door; the API server

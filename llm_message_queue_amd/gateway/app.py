@@ -487,7 +487,7 @@ class GatewayApp:
             if m is None:
                 return False
             removed = bool(m.queue_name and self.standard.has_queue(m.queue_name)
-                           and self.standard.mlq.remove(m.queue_name, m))
+                           and self.standard.remove_message(m.queue_name, m))
             return {"dequeued": removed}
         if op == "stats":
             return self._rank_stats()
@@ -552,7 +552,7 @@ class GatewayApp:
         mgr = self.factory.get_queue_manager(queue_type)
         m = self.messages.get(mid)
         return bool(mgr is not None and m is not None and m.queue_name and mgr.has_queue(m.queue_name)
-                    and mgr.mlq.remove(m.queue_name, m))
+                    and mgr.remove_message(m.queue_name, m))
 
     def dequeue(self, queue_type: str, mid: str) -> bool:
         """Remove a queued message from ``queue_type`` on whichever rank
@@ -617,6 +617,8 @@ class GatewayApp:
         rec = LatencyRecorder(len(self.gateway.tiers))
         tiers = self.gateway.tiers
         return {"ranks": sorted(int(p["rank"]) for p in parts), "dispatch": cnt,
+                # ranks whose answer did not arrive (timed out / dropped): the totals leave them out
+                "missing_ranks": list(self.peers.last_missing) if self.peers is not None else [],
                 "accepted_by_rank": {int(p["rank"]): int(p["accepted"]) for p in parts},
                 "pending_by_tier": {n: sum(int(p.get("pending", [0] * len(tiers))[t]) for p in parts)
                                     for t, n in enumerate(tiers)},

@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import threading
 import time
-from typing import Any, Callable, Dict, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 import msgpack
 
@@ -33,7 +33,19 @@ def _is_error(res: Any) -> bool:
 
 
 class PeerDirectory:
-    REPLY_MAX = 2 << 20              # bytes per answer (the reply ring holds 8 MiB for all peers)
+    """Rank 0 asks, ranks > 0 answer.  Each peer answers into a reply ring of
+    its own (``REPLY_RING`` bytes), so one peer's large answer can never
+    crowd another's out; an answer larger than ``CHUNK`` travels in pages
+    (``[qid, rank, seq, n, bytes]``), so its size is bounded only by
+    ``ANSWER_MAX``.  A page that does not fit is retried until the query's
+    deadline and then counted in ``dropped`` -- never silently lost -- and
+    rank 0 reports the ranks that did not answer (``last_missing``,
+    ``missing_total``).  Late pages of a query that already timed out are
+    discarded on the next ask, so they take no space from it."""
+
+    CHUNK = 1 << 20                  # bytes per reply page
+    REPLY_RING = 4 << 20             # per-peer reply ring (>= 2 pages in flight plus slack)
+    ANSWER_MAX = 256 << 20           # larger answers are replaced by an explicit error
 
     def __init__(self, name: str, rank: int, world: int, handler: Optional[Callable[[str, list], Any]] = None):
         """``handler(op, args)`` answers a query on ranks > 0 (the app's
@@ -43,21 +55,24 @@ class PeerDirectory:
         self.handler = handler
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
-        self.reply = R(f"llmq-{name}-qrep", 8 << 20, "open")
-        self.asked = self.answered = self.timeouts = 0
+        self.asked = self.answered = self.timeouts = self.dropped = self.missing_total = 0
+        self.last_missing: List[int] = []
         if rank == 0:
             self.qrings = {r: R(f"llmq-{name}-q{r}", 1 << 20, "open") for r in range(1, world)}
+            self.replies = {r: R(f"llmq-{name}-qrep{r}", self.REPLY_RING, "open") for r in range(1, world)}
             self._lock = threading.Lock()
             self._qid = 0
         else:
             self.qring = R(f"llmq-{name}-q{rank}", 1 << 20, "open")
+            self.reply = R(f"llmq-{name}-qrep{rank}", self.REPLY_RING, "open")
             self._thread = threading.Thread(target=self._serve, name="peer-queries", daemon=True)
             self._thread.start()
 
     # ------------------------------------------------------------------ rank 0
     def ask(self, op: str, args: list, timeout_s: float = 2.0) -> Dict[int, Any]:
         """Send ``op`` to every peer and collect ``{rank: result}`` (ranks
-        that did not answer within ``timeout_s`` are missing)."""
+        that did not answer within ``timeout_s`` are missing, and listed in
+        ``last_missing``)."""
         if self.rank != 0 or self.world <= 1:
             return {}
         if op not in OPS:
@@ -65,21 +80,45 @@ class PeerDirectory:
         with self._lock:
             self._qid += 1
             qid = self._qid
-            rec = msgpack.packb([qid, op, list(args)], use_bin_type=True)
+            deadline = time.monotonic() + timeout_s
+            # the responder stops retrying a page that does not fit at the deadline
+            rec = msgpack.packb([qid, op, list(args), int(deadline * 1e9)], use_bin_type=True)
+            for r, ring in self.replies.items():
+                while ring.pop(64, 0):                # late pages of earlier queries
+                    pass
             for r, q in self.qrings.items():
                 q.push(rec, 1)
             self.asked += 1
             out: Dict[int, Any] = {}
-            deadline = time.monotonic() + timeout_s
-            while len(out) < self.world - 1:
+            pages: Dict[int, Dict[int, bytes]] = {}
+            pending = set(self.replies)
+
+            def take(r: int, recs) -> bool:
+                for _tag, b in recs:
+                    q, _rr, seq, n, chunk = msgpack.unpackb(b, raw=False, strict_map_key=False)
+                    if q != qid:
+                        continue
+                    pg = pages.setdefault(r, {})
+                    pg[int(seq)] = chunk
+                    if len(pg) == int(n):
+                        out[r] = msgpack.unpackb(b"".join(pg[i] for i in range(int(n))), raw=False,
+                                                 strict_map_key=False)
+                        pending.discard(r)
+                return bool(recs)
+
+            while pending:
                 left = deadline - time.monotonic()
                 if left <= 0:
                     self.timeouts += 1
                     break
-                for _tag, b in self.reply.pop(64, max(1, int(left * 1000))):
-                    q, r, res = msgpack.unpackb(b, raw=False, strict_map_key=False)
-                    if q == qid:                       # (late answers to an earlier query are dropped)
-                        out[int(r)] = res
+                got = False
+                for r in sorted(pending):
+                    got |= take(r, self.replies[r].pop(64, 0))
+                if not got and pending:                # block briefly on one outstanding peer's ring
+                    r0 = min(pending)
+                    take(r0, self.replies[r0].pop(64, max(1, min(20, int(left * 1000)))))
+            self.last_missing = sorted(pending)
+            self.missing_total += len(pending)
             return out
 
     def first(self, op: str, args: list, timeout_s: float = 2.0) -> Any:
@@ -92,21 +131,35 @@ class PeerDirectory:
         return None
 
     # ------------------------------------------------------------------ ranks > 0
+    def _answer(self, qid: int, res: Any, deadline_ns: int) -> bool:
+        body = msgpack.packb(res, use_bin_type=True, default=str)
+        if len(body) > self.ANSWER_MAX:
+            body = msgpack.packb({"error": f"reply of {len(body)} B exceeds {self.ANSWER_MAX} B"},
+                                 use_bin_type=True)
+        n = max(1, -(-len(body) // self.CHUNK))
+        for seq in range(n):
+            rec = msgpack.packb([qid, self.rank, seq, n, body[seq * self.CHUNK:(seq + 1) * self.CHUNK]],
+                                use_bin_type=True)
+            # rank 0 drains the pages while it waits: retry a full ring until
+            # the query's deadline, then give the answer up explicitly
+            while not self.reply.push(rec, 1):
+                if self._stop.is_set() or time.monotonic_ns() > deadline_ns:
+                    self.dropped += 1
+                    return False
+                time.sleep(0.001)
+        return True
+
     def _serve(self) -> None:
         while not self._stop.is_set():
             for _tag, b in self.qring.pop(16, 100):
-                qid = -1
+                qid, deadline_ns = -1, 0
                 try:
-                    qid, op, args = msgpack.unpackb(b, raw=False, strict_map_key=False)
+                    qid, op, args, deadline_ns = msgpack.unpackb(b, raw=False, strict_map_key=False)
                     res = self.handler(op, args) if self.handler is not None else None
                 except Exception as e:                # noqa: BLE001 -- answered, never fatal
                     res = {"error": str(e)}
-                rec = msgpack.packb([qid, self.rank, res], use_bin_type=True, default=str)
-                if len(rec) > self.REPLY_MAX:          # never wedge the shared reply ring
-                    rec = msgpack.packb([qid, self.rank, {"error": f"reply of {len(rec)} B too large"}],
-                                        use_bin_type=True)
-                self.reply.push(rec, 1)
-                self.answered += 1
+                if self._answer(qid, res, int(deadline_ns)):
+                    self.answered += 1
 
     def stop(self) -> None:
         self._stop.set()
@@ -116,7 +169,8 @@ class PeerDirectory:
 
     def close(self, unlink: bool = False) -> None:
         self.stop()
-        rings = [self.reply] + (list(self.qrings.values()) if self.rank == 0 else [self.qring])
+        rings = (list(self.qrings.values()) + list(self.replies.values())) if self.rank == 0 \
+            else [self.qring, self.reply]
         for r in rings:
             if unlink:
                 r.unlink()

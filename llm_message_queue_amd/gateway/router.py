@@ -160,6 +160,9 @@ class Gateway:
         self.max_conc = [lv.max_concurrent for lv in levels]
         for n in self.tiers:                          # D1: the level queues exist
             self.qm.create_queue(n)
+        # a queued message removed other than by dispatch (admin delete,
+        # peer dequeue, retention cleanup) releases its (home GPU, tier) pin
+        self.qm.on_remove.append(lambda m: self._pin(m, -1))
         self.metrics = metrics
         self._inbox: List[Message] = []
         self._inbox_lock = threading.Lock()
@@ -956,7 +959,11 @@ class Gateway:
             wants = []
             if up[self.rank]:
                 for ck, rs in held.items():
-                    for h in sorted({h for _, h in rs if 0 <= h < W and h != self.rank and up[h]}):
+                    # ONE source per conversation: the home its latest held
+                    # turn names.  Wanting from two homes could land a stale
+                    # import over the slot a replay of the other wrote
+                    h = next((h for _, h in reversed(rs) if 0 <= h < W and h != self.rank and up[h]), -1)
+                    if h >= 0:
                         wants.append((ck, h))
                         wanted.add(ck)
             result = self.migrator.execute(orders, wants, self.engine, self.rank)
@@ -1070,6 +1077,11 @@ class Gateway:
             else:
                 origin, handle, tier, _a, _e = r.meta
                 self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
+        if self.migrator is not None:
+            # imports still landing on the side stream write into reserved
+            # slots that abort_all hands back to the free list: the next
+            # forward must wait for them, and their results are void
+            self.engine.fence(self.migrator.abandon())
         for r in self.engine.abort_all():
             n += 1
             if isinstance(r.meta, Message):

@@ -172,10 +172,14 @@ class KVMigrator:
             slot, n = engine.export_kv(conv)
             mine[(dst, conv)] = (slot, n)
             offers[dst].append((OFFER, conv, n))
-        want_set = set()
+        # one source per conversation (the last one listed): the result is
+        # keyed by conversation, so two sources could not be told apart
+        src_of: Dict[int, int] = {}
         for conv, src in wants:
-            if src == me or not 0 <= src < W or (src, conv) in want_set:
-                continue
+            if src != me and 0 <= src < W:
+                src_of[conv] = src
+        want_set = set()
+        for conv, src in src_of.items():
             want_set.add((src, conv))
             offers[src].append((WANT, conv, 0))
         got = self.comm.all_to_all_var([_rows(x) for x in offers], HDR_W)
@@ -282,6 +286,18 @@ class KVMigrator:
                 keep.append((conv, slot, n, ev, buf))
         self._pending = keep
         return out
+
+    def abandon(self) -> List[object]:
+        """Evacuation: forget every import in flight (its slot goes back to
+        the engine's free list) and return the side-stream events the
+        compute stream must wait on before a slot is reused -- a late unpack
+        would otherwise write stale KV under a new request's prefill."""
+        evs = []
+        for _conv, _slot, _n, ev, buf in self._pending:
+            if ev is not None and not any(ev is e for e in evs):
+                evs.append(ev)
+        self._pending = []
+        return evs
 
     def in_flight(self) -> int:
         return len(self._pending)

@@ -62,6 +62,10 @@ class QueueManager:
         self._monitor: Optional[threading.Thread] = None
         self.threshold_events: List[dict] = []   # observable autoscale recommendations
         self.expired_count = 0
+        # called with each message taken out of a queue other than by a pop
+        # (admin delete, peer dequeue, retention cleanup): the gateway
+        # releases the message's (home GPU, tier) pin here
+        self.on_remove: List[Callable[[Message], None]] = []
 
     # ------------------------------------------------------------- lifecycle
     def start(self) -> None:
@@ -299,6 +303,15 @@ class QueueManager:
         self.threshold_events = (self.threshold_events + events)[-100:]
         return events
 
+    def remove_message(self, name: str, m: Message) -> bool:
+        """Take one queued message out of ``name`` (not a dispatch): every
+        removal path goes through here so ``on_remove`` hooks see it."""
+        if not self.mlq.remove(name, m):
+            return False
+        for fn in self.on_remove:
+            fn(m)
+        return True
+
     def cleanup_stale_messages(self) -> int:
         """Expire pending messages older than ``max_retention_period``
         (a no-op stub in the reference, `queue_manager.go:549-553`)."""
@@ -309,7 +322,7 @@ class QueueManager:
         n = 0
         for name in list(self._queues):
             for m in self.mlq.messages(name):
-                if m.enqueued_at and m.enqueued_at < cutoff and self.mlq.remove(name, m):
+                if m.enqueued_at and m.enqueued_at < cutoff and self.remove_message(name, m):
                     m.status = "timeout"
                     n += 1
         self.expired_count += n

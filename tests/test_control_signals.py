@@ -201,3 +201,46 @@ def test_migration_to_a_destination_that_went_unhealthy_leaves_no_mail():
     assert all(not v for v in comms[0].hub.mail.values()), comms[0].hub.mail
     # the KV is still parked at the home or moved once to the third GPU, never lost to the dead one
     assert gws[flipped].engine.kv_imported == 0
+
+
+def test_every_removal_of_a_queued_turn_releases_its_pin():
+    """a queued conversation turn is counted once under
+    its (home GPU, tier) pin.  Admin delete, a peer's remove / dequeue and
+    retention cleanup take it out of the queue without a dispatch; each must
+    release the pin, or the planner (and the extra-step guard, which skips a
+    tier with turns homed elsewhere) reads a phantom turn for good."""
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    comms = FakeComm.make(2)
+    cfg = _cfg()
+    cfg.queue.worker.process_interval = 5_000_000
+    app = GatewayApp(cfg, use_gpu=False, comm=comms[0], start=False)
+    gw = app.gateway
+    assert gw.world == 2
+
+    def queued(mid):
+        m = Message(id=mid, conversation_id="dlg-" + mid, content="hi", priority=3, metadata={"home_gpu": 1})
+        m.queue_name = "normal"
+        assert gw._enqueue([m])[0][1] is None
+        app.messages.put(m)
+        return m
+
+    queued("a")
+    assert gw.pinned[1].sum() == 1
+    assert app.peer_op("remove", ["a"]) == {"dequeued": True}           # peer 'remove'
+    assert gw.pinned.sum() == 0
+    queued("b")
+    assert app.peer_op("dequeue", ["standard", "b"]) is True            # peer 'dequeue'
+    assert gw.pinned.sum() == 0
+    queued("c")
+    from fastapi.testclient import TestClient
+    from llm_message_queue_amd.api.server import create_app
+    with TestClient(create_app(app)) as c:                               # local DELETE route
+        r = c.delete("/api/v1/messages/c")
+        assert r.status_code == 200 and r.json()["dequeued"] is True
+    assert gw.pinned.sum() == 0
+    m = queued("d")                                                      # retention cleanup
+    m.enqueued_at = 1
+    app.standard.config.max_retention_period = 1
+    assert app.standard.cleanup_stale_messages() == 1
+    assert gw.pinned.sum() == 0
+    app.stop()

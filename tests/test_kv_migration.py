@@ -161,3 +161,25 @@ def test_stale_parked_copy_is_not_reused():
     r2 = Request(2, np.arange(20, 26, dtype=np.int32), 3, conv=conv, history=np.zeros(parked, dtype=np.int32))
     e2.admit([r2])
     assert r2.reused == parked and e2.kv_stale == 0
+
+
+def test_a_conversation_is_wanted_from_one_source_only():
+    """held turns of one conversation naming two homes
+    (one of which has nothing) must not produce a replay result while an
+    import from the other is still possible: the destination wants the KV
+    from ONE source -- the last listed -- and its result comes from there."""
+    conv = 777
+    p1 = np.arange(3, 14, dtype=np.int32)
+    comms = FakeComm.make(3, timeout_s=10)
+    g0, g1, g2 = _eng(), _eng(), _eng()
+    _run(g1, Request(1, p1.copy(), 3, conv=conv))          # the KV lives on GPU 1; GPU 0 has none
+    ms = [KVMigrator(g.model, c) for g, c in zip((g0, g1, g2), comms)]
+    got = {}
+    ths = [threading.Thread(target=lambda: got.update(r0=ms[0].execute([(conv, 2)], [], g0, 0))),
+           threading.Thread(target=lambda: got.update(r1=ms[1].execute([(conv, 2)], [], g1, 1)))]
+    for t in ths:
+        t.start()
+    got["r2"] = ms[2].execute([], [(conv, 0), (conv, 1)], g2, 2)
+    for t in ths:
+        t.join()
+    assert got["r2"][conv] == len(p1) + 3 - 1 and g2.kv_imported == 1

@@ -60,3 +60,53 @@ def test_ask_collects_every_rank(dirs):
     assert "error" in got[2]
     with pytest.raises(ValueError):
         root.ask("not-an-op", [])
+
+
+def test_large_answers_from_every_peer_arrive_paged():
+    """7 peers each answering several MiB (more than a reply page
+    and, together, far more than any one ring) all arrive whole."""
+    name = f"ptbig{os.getpid()}"
+    world = 8
+    blob = {r: os.urandom(3 << 20) + bytes([r]) for r in range(1, world)}
+    peers = [PeerDirectory(name, r, world, lambda op, args, r=r: [r, blob[r]]) for r in range(1, world)]
+    root = PeerDirectory(name, 0, world)
+    try:
+        for _ in range(2):
+            got = root.ask("dlq", ["list"], timeout_s=20.0)
+            assert sorted(got) == list(range(1, world)) and root.last_missing == []
+            for r, v in got.items():
+                assert v[0] == r and v[1] == blob[r]
+        assert sum(p.dropped for p in peers) == 0
+    finally:
+        for p in peers:
+            p.close()
+        root.close(unlink=True)
+        for p in peers:
+            p.qring.unlink()
+
+
+def test_a_silent_peer_is_reported_missing_and_its_late_answer_is_discarded():
+    name = f"ptslow{os.getpid()}"
+    import time
+    world = 3
+    gate = {"sleep": 0.6}
+
+    def slow(op, args):
+        time.sleep(gate["sleep"])
+        return "late" if op == "stats" else None
+
+    peers = [PeerDirectory(name, 1, world, lambda op, args: "fast"), PeerDirectory(name, 2, world, slow)]
+    root = PeerDirectory(name, 0, world)
+    try:
+        got = root.ask("stats", [], timeout_s=0.2)
+        assert got == {1: "fast"} and root.last_missing == [2] and root.missing_total == 1
+        time.sleep(0.8)                       # rank 2's late answer lands in its ring now
+        gate["sleep"] = 0.0
+        got = root.ask("get", ["x"], timeout_s=2.0)
+        assert got == {1: "fast", 2: None} and root.last_missing == []   # the stale "late" is not taken
+    finally:
+        for p in peers:
+            p.close()
+        root.close(unlink=True)
+        for p in peers:
+            p.qring.unlink()

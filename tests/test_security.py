@@ -304,3 +304,81 @@ def test_native_ingress_guard_and_envelope():
     finally:
         ing.stop()
         ring.close(unlink=True)
+
+
+def test_per_ip_buckets_survive_the_front_door_proxy():
+    """behind the C++ front door every proxied request reaches the
+    API server from loopback.  With the front door as a trusted proxy the
+    guard keys the per-IP bucket on the X-Forwarded-For the front door sets
+    (the connection's own address), so two clients keep separate buckets;
+    without it they would share the loopback one."""
+    import http.client
+    import socket
+    import threading
+    import time
+
+    import uvicorn
+
+    from llm_message_queue_amd.gateway.native_ingress import NativeIngress
+
+    cfg = default_config()
+    cfg.loadbalancer.rate_limiting.enabled = True
+    cfg.loadbalancer.rate_limiting.per_ip.requests_per_second = 0.001
+    cfg.loadbalancer.rate_limiting.per_ip.burst_size = 2
+    gw = _app(cfg)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        api_port = s.getsockname()[1]
+    server = uvicorn.Server(uvicorn.Config(create_app(gw, trusted_proxies=("127.0.0.1",)), host="127.0.0.1",
+                                           port=api_port, log_level="warning"))
+    th = threading.Thread(target=server.run, daemon=True)
+    th.start()
+    ing = None
+    try:
+        t0 = time.time()
+        while not server.started and time.time() - t0 < 20:
+            time.sleep(0.05)
+        assert server.started
+        ing = NativeIngress(0, f"pyt-xff-{os.getpid()}", threads=1, host="127.0.0.1",
+                            upstream=("127.0.0.1", api_port))
+        port = ing.start()
+
+        def get(src):
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=10, source_address=(src, 0))
+            try:
+                c.request("GET", "/api/v1/queues/stats")
+                r = c.getresponse()
+                r.read()
+                return r.status
+            finally:
+                c.close()
+
+        assert [get("127.0.0.2") for _ in range(3)] == [200, 200, 429]
+        # another client, its own bucket (it would be 429 on a shared loopback bucket)
+        assert [get("127.0.0.3") for _ in range(2)] == [200, 200]
+        assert get("127.0.0.3") == 429
+    finally:
+        if ing is not None:
+            ing.stop()
+            from llm_message_queue_amd import _native
+            _native.shmring().ShmRing(f"llmq-pyt-xff-{os.getpid()}-req", 1 << 20, "open").unlink()
+        server.should_exit = True
+        th.join(timeout=10)
+        gw.stop()
+
+
+def test_untrusted_peer_cannot_pick_its_bucket():
+    """A client talking to the API server directly (not a trusted proxy)
+    cannot choose its bucket with a forged X-Forwarded-For."""
+    cfg = default_config()
+    cfg.loadbalancer.rate_limiting.enabled = True
+    cfg.loadbalancer.rate_limiting.per_ip.requests_per_second = 0.001
+    cfg.loadbalancer.rate_limiting.per_ip.burst_size = 2
+    gw = _app(cfg)
+    try:
+        with TestClient(create_app(gw, trusted_proxies=("127.0.0.1",))) as c:
+            codes = [c.get("/api/v1/queues/stats", headers={"X-Forwarded-For": f"10.0.0.{i}"}).status_code
+                     for i in range(3)]
+            assert codes == [200, 200, 429]
+    finally:
+        gw.stop()
