@@ -666,9 +666,7 @@ class GatewayApp:
 
     def reset_latency(self) -> None:
         """Start a fresh latency window (operators / load tests)."""
-        self.gateway.flush_latency()
-        self.gateway.rec.reset()
-        self.gateway.rec_done.reset()
+        self.gateway.reset_latency()
 
     def _event_loop(self) -> None:
         """Ingress: apply status events from the dispatcher to the message store."""

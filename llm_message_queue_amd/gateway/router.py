@@ -98,11 +98,64 @@ class LatencyRecorder:
         return out
 
 
+# Where a request's arrival -> admission time goes (multi-rank attribution,
+# VERDICT r3 next #1): arrival -> taken from the inbox into a preprocess
+# batch; preprocess + queue push; queue wait until a dispatch decision pops
+# it; decision -> admitted into a backend slot (0 on the own GPU; the
+# descriptor's trip through the all_to_all for another rank's GPU).
+STAGES = ("inbox", "preprocess", "queue", "handoff")
+# how the request got its slot: realtime lane between collectives; own-GPU
+# admission between collectives (extra step / leftover headroom); the
+# tick's plan on the own GPU; the plan on another rank's GPU
+PATHS = ("lane", "own", "plan_local", "plan_remote")
+P_LANE, P_OWN, P_PLAN_LOCAL, P_PLAN_REMOTE = range(4)
+
+
+class StageRecorder:
+    """Per-stage, per-tier latency histograms (``STAGES``) and per-path,
+    per-tier admission counts (``PATHS``)."""
+
+    def __init__(self, ntiers: int = 4):
+        self.ntiers = ntiers
+        self.reset()
+
+    def reset(self):
+        self.h = np.zeros((len(STAGES), self.ntiers + 1, _HBINS), dtype=np.int64)
+        self.paths = np.zeros((len(PATHS), self.ntiers), dtype=np.int64)
+
+    def record(self, stage: int, tiers: np.ndarray, ns: np.ndarray) -> None:
+        if len(tiers) == 0:
+            return
+        b = _hbin(np.maximum(np.asarray(ns, dtype=np.int64), 0))
+        tiers = np.asarray(tiers, dtype=np.int64)
+        for t in range(self.ntiers):
+            m = tiers == t
+            if m.any():
+                np.add.at(self.h[stage, t], b[m], 1)
+        np.add.at(self.h[stage, self.ntiers], b, 1)
+
+    def count(self, path: int, tiers) -> None:
+        for t in tiers:
+            if 0 <= t < self.ntiers:
+                self.paths[path, t] += 1
+
+    @staticmethod
+    def summary(h: np.ndarray, paths: np.ndarray) -> dict:
+        """``h`` [stages, tiers+1, bins], ``paths`` [paths, tiers] -> JSON
+        (p50 / p99 ms per stage: one value per tier, then all tiers)."""
+        out = {}
+        for s, name in enumerate(STAGES):
+            out[name] = {q: [round(hist_percentile(h[s, t], p) / 1e6, 3) for t in range(h.shape[1])]
+                         for q, p in (("p50_ms", 0.5), ("p99_ms", 0.99))}
+        out["admitted_by_path"] = {name: [int(x) for x in paths[k]] for k, name in enumerate(PATHS)}
+        return out
+
+
 # --------------------------------------------------------------------------- descriptors
 K_DISPATCH, K_DONE, K_FAIL = 1, 2, 3     # K_FAIL: an evacuating backend hands a request back
 K_MIGRATE = 4       # [kind, conv lo/hi, dest]: to a conversation's home GPU -- send its KV to dest this tick
 DESC_HDR = 16       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
-#                    dialog history length, -]; flags = (home GPU + 1) | KV_MIGRATE
+#                    dialog history length, decision - enq (us)]; flags = (home GPU + 1) | KV_MIGRATE
 KV_MIGRATE = 1 << 8     # descriptor flag: hold the turn until its KV arrives from the home GPU
 
 
@@ -208,6 +261,7 @@ class Gateway:
         self.foreign: Dict[int, Tuple[int, int, int]] = {}  # my engine req id -> (origin, handle, tier)
         self._done_owed: Dict[int, List[Tuple[int, int, int, int]]] = {r: [] for r in range(self.world)}
         self.rec = LatencyRecorder(len(self.tiers))
+        self.rec_stage = StageRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
                          "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0, "realtime_local": 0,
@@ -316,6 +370,9 @@ class Gateway:
             else:
                 batch = self._inbox[:self.MAX_INGEST_BATCH]
                 del self._inbox[:self.MAX_INGEST_BATCH]
+        now = time.monotonic_ns()
+        for m in batch:
+            m.ingest_ns = now
         return batch
 
     def preprocessing(self) -> int:
@@ -401,8 +458,31 @@ class Gateway:
         while len(self.conv_hist) > self.max_dialogs:
             self.conv_hist.popitem(last=False)
 
-    def _record(self, tiers, arrival, enq, now):
+    def _popped(self, msgs: Sequence[Message], tier_idx) -> None:
+        """A dispatch decision took ``msgs`` out of their queues: stamp it and
+        record the stages before it (inbox, preprocess, queue wait)."""
+        if not len(msgs):
+            return
+        now = time.monotonic_ns()
+        n = len(msgs)
+        a = np.empty((4, n), dtype=np.int64)
+        for k, m in enumerate(msgs):
+            m.popped_ns = now
+            a[0, k] = m.arrival_ns or m.ingest_ns or m.enqueued_at
+            a[1, k] = m.ingest_ns or a[0, k]
+            a[2, k] = m.enqueued_at or a[1, k]
+        t = np.asarray(tier_idx, dtype=np.int64)[:n]
+        rs = self.rec_stage
+        rs.record(0, t, a[1] - a[0])
+        rs.record(1, t, a[2] - a[1])
+        rs.record(2, t, now - a[2])
+
+    def _record(self, tiers, arrival, enq, now, decided=None, path: int = -1):
         tiers = np.asarray(tiers, dtype=np.int64)
+        if decided is not None and len(tiers):
+            self.rec_stage.record(3, tiers, now - np.asarray(decided, dtype=np.int64))
+        if path >= 0:
+            self.rec_stage.count(path, tiers.tolist())
         self.rec.record(tiers, now - np.asarray(arrival, dtype=np.int64), now - np.asarray(enq, dtype=np.int64))
         if self.metrics is not None:
             for t, a in zip(tiers, np.asarray(enq)):
@@ -476,6 +556,8 @@ class Gateway:
         if free > 0:
             msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets(),
                                                     self.lifo_ns)
+            self._popped(msgs, tier_idx)
+        n_head = len(msgs)
         lane = self._lane_budget(len(msgs), int((np.asarray(tier_idx) == 0).sum()))
         if lane > 0:
             # realtime lane: tier-0 requests the step's prefill headroom could
@@ -485,8 +567,10 @@ class Gateway:
             b[0] = lane
             m2, t2, _ = self.qm.pop_tiers(self.tiers, lane, [0] * len(self.tiers), b, None)
             if m2:
+                self._popped(m2, t2)
                 msgs = list(msgs) + list(m2)
                 tier_idx = np.concatenate([np.asarray(tier_idx, dtype=np.int64), np.asarray(t2, dtype=np.int64)])
+        lane_ids = {id(m) for m in msgs[n_head:]}
         if not msgs:
             return 0
         if self.shed_expired:     # expired requests behind a live tier head
@@ -517,8 +601,12 @@ class Gateway:
         if self.lb is not None and admitted:
             for r in admitted:
                 self.lb.mark_admitted(r.meta.endpoint_id)
+        n_lane = sum(1 for r in admitted if id(r.meta) in lane_ids)
+        if n_lane:
+            self.rec_stage.count(P_LANE, [r.tier for r in admitted if id(r.meta) in lane_ids])
+        self.rec_stage.count(P_PLAN_LOCAL, [r.tier for r in admitted if id(r.meta) not in lane_ids])
         self._record([r.tier for r in admitted], [r.meta.arrival_ns for r in admitted],
-                     [r.meta.enqueued_at for r in admitted], now)
+                     [r.meta.enqueued_at for r in admitted], now, [r.meta.popped_ns for r in admitted])
         if len(admitted) < len(reqs):    # cannot happen (free slots were counted); requeue defensively
             for r in reqs[len(admitted):]:
                 self.qm.requeue_after_failure(r.meta.queue_name, r.meta)
@@ -735,6 +823,7 @@ class Gateway:
         per_tier = mine.sum(axis=0)
         msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, int(per_tier.sum()), [0] * len(self.tiers),
                                                 [int(x) for x in per_tier], self.lifo_ns)
+        self._popped(msgs, tier_idx)
         by_tier: Dict[int, List[Message]] = {t: [] for t in range(len(self.tiers))}
         for m, t in zip(msgs, tier_idx):
             self._pin(m, -1)                          # (counted under its queue's tier)
@@ -842,7 +931,7 @@ class Gateway:
         reqs.extend(fresh)
         admitted = self.engine.admit(reqs) if (self.engine is not None and reqs and self.healthy) else []
         now = time.monotonic_ns()
-        tiers, arr, enqs = [], [], []
+        tiers, arr, enqs, decs, remote_t = [], [], [], [], []
         for r in admitted:
             if isinstance(r.meta, Message):
                 m = r.meta
@@ -851,14 +940,18 @@ class Gateway:
                 self.local[m.handle] = m
                 self.inflight_by_tier[r.tier] += 1
                 tiers.append(r.tier); arr.append(m.arrival_ns); enqs.append(m.enqueued_at)
+                decs.append(m.popped_ns or now)
             else:
-                origin, handle, tier, arrival, enq = r.meta
+                origin, handle, tier, arrival, enq, dec = r.meta
                 self.foreign[r.req_id] = (origin, handle, tier)
-                tiers.append(tier); arr.append(arrival); enqs.append(enq)
+                tiers.append(tier); arr.append(arrival); enqs.append(enq); decs.append(dec)
+                remote_t.append(tier)
                 self.counters["remote_recv"] += 1
         for m in local_msgs:
             m.endpoint_id = f"gpu{me}"
-        self._record(tiers, arr, enqs, now)
+        self.rec_stage.count(P_PLAN_REMOTE, remote_t)
+        self.rec_stage.count(P_PLAN_LOCAL, [r.tier for r in admitted if isinstance(r.meta, Message)])
+        self._record(tiers, arr, enqs, now, decs)
         if len(admitted) < len(reqs):
             # the plan only grants what the engine reported it could take, so
             # this is a bug or a concurrent health change -- never a reason to
@@ -874,7 +967,7 @@ class Gateway:
                 if isinstance(r.meta, Message):
                     self._requeue(r.meta)
                 else:
-                    origin, handle, tier, _a, _e = r.meta
+                    origin, handle, tier = r.meta[:3]
                     self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
@@ -1014,6 +1107,9 @@ class Gateway:
         row[11] = (migrate_from + 1) | KV_MIGRATE if migrate_from >= 0 else 0
         hist = self.conv_hist.get(m.conversation_id) if m.conversation_id else None
         row[14] = 0 if hist is None else len(hist)
+        # decision time as microseconds after enqueue (the destination records
+        # the decision -> admission hand-off stage)
+        row[15] = min(0x7FFFFFFF, max(0, (m.popped_ns - m.enqueued_at) // 1000)) if m.popped_ns and m.enqueued_at else 0
         row[DESC_HDR:DESC_HDR + len(p)] = p.view(np.int32)
 
     def _foreign_request(self, row: np.ndarray, cap: int) -> Request:
@@ -1028,8 +1124,9 @@ class Gateway:
         # history, the descriptor carries its length (the replay's prefill
         # cost; generated tokens are placeholders there as well)
         hl = int(row[14])
+        dec = enq + int(row[15]) * 1000
         return Request(req_id=self._next_req, prompt=prompt, gen_tokens=gen, tier=tier,
-                       meta=(origin, handle, tier, arrival, enq), conv=ck,
+                       meta=(origin, handle, tier, arrival, enq, dec), conv=ck,
                        history=np.zeros(hl, dtype=np.int32) if hl > 0 else None)
 
     def _remote_fail(self, row: np.ndarray) -> None:
@@ -1075,7 +1172,7 @@ class Gateway:
             if isinstance(r.meta, Message):
                 self._requeue(r.meta)
             else:
-                origin, handle, tier, _a, _e = r.meta
+                origin, handle, tier = r.meta[:3]
                 self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
         if self.migrator is not None:
             # imports still landing on the side stream write into reserved
@@ -1227,15 +1324,16 @@ class Gateway:
         budgets = [0] * len(self.tiers)
         budgets[0] = room
         msgs, _t, _e = self.qm.pop_tiers(self.tiers, room, [0] * len(self.tiers), budgets, None)
-        n = self._admit_own(msgs, [0] * len(msgs))
+        n = self._admit_own(msgs, [0] * len(msgs), P_LANE)
         self.counters["realtime_local"] += n
         return n
 
-    def _admit_own(self, msgs: Sequence[Message], tiers: Sequence[int]) -> int:
+    def _admit_own(self, msgs: Sequence[Message], tiers: Sequence[int], path: int = P_OWN) -> int:
         """Admit popped queued requests into this rank's OWN GPU (no
         cross-rank decision: the next load vector reports the slots taken)."""
         if not msgs:
             return 0
+        self._popped(msgs, tiers)
         eng = self.engine
         reqs = []
         for m, t in zip(msgs, tiers):
@@ -1254,7 +1352,7 @@ class Gateway:
         for r in reqs[len(admitted):]:             # cannot happen (room was counted); requeue defensively
             self._requeue(r.meta)
         self._record([r.tier for r in admitted], [r.meta.arrival_ns for r in admitted],
-                     [r.meta.enqueued_at for r in admitted], now)
+                     [r.meta.enqueued_at for r in admitted], now, [r.meta.popped_ns for r in admitted], path)
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
 
@@ -1363,6 +1461,13 @@ class Gateway:
         self.counters["ticks"] += 1
         self.flush_latency()
         return n, res
+
+    def reset_latency(self) -> None:
+        """Fresh latency windows: arrival -> dispatch, stages, end to end."""
+        self.flush_latency()
+        self.rec.reset()
+        self.rec_stage.reset()
+        self.rec_done.reset()
 
     def flush_latency(self) -> None:
         """Move buffered completion timestamps into the e2e histogram."""
