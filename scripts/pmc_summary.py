@@ -5,6 +5,7 @@ import csv
 import sys
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
+by_grid = "--by-grid" in sys.argv
 match = None
 if "--match" in sys.argv:
     match = sys.argv[sys.argv.index("--match") + 1]
@@ -15,7 +16,8 @@ for p in args:
         k = r["Kernel_Name"]
         if match and match not in k:
             continue
-        agg[k[:90]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        key = k[:90] + (f"  grid={r.get('Grid_Size', r.get('Grid_Size_X', '?'))}" if by_grid else "")
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     print(k)
     for c, v in sorted(d.items()):
