@@ -102,14 +102,17 @@ def parse(argv=None):
                          "ranks); each rank's backend is a SimEngine (the engine's host side for real, the 8B "
                          "forward as a simulated device clock) at the serving config's slots / token budget -- "
                          "for studying multi-GPU dynamics (lock-step vs GPU speed spread) without the GPUs")
+    ap.add_argument("--pin-cpu", action="store_true",
+                    help="pin rank r to CPU core r (mod the core count) -- CPU-rehearsal hygiene: separates "
+                         "scheduler migrations / contention from design costs in --cpu-dry-run --sim-gpu runs")
     ap.add_argument("--no-extra-steps", action="store_true",
                     help="multi-rank A/B: never launch an extra local forward while the peers are still "
                          "behind at the per-tick exchange (pure lock-step)")
     ap.add_argument("--ingress", default="per-rank", choices=["per-rank", "rank0", "rank0-funnel"],
                     help="per-rank: every GPU process fronts its own Poisson stream (weak scaling, one ingress "
-                         "per GPU); rank0: rank 0 alone receives N x the per-GPU rate (the `cli serve` topology: "
-                         "one front door) and ships the RAW records round-robin through node-shared rings, so "
-                         "every rank decodes and GPU-preprocesses its share; rank0-funnel: the r2 form, rank 0 "
+                         "per GPU); rank0: one front door for the job (the `cli serve` topology): a feeder "
+                         "process writes N x the per-GPU rate as RAW records into ONE shared ring that every "
+                         "rank drains, decodes and GPU-preprocesses; rank0-funnel: the r2 form, rank 0 "
                          "preprocesses the whole job's traffic on GPU 0 and the planner spreads it (A/B)")
     ap.add_argument("--lb", default="least_connections",
                     choices=["round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first"],
@@ -207,68 +210,70 @@ def lockstep_report(gw, engine, comm, elapsed: float) -> dict:
             "slowest_over_mean_gpu_step": round(float(step_mean.max() / max(1e-9, step_mean.mean())), 4)}
 
 
-class FrontDoorRings:
-    """``--ingress rank0``: rank 0 is the job's one front door.  It ships each
-    arrival as the RAW record the native HTTP ingress writes (TAG_RAW:
-    arrival ns, id, JSON body -- `csrc/ingress/http_ingress.cpp`) into the
-    node-shared ring of a destination rank, round-robin; every rank decodes
-    the records it receives and GPU-preprocesses them on its own GPU, so GPU
-    0 does not carry the job's preprocessing.  The
-    bodies come from a pool drawn from the bench workload once, untimed, so
-    the front door's per-request cost is a record header, as in C++."""
+class FrontDoorFeed:
+    """``--ingress rank0``: the job's one front door.  A feeder process
+    (``gateway/door_feed.py``, started by rank 0 before anything touches
+    the GPU) writes every Poisson arrival, at its arrival time, as the RAW
+    record the native HTTP ingress writes (arrival ns, id, JSON body --
+    `csrc/ingress/http_ingress.cpp`) into ONE shared ring, and every rank
+    drains it, decodes and GPU-preprocesses what it pops -- the topology of
+    `cli serve` (its C++ front door feeds one MPMC ring all ranks drain).
+    Until round 4 rank 0's own Python shipped the records round-robin into
+    per-rank rings, so every rank-0 host stall delayed the whole job's
+    arrivals (realtime p99 110 ms in that mode)."""
 
-    POOL = 16384
+    RING_BYTES = 256 << 20
 
-    def __init__(self, world: int, rank: int, job: str, wl):
+    def __init__(self, world: int, rank: int, job: str, seed: int):
+        import subprocess
         from llm_message_queue_amd import _native
-        self.world, self.rank = world, rank
-        self.prefix = f"llmq-benchdoor-{job}-{os.environ.get('MASTER_PORT', '0')}"
+        self.rank = rank
+        self.name = f"llmq-benchdoor-{job}-{os.environ.get('MASTER_PORT', '0')}"
         self._R = _native.shmring().ShmRing
-        self.inbox = self._R(f"{self.prefix}-r{rank}", 64 << 20, "open")
-        while self.inbox.pop(4096, 0):            # records a crashed run of the same name left behind
-            pass                                  # (rank 0 ships only after the next barrier)
-        self.out = []
-        self.serial = 0
-        self.pool = []
+        self.ring = None
+        self.proc = None
         if rank == 0:
-            for m in wl.make(self.POOL):
-                body = {"content": m.content, "user_id": m.user_id}
-                if m.priority:
-                    body["priority"] = int(m.priority)
-                self.pool.append(json.dumps(body).encode())
+            self.ring = self._R(self.name, self.RING_BYTES, "create")
+            self.proc = subprocess.Popen(
+                [sys.executable, "-m", "llm_message_queue_amd.gateway.door_feed", "--ring", self.name,
+                 "--ring-bytes", str(self.RING_BYTES), "--seed", str(seed)],
+                cwd=os.path.dirname(os.path.abspath(__file__)), stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                text=True)
+            self._cmd(None)                      # the pool is built: "ok 0"
 
-    def attach_outboxes(self) -> None:
-        if self.rank == 0:
-            self.out = [self.inbox if r == 0 else self._R(f"{self.prefix}-r{r}", 64 << 20, "open")
-                        for r in range(self.world)]
+    def _cmd(self, line):
+        if self.proc is None:
+            return
+        if line is not None:
+            self.proc.stdin.write(line + "\n")
+            self.proc.stdin.flush()
+        ack = self.proc.stdout.readline()
+        if not ack.startswith("ok"):
+            raise RuntimeError(f"front-door feeder: {ack!r}")
 
-    def ship(self, due) -> None:
-        from llm_message_queue_amd.gateway.shm_bridge import TAG_RAW
-        per = [[] for _ in range(self.world)]
-        s, pool, P = self.serial, self.pool, self.POOL
-        for ts in due:
-            body = pool[s % P]
-            per[s % self.world].append(int(ts * 1e9).to_bytes(8, "little", signed=True)
-                                       + (b"door-%x" % s).ljust(36, b"\0")
-                                       + len(body).to_bytes(4, "little") + body)
-            s += 1
-        self.serial = s
-        for r, recs in enumerate(per):
-            if recs and self.out[r].push_many(recs, TAG_RAW) != len(recs):
-                raise RuntimeError(f"front-door ring of rank {r} full")
+    def attach(self) -> None:
+        if self.ring is None:
+            self.ring = self._R(self.name, 0, "attach")
+
+    def start(self, rate: float, t0: float) -> None:
+        self._cmd(f"rate {rate!r} {t0!r}")
+
+    def stop(self) -> None:
+        self._cmd("stop")
 
     def receive(self):
         from llm_message_queue_amd.gateway.shm_bridge import decode_raw
-        return [decode_raw(b) for _, b in self.inbox.pop(1 << 16, 0)]
+        return [decode_raw(b) for _, b in self.ring.pop(4096, 0)]
 
     def backlog(self) -> int:
-        return int(self.inbox.size())
+        return int(self.ring.size())
 
     def close(self) -> None:
-        self.inbox.unlink()
-        self.inbox.close()
-        for r in self.out[1:]:
-            r.close()
+        if self.proc is not None:
+            self._cmd("exit")
+            self.proc.wait(timeout=30)
+            self.ring.unlink()
+        self.ring.close()
 
 
 def _free_port() -> int:
@@ -304,6 +309,15 @@ def main(argv=None) -> int:
         print(f"bench: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} ranks; refusing to "
               "report a number for a different GPU count", file=sys.stderr, flush=True)
         return 3
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if a.pin_cpu and hasattr(os, "sched_setaffinity"):
+        cores = sorted(os.sched_getaffinity(0))
+        os.sched_setaffinity(0, {cores[int(os.environ.get("LOCAL_RANK", rank)) % len(cores)]})
+    # rank 0 starts the front-door feeder process before anything here
+    # touches the GPU (a child process, never an exec)
+    job = os.environ.get("TORCHELASTIC_RUN_ID", str(os.getpid() if world == 1 else "bench"))
+    door = FrontDoorFeed(world, rank, job, a.seed) if a.ingress == "rank0" and world > 1 else None
     import torch
 
     from llm_message_queue_amd.backend.engine import BackendEngine
@@ -316,8 +330,6 @@ def main(argv=None) -> int:
     from llm_message_queue_amd.preprocess.preprocessor import Preprocessor
     from llm_message_queue_amd.utils.config import default_config
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dry = a.cpu_dry_run
     if dry:
@@ -357,7 +369,6 @@ def main(argv=None) -> int:
     for lv, ms in zip(sorted(cfg.queue.levels, key=lambda lv: lv.priority), aging_ms):
         lv.max_concurrent = a.slots * world
         lv.max_wait_time = int(ms * 1e6)
-    job = os.environ.get("TORCHELASTIC_RUN_ID", str(os.getpid() if world == 1 else "bench"))
     page = SlotPage(f"bench{job}", rank)
     budget = a.token_budget
     for item in filter(None, a.token_budget_by_rank.split(",")):
@@ -444,10 +455,9 @@ def main(argv=None) -> int:
     capacity = float(np.mean(caps))
     # rank0 ingress: one front door takes the whole job's traffic
     front_door = a.ingress in ("rank0", "rank0-funnel")
-    door = FrontDoorRings(world, rank, job, wl) if a.ingress == "rank0" and world > 1 else None
     if door is not None:
-        comm.barrier()                   # every rank's ring exists before rank 0 attaches to it
-        door.attach_outboxes()
+        comm.barrier()                   # the ring exists (rank 0 made it) before the others attach
+        door.attach()
     # drain the calibration backlog (untimed)
     gw.drop_pending()
 
@@ -477,15 +487,13 @@ def main(argv=None) -> int:
     feed = {"arrivals": None}
 
     def pump():
-        arrivals = feed["arrivals"]
-        due = arrivals.due(time.monotonic())
         if door is not None:
-            if due:
-                door.ship(due)
             msgs = door.receive()
             if msgs:
                 gw.submit(msgs)
             return
+        arrivals = feed["arrivals"]
+        due = arrivals.due(time.monotonic())
         if due:
             msgs = wl.make(len(due))
             for m, ts in zip(msgs, due):
@@ -502,7 +510,8 @@ def main(argv=None) -> int:
         now = time.monotonic()
         if tick_s > 0 and now < clock["next_tick"]:
             time.sleep(clock["next_tick"] - now)
-        elif world == 1 and engine.inflight() == 0 and gw.pending() == 0 and arrivals.t_next > now:
+        elif world == 1 and engine.inflight() == 0 and gw.pending() == 0 and arrivals.t_next is not None \
+                and arrivals.t_next > now:
             time.sleep(min(arrivals.t_next - now, 0.05))
         clock["next_tick"] = max(clock["next_tick"] + tick_s, time.monotonic())
         pump()
@@ -522,7 +531,9 @@ def main(argv=None) -> int:
         untimed drain that accounts for every request.  The same number of
         collectives on every rank (each tick is one)."""
         rate = a.rate if a.rate > 0 else util * capacity
-        my_rate = (rate * world if rank == 0 else 0.0) if front_door else rate
+        # rank0: the feeder process offers world x rate into the shared ring;
+        # rank0-funnel: rank 0's own clock does
+        my_rate = 0.0 if door is not None else ((rate * world if rank == 0 else 0.0) if front_door else rate)
         arrivals = feed["arrivals"] = PoissonArrivals(my_rate, seed=a.seed * 1000 + rank + 7919 * attempt)
         gw.reset_latency()
         # ------------------------------------------------------------ steady state (untimed)
@@ -534,6 +545,8 @@ def main(argv=None) -> int:
         sync_all()
         mono0 = time.monotonic()
         arrivals.reset(mono0)
+        if door is not None:
+            door.start(rate * world, mono0)
         clock["next_tick"] = mono0
         for _ in range(steady):
             serve_tick()
@@ -584,6 +597,8 @@ def main(argv=None) -> int:
         # untimed: finish every request offered since the steady phase began
         # and account for all of them (served, rejected or shed -- none lost)
         arrivals.rate = 0.0
+        if door is not None:
+            door.stop()
         drain(pump)
         acct = comm.all_gather_i64(np.array([gw.counters[k] - c0[k] for k in ("submitted", "completed", "rejected",
                                                                               "expired")],

@@ -120,17 +120,40 @@ class ShmCollective {
   // throwing before the publish: every rank then fails the SAME op at once
   // (std::length_error) instead of the others spinning to their timeout.
   void exchange(const void* data, uint64_t n, double timeout_s) {
+    post(data, n, timeout_s);
+    complete(timeout_s);
+  }
+
+  // Split phase (the gateway keeps ingesting while its peers catch up):
+  // post() publishes this rank's payload of the next op and returns at once
+  // (it only waits for every rank to have published the PREVIOUS op, which a
+  // rank that completed that op already knows); ready() tells whether every
+  // rank has published it; complete() waits for that and checks overflow.
+  // payload() is valid after complete().  One op in flight per rank.
+  void post(const void* data, uint64_t n, double timeout_s) {
+    if (posted_) throw std::logic_error("ShmCollective: post() while an op is in flight");
     const bool over = n > buf_bytes_;
     const uint64_t k = seq_ + 1;
-    const auto deadline = clock::now() + std::chrono::duration_cast<clock::duration>(
-                                             std::chrono::duration<double>(timeout_s));
-    wait_all(k - 1, deadline);
+    wait_all(k - 1, deadline_after(timeout_s));
     const int par = (int)(k & 1);
     if (n && !over) std::memcpy(buf(rank_, par), data, n);
     slots_[rank_].nbytes[par] = over ? kOverflow : n;
     slots_[rank_].pub.store(k, std::memory_order_release);
     seq_ = k;
-    wait_all(k, deadline);
+    posted_ = true;
+  }
+
+  bool ready() const {
+    for (int r = 0; r < world_; ++r)
+      if (slots_[r].pub.load(std::memory_order_acquire) < seq_) return false;
+    return true;
+  }
+
+  void complete(double timeout_s) {
+    if (!posted_) throw std::logic_error("ShmCollective: complete() without post()");
+    posted_ = false;
+    wait_all(seq_, deadline_after(timeout_s));
+    const int par = (int)(seq_ & 1);
     for (int r = 0; r < world_; ++r)
       if (slots_[r].nbytes[par] == kOverflow)
         throw std::length_error("ShmCollective: rank " + std::to_string(r) +
@@ -171,6 +194,10 @@ class ShmCollective {
 
   uint8_t* buf(int r, int par) const { return bufs_ + ((uint64_t)r * 2 + par) * buf_bytes_; }
 
+  static clock::time_point deadline_after(double timeout_s) {
+    return clock::now() + std::chrono::duration_cast<clock::duration>(std::chrono::duration<double>(timeout_s));
+  }
+
   void wait_all(uint64_t k, clock::time_point deadline) const {
     if (k == 0) return;
     for (int r = 0; r < world_; ++r) {
@@ -193,6 +220,7 @@ class ShmCollective {
   std::string name_;
   int world_, rank_;
   uint64_t bytes_ = 0, buf_bytes_ = 0, seq_ = 0;
+  bool posted_ = false;
   uint8_t* base_ = nullptr;
   Header* hdr_ = nullptr;
   Slot* slots_ = nullptr;

@@ -9,6 +9,51 @@ namespace py = pybind11;
 using llmq::ShmCollective;
 using llmq::ShmRing;
 
+// the last op's payloads of every rank
+static py::list gathered(const ShmCollective& c) {
+  py::list out;
+  for (int r = 0; r < c.world(); ++r) {
+    uint64_t n = 0;
+    const uint8_t* p = c.payload(r, &n);
+    out.append(py::bytes(reinterpret_cast<const char*>(p), n));
+  }
+  return out;
+}
+
+// all_to_all payload: world x u64 part sizes, then the parts back to back
+static std::string a2a_pack(const ShmCollective& c, const std::vector<py::bytes>& parts) {
+  const int world = c.world();
+  if ((int)parts.size() != world) throw std::invalid_argument("all_to_all: one part per rank");
+  std::string buf(sizeof(uint64_t) * world, '\0');
+  for (int r = 0; r < world; ++r) {
+    std::string s = parts[r];
+    const uint64_t n = s.size();
+    std::memcpy(&buf[sizeof(uint64_t) * r], &n, sizeof(n));
+    buf += s;
+  }
+  return buf;
+}
+
+// after an all_to_all op: the part every rank addressed to this one
+static py::list a2a_mine(const ShmCollective& c) {
+  py::list out;
+  const int world = c.world(), me = c.rank();
+  for (int r = 0; r < world; ++r) {
+    uint64_t total = 0;
+    const uint8_t* p = c.payload(r, &total);
+    uint64_t off = sizeof(uint64_t) * world, n = 0;
+    for (int d = 0; d < world; ++d) {
+      uint64_t sz;
+      std::memcpy(&sz, p + sizeof(uint64_t) * d, sizeof(sz));
+      if (d == me) n = sz;
+      if (d < me) off += sz;
+    }
+    if (off + n > total) throw std::runtime_error("all_to_all: corrupt payload");
+    out.append(py::bytes(reinterpret_cast<const char*>(p + off), n));
+  }
+  return out;
+}
+
 PYBIND11_MODULE(_shmring, m) {
   m.doc() = "llm_message_queue_amd process-shared MPMC request ring (POSIX shm + robust mutex + futex)";
   py::class_<ShmRing>(m, "ShmRing")
@@ -69,50 +114,54 @@ PYBIND11_MODULE(_shmring, m) {
                py::gil_scoped_release nogil;
                c.exchange(s.data(), s.size(), timeout_s);
              }
-             py::list out;
-             const int world = c.world();
-             for (int r = 0; r < world; ++r) {
-               uint64_t n = 0;
-               const uint8_t* p = c.payload(r, &n);
-               out.append(py::bytes(reinterpret_cast<const char*>(p), n));
-             }
-             return out;
+             return gathered(c);
            },
            py::arg("data"), py::arg("timeout_s") = 60.0)
       .def("all_to_all",
            [](ShmCollective& c, const std::vector<py::bytes>& parts, double timeout_s) {
-             const int world = c.world();
-             if ((int)parts.size() != world) throw std::invalid_argument("all_to_all: one part per rank");
-             // payload: world x u64 part sizes, then the parts back to back
-             std::string buf(sizeof(uint64_t) * world, '\0');
-             for (int r = 0; r < world; ++r) {
-               std::string s = parts[r];
-               const uint64_t n = s.size();
-               std::memcpy(&buf[sizeof(uint64_t) * r], &n, sizeof(n));
-               buf += s;
-             }
+             std::string buf = a2a_pack(c, parts);
              {
                py::gil_scoped_release nogil;
                c.exchange(buf.data(), buf.size(), timeout_s);
              }
-             py::list out;
-             const int me = c.rank();
-             for (int r = 0; r < world; ++r) {
-               uint64_t total = 0;
-               const uint8_t* p = c.payload(r, &total);
-               uint64_t off = sizeof(uint64_t) * world, n = 0;
-               for (int d = 0; d < world; ++d) {
-                 uint64_t sz;
-                 std::memcpy(&sz, p + sizeof(uint64_t) * d, sizeof(sz));
-                 if (d == me) n = sz;
-                 if (d < me) off += sz;
-               }
-               if (off + n > total) throw std::runtime_error("all_to_all: corrupt payload");
-               out.append(py::bytes(reinterpret_cast<const char*>(p + off), n));
-             }
-             return out;
+             return a2a_mine(c);
            },
            py::arg("parts"), py::arg("timeout_s") = 60.0)
+      // split phase: post_* publishes and returns; ready() polls; finish_*
+      // waits (GIL released) and returns what all_gather / all_to_all would
+      .def("post_gather",
+           [](ShmCollective& c, py::bytes b, double timeout_s) {
+             std::string s = b;
+             py::gil_scoped_release nogil;
+             c.post(s.data(), s.size(), timeout_s);
+           },
+           py::arg("data"), py::arg("timeout_s") = 60.0)
+      .def("post_a2a",
+           [](ShmCollective& c, const std::vector<py::bytes>& parts, double timeout_s) {
+             std::string buf = a2a_pack(c, parts);
+             py::gil_scoped_release nogil;
+             c.post(buf.data(), buf.size(), timeout_s);
+           },
+           py::arg("parts"), py::arg("timeout_s") = 60.0)
+      .def("ready", &ShmCollective::ready)
+      .def("finish_gather",
+           [](ShmCollective& c, double timeout_s) {
+             {
+               py::gil_scoped_release nogil;
+               c.complete(timeout_s);
+             }
+             return gathered(c);
+           },
+           py::arg("timeout_s") = 60.0)
+      .def("finish_a2a",
+           [](ShmCollective& c, double timeout_s) {
+             {
+               py::gil_scoped_release nogil;
+               c.complete(timeout_s);
+             }
+             return a2a_mine(c);
+           },
+           py::arg("timeout_s") = 60.0)
       .def("attached", &ShmCollective::attached)
       .def("arrived_next", &ShmCollective::arrived_next)
       .def("unlink", &ShmCollective::unlink)

@@ -99,11 +99,13 @@ class LatencyRecorder:
 
 
 # Where a request's arrival -> admission time goes (multi-rank attribution,
-# VERDICT r3 next #1): arrival -> taken from the inbox into a preprocess
-# batch; preprocess + queue push; queue wait until a dispatch decision pops
-# it; decision -> admitted into a backend slot (0 on the own GPU; the
-# descriptor's trip through the all_to_all for another rank's GPU).
-STAGES = ("inbox", "preprocess", "queue", "handoff")
+# VERDICT r3 next #1): arrival -> handed to this rank's gateway (the front
+# door's hop: rank 0 -> a shared-memory ring -> the rank's pump); -> taken
+# from the inbox into a preprocess batch; preprocess + queue push; queue wait
+# until a dispatch decision pops it; decision -> admitted into a backend
+# slot (0 on the own GPU; the descriptor's trip through the all_to_all for
+# another rank's GPU).
+STAGES = ("ingress", "inbox", "preprocess", "queue", "handoff")
 # how the request got its slot: realtime lane between collectives; own-GPU
 # admission between collectives (extra step / leftover headroom); the
 # tick's plan on the own GPU; the plan on another rank's GPU
@@ -167,13 +169,15 @@ def conv_key(conversation_id: str) -> int:
     return int.from_bytes(hashlib.blake2b(conversation_id.encode(), digest_size=8).digest(), "little") >> 1
 
 
-def _split64(a: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-    a = a.astype(np.int64)
-    return (a & 0xFFFFFFFF).astype(np.uint32).view(np.int32), (a >> 32).astype(np.int32)
+def _put64(buf: np.ndarray, col: int, vals) -> None:
+    """Store int64 ``vals`` into int32 columns (col, col + 1) = (lo, hi) of
+    ``buf`` [n][width] (little-endian: an int64 viewed as two int32s)."""
+    buf[:, col:col + 2] = np.asarray(vals, dtype=np.int64).reshape(-1, 1).view(np.int32)
 
 
-def _join64(lo: np.ndarray, hi: np.ndarray) -> np.ndarray:
-    return (hi.astype(np.int64) << 32) | lo.view(np.uint32).astype(np.int64)
+def _get64(buf: np.ndarray, col: int) -> np.ndarray:
+    """int64 from int32 columns (col, col + 1) = (lo, hi) of ``buf`` [n][width]."""
+    return np.ascontiguousarray(buf[:, col:col + 2]).view(np.int64).reshape(-1)
 
 
 class Gateway:
@@ -311,11 +315,35 @@ class Gateway:
         # its control-plane collectives (load all_gather + descriptor
         # all_to_all) -- the wait for the slowest rank plus the exchange
         self.coll_wait_ns: "collections.deque[int]" = collections.deque(maxlen=1 << 16)
+        self._pump = None               # the current tick's arrival feed (collective overlap loops)
+        # Own-arrival reservation (multi-rank): each tick a router holds back,
+        # from the capacity it publishes, what its own arrivals are expected
+        # to need until the plan is applied -- the EWMA of its enqueues during
+        # a tick's collective waits (all tiers -> prefill headroom; tier 0 x 2
+        # -> lane slots).  It
+        # admits arrivals into that reserve while it waits at the collectives,
+        # so the plan, which only sees what was queued when the loads were
+        # published, never stalls fresh local arrivals for a whole tick.
+        self._enq_tick = [0, 0]         # enqueued during this tick's collective waits (all, tier 0)
+        self._enq_ewma = [0.0, 0.0]
+        self._in_wait = False
+        self._reserve = [0, 0]          # [headroom admits, lane slots] left this tick
+        # per-tier depth this rank published and not yet popped its grant of:
+        # own admissions in the wait must leave at least that much queued
+        self._pub_depth: Optional[List[int]] = None
+        self.own_reserve = True
+        # Holding back prefill HEADROOM as well (all tiers) was measured worse:
+        # a faster GPU's unused reserve is lost to the plan that tick, so a
+        # slower GPU's backlog (its low tier) waits for aging instead of
+        # moving (profiles/r4_sim8_own_admission.jsonl).  Lane slots (tier 0)
+        # are plentiful, so holding them back costs the plan nothing.
+        self.reserve_headroom = False
 
     # ------------------------------------------------------------------ ingress
     def submit(self, msgs: Sequence[Message]) -> None:
         now = time.monotonic_ns()
         for m in msgs:
+            m.recv_ns = now
             if not m.arrival_ns:
                 m.arrival_ns = now
         with self._inbox_lock:
@@ -398,7 +426,13 @@ class Gateway:
         self.ingest_ns[1] += time.perf_counter_ns() - t1
         self.ingest_ns[2] += len(batch)
         out = []
+        t0name = self.tiers[0] if self.tiers else None
+        wait = self._in_wait
         for m, e in zip(batch, errs):
+            if e is None and wait:                # enqueued while waiting at a collective
+                self._enq_tick[0] += 1
+                if m.queue_name == t0name:
+                    self._enq_tick[1] += 1
             if e is None and self.world > 1:
                 self._pin(m, +1)
             if e is not None:
@@ -468,19 +502,21 @@ class Gateway:
         a = np.empty((4, n), dtype=np.int64)
         for k, m in enumerate(msgs):
             m.popped_ns = now
-            a[0, k] = m.arrival_ns or m.ingest_ns or m.enqueued_at
-            a[1, k] = m.ingest_ns or a[0, k]
-            a[2, k] = m.enqueued_at or a[1, k]
+            a[0, k] = m.arrival_ns or m.recv_ns or m.ingest_ns or m.enqueued_at
+            a[1, k] = m.recv_ns or a[0, k]
+            a[2, k] = m.ingest_ns or a[1, k]
+            a[3, k] = m.enqueued_at or a[2, k]
         t = np.asarray(tier_idx, dtype=np.int64)[:n]
         rs = self.rec_stage
         rs.record(0, t, a[1] - a[0])
         rs.record(1, t, a[2] - a[1])
-        rs.record(2, t, now - a[2])
+        rs.record(2, t, a[3] - a[2])
+        rs.record(3, t, now - a[3])
 
     def _record(self, tiers, arrival, enq, now, decided=None, path: int = -1):
         tiers = np.asarray(tiers, dtype=np.int64)
         if decided is not None and len(tiers):
-            self.rec_stage.record(3, tiers, now - np.asarray(decided, dtype=np.int64))
+            self.rec_stage.record(4, tiers, now - np.asarray(decided, dtype=np.int64))
         if path >= 0:
             self.rec_stage.count(path, tiers.tolist())
         self.rec.record(tiers, now - np.asarray(arrival, dtype=np.int64), now - np.asarray(enq, dtype=np.int64))
@@ -752,6 +788,23 @@ class Gateway:
         held = self.awaiting_kv()
         free = max(0, eng.admit_capacity() - held) if up else 0
         slots_free = max(0, eng.lane_capacity() - held) if (up and self.realtime_lane) else free
+        if W > 1:
+            # EWMA (alpha 0.25) of own enqueues per tick -> this tick's reserve
+            a = 0.25
+            self._enq_ewma = [(1 - a) * e + a * n for e, n in zip(self._enq_ewma, self._enq_tick)]
+            self._enq_tick = [0, 0]
+            if self.own_reserve and up and self.rank not in self.excluded_peers:
+                # (round robin / weighted random keep their rotation: only the
+                # realtime lane is admitted locally, so only lane slots are held)
+                rh = 0 if (not self.reserve_headroom or self.plan_state.strategy in self.ROTATING_STRATEGIES) \
+                    else min(free, int(np.ceil(self._enq_ewma[0])))
+                rl = min(max(0, slots_free - free), int(np.ceil(2.0 * self._enq_ewma[1]))) \
+                    if self.realtime_lane else 0
+                self._reserve = [rh, rl]
+                free -= rh
+                slots_free -= rh + rl
+            else:
+                self._reserve = [0, 0]
         inflight = (eng.inflight() if eng is not None else 0) + held
         kv_tok = kv_cap = 0
         if eng is not None and hasattr(eng, "resident_kv_tokens"):
@@ -761,6 +814,7 @@ class Gateway:
             used, total = (wb + kv_tok * per) >> 20, (wb + kv_cap * per) >> 20
         else:
             used, total = self._hbm_mib() if eng is not None else (0, 0)
+        self._pub_depth = list(depth) if W > 1 else None
         return planner.make_load(
             free, inflight, depth, age, hbm_used_mib=used, hbm_total_mib=total, healthy=up, epoch=self.epoch,
             done_for=[len(self._done_owed[r]) for r in range(W)],
@@ -812,7 +866,9 @@ class Gateway:
         self._extra_local_step()
         my_load = self._my_load()
         tc0 = time.perf_counter_ns()
-        loads = self.comm.all_gather_i64(my_load)
+        pend = self.comm.all_gather_i64_async(my_load)
+        self._overlap(pend)
+        loads = pend.wait()
         t_wait = time.perf_counter_ns() - tc0
         orders_prev, self._mig_out = self._mig_out, []   # decided last tick: sent / executed now
         held_prev, self._await_kv = self._await_kv, {}   # turns flagged last tick
@@ -824,6 +880,7 @@ class Gateway:
         msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, int(per_tier.sum()), [0] * len(self.tiers),
                                                 [int(x) for x in per_tier], self.lifo_ns)
         self._popped(msgs, tier_idx)
+        self._pub_depth = None
         by_tier: Dict[int, List[Message]] = {t: [] for t in range(len(self.tiers))}
         for m, t in zip(msgs, tier_idx):
             self._pin(m, -1)                          # (counted under its queue's tier)
@@ -859,28 +916,33 @@ class Gateway:
         for j in range(W):
             rows = dest[j] if j != me else []
             buf = np.zeros((len(rows) + done_for[j], width), dtype=np.int32)
-            for k, m in enumerate(rows):
-                self._fill_desc(buf[k], m, me, cap, migrate.get(id(m), -1))
-                self.remote_out[m.handle] = m
-                self.inflight_by_tier[m.tier] += 1
-                m.endpoint_id = f"gpu{j}"
-                m.dispatched_at = now_ns
+            if rows:
+                self._fill_descs(buf[:len(rows)], rows, me, cap, migrate)
+                tname = f"gpu{j}"
+                for m in rows:
+                    self.remote_out[m.handle] = m
+                    self.inflight_by_tier[m.tier] += 1
+                    m.endpoint_id = tname
+                    m.dispatched_at = now_ns
             if rows and self.lb is not None:
                 self.lb.note_dispatch(f"gpu{j}", len(rows))
             mig_rows = [(c, d) for c, h, d in orders_prev if h == j] if j != me else []
             if mig_rows:
                 extra = np.zeros((len(mig_rows), width), dtype=np.int32)
-                for k, (c, d) in enumerate(mig_rows):
-                    extra[k, 0] = K_MIGRATE
-                    extra[k, 1], extra[k, 2] = _split64(np.array([c]))[0][0], _split64(np.array([c]))[1][0]
-                    extra[k, 3] = d
-            for k, rec in enumerate(self._done_owed[j]):
-                row = buf[len(rows) + k]
-                row[0] = rec[4]
-                row[1], row[2] = _split64(np.array([rec[0]]))[0][0], _split64(np.array([rec[0]]))[1][0]
-                row[3], row[4] = me, rec[1]
-                row[5], row[6] = _split64(np.array([rec[2]]))[0][0], _split64(np.array([rec[2]]))[1][0]
-                row[7], row[8] = _split64(np.array([rec[3]]))[0][0], _split64(np.array([rec[3]]))[1][0]
+                extra[:, 0] = K_MIGRATE
+                _put64(extra, 1, [c for c, _d in mig_rows])
+                extra[:, 3] = [d for _c, d in mig_rows]
+            recs = self._done_owed[j]
+            if recs:
+                # completion records: (handle, tier, admitted ns, done ns, kind)
+                a = np.asarray(recs, dtype=np.int64).reshape(-1, 5)
+                d = buf[len(rows):]
+                d[:, 0] = a[:, 4]
+                _put64(d, 1, a[:, 0])
+                d[:, 3] = me
+                d[:, 4] = a[:, 1]
+                _put64(d, 5, a[:, 2])
+                _put64(d, 7, a[:, 3])
             self._done_owed[j] = []
             send.append(np.concatenate([buf, extra]) if mig_rows else buf)
             if j != me:
@@ -889,7 +951,9 @@ class Gateway:
                        + int(loads[i, planner.L_MIGC + me]) if i != me else 0 for i in range(W)]
         send[me] = np.zeros((0, width), dtype=np.int32)
         tc0 = time.perf_counter_ns()
-        got = self.comm.all_to_all_rows(send, recv_counts, width)
+        pend = self.comm.all_to_all_rows_async(send, recv_counts, width)
+        self._overlap(pend)
+        got = pend.wait()
         self.coll_wait_ns.append(t_wait + time.perf_counter_ns() - tc0)
         # orders where I am the home GPU: K_MIGRATE rows from the routers, plus
         # my own router's orders for my own KV
@@ -904,21 +968,25 @@ class Gateway:
                 newly_held.append((r, -1))
         fresh: List[Request] = []
         for src in range(W):
-            for row in got[src]:
-                kind = row[0]
-                if kind == K_DISPATCH:
-                    r = self._foreign_request(row, cap)
-                    fl = int(row[11])
+            g = got[src]
+            if not len(g):
+                continue
+            kinds = g[:, 0]
+            disp = g[kinds == K_DISPATCH]
+            if len(disp):
+                for r, fl in zip(self._foreign_requests(disp, cap), disp[:, 11].tolist()):
                     if fl & KV_MIGRATE:
                         newly_held.append((r, (fl & 0xFF) - 1))
                     else:
                         fresh.append(r)
-                elif kind == K_DONE:
-                    self._remote_done(row)
-                elif kind == K_FAIL:
-                    self._remote_fail(row)
-                elif kind == K_MIGRATE:
-                    src_orders.append((int(_join64(row[1:2], row[2:3])[0]), me, int(row[3])))
+            done = g[kinds == K_DONE]
+            if len(done):
+                self._remote_done_rows(done)
+            for row in g[kinds == K_FAIL]:
+                self._remote_fail(row)
+            mig = g[kinds == K_MIGRATE]
+            if len(mig):
+                src_orders.extend((int(c), me, int(d)) for c, d in zip(_get64(mig, 1), mig[:, 3]))
         # execute last tick's orders (home side: send; dest side: receive),
         # then admit the turns that waited for them, ahead of new work
         ready = self._migrate(loads, src_orders, held_prev)
@@ -970,7 +1038,9 @@ class Gateway:
                     origin, handle, tier = r.meta[:3]
                     self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
         self.counters["dispatched"] += len(admitted)
-        return len(admitted)
+        # requests enqueued while this rank waited at the collectives: into
+        # the capacity the plan left on the own GPU now, not a tick later
+        return len(admitted) + self._dispatch_own()
 
     def _avoid_home(self, pool: List[Message], room: List[int], dest: Dict[int, List[Message]]) -> List[Message]:
         """Place each homed turn on a GPU other than its home (bench knob);
@@ -1092,46 +1162,81 @@ class Gateway:
             return -1
         return h
 
-    def _fill_desc(self, row: np.ndarray, m: Message, origin: int, cap: int, migrate_from: int = -1) -> None:
-        row[0] = K_DISPATCH
-        lo, hi = _split64(np.array([m.handle, m.arrival_ns, m.enqueued_at], dtype=np.int64))
-        row[1], row[2] = lo[0], hi[0]
-        row[3], row[4] = origin, m.tier
-        row[5], row[6] = lo[1], hi[1]
-        row[7], row[8] = lo[2], hi[2]
-        row[9] = self.gen_tokens
-        p = np.asarray(m.prompt_ids if m.prompt_ids is not None else [], dtype=np.uint32)[:cap]
-        row[10] = len(p)
-        ck = conv_key(m.conversation_id) if self.kv_residency else -1
-        row[12], row[13] = _split64(np.array([ck]))[0][0], _split64(np.array([ck]))[1][0]
-        row[11] = (migrate_from + 1) | KV_MIGRATE if migrate_from >= 0 else 0
-        hist = self.conv_hist.get(m.conversation_id) if m.conversation_id else None
-        row[14] = 0 if hist is None else len(hist)
-        # decision time as microseconds after enqueue (the destination records
-        # the decision -> admission hand-off stage)
-        row[15] = min(0x7FFFFFFF, max(0, (m.popped_ns - m.enqueued_at) // 1000)) if m.popped_ns and m.enqueued_at else 0
-        row[DESC_HDR:DESC_HDR + len(p)] = p.view(np.int32)
+    def _fill_descs(self, buf: np.ndarray, msgs: Sequence[Message], origin: int, cap: int,
+                    migrate: Dict[int, int]) -> None:
+        """K_DISPATCH descriptors of ``msgs`` into ``buf`` [n][width], the
+        scalar fields as whole columns (one numpy op per field)."""
+        n = len(msgs)
+        v = np.empty((n, 4), dtype=np.int64)      # handle, arrival, enq, conversation key
+        small = np.zeros((n, 6), dtype=np.int64)  # tier, plen, flags, hist len, decision - enq (us)
+        kv = self.kv_residency
+        hist_of = self.conv_hist
+        prompts = []
+        for k, m in enumerate(msgs):
+            cid = m.conversation_id
+            v[k, 0], v[k, 1], v[k, 2] = m.handle, m.arrival_ns, m.enqueued_at
+            v[k, 3] = conv_key(cid) if (kv and cid) else -1
+            p = m.prompt_ids
+            p = np.asarray(p if p is not None else (), dtype=np.uint32)[:cap]
+            prompts.append(p)
+            mf = migrate.get(id(m), -1)
+            hist = hist_of.get(cid) if cid else None
+            small[k, 0] = m.tier
+            small[k, 1] = len(p)
+            small[k, 2] = (mf + 1) | KV_MIGRATE if mf >= 0 else 0
+            small[k, 3] = 0 if hist is None else len(hist)
+            # decision time as microseconds after enqueue (the destination
+            # records the decision -> admission hand-off stage)
+            small[k, 4] = min(0x7FFFFFFF, max(0, (m.popped_ns - m.enqueued_at) // 1000)) \
+                if (m.popped_ns and m.enqueued_at) else 0
+        buf[:, 0] = K_DISPATCH
+        _put64(buf, 1, v[:, 0])
+        buf[:, 3] = origin
+        buf[:, 4] = small[:, 0]
+        _put64(buf, 5, v[:, 1])
+        _put64(buf, 7, v[:, 2])
+        buf[:, 9] = self.gen_tokens
+        buf[:, 10] = small[:, 1]
+        buf[:, 11] = small[:, 2]
+        _put64(buf, 12, v[:, 3])
+        buf[:, 14] = small[:, 3]
+        buf[:, 15] = small[:, 4]
+        for k, p in enumerate(prompts):
+            if len(p):
+                buf[k, DESC_HDR:DESC_HDR + len(p)] = p.view(np.int32)
 
-    def _foreign_request(self, row: np.ndarray, cap: int) -> Request:
-        handle = int(_join64(row[1:2], row[2:3])[0])
-        arrival = int(_join64(row[5:6], row[6:7])[0])
-        enq = int(_join64(row[7:8], row[8:9])[0])
-        origin, tier, gen, plen = int(row[3]), int(row[4]), int(row[9]), int(row[10])
-        prompt = row[DESC_HDR:DESC_HDR + max(1, plen)].copy()
-        ck = int(_join64(row[12:13], row[13:14])[0])
-        self._next_req += 1
-        # a non-resident turn replays its dialog: the origin router holds the
-        # history, the descriptor carries its length (the replay's prefill
-        # cost; generated tokens are placeholders there as well)
-        hl = int(row[14])
-        dec = enq + int(row[15]) * 1000
-        return Request(req_id=self._next_req, prompt=prompt, gen_tokens=gen, tier=tier,
-                       meta=(origin, handle, tier, arrival, enq, dec), conv=ck,
-                       history=np.zeros(hl, dtype=np.int32) if hl > 0 else None)
+    def _foreign_requests(self, rows: np.ndarray, cap: int) -> List[Request]:
+        """Requests for K_DISPATCH descriptor rows (another router's
+        messages placed on this GPU)."""
+        handle, arrival, enq, ck = _get64(rows, 1), _get64(rows, 5), _get64(rows, 7), _get64(rows, 12)
+        dec = enq + rows[:, 15].astype(np.int64) * 1000
+        out = []
+        for k, (h, a, e, c, d, origin, tier, gen, plen, hl) in enumerate(zip(
+                handle.tolist(), arrival.tolist(), enq.tolist(), ck.tolist(), dec.tolist(), rows[:, 3].tolist(),
+                rows[:, 4].tolist(), rows[:, 9].tolist(), rows[:, 10].tolist(), rows[:, 14].tolist())):
+            self._next_req += 1
+            # a non-resident turn replays its dialog: the origin router holds
+            # the history, the descriptor carries its length (the replay's
+            # prefill cost; generated tokens are placeholders there as well)
+            out.append(Request(req_id=self._next_req, prompt=rows[k, DESC_HDR:DESC_HDR + max(1, plen)].copy(),
+                               gen_tokens=gen, tier=tier, meta=(origin, h, tier, a, e, d), conv=c,
+                               history=np.zeros(hl, dtype=np.int32) if hl > 0 else None))
+        return out
+
+    def _remote_done_rows(self, rows: np.ndarray) -> None:
+        """K_DONE rows: my requests another GPU finished."""
+        for h, gpu, adm, done in zip(_get64(rows, 1).tolist(), rows[:, 3].tolist(), _get64(rows, 5).tolist(),
+                                     _get64(rows, 7).tolist()):
+            m = self.remote_out.pop(h, None)
+            if m is None:
+                continue
+            self.inflight_by_tier[m.tier] -= 1
+            self._remember_dialog(m, int(gpu))
+            self._complete(m, done - adm)     # (releases the balancer's gpu<j> endpoint with this RT)
 
     def _remote_fail(self, row: np.ndarray) -> None:
         """The backend my request was sent to evacuated it: queue it again."""
-        handle = int(_join64(row[1:2], row[2:3])[0])
+        handle = int(_get64(row.reshape(1, -1), 1)[0])
         m = self.remote_out.pop(handle, None)
         if m is None:
             return
@@ -1194,17 +1299,6 @@ class Gateway:
                 self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
         self.counters["evacuated"] += n
         return n
-
-    def _remote_done(self, row: np.ndarray) -> None:
-        handle = int(_join64(row[1:2], row[2:3])[0])
-        m = self.remote_out.pop(handle, None)
-        if m is None:
-            return
-        self.inflight_by_tier[m.tier] -= 1
-        adm = int(_join64(row[5:6], row[6:7])[0])
-        done = int(_join64(row[7:8], row[8:9])[0])
-        self._remember_dialog(m, int(row[3]))
-        self._complete(m, done - adm)     # (releases the balancer's gpu<j> endpoint with this RT)
 
     # ------------------------------------------------------------------ backend step
     def _complete(self, m: Message, process_ns: int) -> None:
@@ -1274,58 +1368,131 @@ class Gateway:
     WAIT_INGEST_NS = 8_000_000      # min spacing of ingest batches while the GPU is busy
     WAIT_INGEST_MSGS = 512          # ... unless this many arrived
 
-    def _while_waiting(self, pump) -> bool:
-        """Work done while the engine waits for the GPU; True if any.
+    def _while_waiting(self, pump, admit: bool = True) -> bool:
+        """Work done while the engine waits for the GPU (or, ``admit`` off,
+        while this rank waits for its peers at a collective); True if any.
         Arrivals are preprocessed in batches (every WAIT_INGEST_NS or
-        WAIT_INGEST_MSGS): each preprocess batch is a fixed chain of small
-        kernels, so tiny batches would cost GPU time the forward needs."""
+        WAIT_INGEST_MSGS): each GPU preprocess batch is a fixed chain of
+        small kernels, so tiny batches would cost GPU time the forward needs
+        (the CPU twin has no such fixed cost: it takes the inbox every time).
+        With ``admit`` the enqueued requests are admitted into this GPU's
+        free slots at once (one rank: the dispatcher; several: own-GPU
+        admission between collectives, ``_dispatch_own``)."""
         if pump is not None:
             pump()
         now = time.monotonic_ns()
         if self._pre_pending is not None and self.pre.batch_ready(self._pre_pending):
             # a finished preprocess batch is enqueued (and dispatched) at once
             self._finish_pending(block=True)
-            if self.world == 1:
-                self._dispatch_local()
-            else:
-                self._dispatch_realtime_local()
+            if admit:
+                self._admit_between()
             return True
-        if len(self._inbox) < self.WAIT_INGEST_MSGS and now - self._last_ingest_ns < self.WAIT_INGEST_NS:
+        if not self._inbox:
+            return False
+        if self.use_gpu_pre and len(self._inbox) < self.WAIT_INGEST_MSGS \
+                and now - self._last_ingest_ns < self.WAIT_INGEST_NS:
             return False
         self._last_ingest_ns = now
         did = self.ingest_async()
-        if self.world == 1:
-            did = self._dispatch_local() > 0 or did
-        else:
-            did = self._dispatch_realtime_local() > 0 or did
+        if admit:
+            did = self._admit_between() > 0 or did
         return did
 
-    def _dispatch_realtime_local(self) -> int:
-        """Multi-rank realtime lane: between the per-tick collectives a router
-        admits its realtime-tier requests straight into free slots of its OWN
-        GPU.  A local placement needs no cross-rank decision (the next load
-        vector reports the slots taken), so realtime dispatch is not paced by
-        the tick.  Skipped while realtime turns homed on another GPU are
-        queued here -- those follow their KV through the planner."""
+    def _admit_between(self) -> int:
+        if self.world == 1:
+            return self._dispatch_local()
+        return self._dispatch_own()
+
+    def _overlap(self, pend) -> None:
+        """A collective is in flight (this rank's contribution is published,
+        a peer has not reached it yet): keep pulling arrivals and
+        preprocessing + enqueueing them instead of idling, so the front end
+        never stalls for the slowest GPU.  Admission here uses only the
+        capacity this rank held back from its published load (``_reserve``):
+        the rest must stay as published until the plan is applied.""" 
+        if pend.ready():
+            return
+        pump = self._pump
+        self._in_wait = True
+        try:
+            self._overlap_loop(pend, pump)
+        finally:
+            self._in_wait = False
+
+    def _overlap_loop(self, pend, pump) -> None:
+        while not pend.ready():
+            did = self._while_waiting(pump, admit=False)
+            if did and (self._reserve[0] > 0 or self._reserve[1] > 0):
+                self._dispatch_own(reserved=True)
+            if not did:
+                time.sleep(0.0001)
+
+    def _dispatch_own(self, reserved: bool = False) -> int:
+        """Multi-rank, between the per-tick collectives: a router admits its
+        own queued requests straight into free capacity of its OWN GPU --
+        every tier into the next step's prefill headroom (strict priority +
+        aging, as the tick's plan would), then the realtime tier into any
+        free slot (the realtime lane).  A local placement needs no cross-rank
+        decision: the next load vector reports the slots taken, and the plan
+        spreads what this GPU cannot take.  So no request waits a whole tick
+        for the exchange while its own GPU has room (the
+        non-realtime tiers used to dispatch only at the collective, and the
+        realtime lane switched off whenever any realtime turn was homed
+        elsewhere).  A tier holding turns homed on another GPU is left to
+        the planner (they follow their KV); under round robin / weighted
+        random only the realtime lane runs (their rotation is the plan's).
+        ``reserved``: while this rank's published load is awaiting the plan,
+        admit only into the capacity it held back (``_reserve``)."""
         eng = self.engine
-        if not self.realtime_lane or eng is None or not self.healthy or not self.tiers:
+        if (eng is None or not self.healthy or self.stopping or not self.tiers
+                or self.rank in self.excluded_peers):
             return 0
-        if self.qm.size(self.tiers[0]) <= 0:
-            return 0
-        homed_elsewhere = int(self.pinned[:, 0].sum()) - int(self.pinned[self.rank, 0])
-        if homed_elsewhere > 0:
-            return 0
-        room = eng.lane_capacity() - self.awaiting_kv()
-        b = self._budgets()[0]
-        if b >= 0:
-            room = min(room, b)
-        if room <= 0:
-            return 0
-        budgets = [0] * len(self.tiers)
-        budgets[0] = room
-        msgs, _t, _e = self.qm.pop_tiers(self.tiers, room, [0] * len(self.tiers), budgets, None)
-        n = self._admit_own(msgs, [0] * len(msgs), P_LANE)
-        self.counters["realtime_local"] += n
+        held = self.awaiting_kv()
+        nt = len(self.tiers)
+        elsewhere = self.pinned.sum(axis=0) - self.pinned[self.rank]
+        # between publishing its load and popping its grant, a rank may only
+        # take what arrived since: the plan grants up to the published depth
+        spare = ([max(0, self.qm.size(n_) - d) for n_, d in zip(self.tiers, self._pub_depth)]
+                 if self._pub_depth is not None else None)
+        n = 0
+        head = eng.admit_capacity() - held
+        if reserved:
+            head = min(head, self._reserve[0])
+        if head > 0 and self.plan_state.strategy not in self.ROTATING_STRATEGIES:
+            b = self._budgets()
+            budgets = [0 if (t < planner.NTIERS and elsewhere[t] > 0) else (head if b[t] < 0 else min(head, b[t]))
+                       for t in range(nt)]
+            if spare is not None:
+                budgets = [min(x, y) for x, y in zip(budgets, spare)]
+            if any(budgets):
+                msgs, tier_idx, _e = self.qm.pop_tiers(self.tiers, head, self.aging_ns, budgets, self.lifo_ns)
+                tl = [int(t) for t in tier_idx]
+                if spare is not None:
+                    for t in tl:
+                        spare[t] -= 1
+                k = self._admit_own(msgs, tl, P_OWN)
+                n += k
+                self.counters["realtime_local"] += tl.count(0)
+                if reserved:
+                    self._reserve[0] -= k
+        if self.realtime_lane and elsewhere[0] == 0 and self.qm.size(self.tiers[0]) > 0:
+            room = eng.lane_capacity() - held
+            if reserved:
+                room = min(room, self._reserve[1])
+            b0 = self._budgets()[0]
+            if b0 >= 0:
+                room = min(room, b0)
+            if spare is not None:
+                room = min(room, spare[0])
+            if room > 0:
+                budgets = [0] * nt
+                budgets[0] = room
+                msgs, _t, _e = self.qm.pop_tiers(self.tiers, room, [0] * nt, budgets, None)
+                k = self._admit_own(msgs, [0] * len(msgs), P_LANE)
+                self.counters["realtime_local"] += k
+                if reserved:
+                    self._reserve[1] -= k
+                n += k
         return n
 
     def _admit_own(self, msgs: Sequence[Message], tiers: Sequence[int], path: int = P_OWN) -> int:
@@ -1429,6 +1596,7 @@ class Gateway:
             self.finish_backend()
 
     def _tick(self, pump=None):
+        self._pump = pump
         res = None
         pc = time.perf_counter_ns
         ht = self.host_ns

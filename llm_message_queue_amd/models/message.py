@@ -195,7 +195,7 @@ class Message:
         "queue_name", "retry_count", "max_retries", "timeout", "created_at",
         "updated_at", "scheduled_at", "completed_at", "metadata", "handle",
         "enqueued_at", "dispatched_at", "arrival_ns", "prompt_ids", "endpoint_id", "tier", "pin_key",
-        "ingest_ns", "popped_ns",
+        "ingest_ns", "popped_ns", "recv_ns",
     )
 
     def __init__(self, id: str = "", conversation_id: str = "", user_id: str = "",
@@ -230,6 +230,7 @@ class Message:
         self.pin_key = -1         # (home GPU, tier) the queued message is counted under (gateway pins)
         self.ingest_ns = 0        # ns, taken from the gateway inbox into a preprocess batch
         self.popped_ns = 0        # ns, popped from its queue by a dispatch decision
+        self.recv_ns = 0          # ns, handed to this process's gateway (Gateway.submit)
 
     # -- JSON ------------------------------------------------------------------
     def to_dict(self) -> Dict[str, Any]:

@@ -39,9 +39,38 @@ class PeerLost(RuntimeError):
 DEFAULT_TIMEOUT_S = 60.0
 
 
+class Pending:
+    """A collective in flight (split phase).  ``ready()`` is non-blocking:
+    True once every rank has contributed; ``wait()`` returns the result.
+    Comms without a split-phase transport complete the op inside ``wait()``
+    (``ready()`` is then always True, so a caller's overlap loop does
+    nothing and the op runs blocking, as before)."""
+
+    def __init__(self, finish, ready=None):
+        self._finish = finish
+        self._ready = ready
+
+    def ready(self) -> bool:
+        return True if self._ready is None else bool(self._ready())
+
+    def wait(self):
+        f, self._finish = self._finish, None
+        if f is None:
+            raise RuntimeError("Pending.wait() called twice")
+        return f()
+
+
 class Comm:
     rank: int = 0
     world: int = 1
+
+    def all_gather_i64_async(self, vec: np.ndarray) -> Pending:
+        """Split-phase ``all_gather_i64``: contribute now, collect later."""
+        return Pending(lambda: self.all_gather_i64(vec))
+
+    def all_to_all_rows_async(self, send: Sequence[np.ndarray], recv_counts: Sequence[int], width: int) -> Pending:
+        """Split-phase ``all_to_all_rows``."""
+        return Pending(lambda: self.all_to_all_rows(send, recv_counts, width))
 
     def all_gather_i64(self, vec: np.ndarray) -> np.ndarray:
         raise NotImplementedError
@@ -322,11 +351,34 @@ class ShmComm(Comm):
     def all_to_all_rows(self, send, recv_counts, width):
         parts = [np.ascontiguousarray(x, dtype=np.int32).reshape(-1, width).tobytes() for x in send]
         got = self._x(self.c.all_to_all, parts)
+        return self._rows(got, recv_counts, width)
+
+    def _rows(self, got, recv_counts, width):
         out = [np.frombuffer(g, dtype=np.int32).reshape(-1, width).copy() for g in got]
         for src, c in enumerate(recv_counts):
             if out[src].shape[0] != c:
                 raise RuntimeError(f"rank {self.rank}: expected {c} rows from {src}, got {out[src].shape[0]}")
         return out
+
+    def _finish(self, fn):
+        try:
+            return fn(self.timeout_s)
+        except TimeoutError as e:
+            raise PeerLost(f"rank {self.rank}: {e}") from e
+        except ValueError as e:
+            raise PeerLost(f"rank {self.rank}: control-plane payload overflow ({e})") from e
+
+    def all_gather_i64_async(self, vec):
+        v = np.ascontiguousarray(vec, dtype=np.int64).reshape(-1)
+        self._x(self.c.post_gather, v.tobytes())
+        return Pending(lambda: np.stack([np.frombuffer(p, dtype=np.int64)
+                                         for p in self._finish(self.c.finish_gather)]), self.c.ready)
+
+    def all_to_all_rows_async(self, send, recv_counts, width):
+        parts = [np.ascontiguousarray(x, dtype=np.int32).reshape(-1, width).tobytes() for x in send]
+        self._x(self.c.post_a2a, parts)
+        counts = list(recv_counts)
+        return Pending(lambda: self._rows(self._finish(self.c.finish_a2a), counts, width), self.c.ready)
 
     def all_to_all_var(self, send, width):
         parts = [np.ascontiguousarray(x, dtype=np.int32).reshape(-1, width).tobytes() for x in send]

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Multi-rank latency attribution on the CPU: the 8-rank
+# bench in simulated-GPU mode (SimEngine at the serving config, speeds
+# 1 / 0.97 / 1.03 cycled over ranks) at 2, 4 and 8 ranks, per-rank and rank-0
+# front-door ingress, with and without one core per rank.  One JSON line per
+# run (bench.py's line + the run's knobs) into $OUT.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=${OUT:-profiles/r4_sim_breakdown.jsonl}
+: > "$OUT"
+for W in ${WORLDS:-2 4 8}; do
+  for ING in per-rank rank0; do
+    for PIN in "" "--pin-cpu"; do
+      timeout -k 10 900 python bench.py --gpus "$W" --cpu-dry-run --sim-gpu 1,0.97,1.03 --steps 100 --warmup 10 \
+        --gateway-only-s 0 --ingress "$ING" $PIN --json-out /tmp/sim_breakdown.json > /tmp/sim_breakdown.log 2>&1 || exit $?
+      python - "$W" "$ING" "${PIN:-none}" "$OUT" <<'PY'
+import json, sys
+d = json.load(open("/tmp/sim_breakdown.json"))
+d["run"] = {"world": int(sys.argv[1]), "ingress": sys.argv[2], "pin": sys.argv[3]}
+open(sys.argv[4], "a").write(json.dumps(d) + "\n")
+lb = d["latency_breakdown"]
+print(sys.argv[1], sys.argv[2], sys.argv[3], d["value"], "rt", d["p99_by_tier_ms"][0], "all", d["p99_ms"],
+      "tiers", d["p99_by_tier_ms"], "queue p99", lb["queue"]["p99_ms"][-1], "ingress p99", lb["ingress"]["p99_ms"][-1])
+PY
+    done
+  done
+done

@@ -49,7 +49,7 @@ def test_bench_single_rank_dry_run():
     assert abs(w - min(d["dispatch_rate_in_window"], d["arrival_rate_in_window"])) < 0.02
     assert d["value"] == (w if d["p99_target_met"] else 0.0)
     lb = d["latency_breakdown"]
-    assert set(lb) >= {"inbox", "preprocess", "queue", "handoff", "admitted_by_path"}
+    assert set(lb) >= {"ingress", "inbox", "preprocess", "queue", "handoff", "admitted_by_path"}
     assert sum(sum(v) for v in lb["admitted_by_path"].values()) > 0
 
 
