@@ -131,6 +131,9 @@ class GatewayApp:
                                state_manager=self.state, use_gpu_preprocess=self.preprocessor.gpu_enabled(),
                                queue_manager=self.standard, dead_letter=self.factory.dead_letter_queue)
         self.gateway.on_complete = self._on_complete
+        # backend-failure retries wait out queue.retry's backoff in the
+        # delayed queue; exhausted ones go to the dead-letter queue
+        self.gateway.attach_retry_queue(self.factory.delayed_queue)
         if engine is not None:
             # per-GPU usage (in-flight slots, HBM) from every tick's load
             # exchange -> /api/v1/resources (multi-rank; one rank keeps its

@@ -269,7 +269,7 @@ class Gateway:
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
                          "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0, "realtime_local": 0,
-                         "extra_steps": 0, "extra_admitted": 0}
+                         "extra_steps": 0, "extra_admitted": 0, "retried": 0, "retry_exhausted": 0}
         # overload shedding (expire_queued) -> dead-letter queue
         self.shed_expired = bool(getattr(q, "shed_expired", True))
         # realtime lane (tier 0 admitted past the step's prefill headroom and
@@ -278,6 +278,17 @@ class Gateway:
         self.extra_steps = bool(getattr(cfg.gpu, "extra_steps", True))
         self.dead_letter = dead_letter
         self.on_expire = None       # optional callback(msg)
+        # Retry policy for requests a backend failure handed back (evacuation,
+        # K_FAIL): with a DelayedQueue attached (``attach_retry_queue``) they
+        # wait out an exponential backoff (queue.retry) before re-entering
+        # their tier, and go to the dead-letter queue once retries are
+        # exhausted -- the reference's intended retry path (`worker.go:202-239`,
+        # SURVEY D15), here on the GPU gateway.  Without one they re-enter
+        # their tier at once (the round-3 behaviour).
+        self.retry_queue = None
+        self.retry_backoff = None
+        self._retry_due: List[Message] = []
+        self._retry_lock = threading.Lock()
         # failure detection: a backend error (HIP error / OOM), the telemetry
         # poller (ECC, amd-smi gone) or an operator marks this GPU unhealthy;
         # it then takes no new work, its in-flight requests are re-routed and
@@ -846,6 +857,11 @@ class Gateway:
         if rs is None or now < self._res_next_ns:
             return
         self._res_next_ns = now + 100_000_000
+        # job-wide backlog: queued requests beyond the free slots of the GPUs
+        # in placement -- the autoscaler's "pending demand"
+        el = planner.eligible(loads)
+        queued = int(loads[:, planner.L_DEPTH:planner.L_DEPTH + planner.NTIERS].sum())
+        rs.note_backlog(queued - int(loads[el, planner.L_SLOTS].sum()))
         from ..scheduler.resource_scheduler import ResourceType
         for j in range(W):
             rid = f"gpu{j}"
@@ -1241,8 +1257,66 @@ class Gateway:
         if m is None:
             return
         self.inflight_by_tier[m.tier] -= 1
-        self._requeue(m)
+        self._retry(m, "backend evacuated the request")
         self.counters["handed_back"] += 1
+
+    def attach_retry_queue(self, delayed, backoff=None) -> None:
+        """Route backend-failure retries through ``delayed`` (a
+        ``queue.delayed.DelayedQueue``) with ``backoff`` (default: the
+        config's exponential ``queue.retry``)."""
+        from ..queue.worker import ExponentialBackoff
+        r = self.cfg.queue.retry
+        self.retry_queue = delayed
+        self.retry_backoff = backoff or ExponentialBackoff(r.initial_backoff, r.max_backoff, r.factor,
+                                                           r.max_retries)
+
+    def _retry(self, m: Message, reason: str) -> None:
+        """A request a backend failure handed back: retry after a backoff, or
+        dead-letter it once its retries are spent."""
+        if self.retry_queue is None:
+            self._requeue(m)
+            return
+        m.retry_count += 1
+        if m.retry_count > self.retry_backoff.max_retries():
+            m.status = MessageStatus.FAILED
+            m.endpoint_id = ""
+            self.counters["retry_exhausted"] += 1
+            self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
+            if self.dead_letter is not None:
+                try:
+                    self.dead_letter.push(m, f"retries exhausted: {reason}", m.queue_name)
+                except QueueError:
+                    self.log.warning("dead-letter queue full; failed request dropped", message_id=m.id)
+            return
+        m.status = MessageStatus.PENDING
+        m.endpoint_id = ""
+        m.dispatched_at = 0
+        self.counters["retried"] += 1
+        self.retry_queue.schedule_after(m, self.retry_backoff.next_backoff(m.retry_count), target=self._retry_ready)
+
+    def retrying(self) -> int:
+        """Requests waiting out a retry backoff (or handed back, not yet requeued)."""
+        q = self.retry_queue
+        return (q.size() if q is not None else 0) + len(self._retry_due)
+
+    def _retry_ready(self, m: Message) -> None:
+        """DelayedQueue delivery (its own thread): hand back to the tick."""
+        with self._retry_lock:
+            self._retry_due.append(m)
+
+    def _drain_retries(self) -> None:
+        q = self.retry_queue
+        if q is None:
+            return
+        if getattr(q, "_thread", None) is None:            # no drain thread: deliver here
+            for m in q.poll_ready(1024, 0.0):
+                self._retry_due.append(m)
+        if not self._retry_due:
+            return
+        with self._retry_lock:
+            due, self._retry_due = self._retry_due, []
+        for m in due:
+            self._requeue(m)
 
     def _requeue(self, m: Message) -> None:
         m.status = MessageStatus.PENDING
@@ -1275,7 +1349,7 @@ class Gateway:
         for r in held:                                  # turns waiting for a KV that will not be used here
             n += 1
             if isinstance(r.meta, Message):
-                self._requeue(r.meta)
+                self._retry(r.meta, reason)
             else:
                 origin, handle, tier = r.meta[:3]
                 self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
@@ -1293,7 +1367,7 @@ class Gateway:
                     self.inflight_by_tier[r.tier] -= 1
                 if m.metadata and m.metadata.get("home_gpu") == self.rank:
                     del m.metadata["home_gpu"]
-                self._requeue(m)
+                self._retry(m, reason)
             else:
                 origin, handle, tier = self.foreign.pop(r.req_id)
                 self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
@@ -1597,6 +1671,7 @@ class Gateway:
 
     def _tick(self, pump=None):
         self._pump = pump
+        self._drain_retries()
         res = None
         pc = time.perf_counter_ns
         ht = self.host_ns

@@ -150,6 +150,12 @@ class ResourceScheduler:
         # resources taken out of service by a scale-down (GPU endpoints parked
         # in the balancer): not counted as active capacity, first to return
         self.parked: List[str] = []
+        # demand waiting outside this scheduler's own pending queue: a gateway
+        # reports its queued requests that no active GPU has a free slot for
+        # (``note_backlog``).  They are pending resource requests in all but
+        # name, so they count where the reference counts its pending queue
+        # (`resource_scheduler.go:525-571`: scale up while it is non-empty).
+        self.external_pending = 0
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
         if start:
@@ -363,6 +369,9 @@ class ResourceScheduler:
             if r is not None:
                 r.metadata.pop("parked", None)
 
+    def note_backlog(self, n: int) -> None:
+        self.external_pending = max(0, int(n))
+
     def check_auto_scaling(self) -> Optional[str]:
         if not self.cfg.enable_auto_scaling:
             return None
@@ -372,7 +381,7 @@ class ResourceScheduler:
             active = sum(1 for r in self.resources.values()
                          if r.status not in (ResourceStatus.OFFLINE, ResourceStatus.ERROR)
                          and r.id not in self.parked)
-            pend = len(self.pending)
+            pend = len(self.pending) + self.external_pending
         avg = self.average_load()
         action = None
         if (avg > self.cfg.scale_up_threshold or pend > 0) and active < self.cfg.max_resources:
