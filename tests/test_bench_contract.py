@@ -161,3 +161,23 @@ def test_bench_slo_search_backs_off_to_a_met_operating_point():
     assert d["value"] == s["attempts"][-1]["value"] > 0
     assert abs(d["offered_rate_per_gpu"] - 0.92 * d["calibrated_capacity_per_gpu"]) < 1.0
     assert d["requests_accounted"]["lost"] == 0
+
+
+def test_overload_bench_multirank_sheds_low_tiers_parks_and_unparks():
+    """BASELINE config 5 across ranks: at 1.5x the
+    job's capacity realtime and high are served in full and the rest is shed
+    to the dead-letter queue at its deadline, nothing lost; a drop to 0.1x
+    parks a GPU through rank 0's resource scheduler and the return of the
+    overload (queued demand no active GPU has room for) unparks it."""
+    d = _run([sys.executable, "bench/overload_bench.py", "--gpus", "2", "--cpu-dry-run", "--sim-gpu", "1",
+              "--seconds", "3", "--policies", "fifo", "--autoscale", "1.5:2,0.1:3,1.5:3",
+              "--scale-cooldown-s", "0.5"], timeout=420)
+    r = d["policies"]["fifo"]
+    assert r["expired_to_dlq_by_tier"][0] == 0 and r["expired_to_dlq_by_tier"][1] == 0
+    assert r["served_by_tier"][0] > 0 and r["served_by_tier"][1] > 0
+    assert r["expired"] > 0 and r["dlq_added"] == r["expired"]
+    assert r["requests_accounted"]["lost"] == 0
+    steps = d["autoscale"]["steps"]
+    assert any(e["action"] == "scale_down" for e in steps[1]["scale_events"]) and steps[1]["parked_at_end"]
+    assert any(e["action"] == "scale_up" for e in steps[2]["scale_events"]) and steps[2]["parked_at_end"] == []
+    assert d["autoscale"]["requests_accounted"]["lost"] == 0
