@@ -181,3 +181,20 @@ def test_overload_bench_multirank_sheds_low_tiers_parks_and_unparks():
     assert any(e["action"] == "scale_down" for e in steps[1]["scale_events"]) and steps[1]["parked_at_end"]
     assert any(e["action"] == "scale_up" for e in steps[2]["scale_events"]) and steps[2]["parked_at_end"] == []
     assert d["autoscale"]["requests_accounted"]["lost"] == 0
+
+
+def test_dialog_bench_multirank_reports_per_rank_kv_counts():
+    """BASELINE config 4 across ranks: conversations
+    entering at rank 0 are homed over the job's GPUs; with KV residency every
+    turn after the first prefills only its new tokens, replay re-prefills the
+    dialog; per-rank counts are reported and every turn completes."""
+    d = _run([sys.executable, "bench/dialog_bench.py", "--gpus", "2", "--cpu-dry-run", "--sim-gpu", "1",
+              "--convs", "64", "--turns", "3", "--ingress", "rank0"], timeout=420)
+    res, rep = d["modes"]["residency"], d["modes"]["replay"]
+    for m in (res, rep):
+        assert m["turns_completed"] == m["turns_offered"] == 2 * 64 * 3
+        assert len(m["by_rank"]["kv_migrated"]) == 2 and len(m["by_rank"]["turns_completed"]) == 2
+    assert res["kv_reused_tokens"] > 0 and rep["kv_reused_tokens"] == 0
+    assert res["forward_tokens_per_turn"] < rep["forward_tokens_per_turn"]
+    assert res["remote_sent"] > 0                     # rank 0's turns run on both GPUs
+    assert rep["kv_migrated"] == 0 and rep["kv_migrate_replays"] == 0
