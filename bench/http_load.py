@@ -121,6 +121,9 @@ def main() -> None:
                     help="multirank: torch.distributed.run --nproc-per-node RANKS cli serve (C++ front door on "
                          "rank 0, every rank drains the shared ring; --gpu: ranks wrap onto the visible GPUs)")
     ap.add_argument("--ranks", type=int, default=2, help="multirank: serving ranks")
+    ap.add_argument("--sim-gpu", default="",
+                    help="multirank on CPU: per-rank relative GPU speeds (each rank a SimEngine at the serving "
+                         "config) -- the front door at the 8-GPU request rate without GPUs")
     ap.add_argument("--server-log", default="", help="file for the spawned server's stdout+stderr")
     ap.add_argument("--slots", type=int, default=1536, help="--bench-config: batch slots per rank")
     ap.add_argument("--threads", type=int, default=4, help="native ingress threads")
@@ -200,7 +203,8 @@ def main() -> None:
                                            f"--nproc-per-node={a.ranks}", "--master-addr=127.0.0.1",
                                            f"--master-port={_port()}", "-m", "llm_message_queue_amd.cli", "serve",
                                            "--port", str(port), "--host", "127.0.0.1", "--ingress-threads",
-                                           str(a.threads)] + ([] if a.gpu else ["--cpu-ranks"]) + cfg_args,
+                                           str(a.threads)] + ([] if a.gpu else ["--cpu-ranks"])
+                                          + (["--sim-gpu", a.sim_gpu] if a.sim_gpu and not a.gpu else []) + cfg_args,
                                           cwd=ROOT, env=env, stdout=slog, stderr=subprocess.STDOUT,
                                           start_new_session=True))
             urls = [f"http://127.0.0.1:{port}"]
@@ -280,6 +284,8 @@ def main() -> None:
                     st, st_end = st["job"], st_end["job"]
                     out["ranks"] = st.get("ranks")
                     out["accepted_by_rank"] = st.get("accepted_by_rank")
+                    out["front_door"] = st.get("front_door")
+                    out["missing_ranks"] = st.get("missing_ranks")
                 out["dispatcher"] = {"dispatch": st.get("dispatch"), "latency": st_end.get("latency"),
                                      "latency_e2e": st_end.get("latency_e2e"),
                                      "note": "latency: HTTP arrival (native ingress clock) -> GPU slot admission; "

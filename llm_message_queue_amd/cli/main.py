@@ -50,14 +50,24 @@ def _build_engine(cfg, model: str, device):
                          token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank), page
 
 
-def _build_cpu_engine(cfg):
+def _build_cpu_engine(cfg, sim_gpu: str = ""):
     """``--cpu-ranks``: a tiny Llama-shaped engine on the CPU reference ops
-    (the multi-rank control flow without a GPU; never a measurement)."""
+    (the multi-rank control flow without a GPU; never a measurement).  With
+    ``--sim-gpu SPEEDS`` each rank runs a SimEngine instead: the engine's
+    host side at the serving config, the 8B step as a simulated device
+    clock at the rank's relative speed (front-door rehearsals at the
+    8-GPU request rate on a CPU box)."""
     from ..backend.engine import BackendEngine
     from ..backend.slot_page import SlotPage
     from ..models.llama_stub import LlamaConfig
     rank = int(os.environ.get("RANK", "0"))
     page = SlotPage(f"serve{os.environ.get('TORCHELASTIC_RUN_ID', os.getpid())}", rank)
+    if sim_gpu:
+        from ..backend.sim_engine import SimEngine
+        speeds = [float(x) for x in sim_gpu.split(",")]
+        return SimEngine(speed=speeds[rank % len(speeds)], slots=cfg.gpu.slots_per_gpu, max_ctx=cfg.backend.max_ctx,
+                         token_budget=cfg.backend.token_budget, page=page, gpu_index=rank,
+                         seed=1000 + rank), page
     return BackendEngine(LlamaConfig.tiny(), slots=min(cfg.gpu.slots_per_gpu, 16), max_ctx=64, token_budget=128,
                          device="cpu", impl="ref", seed=1000 + rank, page=page, gpu_index=rank), page
 
@@ -138,7 +148,7 @@ def cmd_serve(a, role: str = "serve") -> int:
         engine, page = _build_engine(cfg, a.model, torch.device("cuda", local))
         engine.warm_shapes()      # cold-start GEMM shapes before the first request (idle -> busy)
     elif cpu_ranks and role in ("serve", "queue-manager"):
-        engine, page = _build_cpu_engine(cfg)
+        engine, page = _build_cpu_engine(cfg, getattr(a, "sim_gpu", ""))
     ring, app_role = None, "serve"
     # the C++ front door fronts every `serve` with a backend -- one GPU or a
     # whole node (the Python ASGI stack tops out at ~2k req/s for POST
@@ -220,6 +230,7 @@ def cmd_serve(a, role: str = "serve") -> int:
                                     or cfg.server.ingress_threads, cfg.server.host, cfg=cfg,
                                     conv_ring=f"{ring.name}-conv", upstream=(api_host, api_port))
             port = ingress.start()
+            gapp.front_door = ingress
         print(json.dumps({"event": "listening", "host": cfg.server.host, "port": port,
                           "gpu": use_gpu, "role": role, "world": world,
                           "front_door": "native" if front else "python", "api_port": api_port}), flush=True)
@@ -358,6 +369,9 @@ def main(argv=None) -> int:
         p.add_argument("--front-door", default="", choices=["", "native", "python"],
                        help="multi-GPU serve: C++ front door feeding a ring every rank drains (native, "
                             "default) or every route on rank 0's ASGI server (python)")
+        p.add_argument("--sim-gpu", default="",
+                       help="with --cpu-ranks: per-rank relative GPU speeds; each rank's backend is a SimEngine "
+                            "at the serving config (rehearsal, not a measurement)")
         p.add_argument("--cpu-ranks", action="store_true",
                        help="serve / queue-manager: tiny CPU engines per rank over gloo (multi-rank rehearsal "
                             "without a GPU)")

@@ -94,6 +94,7 @@ class GatewayApp:
         self.ring = ring
         self.extra_rings: List[object] = []       # role "rank": e.g. rank 0's conversation ring
         self.peers = None                          # gateway.peers.PeerDirectory (multi-rank front door)
+        self.front_door = None                     # gateway.native_ingress.NativeIngress (rank 0 of cli serve)
         self._ring_thread: Optional[threading.Thread] = None
         self._snap_thread: Optional[threading.Thread] = None
         self.telemetry = None
@@ -622,6 +623,8 @@ class GatewayApp:
         return {"ranks": sorted(int(p["rank"]) for p in parts), "dispatch": cnt,
                 # ranks whose answer did not arrive (timed out / dropped): the totals leave them out
                 "missing_ranks": list(self.peers.last_missing) if self.peers is not None else [],
+                # the C++ front door's counters: accepted, ring-full 503s, proxied routes, proxy errors
+                "front_door": self.front_door.stats() if self.front_door is not None else None,
                 "accepted_by_rank": {int(p["rank"]): int(p["accepted"]) for p in parts},
                 "pending_by_tier": {n: sum(int(p.get("pending", [0] * len(tiers))[t]) for p in parts)
                                     for t, n in enumerate(tiers)},
