@@ -137,8 +137,12 @@ def main() -> int:
     gw.flush_latency()
     st = np.array([engine.total_tokens - tok0, engine.kv_reused_tokens, engine.kv_imported,
                    gw.counters["kv_migrated"], gw.counters["kv_migrate_replays"], gw.counters["remote_sent"],
-                   int(gw.migrator.bytes_sent) if gw.migrator is not None else 0], dtype=np.int64)
-    agg = comm.all_gather_i64(st).sum(axis=0)
+                   int(gw.migrator.bytes_sent) if gw.migrator is not None else 0,
+                   int(gw.migrator.host_ns) if gw.migrator is not None else 0,
+                   int(gw.migrator.ticks) if gw.migrator is not None else 0,
+                   int(gw.migrator.host_max_ns) if gw.migrator is not None else 0], dtype=np.int64)
+    rows = comm.all_gather_i64(st)
+    agg = rows.sum(axis=0)
     lat = gw.rec_done.summary()
     if rank == 0:
         print(json.dumps({
@@ -149,6 +153,11 @@ def main() -> int:
             "forward_tokens": int(agg[0]), "forward_tokens_per_turn": round(int(agg[0]) / max(1, finished[0]), 1),
             "kv_reused_tokens": int(agg[1]), "kv_imported": int(agg[2]), "kv_migrated": int(agg[3]),
             "migrate_replays": int(agg[4]), "remote_dispatched": int(agg[5]), "kv_bytes_moved": int(agg[6]),
+            # host time inside KVMigrator.execute per migration tick (header
+            # exchange + pack / enqueue or, on gloo, the staged copies), by rank
+            "migrator_host_ms_per_tick_by_rank": [round(float(r[7]) / max(1, int(r[8])) / 1e6, 3) for r in rows],
+            "migrator_host_ms_max_by_rank": [round(float(r[9]) / 1e6, 3) for r in rows],
+            "migration_ticks_by_rank": [int(r[8]) for r in rows],
             "data_plane": "gloo (host staging; ranks share one GPU)" if not a.cpu else "gloo (CPU rehearsal)"}),
             flush=True)
     import torch.distributed as dist
