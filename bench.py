@@ -119,6 +119,9 @@ def parse(argv=None):
                          "process writes N x the per-GPU rate as RAW records into ONE shared ring that every "
                          "rank drains, decodes and GPU-preprocesses; rank0-funnel: the r2 form, rank 0 "
                          "preprocesses the whole job's traffic on GPU 0 and the planner spreads it (A/B)")
+    ap.add_argument("--door-share", default="greedy", choices=["greedy", "fair"],
+                    help="--ingress rank0: each pump takes everything the shared ring holds (greedy) or a "
+                         "1/world fair part of it (fair, what `cli serve`'s dedicated ring threads do)")
     ap.add_argument("--lb", default="least_connections",
                     choices=["round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first"],
                     help="multi-GPU placement strategy (loadbalancer.algorithm)")
@@ -144,10 +147,11 @@ class FrontDoorFeed:
 
     RING_BYTES = 256 << 20
 
-    def __init__(self, world: int, rank: int, job: str, seed: int):
+    def __init__(self, world: int, rank: int, job: str, seed: int, share: int = 1):
         import subprocess
         from llm_message_queue_amd import _native
         self.rank = rank
+        self.share = share
         self.name = f"llmq-benchdoor-{job}-{os.environ.get('MASTER_PORT', '0')}"
         self._R = _native.shmring().ShmRing
         self.ring = None
@@ -183,7 +187,7 @@ class FrontDoorFeed:
 
     def receive(self):
         from llm_message_queue_amd.gateway.shm_bridge import decode_raw
-        return [decode_raw(b) for _, b in self.ring.pop(4096, 0)]
+        return [decode_raw(b) for _, b in self.ring.pop(4096, 0, self.share)]
 
     def backlog(self) -> int:
         return int(self.ring.size())
@@ -213,7 +217,8 @@ def main(argv=None) -> int:
     # rank 0 starts the front-door feeder process before anything here
     # touches the GPU (a child process, never an exec)
     job = os.environ.get("TORCHELASTIC_RUN_ID", str(os.getpid() if world == 1 else "bench"))
-    door = FrontDoorFeed(world, rank, job, a.seed) if a.ingress == "rank0" and world > 1 else None
+    door = (FrontDoorFeed(world, rank, job, a.seed, share=world if a.door_share == "fair" else 1)
+            if a.ingress == "rank0" and world > 1 else None)
     import torch
 
     from llm_message_queue_amd.backend.engine import BackendEngine
@@ -591,7 +596,7 @@ def main(argv=None) -> int:
                 "synthetic (Poisson arrivals, 10/30/40/20 tier mix, random-init weights)",
         "config": {"model": f"{a.model}-stub (32L, random bf16)" if a.model == "llama3-8b" else a.model,
                    "global_batch": a.slots * world, "seq_len": a.max_ctx,
-                   "parallelism": f"dp{world}", "ingress": a.ingress, "placement": a.lb,
+                   "parallelism": f"dp{world}", "ingress": a.ingress, "door_share": a.door_share, "placement": a.lb,
                    "token_budget_by_rank": a.token_budget_by_rank or None,
                    "sim_gpu": a.sim_gpu or None, "extra_steps": not a.no_extra_steps,
                    "control_plane": comm_kind, "token_budget": a.token_budget,

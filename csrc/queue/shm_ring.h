@@ -97,14 +97,23 @@ class ShmRing {
 
   // Pop up to max_n records; waits up to timeout_ms for the first one
   // (0 = poll, <0 = wait forever).  Returns (tag, payload) pairs.
-  std::vector<std::pair<uint32_t, std::string>> pop(size_t max_n, int64_t timeout_ms) {
+  // share > 1: take at most ceil(count / share) of the records present (at
+  // least one) -- the fair split of one ring drained by `share` consumers
+  // that all wake on the same push; what is left goes to the next pop, so
+  // nothing is stranded.
+  std::vector<std::pair<uint32_t, std::string>> pop(size_t max_n, int64_t timeout_ms, uint32_t share = 1) {
     std::vector<std::pair<uint32_t, std::string>> out;
+    auto quota = [&]() -> size_t {
+      if (share <= 1) return max_n;
+      const size_t fair = (size_t)((h_->count + share - 1) / share);
+      return std::min(max_n, fair < 1 ? (size_t)1 : fair);
+    };
     auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
     for (;;) {
       uint32_t seen;
       {
         Lock l(h_);
-        pop_locked(max_n, out);
+        pop_locked(quota(), out);
         if (!out.empty()) return out;
         seen = h_->seq.load(std::memory_order_acquire);
       }
@@ -125,7 +134,7 @@ class ShmRing {
         // woken: return what is there -- possibly nothing after a wake_all,
         // so the caller can test its own stop flag
         Lock l(h_);
-        pop_locked(max_n, out);
+        pop_locked(quota(), out);
         return out;
       }
     }

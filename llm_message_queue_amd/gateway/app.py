@@ -416,18 +416,24 @@ class GatewayApp:
         (the native front door routes them there): rank 0 owns conversation
         state and records the turn like ``POST /api/v1/messages`` does."""
         from .shm_bridge import TAG_RAW, decode_message, decode_raw
-        # Greedy: the ring is FIFO and the per-rank queues are priority
-        # queues, so requests leave the ring as fast as any rank can take them
-        # (a per-rank backpressure threshold was measured to hold realtime
-        # requests behind normal ones in the ring: realtime p99 160 -> 214 ms,
-        # profiles/r3_http_multirank_2ranks_1gpu_5000_backpressure.json); an
-        # uneven split between ranks is what the per-tick planner rebalances.
+        # No backpressure: the ring is FIFO and the per-rank queues are
+        # priority queues, so requests leave the ring as fast as the ranks can
+        # take them (a per-rank backpressure threshold was measured to hold
+        # realtime requests behind normal ones in the ring: realtime p99 160
+        # -> 214 ms, profiles/r3_http_multirank_2ranks_1gpu_5000_backpressure.json).
+        # Every rank's ring thread wakes on the same push and takes a fair
+        # 1/world part of what is queued (``share``), then comes straight back
+        # for more: the split between ranks stays even without any rank
+        # waiting (greedy pops gave 47-74k per rank at 33k req/s,
+        # profiles/r4_http_frontdoor_8ranks_box16.jsonl).
         mb = self.cfg.preprocessor.max_batch
+        share = max(1, self.gateway.world)
         while not self._stop.is_set():
             got = []
             for r in self.extra_rings:               # rank 0's conversation ring
                 got.extend(r.get_records(mb, timeout_ms=0))
-            got.extend(self.ring.get_records(mb, timeout_ms=0 if got else (5 if self.extra_rings else 20)))
+            got.extend(self.ring.get_records(mb, timeout_ms=0 if got else (5 if self.extra_rings else 20),
+                                             share=share))
             if not got:
                 continue
             now = time.time_ns()

@@ -98,9 +98,11 @@ class RingPair:
     def get_messages(self, max_n: int = 4096, timeout_ms: int = 0) -> List[Message]:
         return [decode_message(b) for _, b in self.requests.pop(max_n, timeout_ms)]
 
-    def get_records(self, max_n: int = 4096, timeout_ms: int = 0):
-        """[(tag, payload)]: TAG_MESSAGE records and TAG_RAW records."""
-        return self.requests.pop(max_n, timeout_ms)
+    def get_records(self, max_n: int = 4096, timeout_ms: int = 0, share: int = 1):
+        """[(tag, payload)]: TAG_MESSAGE records and TAG_RAW records.
+        ``share``: consumers draining this ring together -- take at most a
+        1/share fair part of what is queued (``ShmRing::pop``)."""
+        return self.requests.pop(max_n, timeout_ms, share)
 
     def put_events(self, msgs: Iterable[Message], error: str = "") -> int:
         recs = [encode_event(m, error) for m in msgs]

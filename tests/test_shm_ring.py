@@ -69,6 +69,32 @@ def test_pop_timeout_and_wake(ring):
     assert out[-1] == [] and time.monotonic() - t0 < 1.0
 
 
+def test_fair_share_pop(ring):
+    """``share``: at most ceil(count / share) per pop (at least one), FIFO
+    order kept, nothing stranded; share 1 is the greedy pop."""
+    ring.push_many([bytes([i]) for i in range(17)], 3)
+    got = []
+    sizes = []
+    while True:
+        part = ring.pop(100, 0, 8)
+        if not part:
+            break
+        sizes.append(len(part))
+        got += part
+    assert sizes[:3] == [3, 2, 2] and sizes[-1] == 1 and sum(sizes) == 17
+    assert [b for _, b in got] == [bytes([i]) for i in range(17)]
+    ring.push_many([b"a"] * 5, 1)
+    assert len(ring.pop(2, 0, 1)) == 2 and len(ring.pop(100, 0)) == 3
+    # a consumer blocked in pop takes its share of what the waking push brought
+    out = []
+    th = threading.Thread(target=lambda: out.append(ring.pop(100, 5000, 4)))
+    th.start()
+    time.sleep(0.05)
+    ring.push_many([b"w"] * 8, 2)
+    th.join(2)
+    assert len(out[0]) == 2 and ring.size() == 6
+
+
 def _producer(name, k, n):
     R = _native.shmring().ShmRing
     r = R(name, 0, "attach")
