@@ -58,7 +58,16 @@ def test_bench_four_ranks_torchrun_dry_run():
               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "4",
               "--cpu-dry-run", "--steps", "5", "--warmup", "2", "--gateway-only-s", "0.5",
               "--gateway-only-rate", "200"])
-    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["value"] > 0
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4"
+    # 4 CPU ranks of a tiny model on a shared host: whether a util holds the
+    # SLO is timing noise here, so pin the contract, not the outcome -- every
+    # attempt served requests, and value is the best attempt that held the
+    # target or 0 with the reason stated
+    slo = d["slo_search"]
+    assert all(a["value"] > 0 for a in slo["attempts"])
+    met = [a["value"] for a in slo["attempts"] if a["met"]]
+    assert d["value"] == (met[0] if met else 0.0)
+    assert met or "reason" in slo
     # the secondary null-backend phase runs multi-rank too (the driver's 8-GPU run does it)
     assert d["gateway_only"]["requests_per_s"] > 0
 
