@@ -1,0 +1,133 @@
+// Where does the gate/up GEMM's time go on a power-bound MI355X?  A/B of the
+// production 8-wave kernel (SCHED 2) against diagnostic builds of the same
+// template that drop one kind of work from the steady-state K loop while
+// keeping every MFMA (numerics are WRONG for 5-7; timing only):
+//
+//   2  production
+//   5  A fragment reads of phases 3 / 7 skipped: one third fewer LDS read
+//      bytes -- what a 128 x 128 wave tile (4 waves) would read per MFMA
+//   6  no fragment reads in the loop (MFMA + staging DMA only)
+//   7  no staging DMA in the loop (MFMA + LDS fragment reads only)
+//
+// If 5 or 6 run much faster, LDS read traffic (its issue time or its energy
+// under the power cap) limits the kernel and a bigger wave tile pays; if only
+// 7 does, it is the L2 / HBM side.  Interleaved rounds in one process,
+// random operands (cdna_hip_programming.md §5.4 rules 24 / 25).
+//
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I csrc bench/gemm_energy_diag.hip -o /tmp/gemm_energy_diag
+//   /tmp/gemm_energy_diag [M N K rounds]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "kernels/gemm_kernels.h"
+
+using namespace llmq;
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+// approximately N(0, scale^2) bf16 from a counter hash (sum of 4 uniforms)
+__global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed, float scale) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    float s = 0.f;
+    for (int k = 0; k < 4; ++k) {
+      h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
+      s += (float)(h >> 8) * (1.0f / 16777216.0f);
+    }
+    const float v = (s - 2.0f) * 1.7320508f * scale;  // var of the sum of 4 U(0,1) = 1/3
+    uint32_t u = __float_as_uint(v);
+    p[i] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  }
+}
+
+template <int SCHED>
+static void launch(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K) {
+  static bool attr = false;
+  if (!attr) {
+    CK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<GM_EPI_SWIGLU, true, SCHED>,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, GM_LDS_BYTES));
+    attr = true;
+  }
+  const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  hipLaunchKernelGGL((gemm_bf16_kernel<GM_EPI_SWIGLU, true, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, 0,
+                     a, w, c, M, N, K, GM_GROUP_M, nullptr, GmRope{}, GmSplit{0, nullptr, nullptr},
+                     GmArgmax{nullptr, nullptr});
+}
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 4096;
+  const int N = argc > 2 ? atoi(argv[2]) : 28672;
+  const int K = argc > 3 ? atoi(argv[3]) : 4096;
+  const int rounds = argc > 4 ? atoi(argv[4]) : 9;
+  const int iters = 10;
+  if (N % GM_BN || K % (2 * GM_BK) || M <= 0) {
+    fprintf(stderr, "shape: N %% 256, K %% 128\n");
+    return 2;
+  }
+  uint16_t *a, *w, *c;
+  CK(hipMalloc(&a, (size_t)M * K * 2));
+  CK(hipMalloc(&w, (size_t)N * K * 2));
+  CK(hipMalloc(&c, (size_t)M * (N / 2) * 2));
+  hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, a, (size_t)M * K, 1u, 1.0f);
+  hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, w, (size_t)N * K, 2u, 0.02f);
+  CK(hipDeviceSynchronize());
+
+  const int scheds[4] = {2, 5, 6, 7};
+  auto run = [&](int s) {
+    switch (s) {
+      case 2: launch<2>(a, w, c, M, N, K); break;
+      case 5: launch<5>(a, w, c, M, N, K); break;
+      case 6: launch<6>(a, w, c, M, N, K); break;
+      default: launch<7>(a, w, c, M, N, K); break;
+    }
+  };
+  // ~2 s of back-to-back launches first so the clock has settled (DVFS give-back)
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 3000; ++i) {
+    run(2);
+    if (i % 100 == 99) {
+      CK(hipDeviceSynchronize());
+      float ms = 0;
+      CK(hipEventRecord(e0));
+      run(2);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms * (i + 1) > 2500.f) break;
+    }
+  }
+  CK(hipDeviceSynchronize());
+  std::vector<std::vector<float>> t(4);
+  for (int r = 0; r < rounds; ++r)
+    for (int v = 0; v < 4; ++v) {
+      run(scheds[v]);
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < iters; ++i) run(scheds[v]);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[v].push_back(ms / iters);
+    }
+  const double flop = 2.0 * M * (double)N * K;
+  for (int v = 0; v < 4; ++v) {
+    std::sort(t[v].begin(), t[v].end());
+    const float med = t[v][t[v].size() / 2];
+    printf("{\"sched\": %d, \"M\": %d, \"N\": %d, \"K\": %d, \"ms_median\": %.4f, \"ms_min\": %.4f, \"tflops\": %.1f}\n",
+           scheds[v], M, N, K, med, t[v][0], flop / med / 1e9);
+  }
+  return 0;
+}

@@ -292,8 +292,8 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     // no per-cluster flips -- 1.7 % faster than SCHED 1 (s_setprio 1 around
     // every MFMA cluster) at T = 4041 (profiles/r2_gemm_prio_ab.jsonl).
     // SCHED 3 / 4 (A/B only): the static priority on wave row 0 / none.
-    if constexpr (SCHED == 2 || SCHED == 3) {
-      if (wr == (SCHED == 2 ? 1 : 0)) __builtin_amdgcn_s_setprio(1);
+    if constexpr (SCHED == 2 || SCHED == 3 || SCHED >= 5) {
+      if (wr == (SCHED == 3 ? 0 : 1)) __builtin_amdgcn_s_setprio(1);
     }
     // Balanced schedule: every phase retires the half-tile staged 3 phases
     // earlier (vmcnt(6) each phase), so the NEXT buffer's B0 fragments can be
@@ -311,6 +311,11 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     GM_VMCNT(6);
     GM_BARRIER();
     GM_READ_B0_INTO(0, bfr[0]);
+    if constexpr (SCHED >= 5) {                    // diagnostics: every fragment register defined
+      GM_READ_A(0, 0);
+      GM_READ_B(0, 1);
+      GM_READ_B0_INTO(1, b0y);
+    }
     if (STAGGER && wr == 1) GM_BARRIER();
 
 #define GM_PHASE_END(MH, NH, BREG) \
@@ -322,18 +327,32 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   } while (0)
 
     int t = 0;
+    // SCHED 5-7: power/energy DIAGNOSTICS only (bench/gemm_energy_diag.hip; wrong
+    // numerics, never dispatched by the library): 5 skips the A fragment
+    // reads of phases 3 / 7 (one third fewer LDS read bytes, what a 128x128
+    // wave tile would read), 6 skips every fragment read of the loop, 7 skips
+    // every staging DMA of the loop (no L2 / HBM traffic in steady state).
+    constexpr bool kRdA = SCHED != 6, kRdA2 = SCHED != 5 && SCHED != 6, kRdB = SCHED != 6, kDma = SCHED != 7;
+#define GM_D_READ_A(C, B, H) do { if constexpr (C) GM_READ_A(B, H); } while (0)
+#define GM_D_READ_B(B, H) do { if constexpr (kRdB) GM_READ_B(B, H); } while (0)
+#define GM_D_READ_B0(B, D) do { if constexpr (kRdB) GM_READ_B0_INTO(B, D); } while (0)
+#define GM_D_STAGE(B, H, K) do { if constexpr (kDma) GM_STAGE(B, H, K); } while (0)
     for (; t < nt - 2; t += 2) {
       {
-        GM_READ_A(0, 0); GM_STAGE(1, GM_A1, t + 1); GM_VMCNT(6); GM_PHASE_END(0, 0, bfr[0]);
-        GM_READ_B(0, 1); GM_STAGE(0, GM_B0, t + 2); GM_VMCNT(6); GM_PHASE_END(0, 1, bfr[1]);
-        GM_READ_A(0, 1); GM_STAGE(0, GM_A0, t + 2); GM_VMCNT(6); GM_PHASE_END(1, 1, bfr[1]);
-        GM_READ_B0_INTO(1, b0y); GM_STAGE(0, GM_B1, t + 2); GM_VMCNT(6); GM_PHASE_END(1, 0, bfr[0]);
-        GM_READ_A(1, 0); GM_STAGE(0, GM_A1, t + 2); GM_VMCNT(6); GM_PHASE_END(0, 0, b0y);
-        GM_READ_B(1, 1); GM_STAGE(1, GM_B0, t + 3); GM_VMCNT(6); GM_PHASE_END(0, 1, bfr[1]);
-        GM_READ_A(1, 1); GM_STAGE(1, GM_A0, t + 3); GM_VMCNT(6); GM_PHASE_END(1, 1, bfr[1]);
-        GM_READ_B0_INTO(0, bfr[0]); GM_STAGE(1, GM_B1, t + 3); GM_VMCNT(6); GM_PHASE_END(1, 0, b0y);
+        GM_D_READ_A(kRdA, 0, 0); GM_D_STAGE(1, GM_A1, t + 1); GM_VMCNT(6); GM_PHASE_END(0, 0, bfr[0]);
+        GM_D_READ_B(0, 1); GM_D_STAGE(0, GM_B0, t + 2); GM_VMCNT(6); GM_PHASE_END(0, 1, bfr[1]);
+        GM_D_READ_A(kRdA2, 0, 1); GM_D_STAGE(0, GM_A0, t + 2); GM_VMCNT(6); GM_PHASE_END(1, 1, bfr[1]);
+        GM_D_READ_B0(1, b0y); GM_D_STAGE(0, GM_B1, t + 2); GM_VMCNT(6); GM_PHASE_END(1, 0, bfr[0]);
+        GM_D_READ_A(kRdA, 1, 0); GM_D_STAGE(0, GM_A1, t + 2); GM_VMCNT(6); GM_PHASE_END(0, 0, b0y);
+        GM_D_READ_B(1, 1); GM_D_STAGE(1, GM_B0, t + 3); GM_VMCNT(6); GM_PHASE_END(0, 1, bfr[1]);
+        GM_D_READ_A(kRdA2, 1, 1); GM_D_STAGE(1, GM_A0, t + 3); GM_VMCNT(6); GM_PHASE_END(1, 1, bfr[1]);
+        GM_D_READ_B0(0, bfr[0]); GM_D_STAGE(1, GM_B1, t + 3); GM_VMCNT(6); GM_PHASE_END(1, 0, b0y);
       }
     }
+#undef GM_D_READ_A
+#undef GM_D_READ_B
+#undef GM_D_READ_B0
+#undef GM_D_STAGE
     {                                              // last two K-tiles: drain
         GM_READ_A(0, 0); GM_STAGE(1, GM_A1, t + 1); GM_VMCNT(6); GM_PHASE_END(0, 0, bfr[0]);
         GM_READ_B(0, 1); GM_VMCNT(4); GM_PHASE_END(0, 1, bfr[1]);
@@ -344,7 +363,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         GM_READ_A(1, 1); GM_PHASE_END(1, 1, bfr[1]);
         GM_PHASE_END(1, 0, b0y);
     }
-    if constexpr (SCHED == 2 || SCHED == 3) __builtin_amdgcn_s_setprio(0);
+    if constexpr (SCHED == 2 || SCHED == 3 || SCHED >= 5) __builtin_amdgcn_s_setprio(0);
 #undef GM_PHASE_END
   } else {
     // prologue: tile 0 -> buffer 0 (all halves), tile 1 -> buffer 1 (B0, A0, B1)
