@@ -15,7 +15,7 @@
 // random operands (cdna_hip_programming.md §5.4 rules 24 / 25).
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I csrc bench/gemm_energy_diag.hip -o /tmp/gemm_energy_diag
-//   /tmp/gemm_energy_diag [M N K rounds]
+//   /tmp/gemm_energy_diag [M N K rounds warm_ms]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -70,6 +70,7 @@ int main(int argc, char** argv) {
   const int N = argc > 2 ? atoi(argv[2]) : 28672;
   const int K = argc > 3 ? atoi(argv[3]) : 4096;
   const int rounds = argc > 4 ? atoi(argv[4]) : 9;
+  const float warm_ms = argc > 5 ? (float)atof(argv[5]) : 2500.f;   // 0 under a PMC pass
   const int iters = 10;
   if (N % GM_BN || K % (2 * GM_BK) || M <= 0) {
     fprintf(stderr, "shape: N %% 256, K %% 128\n");
@@ -96,7 +97,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3000; ++i) {
+  for (int i = 0; warm_ms > 0.f && i < 3000; ++i) {
     run(2);
     if (i % 100 == 99) {
       CK(hipDeviceSynchronize());
@@ -106,7 +107,7 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       CK(hipEventElapsedTime(&ms, e0, e1));
-      if (ms * (i + 1) > 2500.f) break;
+      if (ms * (i + 1) > warm_ms) break;
     }
   }
   CK(hipDeviceSynchronize());
