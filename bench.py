@@ -120,8 +120,9 @@ def parse(argv=None):
                          "rank drains, decodes and GPU-preprocesses; rank0-funnel: the r2 form, rank 0 "
                          "preprocesses the whole job's traffic on GPU 0 and the planner spreads it (A/B)")
     ap.add_argument("--door-share", default="greedy", choices=["greedy", "fair"],
-                    help="--ingress rank0: each pump takes everything the shared ring holds (greedy) or a "
-                         "1/world fair part of it (fair, what `cli serve`'s dedicated ring threads do)")
+                    help="--ingress rank0: each pump takes everything the shared ring holds (greedy) or only up "
+                         "to an even 1/world share of the ring's traffic (fair: ShmRing balanced pop, what "
+                         "`cli serve`'s ring threads do)")
     ap.add_argument("--lb", default="least_connections",
                     choices=["round_robin", "least_connections", "weighted_random", "adaptive_load", "local_first"],
                     help="multi-GPU placement strategy (loadbalancer.algorithm)")
@@ -187,7 +188,7 @@ class FrontDoorFeed:
 
     def receive(self):
         from llm_message_queue_amd.gateway.shm_bridge import decode_raw
-        return [decode_raw(b) for _, b in self.ring.pop(4096, 0, self.share)]
+        return [decode_raw(b) for _, b in self.ring.pop(4096, 0, self.share, self.rank if self.share > 1 else -1)]
 
     def backlog(self) -> int:
         return int(self.ring.size())

@@ -76,17 +76,18 @@ PYBIND11_MODULE(_shmring, m) {
            },
            py::arg("records"), py::arg("tag") = 0)
       .def("pop",
-           [](ShmRing& r, size_t max_n, int64_t timeout_ms, uint32_t share) {
+           [](ShmRing& r, size_t max_n, int64_t timeout_ms, uint32_t share, int who) {
              std::vector<std::pair<uint32_t, std::string>> v;
              {
                py::gil_scoped_release nogil;
-               v = r.pop(max_n, timeout_ms, share);
+               v = r.pop(max_n, timeout_ms, share, who);
              }
              py::list out;
              for (auto& p : v) out.append(py::make_tuple(p.first, py::bytes(p.second)));
              return out;
            },
-           py::arg("max_n") = 1024, py::arg("timeout_ms") = 0, py::arg("share") = 1)
+           py::arg("max_n") = 1024, py::arg("timeout_ms") = 0, py::arg("share") = 1, py::arg("who") = -1)
+      .def("taken", &ShmRing::taken, py::arg("n"))
       .def("size", &ShmRing::size)
       .def("bytes_used", &ShmRing::bytes_used)
       .def_property_readonly("capacity", &ShmRing::capacity)

@@ -40,7 +40,8 @@
 namespace llmq {
 
 constexpr uint64_t kMagic = 0x4c4c4d5152494e47ull;   // "LLMQRING"
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;
+constexpr int kMaxConsumers = 64;     // consumer ids of the balanced share (pop `who`)
 constexpr uint32_t kWrap = 0xffffffffu;
 
 struct alignas(64) Header {
@@ -56,6 +57,12 @@ struct alignas(64) Header {
   alignas(64) std::atomic<uint32_t> seq;      // futex word: bumped by every push
   std::atomic<uint32_t> waiters;
   uint32_t _pad1;
+  // balanced share (pop with `who`): records taken and the last pop attempt
+  // (steady-clock ns) per consumer id, and whether it is parked in the futex
+  // wait -- guarded by `mu` like the offsets
+  alignas(64) uint64_t taken[kMaxConsumers];
+  int64_t polled_ns[kMaxConsumers];
+  uint8_t parked[kMaxConsumers];
 };
 static_assert(sizeof(Header) % 64 == 0, "header must be cache-line sized");
 
@@ -97,44 +104,91 @@ class ShmRing {
 
   // Pop up to max_n records; waits up to timeout_ms for the first one
   // (0 = poll, <0 = wait forever).  Returns (tag, payload) pairs.
-  // share > 1: take at most ceil(count / share) of the records present (at
-  // least one) -- the fair split of one ring drained by `share` consumers
-  // that all wake on the same push; what is left goes to the next pop, so
-  // nothing is stranded.
-  std::vector<std::pair<uint32_t, std::string>> pop(size_t max_n, int64_t timeout_ms, uint32_t share = 1) {
+  // share > 1, who < 0: take at most ceil(count / share) of the records
+  // present (at least one) -- a per-pop split of one ring drained by `share`
+  // consumers; what is left goes to the next pop, so nothing is stranded.
+  // That alone does not even out the totals: whichever consumer polls most
+  // often still takes most (47-74k vs 37-69k per rank at 33k req/s,
+  // profiles/r4_http_frontdoor_8ranks_box16{,_fair}.jsonl).
+  // share > 1, 0 <= who < share: BALANCED -- consumer `who` takes what
+  // brings its running total up to the even share of everything taken or
+  // queued, and nothing once it is there, leaving the rest to the consumers
+  // behind.  A consumer behind that has not polled for kStallNs (kParkedNs
+  // while it sleeps in pop's futex wait, which a push ends) is skipped: the
+  // others then take the per-pop split, so a busy, slow or dead consumer
+  // delays records by at most that long and never strands them.  A deficit
+  // is forgiven beyond kCatchUp records, so a consumer coming back does not
+  // take the whole ring.
+  static constexpr int64_t kStallNs = 2'000'000, kParkedNs = 100'000'000;
+  static constexpr int64_t kCatchUp = 256;
+  std::vector<std::pair<uint32_t, std::string>> pop(size_t max_n, int64_t timeout_ms, uint32_t share = 1,
+                                                    int who = -1) {
     std::vector<std::pair<uint32_t, std::string>> out;
+    const bool bal = share > 1 && who >= 0 && who < (int)share && share <= (uint32_t)kMaxConsumers;
+    bool deferred = false;   // records were left to consumers behind: re-check within kStallNs
     auto quota = [&]() -> size_t {
+      deferred = false;
       if (share <= 1) return max_n;
-      const size_t fair = (size_t)((h_->count + share - 1) / share);
-      return std::min(max_n, fair < 1 ? (size_t)1 : fair);
+      const size_t fair = std::max<size_t>(1, (size_t)((h_->count + share - 1) / share));
+      if (!bal) return std::min(max_n, fair);
+      const int64_t now = steady_ns();
+      h_->polled_ns[who] = now;
+      uint64_t total = 0;
+      for (uint32_t j = 0; j < share; ++j) total += h_->taken[j];
+      const int64_t target = (int64_t)((total + h_->count + share - 1) / share);
+      if (target - (int64_t)h_->taken[who] > kCatchUp) h_->taken[who] = (uint64_t)(target - kCatchUp);
+      const int64_t mine = target - (int64_t)h_->taken[who];
+      if (mine > 0) return std::min(max_n, (size_t)mine);
+      for (uint32_t j = 0; j < share; ++j) {
+        if ((int)j == who || (int64_t)h_->taken[j] >= target) continue;
+        if (now - h_->polled_ns[j] > (h_->parked[j] ? kParkedNs : kStallNs)) return std::min(max_n, fair);
+      }
+      deferred = h_->count > 0;
+      return 0;
+    };
+    auto take = [&]() {
+      const size_t before = out.size();
+      pop_locked(quota(), out);
+      if (bal) h_->taken[who] += out.size() - before;
+    };
+    auto park = [&](bool on) {
+      if (!bal) return;
+      Lock l(h_);
+      h_->parked[who] = on ? 1 : 0;
+      h_->polled_ns[who] = steady_ns();
     };
     auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
     for (;;) {
       uint32_t seen;
       {
         Lock l(h_);
-        pop_locked(quota(), out);
+        take();
         if (!out.empty()) return out;
         seen = h_->seq.load(std::memory_order_acquire);
       }
       if (timeout_ms == 0) return out;
       timespec ts{}, *tsp = nullptr;
-      if (timeout_ms > 0) {
-        auto left = deadline - std::chrono::steady_clock::now();
-        if (left <= std::chrono::steady_clock::duration::zero()) return out;
-        auto ns = std::chrono::duration_cast<std::chrono::nanoseconds>(left).count();
+      if (timeout_ms > 0 || deferred) {
+        int64_t ns = deferred ? kStallNs : INT64_MAX;
+        if (timeout_ms > 0) {
+          auto left = deadline - std::chrono::steady_clock::now();
+          if (left <= std::chrono::steady_clock::duration::zero()) return out;
+          ns = std::min<int64_t>(ns, std::chrono::duration_cast<std::chrono::nanoseconds>(left).count());
+        }
         ts.tv_sec = ns / 1000000000;
         ts.tv_nsec = ns % 1000000000;
         tsp = &ts;
       }
+      park(true);
       h_->waiters.fetch_add(1);
       long r = futex(&h_->seq, FUTEX_WAIT, seen, tsp);   // wake, timeout, or seq already changed
       h_->waiters.fetch_sub(1);
+      park(false);
       if (r == 0) {
         // woken: return what is there -- possibly nothing after a wake_all,
         // so the caller can test its own stop flag
         Lock l(h_);
-        pop_locked(quota(), out);
+        take();
         return out;
       }
     }
@@ -151,6 +205,14 @@ class ShmRing {
   }
 
   uint64_t capacity() const { return h_ ? h_->cap : 0; }
+
+  // records taken by balanced-share consumers 0 .. n-1
+  std::vector<uint64_t> taken(int n) {
+    Lock l(h_);
+    std::vector<uint64_t> v;
+    for (int j = 0; j < n && j < kMaxConsumers; ++j) v.push_back(h_->taken[j]);
+    return v;
+  }
 
   struct Stats {
     uint64_t size, pushed, popped, dropped_full, bytes_in, bytes_used, capacity;
@@ -197,6 +259,12 @@ class ShmRing {
   };
 
   uint8_t* data() const { return reinterpret_cast<uint8_t*>(base_) + sizeof(Header); }
+
+  static int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
 
   void map(int fd, uint64_t bytes) {
     void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);

@@ -421,11 +421,13 @@ class GatewayApp:
         # take them (a per-rank backpressure threshold was measured to hold
         # realtime requests behind normal ones in the ring: realtime p99 160
         # -> 214 ms, profiles/r3_http_multirank_2ranks_1gpu_5000_backpressure.json).
-        # Every rank's ring thread wakes on the same push and takes a fair
-        # 1/world part of what is queued (``share``), then comes straight back
-        # for more: the split between ranks stays even without any rank
-        # waiting (greedy pops gave 47-74k per rank at 33k req/s,
-        # profiles/r4_http_frontdoor_8ranks_box16.jsonl).
+        # Every rank's ring thread wakes on the same push and takes what
+        # brings its total up to an even 1/world share of the ring's traffic
+        # (``ShmRing::pop`` balanced: ``share`` + ``who``); a rank that has
+        # not polled for 2 ms is skipped, so a busy or dead rank never
+        # strands records.  Greedy pops gave 47-74k per rank at 33k req/s,
+        # a per-pop 1/world split 37-69k
+        # (profiles/r4_http_frontdoor_8ranks_box16{,_fair}.jsonl).
         mb = self.cfg.preprocessor.max_batch
         share = max(1, self.gateway.world)
         while not self._stop.is_set():
@@ -433,7 +435,7 @@ class GatewayApp:
             for r in self.extra_rings:               # rank 0's conversation ring
                 got.extend(r.get_records(mb, timeout_ms=0))
             got.extend(self.ring.get_records(mb, timeout_ms=0 if got else (5 if self.extra_rings else 20),
-                                             share=share))
+                                             share=share, who=self.gateway.rank if share > 1 else -1))
             if not got:
                 continue
             now = time.time_ns()

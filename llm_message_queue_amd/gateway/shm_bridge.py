@@ -98,11 +98,13 @@ class RingPair:
     def get_messages(self, max_n: int = 4096, timeout_ms: int = 0) -> List[Message]:
         return [decode_message(b) for _, b in self.requests.pop(max_n, timeout_ms)]
 
-    def get_records(self, max_n: int = 4096, timeout_ms: int = 0, share: int = 1):
+    def get_records(self, max_n: int = 4096, timeout_ms: int = 0, share: int = 1, who: int = -1):
         """[(tag, payload)]: TAG_MESSAGE records and TAG_RAW records.
-        ``share``: consumers draining this ring together -- take at most a
-        1/share fair part of what is queued (``ShmRing::pop``)."""
-        return self.requests.pop(max_n, timeout_ms, share)
+        ``share``: consumers draining this ring together; ``who`` (0 ..
+        share-1): this consumer's id -- take only up to an even share of
+        everything taken so far (``ShmRing::pop``, balanced); without it a
+        per-pop 1/share part of what is queued."""
+        return self.requests.pop(max_n, timeout_ms, share, who)
 
     def put_events(self, msgs: Iterable[Message], error: str = "") -> int:
         recs = [encode_event(m, error) for m in msgs]

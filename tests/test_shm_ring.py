@@ -95,6 +95,82 @@ def test_fair_share_pop(ring):
     assert len(out[0]) == 2 and ring.size() == 6
 
 
+def test_balanced_share_pop(ring):
+    """``who``: a consumer takes only up to the even share of everything
+    taken + queued, so a consumer that polls far more often than its peers
+    still ends at its 1/share; a peer that stops polling (no pop for 2 ms)
+    no longer holds its share back; a deficit is forgiven past 256."""
+    taken = [0, 0, 0, 0]
+    for _ in range(10):                   # consumer 0 polls 3x as often as 1-3
+        ring.push_many([b"x"] * 12, 1)
+        for who in (0, 0, 0, 1, 2, 3):
+            taken[who] += len(ring.pop(100, 0, 4, who))
+    assert taken == [30, 30, 30, 30] and ring.size() == 0
+    assert ring.taken(4) == [30, 30, 30, 30]
+    # FIFO across consumers is the ring's order
+    ring.push_many([bytes([i]) for i in range(8)], 1)
+    a, b = ring.pop(100, 0, 4, 0), ring.pop(100, 0, 4, 1)
+    assert [x for _, x in a] == [bytes([0]), bytes([1])] and [x for _, x in b] == [bytes([2]), bytes([3])]
+    # consumer 0 is at its share: the rest waits for 2 and 3 while they poll ...
+    assert ring.pop(100, 0, 4, 0) == [] and ring.size() == 4
+    time.sleep(0.01)                      # ... 2 and 3 stop polling: 0 takes the per-pop split
+    assert len(ring.pop(100, 0, 4, 0)) == 1 and ring.size() == 3
+    # a waiting consumer that is ahead re-checks within the stall window
+    # instead of sleeping out its whole timeout while records sit for others
+    while ring.size():
+        ring.pop(100, 0, 4, 1)
+    ring.push_many([b"y"] * 40, 1)        # 1 takes up to its share, leaves the rest
+    n1 = len(ring.pop(100, 0, 4, 1))
+    assert 0 < n1 < 40
+    t0 = time.monotonic()
+    got = ring.pop(100, 1000, 4, 1)       # 0, 2, 3 are idle (> 2 ms): 1 takes a split
+    assert got and time.monotonic() - t0 < 0.5
+    # a long-absent consumer does not take the whole ring when it returns
+    ring.push_many([b"z"] * 300, 1)
+    for _ in range(2):
+        ring.pop(1000, 0, 4, 1)
+    assert len(ring.pop(1000, 0, 4, 2)) <= 256 + 1
+
+
+def test_balanced_share_threads(ring):
+    """Four consumer threads blocked in pop on one ring, one producer: the
+    balanced pop splits the records evenly whatever the wake order."""
+    R = _native.shmring().ShmRing
+    name = ring_name("bal")
+    big = R(name, 1 << 22, "create")
+    stop = threading.Event()
+    counts = [0] * 4
+
+    def consume(who):
+        r = R(name, 0, "attach")
+        while not stop.is_set():
+            counts[who] += len(r.pop(64, 20, 4, who))
+            if who == 0:
+                time.sleep(0)             # the eager one
+        counts[who] += len(r.pop(4096, 0, 4, who))
+        r.close()
+
+    ths = [threading.Thread(target=consume, args=(w,)) for w in range(4)]
+    for t in ths:
+        t.start()
+    total = 4000
+    for i in range(total // 8):
+        big.push_many([b"r"] * 8, 1)
+        if i % 50 == 0:
+            time.sleep(0.002)
+    deadline = time.monotonic() + 5
+    while big.size() and time.monotonic() < deadline:
+        time.sleep(0.01)
+    stop.set()
+    big.wake_all()
+    for t in ths:
+        t.join(5)
+    assert sum(counts) == total and big.size() == 0
+    assert max(counts) - min(counts) <= 0.05 * total / 4 + 8, counts
+    big.unlink()
+    big.close()
+
+
 def _producer(name, k, n):
     R = _native.shmring().ShmRing
     r = R(name, 0, "attach")
