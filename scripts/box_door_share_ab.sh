@@ -7,7 +7,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for SH in greedy fair; do
+for SH in ${SHARES:-greedy fair}; do
   LOG=gpurun_out/box_share_$SH.log OUT=gpurun_out/box_share_$SH.jsonl WORLDS=8 INGRESS=rank0 PINS=none \
     EXTRA="--door-share $SH" timeout -k 10 400 bash scripts/sim_breakdown.sh || exit $?
 done
