@@ -119,7 +119,7 @@ def parse(argv=None):
                          "process writes N x the per-GPU rate as RAW records into ONE shared ring that every "
                          "rank drains, decodes and GPU-preprocesses; rank0-funnel: the r2 form, rank 0 "
                          "preprocesses the whole job's traffic on GPU 0 and the planner spreads it (A/B)")
-    ap.add_argument("--door-share", default="greedy", choices=["greedy", "fair"],
+    ap.add_argument("--door-share", default="fair", choices=["greedy", "fair"],
                     help="--ingress rank0: each pump takes everything the shared ring holds (greedy) or only up "
                          "to an even 1/world share of the ring's traffic (fair: ShmRing balanced pop, what "
                          "`cli serve`'s ring threads do)")
