@@ -24,6 +24,7 @@ multi-rank logic is testable on a CPU box at world sizes 2/4/8.
 from __future__ import annotations
 
 import threading
+import time
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -41,17 +42,23 @@ DEFAULT_TIMEOUT_S = 60.0
 
 class Pending:
     """A collective in flight (split phase).  ``ready()`` is non-blocking:
-    True once every rank has contributed; ``wait()`` returns the result.
+    True once every rank has contributed -- or once ``deadline`` (monotonic
+    s) has passed, so a caller's ``while not ready()`` overlap loop always
+    ends and ``wait()`` raises the comm's timeout (``PeerLost``) for a dead
+    or hung peer instead of spinning forever.  ``wait()`` returns the result.
     Comms without a split-phase transport complete the op inside ``wait()``
     (``ready()`` is then always True, so a caller's overlap loop does
     nothing and the op runs blocking, as before)."""
 
-    def __init__(self, finish, ready=None):
+    def __init__(self, finish, ready=None, deadline: Optional[float] = None):
         self._finish = finish
         self._ready = ready
+        self.deadline = deadline
 
     def ready(self) -> bool:
-        return True if self._ready is None else bool(self._ready())
+        if self._ready is None or self._ready():
+            return True
+        return self.deadline is not None and time.monotonic() >= self.deadline
 
     def wait(self):
         f, self._finish = self._finish, None
@@ -360,9 +367,12 @@ class ShmComm(Comm):
                 raise RuntimeError(f"rank {self.rank}: expected {c} rows from {src}, got {out[src].shape[0]}")
         return out
 
-    def _finish(self, fn):
+    def _finish(self, fn, deadline: Optional[float] = None):
+        # a split-phase op waits out what is left of its deadline (the overlap
+        # loop before it already spent the rest), at least a millisecond
+        t = self.timeout_s if deadline is None else max(1e-3, deadline - time.monotonic())
         try:
-            return fn(self.timeout_s)
+            return fn(t)
         except TimeoutError as e:
             raise PeerLost(f"rank {self.rank}: {e}") from e
         except ValueError as e:
@@ -371,14 +381,16 @@ class ShmComm(Comm):
     def all_gather_i64_async(self, vec):
         v = np.ascontiguousarray(vec, dtype=np.int64).reshape(-1)
         self._x(self.c.post_gather, v.tobytes())
+        dl = time.monotonic() + self.timeout_s
         return Pending(lambda: np.stack([np.frombuffer(p, dtype=np.int64)
-                                         for p in self._finish(self.c.finish_gather)]), self.c.ready)
+                                         for p in self._finish(self.c.finish_gather, dl)]), self.c.ready, dl)
 
     def all_to_all_rows_async(self, send, recv_counts, width):
         parts = [np.ascontiguousarray(x, dtype=np.int32).reshape(-1, width).tobytes() for x in send]
         self._x(self.c.post_a2a, parts)
         counts = list(recv_counts)
-        return Pending(lambda: self._rows(self._finish(self.c.finish_a2a), counts, width), self.c.ready)
+        dl = time.monotonic() + self.timeout_s
+        return Pending(lambda: self._rows(self._finish(self.c.finish_a2a, dl), counts, width), self.c.ready, dl)
 
     def all_to_all_var(self, send, width):
         parts = [np.ascontiguousarray(x, dtype=np.int32).reshape(-1, width).tobytes() for x in send]

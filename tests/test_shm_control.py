@@ -162,6 +162,47 @@ def _gateway_worker(rank, world, port, out):
     out.put((rank, done, g.tolist()))
 
 
+def _gateway_dead_peer_worker(rank, world, port, out):
+    """Gateways on the shm control plane; the last rank dies after a few
+    ticks.  The survivors' ticks wait in the split-phase overlap loop
+    (``Gateway._overlap``: ingest while peers catch up), which must end at
+    the collective's deadline and raise PeerLost -- not spin forever."""
+    _env(rank, world, port)
+    from llm_message_queue_amd.backend.engine import BackendEngine
+    from llm_message_queue_amd.gateway.router import Gateway
+    from llm_message_queue_amd.gateway.workload import Workload
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.parallel.comm import PeerLost, ShmComm, init_from_env
+    from llm_message_queue_amd.utils.config import default_config
+    comm = init_from_env(backend="gloo", control="shm", timeout_s=3)
+    assert isinstance(comm, ShmComm)
+    cfg = default_config()
+    cfg.queue.enable_metrics = False
+    micro = LlamaConfig(vocab=256, dim=256, layers=1, heads=2, kv_heads=1, ffn=256)
+    eng = BackendEngine(micro, slots=4, max_ctx=64, token_budget=32, device="cpu", impl="ref", seed=rank)
+    gw = Gateway(cfg, engine=eng, comm=comm, use_gpu_preprocess=False, prompt_cap=8, gen_tokens=2)
+    gw.submit(Workload(seed=rank).make(8))
+    for _ in range(3):
+        gw.tick()
+    if rank == world - 1:
+        os._exit(0)                                       # dies without a goodbye
+    t0 = time.time()
+    try:
+        for _ in range(50):
+            gw.submit(Workload(seed=100 + rank).make(2))  # arrivals keep the overlap loop busy
+            gw.tick()
+        out.put((rank, "no error", 0.0))
+    except PeerLost:
+        out.put((rank, "PeerLost", time.time() - t0))
+
+
+def test_gateway_tick_with_dead_peer_raises_peer_lost():
+    res, codes = _run(_gateway_dead_peer_worker, 3, timeout=120)
+    assert len(res) == 2, codes
+    for _, what, dt in res:
+        assert what == "PeerLost" and dt < 15, res
+
+
 def test_gateway_dispatch_over_shm_control_plane():
     res, codes = _run(_gateway_worker, 2, timeout=240)
     assert len(res) == 2, codes
