@@ -286,6 +286,7 @@ def main() -> None:
                     out["accepted_by_rank"] = st.get("accepted_by_rank")
                     out["front_door"] = st.get("front_door")
                     out["missing_ranks"] = st.get("missing_ranks")
+                    out["profile_by_rank"] = st_end.get("profile_by_rank")
                 out["dispatcher"] = {"dispatch": st.get("dispatch"), "latency": st_end.get("latency"),
                                      "latency_e2e": st_end.get("latency_e2e"),
                                      "note": "latency: HTTP arrival (native ingress clock) -> GPU slot admission; "

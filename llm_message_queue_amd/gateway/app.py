@@ -30,7 +30,7 @@ from ..scheduler.resource_scheduler import ResourceScheduler
 from ..utils.logging import get_logger
 from ..utils.metrics import QueueMetrics, default_metrics
 from .ingress import MicroBatcher
-from .router import Gateway
+from .router import Gateway, StageRecorder
 
 # reference fixed estimates (api/handlers.go:729-744), used before rates exist
 _REF_WAIT_NS = {1: 1_000_000_000, 2: 5_000_000_000, 3: 15_000_000_000, 4: 30_000_000_000}
@@ -592,7 +592,11 @@ class GatewayApp:
                 "arr": gw.rec.arr.tolist(), "enq": gw.rec.enq.tolist(), "done": gw.rec_done.arr.tolist(),
                 "pending": [self.standard.size(n) for n in gw.tiers],
                 "tier_stats": [self._tier_counts(n) for n in gw.tiers],
-                "dead_letter": self.factory.dead_letter_queue.size(), "delayed": self.factory.delayed_queue.size()}
+                "dead_letter": self.factory.dead_letter_queue.size(), "delayed": self.factory.delayed_queue.size(),
+                # where this rank's serve loop spends a tick (same fields as bench.py's JSON)
+                "profile": {"ticks": int(gw.counters["ticks"] - gw._ticks0), "host_ms_per_tick": gw.host_profile(),
+                            "collective": gw.lockstep_stats(),
+                            "latency_breakdown": StageRecorder.summary(gw.rec_stage.h, gw.rec_stage.paths)}}
 
     def metrics_exposition(self) -> bytes:
         """``/metrics``: this process's registry; in a multi-GPU job every
@@ -642,6 +646,7 @@ class GatewayApp:
                           for t, n in enumerate(tiers)},
                 "dead_letter": sum(int(p.get("dead_letter", 0)) for p in parts),
                 "delayed": sum(int(p.get("delayed", 0)) for p in parts),
+                "profile_by_rank": {int(p["rank"]): p.get("profile") for p in parts},
                 "latency": rec.summary(arr, enq), "latency_e2e": rec.summary(done, done)}
 
     def reset_latency_all(self) -> None:

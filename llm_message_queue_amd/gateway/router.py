@@ -1706,11 +1706,14 @@ class Gateway:
         return n, res
 
     def reset_latency(self) -> None:
-        """Fresh latency windows: arrival -> dispatch, stages, end to end."""
+        """Fresh latency windows: arrival -> dispatch, stages, end to end, and
+        the per-tick host / collective profile."""
         self.flush_latency()
         self.rec.reset()
         self.rec_stage.reset()
         self.rec_done.reset()
+        self.host_profile(reset=True)
+        self.lockstep_stats(reset=True)
 
     def flush_latency(self) -> None:
         """Move buffered completion timestamps into the e2e histogram."""
