@@ -214,7 +214,8 @@ class Gateway:
         la = int(getattr(q, "lifo_after", 0))
         self.lifo_ns = ([la if la > 0 else int(lv.max_wait_time) for lv in levels]
                         if getattr(q, "adaptive_lifo", False) else None)
-        self.max_conc = [lv.max_concurrent for lv in levels]
+        self.max_conc = self._tier_caps([lv.max_concurrent for lv in levels],
+                                        bool(getattr(q, "priority_monotone_caps", True)))
         for n in self.tiers:                          # D1: the level queues exist
             self.qm.create_queue(n)
         # a queued message removed other than by dispatch (admin delete,
@@ -455,6 +456,20 @@ class Gateway:
         return out
 
     # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _tier_caps(caps: List[int], monotone: bool) -> List[int]:
+        """In-flight cap per tier (most urgent first; <= 0 = no cap).
+        ``monotone``: a tier's cap is at least every less urgent tier's, so a
+        cap can never make an urgent request wait while a less urgent one is
+        admitted (``queue.priority_monotone_caps``)."""
+        if not monotone:
+            return list(caps)
+        out, run = [], 0
+        for c in reversed(caps):                      # least urgent first
+            run = -1 if (c <= 0 or run < 0) else max(run, c)
+            out.append(run)
+        return out[::-1]
+
     def _budgets(self) -> List[int]:
         return [(-1 if c <= 0 else max(0, int(c - self.inflight_by_tier[i])))
                 for i, c in enumerate(self.max_conc)]
