@@ -188,6 +188,8 @@ class GatewayApp:
         if self.engine is not None:
             self._loop_thread = threading.Thread(target=self._serve_loop, name="gateway-loop", daemon=True)
             self._loop_thread.start()
+            if self.cfg.server.stall_dump_after > 0:
+                threading.Thread(target=self._stall_watchdog, name="stall-watchdog", daemon=True).start()
         else:
             if not self.lb.get_all_endpoints():
                 self.lb.add_endpoint(Endpoint(id="local-sim", url="", name="simulated LLM", type="llm",
@@ -718,6 +720,28 @@ class GatewayApp:
         if now - self._gc_freeze_at >= fi:
             gc.freeze()
             self._gc_freeze_at = now
+
+    def _stall_watchdog(self) -> None:
+        """``server.stall_dump_after``: the serve loop has completed no tick
+        for that long while requests wait -> one error log and a dump of
+        every thread's stack (faulthandler, stderr), re-armed when ticks
+        resume."""
+        import faulthandler
+        gw = self.gateway
+        limit = self.cfg.server.stall_dump_after / 1e9
+        last, since, dumped = -1, time.monotonic(), False
+        while not self._stop.wait(min(1.0, limit / 4)):
+            t = gw.counters["ticks"]
+            now = time.monotonic()
+            if t != last:
+                last, since, dumped = t, now, False
+                continue
+            waiting = gw.pending() + (gw.engine.inflight() if gw.engine is not None else 0)
+            if not dumped and waiting > 0 and now - since >= limit:
+                dumped = True
+                self.log.error("serve loop stalled: no tick while requests wait; dumping thread stacks",
+                               rank=gw.rank, stalled_s=round(now - since, 1), waiting=int(waiting), ticks=int(t))
+                faulthandler.dump_traceback(all_threads=True)
 
     def _serve_loop(self) -> None:
         import gc

@@ -63,6 +63,11 @@ class ServerConfig:
     # runs a full collection only every gc_full_interval.  0 disables.
     gc_freeze_interval: int = 1_000_000_000
     gc_full_interval: int = 600_000_000_000
+    # stall watchdog: when the serve loop completes no tick for this long
+    # while requests wait, log an error and dump every thread's Python stack
+    # to stderr once per stall (what a hung rank is doing, without a
+    # debugger).  0 disables.
+    stall_dump_after: int = 15_000_000_000
 
 
 @dataclass
@@ -354,7 +359,7 @@ _DURATION_FIELDS = {
     "max_wait_time", "monitor_interval", "cleanup_interval", "max_retention_period",
     "process_interval", "initial_backoff", "max_backoff", "check_interval", "timeout",
     "health_check_interval", "session_timeout", "heartbeat_timeout", "autoscale_cooldown",
-    "max_idle_time", "lifo_after", "idle_timeout", "gc_freeze_interval", "gc_full_interval",
+    "max_idle_time", "lifo_after", "idle_timeout", "gc_freeze_interval", "gc_full_interval", "stall_dump_after",
 }
 
 

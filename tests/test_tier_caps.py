@@ -48,3 +48,4 @@ def test_high_tier_not_held_behind_normal_by_its_cap():
         gw.ingest()
         gw.dispatch()
         assert gw.inflight_by_tier.tolist() == want, (monotone, gw.inflight_by_tier)
+
