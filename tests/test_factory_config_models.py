@@ -145,6 +145,35 @@ def test_grafana_dashboard_queries_only_exported_series():
     assert used and not missing, missing
 
 
+def test_alert_rules_query_only_exported_series_and_labels():
+    """deployments/alert_rules.yml: every llm_* series an alert evaluates is
+    one the gateway registers, with label names that series carries."""
+    import os as _os
+    import re as _re
+    import yaml as _yaml
+    from llm_message_queue_amd.utils.metrics import QueueMetrics
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    rules = _yaml.safe_load(open(_os.path.join(root, "deployments", "alert_rules.yml")))
+    exprs = [r["expr"] for g in rules["groups"] for r in g["rules"]]
+    labels = {}
+    suffix = {"counter": ("_total",), "histogram": ("_bucket", "_sum", "_count"), "gauge": ("",)}
+    m = QueueMetrics()
+    for fam in m.registry.collect():
+        for x in suffix.get(fam.type, ("",)):
+            labels[fam.name + x] = None
+    lab_of = {c._name + x: set(c._labelnames) | ({"le"} if x == "_bucket" else set())
+              for c in (m.pending, m.dispatch_latency, m.inflight, m.dead_letter, m.requests_rejected)
+              for x in ("", "_total", "_bucket")}
+    used = 0
+    for e in exprs:
+        for name, sel in _re.findall(r"\b(llm_[a-z0-9_]+)(\{[^}]*\})?", e):
+            used += 1
+            assert name in labels, name
+            for lab in _re.findall(r"(\w+)\s*=~?", sel or ""):
+                assert lab in lab_of.get(name, set()) | {"rank"}, (name, lab)
+    assert used >= 5
+
+
 REFERENCE_CONFIG = "/root/reference/configs/config.yaml"
 
 
