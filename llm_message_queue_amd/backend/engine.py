@@ -65,6 +65,15 @@ class StepResult:
     elapsed_ms: float
 
 
+class BackendHung(Exception):
+    """A forward step has not completed on the GPU within the engine's
+    ``step_timeout_s``.  Not a RuntimeError on purpose: a recoverable
+    backend error (HIP error, OOM) evacuates this GPU and keeps serving, but
+    a step that never completes leaves nothing to evacuate to -- the work
+    queued behind it waits forever -- so the process must end (the serve
+    loop treats it like ``PeerLost``) and the launcher restarts the job."""
+
+
 @dataclass
 class _Inflight:
     step: int
@@ -85,8 +94,10 @@ class BackendEngine:
                  token_budget: int = 2048, device="cuda", impl: str = "hip", seed: int = 0,
                  page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True,
                  split_qkv: bool = False, fused_mlp=None, fused_qkv=None, row_scale_norm: bool = True,
-                 fused_head=None, fused_resid=None, prune_last: bool = True):
+                 fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0):
         self.cfg = model_cfg
+        # a queued forward older than this raises BackendHung (0 = wait forever)
+        self.step_timeout_s = float(step_timeout_s)
         self.slots = slots
         self.max_ctx = max_ctx
         # every generating slot gets its decode token each step (the on-device
@@ -636,14 +647,26 @@ class BackendEngine:
         ev.record()
         return ev
 
+    def _check_hung(self, f: _Inflight) -> None:
+        if self.step_timeout_s > 0 and f.t0_ns and \
+                time.monotonic_ns() - f.t0_ns > self.step_timeout_s * 1e9:
+            raise BackendHung(f"forward step {f.step} ({f.T} tokens) incomplete "
+                              f"{(time.monotonic_ns() - f.t0_ns) / 1e9:.1f} s after launch")
+
     def _reap(self, block: bool) -> Optional[_Inflight]:
         if not self._q:
             return None
         f = self._q[0]
         if f.event is not None:
             if block:
-                f.event.synchronize()
+                if self.step_timeout_s > 0:
+                    while not f.event.query():         # bounded: a hung GPU surfaces as BackendHung
+                        self._check_hung(f)
+                        time.sleep(0.0001)
+                else:
+                    f.event.synchronize()
             elif not f.event.query():
+                self._check_hung(f)
                 return None
         self._q.popleft()
         now = time.monotonic_ns()

@@ -47,7 +47,8 @@ def _build_engine(cfg, model: str, device):
     rank = int(os.environ.get("RANK", "0"))
     page = SlotPage(f"serve{os.environ.get('TORCHELASTIC_RUN_ID', os.getpid())}", rank)
     return BackendEngine(LlamaConfig.by_name(model), slots=cfg.gpu.slots_per_gpu, max_ctx=cfg.backend.max_ctx,
-                         token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank), page
+                         token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank,
+                         step_timeout_s=cfg.backend.step_timeout / 1e9), page
 
 
 def _build_cpu_engine(cfg, sim_gpu: str = ""):

@@ -745,6 +745,7 @@ class GatewayApp:
 
     def _serve_loop(self) -> None:
         import gc
+        from ..backend.engine import BackendHung
         from ..parallel.comm import PeerLost
         gw = self.gateway
         self._bind_device()
@@ -760,11 +761,13 @@ class GatewayApp:
                 break
             try:
                 gw.tick()
-            except PeerLost as e:
-                # a peer rank died: this job cannot tick any more; leave with
-                # a failure status so the launcher restarts a fresh group
+            except (PeerLost, BackendHung) as e:
+                # a peer rank died, or this GPU stopped completing steps: this
+                # job cannot tick any more; leave with a failure status so the
+                # launcher restarts a fresh group
                 self.fatal = e
-                self.log.error("peer rank lost; stopping", error=str(e))
+                self.log.error("peer rank lost; stopping" if isinstance(e, PeerLost)
+                               else "GPU step hung; stopping", error=str(e))
                 self._stop.set()
                 break
             self._dispatch_times.append((time.monotonic(), gw.counters["dispatched"]))

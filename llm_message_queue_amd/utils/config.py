@@ -277,6 +277,10 @@ class BackendConfig:
     gen_tokens: int = 4                # decode steps per request
     dtype: str = "bf16"
     token_budget: int = 4096           # max tokens per forward step (prefill chunking)
+    # a forward still incomplete this long after launch = a hung GPU: the
+    # serve loop stops with a failure status (BackendHung) so the launcher
+    # restarts the job; 0 waits forever
+    step_timeout: int = 60 * S
 
 
 @dataclass
@@ -360,6 +364,7 @@ _DURATION_FIELDS = {
     "process_interval", "initial_backoff", "max_backoff", "check_interval", "timeout",
     "health_check_interval", "session_timeout", "heartbeat_timeout", "autoscale_cooldown",
     "max_idle_time", "lifo_after", "idle_timeout", "gc_freeze_interval", "gc_full_interval", "stall_dump_after",
+    "step_timeout",
 }
 
 

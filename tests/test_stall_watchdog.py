@@ -22,3 +22,49 @@ def test_stall_watchdog_dumps_stacks_once(capfd):
     th.join(2)
     assert len(logged) == 1 and logged[0][1]["waiting"] == 3
     assert "_stall_watchdog" in capfd.readouterr().err   # the dump names the watchdog's own frame
+
+
+def test_engine_step_timeout_raises_backend_hung():
+    """A queued forward whose completion event never fires: the engine's
+    non-blocking poll and its blocking reap both raise BackendHung once the
+    step is older than ``step_timeout_s`` instead of waiting forever."""
+    import time as _t
+    import pytest
+    from llm_message_queue_amd.backend.engine import BackendEngine, BackendHung, _Inflight
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+
+    class NeverDone:
+        def query(self):
+            return False
+
+        def synchronize(self):
+            raise AssertionError("must not block unbounded")
+
+    eng = BackendEngine(LlamaConfig.tiny(), slots=4, max_ctx=64, token_budget=64, device="cpu", impl="ref",
+                        step_timeout_s=0.05)
+    eng._q.append(_Inflight(1, NeverDone(), 8, 8, 0, [], [], _t.perf_counter(), None, _t.monotonic_ns()))
+    assert eng.poll_one() is False                 # young step: just not done yet
+    _t.sleep(0.08)
+    with pytest.raises(BackendHung):
+        eng.poll_one()
+    with pytest.raises(BackendHung):
+        eng.finish(block=True)
+
+
+def test_serve_loop_exits_on_backend_hung():
+    from llm_message_queue_amd.backend.engine import BackendEngine, BackendHung
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.utils.config import default_config
+    cfg = default_config()
+    cfg.queue.enable_metrics = False
+    eng = BackendEngine(LlamaConfig.tiny(), slots=4, max_ctx=64, token_budget=64, device="cpu", impl="ref")
+    app = GatewayApp(cfg, use_gpu=False, engine=eng, start=False)
+
+    def boom(*a, **k):
+        raise BackendHung("forward step 7 incomplete 60.0 s after launch")
+    app.gateway.tick = boom
+    app.start()
+    app._loop_thread.join(5)
+    assert isinstance(app.fatal, BackendHung) and app._stop.is_set()
+    app.stop()
