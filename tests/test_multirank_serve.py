@@ -160,6 +160,14 @@ def test_two_rank_serve_native_front_door():
         on1 = [it["message"]["id"] for it in items if it["rank"] == 1]
         st, qs = _req("GET", base + "/api/v1/queues/status")
         assert st == 200 and qs["job"]["dead_letter"] >= len(exp)
+        # every rank's serve-loop profile (host ms per tick, collective wait,
+        # stage breakdown) rides in the job stats
+        st, js = _req("GET", base + "/api/v1/queues/stats")
+        prof = js["job"]["profile_by_rank"]
+        assert sorted(int(r) for r in prof) == [0, 1], prof
+        for p_ in prof.values():
+            assert p_["ticks"] > 0 and "launch" in p_["host_ms_per_tick"] and "p99_ms" in p_["collective"]
+            assert set(p_["latency_breakdown"]) >= {"ingress", "queue", "handoff", "admitted_by_path"}
         assert _req("DELETE", base + f"/api/v1/admin/queues/dead_letter/{on1[0]}")[0] == 200
         assert _req("DELETE", base + f"/api/v1/admin/queues/dead_letter/{on1[0]}")[0] == 404
         assert _req("POST", base + f"/api/v1/admin/dead-letter/requeue/{on1[1]}")[0] == 200
