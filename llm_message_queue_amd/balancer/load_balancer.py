@@ -192,6 +192,8 @@ class LoadBalancer:
         self._cursor: Dict[str, int] = {}
         self._rand = random.Random(seed)
         self._default_probe = default_probe
+        # URL endpoints without a probe of their own: a real HTTP health check (D9)
+        self._http_probe = http_probe() if getattr(cfg, "http_health_probe", True) else None
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
         if cfg.health_check_interval > 0:
@@ -457,7 +459,8 @@ class LoadBalancer:
 
     # ------------------------------------------------------------------ health
     def check_endpoint_health(self, ep: Endpoint) -> bool:
-        probe = ep.probe or self._default_probe or (page_probe() if ep.page is not None else None)
+        probe = ep.probe or self._default_probe or (
+            page_probe() if ep.page is not None else (self._http_probe if ep.url else None))
         ok = True if probe is None else bool(probe(ep))
         with self._lock:
             ep.last_check = time.time_ns()

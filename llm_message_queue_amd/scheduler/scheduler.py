@@ -68,6 +68,10 @@ class EndpointPool:
             return len(self._parked)
 
 
+def _always_healthy(ep) -> bool:
+    return True
+
+
 def generate_endpoint_url(index: int) -> str:
     return f"http://llm-processor-{index}:8080"
 
@@ -145,6 +149,9 @@ class Scheduler:
             i = n_now + 1
             ep = Endpoint(id=f"{prefix}-{i}", url=generate_endpoint_url(i), name=f"Endpoint {i}", type="llm",
                           weight=1, max_connections=100)
+            # a placeholder replica (the reference's generated URL is never
+            # called, scheduler.go:299-301): nothing to probe over HTTP
+            ep.probe = _always_healthy
         self.lb.add_endpoint(ep)
         self.events.append({"action": "add", "endpoint": ep.id})
         return ep

@@ -215,6 +215,10 @@ class LoadBalancerConfig:
     enable_session_affinity: bool = True
     session_timeout: int = 0           # 0 = never expires (reference behaviour)
     healthy_threshold: int = 2
+    # endpoints with a URL (registered through the API) are probed with
+    # GET <url>/health every health_check_interval; the reference's check
+    # was a stub that always reported healthy (load_balancer.go:588-616, D9)
+    http_health_probe: bool = True
     rate_limiting: RateLimitConfig = field(default_factory=RateLimitConfig)
 
 

@@ -187,3 +187,42 @@ def test_gpu_pages_drive_least_connections():
     finally:
         for p in pages:
             p.close(unlink=True)
+
+
+def test_url_endpoints_get_a_real_http_probe():
+    """D9: the reference's health check always reported healthy.  An
+    endpoint registered with a URL (and no probe of its own) is probed with
+    GET <url>/health: a dead URL goes UNHEALTHY after max_failures checks, a
+    live one stays HEALTHY; the autoscaler's placeholder replicas (never
+    called, as in the reference) are not probed over HTTP."""
+    import http.server
+    import socket
+    import threading
+    from llm_message_queue_amd.scheduler.scheduler import _always_healthy
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            self.send_response(200 if self.path == "/health" else 404)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.HTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    dead_port = s.getsockname()[1]
+    s.close()                                   # nothing listens there any more
+    live = Endpoint(id="live", url=f"http://127.0.0.1:{srv.server_port}", type="llm")
+    dead = Endpoint(id="dead", url=f"http://127.0.0.1:{dead_port}", type="llm")
+    placeholder = Endpoint(id="ph", url="http://llm-processor-9:8080", type="llm")
+    placeholder.probe = _always_healthy
+    lb = lb_with("round_robin", [live, dead, placeholder], max_failures=2)
+    for _ in range(2):
+        lb.perform_health_checks()
+    assert live.status == EndpointStatus.HEALTHY
+    assert dead.status == EndpointStatus.UNHEALTHY
+    assert placeholder.status == EndpointStatus.HEALTHY
+    srv.shutdown()
+    lb.stop()
