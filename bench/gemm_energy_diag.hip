@@ -8,6 +8,8 @@
 //      bytes -- what a 128 x 128 wave tile (4 waves) would read per MFMA
 //   6  no fragment reads in the loop (MFMA + staging DMA only)
 //   7  no staging DMA in the loop (MFMA + LDS fragment reads only)
+//   8 / 9  2 / 7 with entry and exit clock stamps: the in-kernel shader
+//      clock, unprofiled
 //
 // If 5 or 6 run much faster, LDS read traffic (its issue time or its energy
 // under the power cap) limits the kernel and a bigger wave tile pays; if only
@@ -52,7 +54,8 @@ __global__ void fill_bf16(uint16_t* p, size_t n, uint32_t seed, float scale) {
 }
 
 template <int SCHED>
-static void launch(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K) {
+static void launch(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K,
+                   uint64_t* dbg = nullptr) {
   static bool attr = false;
   if (!attr) {
     CK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<GM_EPI_SWIGLU, true, SCHED>,
@@ -62,7 +65,7 @@ static void launch(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int
   const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
   hipLaunchKernelGGL((gemm_bf16_kernel<GM_EPI_SWIGLU, true, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, 0,
                      a, w, c, M, N, K, GM_GROUP_M, nullptr, GmRope{}, GmSplit{0, nullptr, nullptr},
-                     GmArgmax{nullptr, nullptr});
+                     GmArgmax{reinterpret_cast<float*>(dbg), nullptr});
 }
 
 int main(int argc, char** argv) {
@@ -129,6 +132,42 @@ int main(int argc, char** argv) {
     const float med = t[v][t[v].size() / 2];
     printf("{\"sched\": %d, \"M\": %d, \"N\": %d, \"K\": %d, \"ms_median\": %.4f, \"ms_min\": %.4f, \"tflops\": %.1f}\n",
            scheds[v], M, N, K, med, t[v][0], flop / med / 1e9);
+  }
+  // In-kernel clock, unprofiled: the production schedule (8) and the
+  // no-DMA build (9) with entry / exit stamps, each after 1 s of its own
+  // back-to-back launches; median over the last launch's blocks.
+  const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  uint64_t* dbg;
+  CK(hipMalloc(&dbg, (size_t)tiles * 4 * sizeof(uint64_t)));
+  for (int sv : {8, 9}) {
+    auto go = [&]() { if (sv == 8) launch<8>(a, w, c, M, N, K, dbg); else launch<9>(a, w, c, M, N, K, dbg); };
+    CK(hipEventRecord(e0));
+    int n = 0;
+    for (;; ++n) {
+      go();
+      if (n % 50 == 49) {
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms > 1000.f) break;
+      }
+    }
+    CK(hipMemset(dbg, 0, (size_t)tiles * 4 * sizeof(uint64_t)));
+    go();
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> h((size_t)tiles * 4);
+    CK(hipMemcpy(h.data(), dbg, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    std::vector<double> ghz;
+    for (int b = 0; b < tiles; ++b) {
+      const double dt = (double)(h[b * 4 + 1] - h[b * 4 + 0]), dr = (double)(h[b * 4 + 3] - h[b * 4 + 2]);
+      if (dr > 0) ghz.push_back(dt / dr * 0.1);             // memrealtime ticks at 100 MHz
+    }
+    std::sort(ghz.begin(), ghz.end());
+    if (!ghz.empty())
+      printf("{\"sched\": %d, \"M\": %d, \"N\": %d, \"K\": %d, \"clock_ghz_median\": %.3f, \"clock_ghz_p10\": %.3f, "
+             "\"clock_ghz_p90\": %.3f, \"blocks\": %zu, \"warm_launches\": %d}\n",
+             sv, M, N, K, ghz[ghz.size() / 2], ghz[ghz.size() / 10], ghz[ghz.size() * 9 / 10], ghz.size(), n + 1);
   }
   return 0;
 }

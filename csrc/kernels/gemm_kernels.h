@@ -176,6 +176,15 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // SCHED 8 / 9 (diagnostics): shader-clock and 100 MHz reference stamps at
+  // entry and exit, written by thread 0 to am.pv as 4 x u64 per block --
+  // the in-kernel clock = d(memtime) / d(memrealtime) x 100 MHz, unprofiled
+  // (MI355X_MICROARCH.md 'DVFS give-back' item 6)
+  uint64_t st_t0 = 0, st_r0 = 0;
+  if constexpr (SCHED >= 8) {
+    st_t0 = __builtin_amdgcn_s_memtime();
+    st_r0 = __builtin_amdgcn_s_memrealtime();
+  }
   const int wr = w >> 2, wc = w & 3;
 
   // ---- staging sources: half h, instruction i -> LDS local row lr = i*64 + w*8 + lane/8
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     GM_VMCNT(6);
     GM_BARRIER();
     GM_READ_B0_INTO(0, bfr[0]);
-    if constexpr (SCHED >= 5) {                    // diagnostics: every fragment register defined
+    if constexpr (SCHED >= 5 && SCHED <= 7) {      // diagnostics: every fragment register defined
       GM_READ_A(0, 0);
       GM_READ_B(0, 1);
       GM_READ_B0_INTO(1, b0y);
@@ -332,7 +341,9 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     // reads of phases 3 / 7 (one third fewer LDS read bytes, what a 128x128
     // wave tile would read), 6 skips every fragment read of the loop, 7 skips
     // every staging DMA of the loop (no L2 / HBM traffic in steady state).
-    constexpr bool kRdA = SCHED != 6, kRdA2 = SCHED != 5 && SCHED != 6, kRdB = SCHED != 6, kDma = SCHED != 7;
+    // SCHED 8 / 9: production / no-DMA with in-kernel clock stamps (below).
+    constexpr bool kRdA = SCHED != 6, kRdA2 = SCHED != 5 && SCHED != 6, kRdB = SCHED != 6;
+    constexpr bool kDma = SCHED != 7 && SCHED != 9;
 #define GM_D_READ_A(C, B, H) do { if constexpr (C) GM_READ_A(B, H); } while (0)
 #define GM_D_READ_B(B, H) do { if constexpr (kRdB) GM_READ_B(B, H); } while (0)
 #define GM_D_READ_B0(B, D) do { if constexpr (kRdB) GM_READ_B0_INTO(B, D); } while (0)
@@ -756,6 +767,16 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
           *reinterpret_cast<gm_u32x4*>(dst + 8 * cb) = *reinterpret_cast<const gm_u32x4*>(at(r, hh * 128 + 8 * cb));
         }
       }
+    }
+  }
+  if constexpr (SCHED >= 8) {
+    const uint64_t st_t1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && am.pv != nullptr) {
+      uint64_t* dbg = reinterpret_cast<uint64_t*>(am.pv) + (size_t)blockIdx.x * 4;
+      dbg[0] = st_t0;
+      dbg[1] = st_t1;
+      dbg[2] = st_r0;
+      dbg[3] = st_r1;
     }
   }
 }
