@@ -152,7 +152,7 @@ def main() -> None:
     procs, urls = [], []
     slog = open(a.server_log, "w") if a.server_log else subprocess.DEVNULL
     api_url = ""
-    env = dict(os.environ, PYTHONUNBUFFERED="1", LLMQ_LOGGING__LEVEL="warning",
+    env = dict(os.environ, PYTHONUNBUFFERED="1", LLMQ_LOGGING__LEVEL="warning", LLMQ_SERVER__MODE="release",
                LLMQ_QUEUE__WORKER__MAX_CONCURRENT="512", LLMQ_QUEUE__WORKER__MAX_BATCH_SIZE="256",
                LLMQ_QUEUE__WORKER__PROCESS_INTERVAL="5ms")
     gpu = [] if a.gpu else ["--no-gpu"]

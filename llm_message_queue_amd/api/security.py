@@ -33,6 +33,10 @@ def guard_from_config(cfg) -> Optional[Any]:
         rates = dict(global_rps=rl.global_.requests_per_second, global_burst=float(rl.global_.burst_size),
                      ip_rps=rl.per_ip.requests_per_second, ip_burst=float(rl.per_ip.burst_size),
                      user_rps=rl.per_user.requests_per_second, user_burst=float(rl.per_user.burst_size))
+    if az.enabled and az.policy != "rbac":
+        # the reference documents role-based access (docs/configuration.md:
+        # 760-828 there); RBAC is the policy the native guard implements
+        raise ValueError(f"security.authorization.policy {az.policy!r}: only 'rbac' is implemented")
     if auth.method == "none" and not az.enabled and not any(v > 0 for k, v in rates.items() if k.endswith("rps")):
         return None
     # /health and /metrics stay public and unthrottled (Guard.permission_for == "")

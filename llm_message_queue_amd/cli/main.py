@@ -46,9 +46,30 @@ def _build_engine(cfg, model: str, device):
     from ..models.llama_stub import LlamaConfig
     rank = int(os.environ.get("RANK", "0"))
     page = SlotPage(f"serve{os.environ.get('TORCHELASTIC_RUN_ID', os.getpid())}", rank)
-    return BackendEngine(LlamaConfig.by_name(model), slots=cfg.gpu.slots_per_gpu, max_ctx=cfg.backend.max_ctx,
+    mcfg = LlamaConfig.by_name(model)
+    slots = fit_slots(mcfg, cfg.gpu.slots_per_gpu, cfg.backend.max_ctx, cfg.gpu.hbm_reserve_gb,
+                      torch.cuda.get_device_properties(device).total_memory)
+    return BackendEngine(mcfg, slots=slots, max_ctx=cfg.backend.max_ctx,
                          token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank,
                          step_timeout_s=cfg.backend.step_timeout / 1e9), page
+
+
+def fit_slots(mcfg, slots: int, max_ctx: int, reserve_gb: float, total_bytes: int) -> int:
+    """``gpu.hbm_reserve_gb``: batch slots whose KV cache (slots x max_ctx x
+    K/V bytes per token) fits next to the bf16 weights with that much HBM
+    left free; fewer than configured -> capped, with a warning."""
+    per_slot = max_ctx * mcfg.layers * 2 * mcfg.kv_heads * mcfg.head_dim * 2
+    room = total_bytes - int(reserve_gb * (1 << 30)) - mcfg.param_count() * 2
+    fit = max(0, room // per_slot) if per_slot > 0 else slots
+    if fit < slots:
+        from ..utils.logging import get_logger
+        get_logger("serve").warning("gpu.slots_per_gpu capped to fit HBM", configured=slots, fitted=int(fit),
+                    hbm_gib=round(total_bytes / (1 << 30), 1), reserve_gib=reserve_gb,
+                    kv_gib_per_slot=round(per_slot / (1 << 30), 4))
+        if fit < 1:
+            raise SystemExit("gpu.hbm_reserve_gb leaves no HBM for the KV cache")
+        return int(fit)
+    return slots
 
 
 def _build_cpu_engine(cfg, sim_gpu: str = ""):
@@ -137,7 +158,9 @@ def cmd_serve(a, role: str = "serve") -> int:
     use_gpu = torch.cuda.is_available() and not a.no_gpu and not cpu_ranks
     comm = None
     if use_gpu:
-        comm = init_from_env(control=cfg.gpu.control_plane)
+        from ..parallel.comm import set_device_list
+        set_device_list(cfg.gpu.devices)                    # gpu.devices (empty: every visible GPU)
+        comm = init_from_env(backend=cfg.gpu.comm_backend, control=cfg.gpu.control_plane)
     elif cpu_ranks and world > 1:
         # CPU rehearsal of the multi-GPU job: gloo data plane, the same
         # control plane, tiny reference-op engines (tests / CI)
@@ -220,7 +243,11 @@ def cmd_serve(a, role: str = "serve") -> int:
             # the public port belongs to the C++ front door; the API server
             # listens on loopback behind it (reverse-proxied routes)
             api_host, api_port = "127.0.0.1", _free_port()
-        server = uvicorn.Server(uvicorn.Config(app, host=api_host, port=api_port, log_level="warning"))
+        # server.mode (gin's debug / release in the reference): debug logs
+        # every request the API server answers, release only warnings
+        debug = cfg.server.mode == "debug"
+        server = uvicorn.Server(uvicorn.Config(app, host=api_host, port=api_port,
+                                               log_level="info" if debug else "warning", access_log=debug))
         t = threading.Thread(target=server.run, daemon=True)
         t.start()
         port = api_port

@@ -229,7 +229,7 @@ def make_store(cfg) -> Optional[PersistenceStore]:
     if b == "redis":
         from .resp import RespClient
         r = cfg.database.redis
-        return RedisPersistenceStore(RespClient(r.addr, r.password, r.db), "conversation:",
+        return RedisPersistenceStore(RespClient(r.addr, r.password, r.db, pool_size=r.pool_size), "conversation:",
                                      cfg.queue.max_retention_period)
     if b == "postgres":
         return PostgresPersistenceStore(postgres_dsn(cfg))

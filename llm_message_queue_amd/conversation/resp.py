@@ -69,53 +69,90 @@ class _Reader:
         raise RedisError(f"bad RESP type {t!r}")
 
 
-class RespClient:
-    def __init__(self, addr: str = "localhost:6379", password: str = "", db: int = 0, timeout: float = 5.0):
-        host, _, port = addr.rpartition(":")
-        self.host, self.port = host or "localhost", int(port or 6379)
-        self.password, self.db, self.timeout = password, db, timeout
-        self._lock = threading.Lock()
-        self._sock: Optional[socket.socket] = None
-        self._reader: Optional[_Reader] = None
+class _Conn:
+    """One RESP connection of a ``RespClient`` pool (connected lazily)."""
 
-    def _connect(self):
-        s = socket.create_connection((self.host, self.port), timeout=self.timeout)
-        self._sock, self._reader = s, _Reader(s)
-        if self.password:
-            self._call_locked("AUTH", self.password)
-        if self.db:
-            self._call_locked("SELECT", self.db)
+    def __init__(self, owner: "RespClient"):
+        self.o = owner
+        self.sock: Optional[socket.socket] = None
+        self.reader: Optional[_Reader] = None
 
-    def _call_locked(self, *args) -> Reply:
-        self._sock.sendall(_encode(args))
-        r = self._reader.reply()
+    def connect(self):
+        o = self.o
+        s = socket.create_connection((o.host, o.port), timeout=o.timeout)
+        self.sock, self.reader = s, _Reader(s)
+        if o.password:
+            self.call_once("AUTH", o.password)
+        if o.db:
+            self.call_once("SELECT", o.db)
+
+    def call_once(self, *args) -> Reply:
+        self.sock.sendall(_encode(args))
+        r = self.reader.reply()
         if isinstance(r, RedisError):
             raise r
         return r
 
-    def call(self, *args) -> Reply:
-        with self._lock:
-            for attempt in (0, 1):
-                try:
-                    if self._sock is None:
-                        self._connect()
-                    return self._call_locked(*args)
-                except (ConnectionError, OSError):
-                    self.close_locked()
-                    if attempt:
-                        raise
-
-    def close_locked(self):
-        if self._sock is not None:
+    def close(self):
+        if self.sock is not None:
             try:
-                self._sock.close()
+                self.sock.close()
             except OSError:
                 pass
-        self._sock = self._reader = None
+        self.sock = self.reader = None
+
+
+class RespClient:
+    """Thread-safe RESP client over a pool of up to ``pool_size`` connections
+    (``database.redis.pool_size``, the go-redis pool option the reference
+    sets): each call borrows one, so concurrent callers -- the state
+    manager's write-behind thread, API readers -- do not queue behind one
+    socket.  Connections open on first use; the most recently returned is
+    reused first, so the pool only grows to the concurrency it sees."""
+
+    def __init__(self, addr: str = "localhost:6379", password: str = "", db: int = 0, timeout: float = 5.0,
+                 pool_size: int = 1):
+        import queue
+        host, _, port = addr.rpartition(":")
+        self.host, self.port = host or "localhost", int(port or 6379)
+        self.password, self.db, self.timeout = password, db, timeout
+        self.pool_size = max(1, int(pool_size))
+        self._conns = [_Conn(self) for _ in range(self.pool_size)]
+        self._free: "queue.LifoQueue[_Conn]" = queue.LifoQueue()
+        for c in reversed(self._conns):
+            self._free.put(c)
+
+    def call(self, *args) -> Reply:
+        c = self._free.get()
+        try:
+            for attempt in (0, 1):
+                try:
+                    if c.sock is None:
+                        c.connect()
+                    return c.call_once(*args)
+                except (ConnectionError, OSError):
+                    c.close()
+                    if attempt:
+                        raise
+        finally:
+            self._free.put(c)
+
+    def connections(self) -> int:
+        """Pool connections currently open."""
+        return sum(c.sock is not None for c in self._conns)
 
     def close(self):
-        with self._lock:
-            self.close_locked()
+        """Close every idle connection (a busy one closes when its call
+        returns it and the next call reconnects)."""
+        held = []
+        while True:
+            try:
+                held.append(self._free.get_nowait())
+            except Exception:                 # queue.Empty
+                break
+        for c in held:
+            c.close()
+            self._free.put(c)
 
     # convenience wrappers
     def ping(self) -> bool:

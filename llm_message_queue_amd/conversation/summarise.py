@@ -17,13 +17,14 @@ from ..preprocess import oracle
 
 
 class SummaryEngine:
-    def __init__(self, cfg=None, *, device: Optional[str] = None, k: int = 8, alpha: float = 0.8):
+    def __init__(self, cfg=None, *, device: Optional[str] = None, k: int = 8, alpha: float = 0.8, dim: int = 256):
         import torch
         from ..utils.config import PreprocessorConfig
         self.torch = torch
         self.cfg = cfg or PreprocessorConfig()
         self.k = k
         self.alpha = alpha
+        self.dim = int(dim)                 # conversation.summary_dim (the kernels are built for 256)
         if device is None:
             device = "cuda" if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -40,7 +41,7 @@ class SummaryEngine:
             from ..ops.summarise import Summariser
             from ..ops.text import TextPipeline
             self._pipe = TextPipeline(self.cfg, device=str(self.device))
-            self._sm = Summariser(dim=256, hidden=self.cfg.hidden_dim, alpha=self.alpha, device=str(self.device))
+            self._sm = Summariser(dim=self.dim, hidden=self.cfg.hidden_dim, alpha=self.alpha, device=str(self.device))
         return self._pipe, self._sm
 
     # --------------------------------------------------------------- CPU reference
@@ -51,7 +52,7 @@ class SummaryEngine:
             w = ClassifierWeights(self.cfg.vocab_buckets, self.cfg.embed_dim, self.cfg.hidden_dim, self.cfg.seed,
                                   device="cpu")
             g = torch.Generator(device="cpu").manual_seed(4321)
-            Pt = (torch.randn(256, self.cfg.hidden_dim, generator=g) / self.cfg.hidden_dim ** 0.5).to(torch.bfloat16)
+            Pt = (torch.randn(self.dim, self.cfg.hidden_dim, generator=g) / self.cfg.hidden_dim ** 0.5).to(torch.bfloat16)
             self._cpu_w = (w, Pt)
         return self._cpu_w
 

@@ -123,7 +123,8 @@ class GatewayApp:
         if cfg.conversation.summarise_on_evict:
             from ..conversation.summarise import SummaryEngine
             summary = SummaryEngine(cfg.preprocessor, device="cuda" if gpu else "cpu",
-                                    k=cfg.conversation.salient_tokens, alpha=cfg.conversation.summary_alpha)
+                                    k=cfg.conversation.salient_tokens, alpha=cfg.conversation.summary_alpha,
+                                    dim=cfg.conversation.summary_dim)
         self.state = StateManager.from_config(cfg, persistence=store, summary_engine=summary)
         self.messages = MessageStore()
         self.engine = engine

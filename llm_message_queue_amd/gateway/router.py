@@ -234,6 +234,9 @@ class Gateway:
         self.resources = None          # optional ResourceScheduler: per-GPU usage from the load exchange
         self._parked_eps: Dict[str, object] = {}   # GPU endpoints the resource scheduler parked
         self._res_next_ns = 0
+        # ResourceScheduler cadence: heartbeats / loads / backlog from the
+        # tick's load vectors at most this often (gpu.rebalance_interval_ms)
+        self.res_interval_ns = int(max(1, getattr(cfg.gpu, "rebalance_interval_ms", 100)) * 1_000_000)
         self.hbm_fn = None             # optional () -> (used MiB, total MiB) of this rank's GPU
         self._hbm_cache = (0, 0, 0)    # (used, total, refreshed at ns)
         self._rt_ewma_us = 0.0         # service time (admit -> done) EWMA of this GPU
@@ -854,7 +857,7 @@ class Gateway:
 
     def _observe_loads(self, loads: np.ndarray) -> None:
         """Per-tick bookkeeping on the gathered load matrix: peers' health and
-        stop flags, and (at most every 100 ms) the ResourceScheduler's
+        stop flags, and (at most every gpu.rebalance_interval_ms) the ResourceScheduler's
         per-GPU usage -- in-flight slots, HBM, KV tokens -- so
         ``/api/v1/resources/stats`` tracks real GPU use on every rank."""
         W = self.world
@@ -871,7 +874,7 @@ class Gateway:
         now = time.monotonic_ns()
         if rs is None or now < self._res_next_ns:
             return
-        self._res_next_ns = now + 100_000_000
+        self._res_next_ns = now + self.res_interval_ns
         # job-wide backlog: queued requests beyond the free slots of the GPUs
         # in placement -- the autoscaler's "pending demand"
         el = planner.eligible(loads)

@@ -511,15 +511,27 @@ class FakeComm(Comm):
         self._wait()
 
 
+_DEVICES: List[int] = []
+
+
+def set_device_list(devices: Sequence[int]) -> None:
+    """``gpu.devices``: the HIP devices this node's ranks use, in local-rank
+    order (empty = every visible device)."""
+    _DEVICES[:] = [int(d) for d in devices]
+
+
 def local_device_index() -> int:
     """HIP device of this rank: ``LOCAL_RANK`` on a node with one GPU per rank
-    (the production layout).  When more ranks than GPUs share the node
+    (the production layout), or the LOCAL_RANK-th entry of ``gpu.devices``
+    when that list is set.  When more ranks than GPUs share the node
     (rehearsing a multi-rank job on a 1-GPU box) ranks wrap round the devices;
     ``init_from_env`` then keeps RCCL out of it (RCCL refuses two ranks on one
     device) and runs every group on gloo."""
     import os
     import torch
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if _DEVICES:
+        return _DEVICES[local % len(_DEVICES)]
     n = torch.cuda.device_count() if torch.cuda.is_available() else 0
     return local % n if n > 0 else local
 
@@ -528,6 +540,8 @@ def gpus_oversubscribed() -> bool:
     import os
     import torch
     n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if _DEVICES:
+        n = min(n, len(set(_DEVICES)))
     return 0 < n < int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
 
 

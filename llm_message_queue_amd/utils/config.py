@@ -471,6 +471,13 @@ def _apply_env(cfg: Config, environ: Dict[str, str], prefix: str = "LLMQ_") -> N
 
 
 def validate(cfg: Config) -> Config:
+    if cfg.conversation.summary_dim != 256:
+        raise ConfigError("conversation.summary_dim must be 256: the context_summarise kernels project the "
+                          "classifier's hidden layer to a 256-wide summary")
+    if cfg.gpu.hbm_reserve_gb < 0 or cfg.gpu.rebalance_interval_ms <= 0:
+        raise ConfigError("gpu.hbm_reserve_gb must be >= 0 and gpu.rebalance_interval_ms > 0")
+    if cfg.gpu.comm_backend not in ("nccl", "gloo"):
+        raise ConfigError("gpu.comm_backend must be nccl (RCCL) or gloo")
     q = cfg.queue
     for name in ("monitor_interval", "cleanup_interval"):
         if getattr(q, name) <= 0:

@@ -256,3 +256,37 @@ def test_resp_client_ttl_and_sets():
         assert r.get("k") is None
     finally:
         srv.close()
+
+
+def test_resp_client_pool_serves_concurrent_callers():
+    """database.redis.pool_size: callers borrow pooled connections -- 8
+    threads over a 4-connection pool all get their own writes back and the
+    pool never opens more than 4 sockets; a single caller uses one."""
+    import threading
+    from llm_message_queue_amd.conversation.resp import MiniRedis, RespClient
+    srv = MiniRedis()
+    try:
+        one = RespClient(srv.addr, pool_size=4)
+        for i in range(20):
+            one.set(f"k{i}", b"v")
+        assert one.connections() == 1
+        errs = []
+
+        def worker(t):
+            try:
+                for i in range(50):
+                    one.set(f"t{t}-{i}", str(i).encode())
+                    assert one.get(f"t{t}-{i}") == str(i).encode()
+            except Exception as e:                     # noqa: BLE001
+                errs.append(e)
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(30)
+        assert not errs, errs
+        assert 1 <= one.connections() <= 4
+        one.close()
+        assert one.connections() == 0 and one.get("k3") == b"v"     # reconnects on demand
+    finally:
+        srv.close()

@@ -191,3 +191,28 @@ def test_reference_config_file_loads_unchanged():
     assert c.queue.levels[0].max_wait_time == 1_000_000_000              # "1s" -> ns
     assert c.loadbalancer.algorithm == "weighted_round_robin"
     assert c.database.redis.addr and c.database.postgres.dbname
+
+
+def test_every_config_key_is_read_somewhere():
+    """The reference shipped keys its code never read (per-level
+    max_wait_time / max_concurrent, health_check_interval, ...).  Every field
+    of our config dataclasses must be read outside utils/config.py."""
+    import dataclasses
+    import os as _os
+    import re as _re
+    import llm_message_queue_amd.utils.config as C
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    src = []
+    for dp, _dn, fn in _os.walk(_os.path.join(root, "llm_message_queue_amd")):
+        for f in fn:
+            if f.endswith(".py") and not (dp.endswith("utils") and f == "config.py"):
+                src.append(open(_os.path.join(dp, f)).read())
+    src.append(open(_os.path.join(root, "bench.py")).read())
+    text = "\n".join(src)
+    dead = []
+    for obj in vars(C).values():
+        if dataclasses.is_dataclass(obj) and isinstance(obj, type):
+            for f in dataclasses.fields(obj):
+                if not _re.search(r"(\.|\")" + f.name + r"\b", text):
+                    dead.append(f"{obj.__name__}.{f.name}")
+    assert not dead, dead
