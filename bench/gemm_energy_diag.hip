@@ -10,6 +10,8 @@
 //   7  no staging DMA in the loop (MFMA + LDS fragment reads only)
 //   8 / 9  2 / 7 with entry and exit clock stamps: the in-kernel shader
 //      clock, unprofiled
+//   10 every block stages tile (0, 0)'s panels: staging served from L2
+//      (what better L2 reuse could be worth at most)
 //
 // If 5 or 6 run much faster, LDS read traffic (its issue time or its energy
 // under the power cap) limits the kernel and a bigger wave tile pays; if only
@@ -87,13 +89,15 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, 0, w, (size_t)N * K, 2u, 0.02f);
   CK(hipDeviceSynchronize());
 
-  const int scheds[4] = {2, 5, 6, 7};
+  const int NV = 5;
+  const int scheds[NV] = {2, 5, 6, 7, 10};
   auto run = [&](int s) {
     switch (s) {
       case 2: launch<2>(a, w, c, M, N, K); break;
       case 5: launch<5>(a, w, c, M, N, K); break;
       case 6: launch<6>(a, w, c, M, N, K); break;
-      default: launch<7>(a, w, c, M, N, K); break;
+      case 7: launch<7>(a, w, c, M, N, K); break;
+      default: launch<10>(a, w, c, M, N, K); break;
     }
   };
   // ~2 s of back-to-back launches first so the clock has settled (DVFS give-back)
@@ -114,9 +118,9 @@ int main(int argc, char** argv) {
     }
   }
   CK(hipDeviceSynchronize());
-  std::vector<std::vector<float>> t(4);
+  std::vector<std::vector<float>> t(NV);
   for (int r = 0; r < rounds; ++r)
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < NV; ++v) {
       run(scheds[v]);
       CK(hipEventRecord(e0));
       for (int i = 0; i < iters; ++i) run(scheds[v]);
@@ -127,7 +131,7 @@ int main(int argc, char** argv) {
       t[v].push_back(ms / iters);
     }
   const double flop = 2.0 * M * (double)N * K;
-  for (int v = 0; v < 4; ++v) {
+  for (int v = 0; v < NV; ++v) {
     std::sort(t[v].begin(), t[v].end());
     const float med = t[v][t[v].size() / 2];
     printf("{\"sched\": %d, \"M\": %d, \"N\": %d, \"K\": %d, \"ms_median\": %.4f, \"ms_min\": %.4f, \"tflops\": %.1f}\n",

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   // the in-kernel clock = d(memtime) / d(memrealtime) x 100 MHz, unprofiled
   // (MI355X_MICROARCH.md 'DVFS give-back' item 6)
   uint64_t st_t0 = 0, st_r0 = 0;
-  if constexpr (SCHED >= 8) {
+  if constexpr (SCHED == 8 || SCHED == 9) {
     st_t0 = __builtin_amdgcn_s_memtime();
     st_r0 = __builtin_amdgcn_s_memrealtime();
   }
@@ -193,14 +193,17 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, M * K * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, N * K * 2, 0x00020000);
   uint32_t va[2][2], vb[2][2];                     // byte offsets (row, chunk) of K-tile 0
+  // SCHED 10 (diagnostic, wrong numerics): every block stages the panels of
+  // tile (0, 0), so nearly every staging read hits the XCD's L2
+  const int ltm = SCHED == 10 ? 0 : tm, ltn = SCHED == 10 ? 0 : tn;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      int row = tm * GM_BM + i * 128 + h * 64 + srow;
+      int row = ltm * GM_BM + i * 128 + h * 64 + srow;
       row = row < M ? row : M - 1;
       va[h][i] = (uint32_t)row * (uint32_t)K * 2u + (uint32_t)schunk * 16u;
-      const int col = tn * GM_BN + (2 * i + (w >> 2)) * 64 + h * 32 + (w & 3) * 8 + (lane >> 3);
+      const int col = ltn * GM_BN + (2 * i + (w >> 2)) * 64 + h * 32 + (w & 3) * 8 + (lane >> 3);
       vb[h][i] = (uint32_t)col * (uint32_t)K * 2u + (uint32_t)schunk * 16u;
     }
   }
@@ -769,7 +772,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
       }
     }
   }
-  if constexpr (SCHED >= 8) {
+  if constexpr (SCHED == 8 || SCHED == 9) {
     const uint64_t st_t1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
     if (tid == 0 && am.pv != nullptr) {
       uint64_t* dbg = reinterpret_cast<uint64_t*>(am.pv) + (size_t)blockIdx.x * 4;
