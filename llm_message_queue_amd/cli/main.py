@@ -41,6 +41,7 @@ def _load_cfg(path):
 
 
 def _build_engine(cfg, model: str, device):
+    import torch
     from ..backend.engine import BackendEngine
     from ..backend.slot_page import SlotPage
     from ..models.llama_stub import LlamaConfig

@@ -216,3 +216,28 @@ def test_every_config_key_is_read_somewhere():
                 if not _re.search(r"(\.|\")" + f.name + r"\b", text):
                     dead.append(f"{obj.__name__}.{f.name}")
     assert not dead, dead
+
+
+def test_serve_engine_builder_applies_gpu_config(monkeypatch):
+    """cli serve's GPU engine builder (not reachable without a GPU otherwise):
+    slots capped by gpu.hbm_reserve_gb, backend.step_timeout passed through."""
+    import types
+    import torch
+    import llm_message_queue_amd.backend.engine as E
+    from llm_message_queue_amd.cli import main as M
+    got = {}
+
+    class FakeEngine:
+        def __init__(self, mcfg, **kw):
+            got.update(kw)
+
+    monkeypatch.setattr(E, "BackendEngine", FakeEngine)
+    monkeypatch.setattr(torch.cuda, "get_device_properties",
+                        lambda dev: types.SimpleNamespace(total_memory=64 << 30))
+    cfg = default_config()
+    cfg.gpu.slots_per_gpu = 4096
+    cfg.gpu.hbm_reserve_gb = 16
+    cfg.backend.step_timeout = 5_000_000_000
+    M._build_engine(cfg, "llama3-8b", "cpu")
+    # 64 GiB - 16 GiB reserve - ~15 GiB of weights, 64 MiB of KV per 512-token slot
+    assert 400 < got["slots"] < 600 and got["step_timeout_s"] == 5.0
