@@ -112,6 +112,9 @@ class GatewayApp:
         # handler that records metadata["analysis"] for the other paths
         self.preprocessor.record_analysis = bool(cfg.queue.enable_metrics) and role in ("rank", "dispatcher")
         self.factory = QueueFactory(cfg.queue, metrics=self.metrics)
+        if getattr(self.metrics, "registry", None) is not None:
+            # read at scrape time, so every path that changes the DLQ counts
+            self.metrics.dead_letter.labels("factory").set_function(self.factory.dead_letter_queue.size)
         self.standard = self.factory.create_queue_manager("standard", QueueType.STANDARD)
         self.factory.create_queue_manager("delayed", QueueType.DELAYED)
         self.factory.create_queue_manager("dead_letter", QueueType.DEAD_LETTER)
@@ -769,6 +772,16 @@ class GatewayApp:
                 self.fatal = e
                 self.log.error("peer rank lost; stopping" if isinstance(e, PeerLost)
                                else "GPU step hung; stopping", error=str(e))
+                self._stop.set()
+                break
+            except Exception as e:                    # noqa: BLE001 -- a bug must not leave a zombie
+                # anything else is a defect: without this the dispatcher thread
+                # would die silently and the API keep accepting requests that
+                # nothing dispatches; fail the process so it is restarted
+                import traceback
+                self.fatal = e
+                self.log.error("serve loop failed; stopping", error=repr(e),
+                               traceback=traceback.format_exc(limit=20))
                 self._stop.set()
                 break
             self._dispatch_times.append((time.monotonic(), gw.counters["dispatched"]))

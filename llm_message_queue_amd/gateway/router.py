@@ -373,9 +373,23 @@ class Gateway:
         if not batch:
             return out
         t0 = time.perf_counter_ns()
+        g0 = self.pre.stats.get("gpu_batches", 0)
         self.pre.process_batch(batch, use_gpu=self.use_gpu_pre, prompt_cap=self.prompt_cap)
-        self.ingest_ns[0] += time.perf_counter_ns() - t0
+        dt = time.perf_counter_ns() - t0
+        self.ingest_ns[0] += dt
+        self._observe_preprocess(g0, dt, "sync_batch")
         return out + self._enqueue(batch)
+
+    def _observe_preprocess(self, gpu_batches_before: int, host_ns: int, stage: str) -> None:
+        """llm_preprocess_kernel_seconds{stage}: ``gpu_batch`` = a GPU batch
+        from launch to its results on the host; ``stage`` = the host time of
+        the call (a whole synchronous batch, or the decode of a finished one)."""
+        if self.metrics is None:
+            return
+        ps = self.metrics.preprocess_seconds
+        if self.pre.stats.get("gpu_batches", 0) != gpu_batches_before:
+            ps.labels("gpu_batch").observe(self.pre.stats["last_gpu_ms"] / 1e3)
+        ps.labels(stage).observe(host_ns / 1e9)
 
     def ingest_async(self) -> bool:
         """Overlapped ingest (GPU preprocess only): enqueue the outstanding
@@ -428,8 +442,11 @@ class Gateway:
             return []
         self._pre_pending = None
         t0 = time.perf_counter_ns()
+        g0 = self.pre.stats.get("gpu_batches", 0)
         self.pre.end_batch(tok)
-        self.ingest_ns[0] += time.perf_counter_ns() - t0
+        dt = time.perf_counter_ns() - t0
+        self.ingest_ns[0] += dt
+        self._observe_preprocess(g0, dt, "host_finish")
         return self._enqueue(tok["msgs"])
 
     def _enqueue(self, batch) -> List[Tuple[Message, Optional[QueueError]]]:

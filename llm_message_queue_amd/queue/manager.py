@@ -181,7 +181,19 @@ class QueueManager:
             p = priority_name(m.priority)
             self.metrics.pending.labels(self.name, queue_name, p).dec()
             self.metrics.processing.labels(self.name, queue_name, p).inc()
+            self._observe_wait([m])
         return m
+
+    def _observe_wait(self, msgs) -> None:
+        """``llm_queue_messages_wait_time_seconds``: enqueue -> taken off the
+        queue, per (manager, queue, priority) -- the reference's histogram,
+        which its code never observed (D23)."""
+        now = time.monotonic_ns()                 # enqueued_at: the queue's steady clock
+        h = self.metrics.wait_time
+        for m in msgs:
+            if m.enqueued_at:
+                h.labels(self.name, m.queue_name, priority_name(m.priority)).observe(
+                    max(0, now - m.enqueued_at) / 1e9)
 
     def batch_pop_messages(self, queue_name: str, count: int) -> List[Message]:
         if queue_name not in self._queues:
@@ -193,6 +205,7 @@ class QueueManager:
                 self.metrics.pending.labels(self.name, queue_name, p).dec()
                 self.metrics.processing.labels(self.name, queue_name, p).inc()
             self.metrics.operations.labels(self.name, queue_name, "batch_pop").inc()
+            self._observe_wait(msgs)
         return msgs
 
     def pop_tiers(self, tiers: Sequence[str], count: int, aging_ns: Sequence[int],
@@ -207,6 +220,7 @@ class QueueManager:
                 p = priority_name(pr)
                 self.metrics.pending.labels(self.name, q, p).dec(n)
                 self.metrics.processing.labels(self.name, q, p).inc(n)
+            self._observe_wait(msgs)
         return msgs, tier_idx, enq
 
     def peek_message(self, queue_name: str) -> Message:

@@ -44,6 +44,9 @@ class _Noop:
     def observe(self, *a, **k):
         pass
 
+    def set_function(self, *a, **k):
+        pass
+
 
 class QueueMetrics:
     """All gateway series, registered once per registry."""

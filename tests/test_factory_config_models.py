@@ -241,3 +241,37 @@ def test_serve_engine_builder_applies_gpu_config(monkeypatch):
     M._build_engine(cfg, "llama3-8b", "cpu")
     # 64 GiB - 16 GiB reserve - ~15 GiB of weights, 64 MiB of KV per 512-token slot
     assert 400 < got["slots"] < 600 and got["step_timeout_s"] == 5.0
+
+
+def test_dashboard_series_are_all_fed():
+    """Every series the Grafana dashboard plots gets samples from a serving
+    gateway (three panels used to stay empty: DLQ size, preprocess time,
+    queue wait).  A CPU gateway app serves a few requests and dead-letters
+    one; the exposition then carries samples of each."""
+    import time as _t
+    from llm_message_queue_amd.backend.engine import BackendEngine
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    from llm_message_queue_amd.gateway.workload import Workload
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.utils.metrics import reset_default_metrics
+    reset_default_metrics()
+    cfg = default_config()
+    eng = BackendEngine(LlamaConfig.tiny(), slots=8, max_ctx=64, token_budget=128, device="cpu", impl="ref")
+    app = GatewayApp(cfg, use_gpu=False, engine=eng, start=False)
+    from llm_message_queue_amd.balancer.load_balancer import Endpoint
+    app.lb.add_endpoint(Endpoint(id="gpu0", type="llm", gpu_index=0, max_connections=8))   # as cli serve does
+    try:
+        app.start()
+        app.factory.dead_letter_queue.push(new_message("c", "u", "x", 3), "test", "normal")
+        app.gateway.submit(Workload(seed=3).make(8))
+        deadline = _t.time() + 30
+        while app.gateway.counters["completed"] < 8 and _t.time() < deadline:
+            _t.sleep(0.05)
+        text = app.metrics.render().decode()
+        for series in ("llm_queue_dead_letter_size{", "llm_queue_messages_wait_time_seconds_count{",
+                       "llm_preprocess_kernel_seconds_count{", "llm_queue_enqueue_to_dispatch_seconds_count{"):
+            lines = [ln for ln in text.splitlines() if ln.startswith(series)]
+            assert lines and any(float(ln.rsplit(" ", 1)[1]) > 0 for ln in lines), series
+    finally:
+        app.stop()
+        reset_default_metrics()

@@ -68,3 +68,25 @@ def test_serve_loop_exits_on_backend_hung():
     app._loop_thread.join(5)
     assert isinstance(app.fatal, BackendHung) and app._stop.is_set()
     app.stop()
+
+
+def test_serve_loop_defect_is_fatal_not_a_zombie():
+    """An unexpected exception in the tick used to end the dispatcher thread
+    silently while the API kept accepting requests; now it is logged and
+    fatal (the process exits non-zero and is restarted)."""
+    from llm_message_queue_amd.backend.engine import BackendEngine
+    from llm_message_queue_amd.gateway.app import GatewayApp
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    from llm_message_queue_amd.utils.config import default_config
+    cfg = default_config()
+    cfg.queue.enable_metrics = False
+    eng = BackendEngine(LlamaConfig.tiny(), slots=4, max_ctx=64, token_budget=64, device="cpu", impl="ref")
+    app = GatewayApp(cfg, use_gpu=False, engine=eng, start=False)
+
+    def boom(*a, **k):
+        raise KeyError("a bug")
+    app.gateway.tick = boom
+    app.start()
+    app._loop_thread.join(5)
+    assert isinstance(app.fatal, KeyError) and app._stop.is_set()
+    app.stop()
