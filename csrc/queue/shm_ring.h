@@ -206,7 +206,8 @@ class ShmRing {
 
   uint64_t capacity() const { return h_ ? h_->cap : 0; }
 
-  // records taken by balanced-share consumers 0 .. n-1
+  // balanced-share ledger of consumers 0 .. n-1: records taken, plus any
+  // deficit forgiven past kCatchUp (so >= what each actually took)
   std::vector<uint64_t> taken(int n) {
     Lock l(h_);
     std::vector<uint64_t> v;

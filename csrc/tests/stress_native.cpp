@@ -189,7 +189,7 @@ static void stress_ring() {
     th.emplace_back([&, c] {
       ShmRing& r = c ? a : b;
       while (total.load() < P * N) {
-        auto v = r.pop(32, 5);
+        auto v = r.pop(32, 5, 2, c);          // balanced share between the two consumers
         for (auto& kv : v) {
           int id = std::atoi(kv.second.c_str());
           CHECK((int)kv.first == id / N);
@@ -206,10 +206,16 @@ static void stress_ring() {
   std::sort(all.begin(), all.end());
   CHECK((int)all.size() == P * N);
   for (int i = 0; i < P * N; ++i) CHECK(all[i] == i);
+  CHECK(!got[0].empty() && !got[1].empty());
+  auto tk = a.taken(2);
+  // the balance ledger counts what each consumer took, plus deficits forgiven
+  // past kCatchUp (a consumer far behind is not owed the whole ring)
+  CHECK(tk[0] >= got[0].size() && tk[1] >= got[1].size());
   auto s = a.stats();
   CHECK(s.size == 0 && s.pushed == (uint64_t)P * N && s.popped == (uint64_t)P * N);
   a.unlink();
-  std::printf("shm ring: %d records, 3 producers / 2 consumers OK\n", P * N);
+  std::printf("shm ring: %d records, 3 producers / 2 balanced consumers (%zu / %zu) OK\n", P * N, got[0].size(),
+              got[1].size());
 }
 
 static void stress_shm_coll() {
