@@ -41,13 +41,16 @@ std::vector<int> push_batch(MultiLevelQueue& q, const std::vector<std::string>& 
 
 py::tuple pop_tiers(MultiLevelQueue& q, const std::vector<std::string>& tiers, int64_t count,
                     const std::vector<int64_t>& aging_ns, std::vector<int64_t> budget,
-                    const std::vector<int64_t>& lifo_ns) {
+                    const std::vector<int64_t>& lifo_ns, py::array_t<int64_t, py::array::c_style | py::array::forcecast> skip) {
+  // skip: handles to leave queued (any order; sorted here for the binary search)
+  std::vector<int64_t> sk(skip.data(), skip.data() + skip.size());
+  std::sort(sk.begin(), sk.end());
   std::vector<int64_t> hs, enq;
   std::vector<int32_t> ti;
   {
     py::gil_scoped_release nogil;
     hs.reserve(count > 0 ? count : 0);
-    q.pop_tiers(tiers, count, aging_ns, std::move(budget), hs, ti, enq, lifo_ns);
+    q.pop_tiers(tiers, count, aging_ns, std::move(budget), hs, ti, enq, lifo_ns, sk);
   }
   py::array_t<int64_t> a_h(hs.size()), a_e(enq.size());
   py::array_t<int32_t> a_t(ti.size());
@@ -79,7 +82,7 @@ PYBIND11_MODULE(_mlq, m) {
       .def("peek", &MultiLevelQueue::peek)
       .def("pop_batch", &MultiLevelQueue::pop_batch, py::call_guard<py::gil_scoped_release>())
       .def("pop_tiers", &pop_tiers, py::arg("tiers"), py::arg("count"), py::arg("aging_ns"), py::arg("budget"),
-           py::arg("lifo_ns") = std::vector<int64_t>{})
+           py::arg("lifo_ns") = std::vector<int64_t>{}, py::arg("skip") = py::array_t<int64_t>(0))
       .def("size", &MultiLevelQueue::size)
       .def("total_size", &MultiLevelQueue::total_size)
       .def("stats", &stats_dict)

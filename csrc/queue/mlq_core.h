@@ -133,6 +133,45 @@ class NamedQueue {
     return false;
   }
 
+  // Skip-aware variants: `skip` is a sorted list of handles the caller must
+  // not take (turns that belong to another GPU).  Position = (bucket, index).
+  static bool skipped(const std::vector<int64_t>& skip, int64_t h) {
+    return std::binary_search(skip.begin(), skip.end(), h);
+  }
+  // oldest (tail=false) or newest (tail=true) item of the most urgent
+  // bucket holding one that is not skipped
+  const Item* find_locked(const std::vector<int64_t>& skip, bool tail, size_t* bi, size_t* ii) const {
+    for (size_t b = 0; b < buckets_.size(); ++b) {
+      const auto& r = buckets_[b].ring;
+      const size_t n = r.size();
+      for (size_t k = 0; k < n; ++k) {
+        const size_t i = tail ? n - 1 - k : k;
+        if (!skipped(skip, r[i].handle)) {
+          *bi = b;
+          *ii = i;
+          return &r[i];
+        }
+      }
+    }
+    return nullptr;
+  }
+  void take_locked(size_t bi, size_t ii, Item* out, int64_t now) {
+    auto& r = buckets_[bi].ring;
+    *out = r[ii];
+    if (ii == 0)
+      r.pop_front();
+    else if (ii + 1 == r.size())
+      r.pop_back();
+    else
+      r.erase(r.begin() + (std::ptrdiff_t)ii);
+    size_--;
+    st_.pending--;
+    st_.processing++;
+    st_.popped++;
+    st_.total_wait_ns += now - out->enq_ns;
+    st_.last_update_ns = now;
+  }
+
   // remove a specific handle (admin DELETE /queues/:type/:id)
   bool remove_locked(int64_t handle, int64_t now) {
     for (auto& b : buckets_) {
@@ -277,9 +316,15 @@ class MultiLevelQueue {
   // short queue wait and the stale head runs into its deadline and is shed
   // (the gateway's expiry), instead of every request waiting nearly the
   // whole deadline under FIFO.  FIFO resumes once the head is younger.
+  //
+  // `skip` (optional, sorted handles): requests the caller must leave queued
+  // -- a rank admitting into its own GPU passes the turns whose KV lives on
+  // another GPU; they keep their queue position for the tick's plan, and
+  // "head" / "newest" below mean the first / last request not skipped.
   void pop_tiers(const std::vector<std::string>& tiers, int64_t count, const std::vector<int64_t>& aging_ns,
                  std::vector<int64_t> budget, std::vector<int64_t>& hs, std::vector<int32_t>& ti,
-                 std::vector<int64_t>& enq, const std::vector<int64_t>& lifo_ns = {}) {
+                 std::vector<int64_t>& enq, const std::vector<int64_t>& lifo_ns = {},
+                 const std::vector<int64_t>& skip = {}) {
     const size_t T = tiers.size();
     if (aging_ns.size() != T || budget.size() != T || (!lifo_ns.empty() && lifo_ns.size() != T))
       throw std::invalid_argument("tier arg mismatch");
@@ -292,6 +337,10 @@ class MultiLevelQueue {
         if (qs[i]) locks.emplace_back(qs[i]->mu);
       int64_t now = mono_ns();
       hs.reserve(count);
+      if (!skip.empty()) {
+        pop_tiers_skip_locked(qs, count, aging_ns, budget, hs, ti, enq, lifo_ns, skip, now);
+        return;
+      }
       while ((int64_t)hs.size() < count) {
         int pick = -1;
         // 1) an overdue head (waited past its tier's max_wait_time): serve the
@@ -320,6 +369,43 @@ class MultiLevelQueue {
       }
     }
   }
+
+ private:
+  // pop_tiers' loop over the first / last request of each tier that is not
+  // in `skip` (every tier locked by the caller)
+  static void pop_tiers_skip_locked(const std::vector<std::shared_ptr<NamedQueue>>& qs, int64_t count,
+                                    const std::vector<int64_t>& aging_ns, std::vector<int64_t>& budget,
+                                    std::vector<int64_t>& hs, std::vector<int32_t>& ti, std::vector<int64_t>& enq,
+                                    const std::vector<int64_t>& lifo_ns, const std::vector<int64_t>& skip,
+                                    int64_t now) {
+    const size_t T = qs.size();
+    while ((int64_t)hs.size() < count) {
+      int pick = -1;
+      size_t bi = 0, ii = 0;
+      const Item* h = nullptr;
+      for (size_t i = 0; i < T && pick < 0; ++i) {
+        if (!qs[i] || budget[i] == 0 || aging_ns[i] <= 0) continue;
+        const Item* c = qs[i]->find_locked(skip, false, &bi, &ii);
+        if (c && now - c->enq_ns > aging_ns[i]) pick = (int)i, h = c;
+      }
+      for (size_t i = 0; i < T && pick < 0; ++i) {
+        if (!qs[i] || budget[i] == 0) continue;
+        const Item* c = qs[i]->find_locked(skip, false, &bi, &ii);
+        if (c) pick = (int)i, h = c;
+      }
+      if (pick < 0) break;
+      if (!lifo_ns.empty() && lifo_ns[pick] > 0 && now - h->enq_ns > lifo_ns[pick])
+        qs[pick]->find_locked(skip, true, &bi, &ii);
+      Item it;
+      qs[pick]->take_locked(bi, ii, &it, now);
+      hs.push_back(it.handle);
+      enq.push_back(it.enq_ns);
+      ti.push_back(pick);
+      if (budget[pick] > 0) budget[pick]--;
+    }
+  }
+
+ public:
 
   int64_t size(const std::string& name) {
     auto q = get(name);

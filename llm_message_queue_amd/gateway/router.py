@@ -228,6 +228,7 @@ class Gateway:
         self.inflight_by_tier = np.zeros(len(self.tiers), dtype=np.int64)
         # queued requests per (home GPU, tier): KV-residency pins (planner L_PIN)
         self.pinned = np.zeros((self.world, planner.NTIERS), dtype=np.int64)
+        self._away: set = set()        # handles of queued turns pinned to another GPU
         # multi-GPU placement follows loadbalancer.algorithm (planner.PlanState;
         # identical on every rank, advanced identically by every plan)
         self.plan_state = planner.PlanState(strategy=str(getattr(cfg.loadbalancer, "algorithm", "")))
@@ -722,6 +723,7 @@ class Gateway:
                 if h < self.world:
                     self.pinned[h, t] = max(0, int(self.pinned[h, t]) - 1)
                 m.pin_key = -1
+                self._away.discard(m.handle)
             return
         if m.pin_key >= 0:
             return                                   # already counted
@@ -731,6 +733,14 @@ class Gateway:
             t = min(max(int(t), 0), planner.NTIERS - 1)
             self.pinned[h, t] += 1
             m.pin_key = h * planner.NTIERS + t
+            if h != self.rank:
+                self._away.add(m.handle)
+
+    def _skip_away(self):
+        """Handles of queued turns homed on another GPU: a rank admitting into
+        its own GPU leaves them queued, in place, for the tick's plan."""
+        a = self._away
+        return np.fromiter(a, dtype=np.int64, count=len(a)) if a else None
 
     def _exclude_mask(self) -> int:
         """GPUs this rank's balancer view rules out for new work: parked by
@@ -1547,9 +1557,11 @@ class Gateway:
         for the exchange while its own GPU has room (the
         non-realtime tiers used to dispatch only at the collective, and the
         realtime lane switched off whenever any realtime turn was homed
-        elsewhere).  A tier holding turns homed on another GPU is left to
-        the planner (they follow their KV); under round robin / weighted
-        random only the realtime lane runs (their rotation is the plan's).
+        elsewhere).  Turns homed on another GPU are passed over in place
+        (``pop_tiers(skip=...)``) and left to the planner -- they follow
+        their KV -- while the rest of their tier, before or behind them, is
+        still admitted here; under round robin / weighted random only the
+        realtime lane runs (their rotation is the plan's).
         ``reserved``: while this rank's published load is awaiting the plan,
         admit only into the capacity it held back (``_reserve``)."""
         eng = self.engine
@@ -1558,7 +1570,7 @@ class Gateway:
             return 0
         held = self.awaiting_kv()
         nt = len(self.tiers)
-        elsewhere = self.pinned.sum(axis=0) - self.pinned[self.rank]
+        skip = self._skip_away()
         # between publishing its load and popping its grant, a rank may only
         # take what arrived since: the plan grants up to the published depth
         spare = ([max(0, self.qm.size(n_) - d) for n_, d in zip(self.tiers, self._pub_depth)]
@@ -1569,12 +1581,11 @@ class Gateway:
             head = min(head, self._reserve[0])
         if head > 0 and self.plan_state.strategy not in self.ROTATING_STRATEGIES:
             b = self._budgets()
-            budgets = [0 if (t < planner.NTIERS and elsewhere[t] > 0) else (head if b[t] < 0 else min(head, b[t]))
-                       for t in range(nt)]
+            budgets = [head if b[t] < 0 else min(head, b[t]) for t in range(nt)]
             if spare is not None:
                 budgets = [min(x, y) for x, y in zip(budgets, spare)]
             if any(budgets):
-                msgs, tier_idx, _e = self.qm.pop_tiers(self.tiers, head, self.aging_ns, budgets, self.lifo_ns)
+                msgs, tier_idx, _e = self.qm.pop_tiers(self.tiers, head, self.aging_ns, budgets, self.lifo_ns, skip)
                 tl = [int(t) for t in tier_idx]
                 if spare is not None:
                     for t in tl:
@@ -1584,7 +1595,7 @@ class Gateway:
                 self.counters["realtime_local"] += tl.count(0)
                 if reserved:
                     self._reserve[0] -= k
-        if self.realtime_lane and elsewhere[0] == 0 and self.qm.size(self.tiers[0]) > 0:
+        if self.realtime_lane and self.qm.size(self.tiers[0]) > 0:
             room = eng.lane_capacity() - held
             if reserved:
                 room = min(room, self._reserve[1])
@@ -1596,7 +1607,7 @@ class Gateway:
             if room > 0:
                 budgets = [0] * nt
                 budgets[0] = room
-                msgs, _t, _e = self.qm.pop_tiers(self.tiers, room, [0] * nt, budgets, None)
+                msgs, _t, _e = self.qm.pop_tiers(self.tiers, room, [0] * nt, budgets, None, skip)
                 k = self._admit_own(msgs, [0] * len(msgs), P_LANE)
                 self.counters["realtime_local"] += k
                 if reserved:
@@ -1671,11 +1682,10 @@ class Gateway:
         # extra step then runs only the work already admitted)
         if room > 0 and self.plan_state.strategy not in self.ROTATING_STRATEGIES:
             b = self._budgets()
-            elsewhere = self.pinned.sum(axis=0) - self.pinned[self.rank]
-            budgets = [0 if (t < planner.NTIERS and elsewhere[t] > 0) else (room if b[t] < 0 else min(room, b[t]))
-                       for t in range(len(self.tiers))]
+            budgets = [room if b[t] < 0 else min(room, b[t]) for t in range(len(self.tiers))]
             if any(budgets):
-                msgs, tier_idx, _e = self.qm.pop_tiers(self.tiers, room, self.aging_ns, budgets, self.lifo_ns)
+                msgs, tier_idx, _e = self.qm.pop_tiers(self.tiers, room, self.aging_ns, budgets, self.lifo_ns,
+                                                       self._skip_away())
                 self.counters["extra_admitted"] += self._admit_own(msgs, [int(t) for t in tier_idx])
         if eng.ready_tokens() < self.EXTRA_STEP_MIN_FRAC * eng.token_budget:
             return False

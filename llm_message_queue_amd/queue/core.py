@@ -138,13 +138,16 @@ class MultiLevelQueue:
         return [store.pop(h) for h in self._q.pop_batch(queue_name, int(count))]
 
     def pop_tiers(self, tiers: Sequence[str], count: int, aging_ns: Sequence[int],
-                  budget: Sequence[int], lifo_ns: Optional[Sequence[int]] = None
-                  ) -> Tuple[List[Message], np.ndarray, np.ndarray]:
+                  budget: Sequence[int], lifo_ns: Optional[Sequence[int]] = None,
+                  skip: Optional[np.ndarray] = None) -> Tuple[List[Message], np.ndarray, np.ndarray]:
         """Dispatcher pop: strict priority with aging + per-tier budgets.
         ``budget[i] < 0`` means unlimited.  ``lifo_ns`` (optional): adaptive
-        LIFO thresholds per tier (serve newest while the head is older)."""
-        hs, tier_idx, enq = self._q.pop_tiers(list(tiers), int(count), list(aging_ns), list(budget),
-                                              list(lifo_ns or []))
+        LIFO thresholds per tier (serve newest while the head is older).
+        ``skip`` (optional int64 handles): requests to pass over, left queued
+        in place."""
+        args = (list(tiers), int(count), list(aging_ns), list(budget), list(lifo_ns or []))
+        hs, tier_idx, enq = (self._q.pop_tiers(*args, skip) if skip is not None and len(skip)
+                             else self._q.pop_tiers(*args))
         store = self._store
         return [store.pop(int(h)) for h in hs], tier_idx, enq
 

@@ -209,8 +209,8 @@ class QueueManager:
         return msgs
 
     def pop_tiers(self, tiers: Sequence[str], count: int, aging_ns: Sequence[int],
-                  budget: Sequence[int], lifo_ns: Optional[Sequence[int]] = None):
-        msgs, tier_idx, enq = self.mlq.pop_tiers(tiers, count, aging_ns, budget, lifo_ns)
+                  budget: Sequence[int], lifo_ns: Optional[Sequence[int]] = None, skip=None):
+        msgs, tier_idx, enq = self.mlq.pop_tiers(tiers, count, aging_ns, budget, lifo_ns, skip)
         if self.metrics and msgs:
             cnt: Dict[tuple, int] = {}
             for m in msgs:

@@ -277,3 +277,36 @@ def test_multirank_realtime_lane_dispatches_between_ticks():
         if gws[0].counters["completed"] >= 3:
             break
     assert gws[0].counters["completed"] == 3
+
+
+def test_own_dispatch_passes_over_turns_homed_elsewhere():
+    """the realtime lane (and the own-GPU dispatch of
+    every tier) used to switch off while ANY queued turn of the tier was
+    homed on another GPU.  Now those turns are passed over in place -- they
+    wait for the tick's plan, which sends them to their KV -- and the rest of
+    the tier is still admitted into this rank's own GPU between ticks."""
+    from llm_message_queue_amd.models.message import Message
+    W = 2
+    gws, _ = _cluster(W, "least_connections", slots=16)
+    g = gws[0]
+    g.conv_home["dlg-away"] = 1
+    away = [Message(id=f"a{i}", conversation_id="dlg-away", content="and then?", priority=p, user_id="u")
+            for i, p in enumerate((1, 3))]
+    rt = [Message(id=f"rt{i}", content="outage now", priority=1, user_id="u") for i in range(3)]
+    nm = [Message(id=f"n{i}", content="summarise this", priority=3, user_id="u") for i in range(2)]
+    g.submit(away[:1] + rt + away[1:] + nm)
+    g._last_ingest_ns = 0
+    assert g._while_waiting(None)
+    # the prefill headroom (4 here) takes realtime then normal, the lane the
+    # rest of realtime; the old code admitted none of them (both tiers held a
+    # turn homed on GPU1)
+    assert all(m.dispatched_at > 0 and m.endpoint_id == "gpu0" for m in rt + nm[:1])
+    assert all(m.dispatched_at == 0 for m in away)
+    assert g.pinned[1].tolist()[:3] == [1, 0, 1] and len(g._away) == 2
+    for _ in range(40):
+        _tick_all(gws)
+        if g.counters["completed"] >= 7:
+            break
+    assert g.counters["completed"] == 7
+    assert all(m.endpoint_id == "gpu1" for m in away)         # followed their home
+    assert g.pinned.sum() == 0 and not g._away

@@ -140,6 +140,39 @@ def test_pop_tiers_adaptive_lifo():
         q.pop_tiers(LEVELS, 1, [0] * 4, [-1] * 4, [0, 0])          # per-tier lengths must match
 
 
+def test_pop_tiers_skip_leaves_requests_in_place():
+    """``skip``: requests homed on another GPU are passed over (aging, strict
+    priority and LIFO look at the first / last request not skipped) and stay
+    queued in their original order for the tick's plan."""
+    import numpy as np
+    q = mlq4()
+    r = [new_message("c", "u", f"r{i}", 1) for i in range(4)]
+    n = [new_message("c", "u", f"n{i}", 3) for i in range(3)]
+    for m in r:
+        q.push("realtime", m)
+    for m in n:
+        q.push("normal", m)
+    skip = np.array([r[0].handle, r[2].handle, n[2].handle], dtype=np.int64)
+    msgs, tiers, _ = q.pop_tiers(LEVELS, 10, [0] * 4, [-1] * 4, None, skip)
+    assert [m.content for m in msgs] == ["r1", "r3", "n0", "n1"] and list(tiers) == [0, 0, 2, 2]
+    assert [m.content for m in q.messages("realtime")] == ["r0", "r2"]
+    st = q.get_stats("realtime")
+    assert st.pending_count == 2 and st.processing_count == 2
+    # LIFO picks the newest request that is not skipped
+    for i in range(3, 6):
+        q.push("normal", new_message("c", "u", f"n{i}", 3))
+    time.sleep(0.005)
+    last = q.messages("normal")[-1]
+    msgs, _, _ = q.pop_tiers(LEVELS, 1, [0] * 4, [0, -1, -1, -1], [0, 0, 1_000_000, 0],
+                             np.array([last.handle], dtype=np.int64))
+    assert msgs[0].content == "n4"
+    # a fully skipped tier yields nothing; without skip the plan takes them in order
+    msgs, _, _ = q.pop_tiers(LEVELS, 5, [0] * 4, [-1, 0, 0, 0], None, skip)
+    assert msgs == []
+    msgs, _, _ = q.pop_tiers(LEVELS, 5, [0] * 4, [-1, 0, 0, 0])
+    assert [m.content for m in msgs] == ["r0", "r2"]
+
+
 def test_concurrent_push_pop_no_loss():
     q = MultiLevelQueue(0)
     for n in LEVELS:
