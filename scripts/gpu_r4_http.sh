@@ -6,9 +6,11 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+i=0
 for V in ${VARIANTS:-1:5300:--bench-config 2:5000:--bench-config}; do
   IFS=: read -r RANKS RATE EXTRA <<< "$V"
-  tag=r4_http_${RANKS}ranks_1gpu_${RATE}${EXTRA:+_bc}
+  i=$((i + 1))
+  tag=r4_http_${RANKS}ranks_1gpu_${RATE}${EXTRA:+_bc}${REPEAT_TAG:+_$i}
   timeout -k 10 300 python bench/http_load.py --spawn multirank --ranks "$RANKS" --gpu $EXTRA --client native \
     --workload --procs 2 --conns 16 --threads 2 --rate "$RATE" --duration 15 --warmup 10 --admin-churn 2 \
     --server-log gpurun_out/$tag.log > gpurun_out/$tag.json 2> gpurun_out/$tag.err
