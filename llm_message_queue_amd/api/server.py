@@ -38,7 +38,6 @@ from ..balancer.load_balancer import Endpoint, LoadBalancerError
 from ..models.message import (ConversationNotFound, Message, MessageStatus,
                               PriorityParseError, format_time, level_priority_from_name, parse_priority,
                               priority_name)
-from ..queue.core import QueueError
 from ..scheduler.resource_scheduler import Resource, ResourceError
 from ..utils.metrics import CONTENT_TYPE_LATEST
 from .security import guard_from_config, redact_config
