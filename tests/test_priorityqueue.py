@@ -414,3 +414,54 @@ def test_dlq_bulk_handlers_run_on_one_worker_thread():
     while len(seen) < 5000 and time.time() - t0 < 10:
         time.sleep(0.01)
     assert seen == [m.id for m in msgs]
+
+
+def test_pop_tiers_matches_a_python_model():
+    """Property test of the native dispatcher pop against a plain-Python
+    model: strict priority over tiers, priority buckets then FIFO inside a
+    tier, per-tier budgets, and ``skip`` (handles passed over in place)."""
+    import numpy as np
+    from hypothesis import given, settings, strategies as st
+    from llm_message_queue_amd import _native
+
+    item = st.tuples(st.integers(0, 2), st.integers(1, 3))          # (tier, priority)
+
+    @settings(max_examples=150, deadline=None)
+    @given(st.lists(item, max_size=40), st.data())
+    def run(items, data):
+        q = _native.mlq().MultiLevelQueue(0)
+        names = ["t0", "t1", "t2"]
+        for n in names:
+            q.add_queue(n)
+        model = {t: [] for t in range(3)}
+        for h, (t, p) in enumerate(items):
+            q.push(names[t], h, p)
+            model[t].append((p, h))
+        for _round in range(3):
+            skip = set(data.draw(st.lists(st.integers(0, max(0, len(items) - 1)), max_size=10)))
+            budget = data.draw(st.lists(st.integers(-1, 5), min_size=3, max_size=3))
+            count = data.draw(st.integers(0, 12))
+            hs, ti, _e = q.pop_tiers(names, count, [0, 0, 0], budget, [],
+                                     np.array(sorted(skip), dtype=np.int64))
+            want, b = [], list(budget)
+            while len(want) < count:
+                pick = None
+                for t in range(3):
+                    if b[t] == 0:
+                        continue
+                    cand = sorted((p, k, h) for k, (p, h) in enumerate(model[t]) if h not in skip)
+                    if cand:
+                        pick = (t, cand[0])
+                        break
+                if pick is None:
+                    break
+                t, (_p, k, h) = pick
+                model[t].pop(k)
+                want.append((h, t))
+                if b[t] > 0:
+                    b[t] -= 1
+            assert list(zip(hs.tolist(), ti.tolist())) == want
+            for t in range(3):
+                assert q.size(names[t]) == len(model[t])
+
+    run()
