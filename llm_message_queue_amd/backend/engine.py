@@ -18,6 +18,11 @@ and returns immediately.  The pipeline is fully asynchronous:
 The slot census of every step is written by the ``slot_census`` kernel into
 the node-shared load page (zero-copy for routers, N9).
 
+Reference: the reference has no model backend -- its workers call a
+``ProcessFunc`` (`internal/priorityqueue/worker.go:162-189`) that
+`cmd/server/main.go:172-193` (`startWorkers`) stubs out; this engine is what a
+dispatched request runs on instead.
+
 Request cost model (README/bench): prompt = the message's tokens from the
 GPU tokenizer (capped), generation = ``gen_tokens`` greedy tokens, all 32
 layers of the stub, never skipped.

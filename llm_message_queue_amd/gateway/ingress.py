@@ -2,6 +2,9 @@
 thread that flushes them in batches (every ``window_us`` or ``max_batch``) so
 the GPU preprocess pipeline runs one fused launch chain per batch instead of
 one per request.  Each caller blocks on its own future.
+
+Reference: `api/handlers.go:160-219` preprocesses and enqueues each request
+inside its own handler; here the handlers only hand off.
 """
 from __future__ import annotations
 

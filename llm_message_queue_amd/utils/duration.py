@@ -1,4 +1,8 @@
-"""Go ``time.Duration`` text parsing/formatting (viper decodes "100ms", "5m", "1h30m")."""
+"""Go ``time.Duration`` text parsing/formatting (viper decodes "100ms", "5m", "1h30m").
+
+Reference: the duration-typed config fields, e.g. ``max_wait_time``,
+``monitor_interval``, ``process_interval`` (`pkg/config/config.go:49-68`), so
+`configs/config.yaml` loads unchanged."""
 from __future__ import annotations
 
 import re
