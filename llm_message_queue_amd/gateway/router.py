@@ -229,6 +229,7 @@ class Gateway:
         # queued requests per (home GPU, tier): KV-residency pins (planner L_PIN)
         self.pinned = np.zeros((self.world, planner.NTIERS), dtype=np.int64)
         self._away: set = set()        # handles of queued turns pinned to another GPU
+        self._pin_lock = threading.Lock()
         # multi-GPU placement follows loadbalancer.algorithm (planner.PlanState;
         # identical on every rank, advanced identically by every plan)
         self.plan_state = planner.PlanState(strategy=str(getattr(cfg.loadbalancer, "algorithm", "")))
@@ -715,15 +716,17 @@ class Gateway:
         exactly (the conversation may be re-homed -- migration, a completed
         turn elsewhere -- while this turn waits, and recomputing the home at
         pop time would decrement the wrong GPU and leave the old one
-        inflated for good)."""
+        inflated for good).  Removals also arrive from API and peer-query
+        threads (``qm.on_remove``), hence the lock."""
         if delta < 0:
-            k = m.pin_key
-            if k >= 0:
-                h, t = divmod(k, planner.NTIERS)
-                if h < self.world:
-                    self.pinned[h, t] = max(0, int(self.pinned[h, t]) - 1)
-                m.pin_key = -1
-                self._away.discard(m.handle)
+            with self._pin_lock:
+                k = m.pin_key
+                if k >= 0:
+                    h, t = divmod(k, planner.NTIERS)
+                    if h < self.world:
+                        self.pinned[h, t] = max(0, int(self.pinned[h, t]) - 1)
+                    m.pin_key = -1
+                    self._away.discard(m.handle)
             return
         if m.pin_key >= 0:
             return                                   # already counted
@@ -731,16 +734,19 @@ class Gateway:
         if 0 <= h < self.world:
             t = self.tier_of_queue.get(m.queue_name, 2) if m.tier < 0 else m.tier
             t = min(max(int(t), 0), planner.NTIERS - 1)
-            self.pinned[h, t] += 1
-            m.pin_key = h * planner.NTIERS + t
-            if h != self.rank:
-                self._away.add(m.handle)
+            with self._pin_lock:
+                self.pinned[h, t] += 1
+                m.pin_key = h * planner.NTIERS + t
+                if h != self.rank:
+                    self._away.add(m.handle)
 
     def _skip_away(self):
         """Handles of queued turns homed on another GPU: a rank admitting into
         its own GPU leaves them queued, in place, for the tick's plan."""
-        a = self._away
-        return np.fromiter(a, dtype=np.int64, count=len(a)) if a else None
+        if not self._away:
+            return None
+        with self._pin_lock:
+            return np.fromiter(self._away, dtype=np.int64, count=len(self._away))
 
     def _exclude_mask(self) -> int:
         """GPUs this rank's balancer view rules out for new work: parked by

@@ -244,3 +244,47 @@ def test_every_removal_of_a_queued_turn_releases_its_pin():
     assert app.standard.cleanup_stale_messages() == 1
     assert gw.pinned.sum() == 0
     app.stop()
+
+
+def test_pin_bookkeeping_is_thread_safe():
+    """Admin deletes and peer dequeues release pins from other threads
+    (``qm.on_remove``) while the serve loop reads the homed-away set for
+    its own-GPU pops: no torn update, no 'set changed size' in the loop."""
+    import threading
+    comms = FakeComm.make(2)
+    gw = Gateway(_cfg(), engine=None, comm=comms[0], use_gpu_preprocess=False)
+    gw.conv_home["far"] = 1
+    msgs = [Message(id=f"x{i}", conversation_id="far", content="hi", priority=3) for i in range(400)]
+    for m in msgs:
+        m.queue_name = "normal"
+    stop = threading.Event()
+    errs = []
+
+    def churn(part):
+        try:
+            for _ in range(20):
+                for m in part:
+                    gw._pin(m, +1)
+                for m in part:
+                    gw._pin(m, -1)
+        except Exception as e:          # noqa: BLE001
+            errs.append(e)
+
+    def reader():
+        try:
+            while not stop.is_set():
+                gw._skip_away()
+        except Exception as e:          # noqa: BLE001
+            errs.append(e)
+
+    r = threading.Thread(target=reader)
+    r.start()
+    ths = [threading.Thread(target=churn, args=(msgs[i::4],)) for i in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    stop.set()
+    r.join()
+    assert not errs
+    assert gw.pinned.sum() == 0 and not gw._away
