@@ -135,6 +135,8 @@ def main() -> None:
     ap.add_argument("--client", choices=["python", "native"], default="python",
                     help="native = csrc/tools/http_bench.cpp (open-loop, keep-alive, no coordinated omission)")
     ap.add_argument("--conns", type=int, default=16, help="native client: connections per thread")
+    ap.add_argument("--rss-every", type=float, default=10.0,
+                    help="seconds between server RSS samples over the measured run (native client)")
     ap.add_argument("--warmup", type=float, default=0.0,
                     help="seconds of load before the measured window (the dispatcher's latency window is reset "
                          "after it)")
@@ -267,9 +269,34 @@ def main() -> None:
                         churn["ms"].append((time.perf_counter() - t0) * 1e3)
             if a.admin_churn > 0 and api_url:
                 threading.Thread(target=_churn, daemon=True).start()
+            # server memory over the measured run (every spawned process and
+            # its children): a leak shows up as a growing series; a progress
+            # line on stderr every sample keeps long soaks visibly alive
+            rss = []
+            rss_stop = threading.Event()
+
+            def _rss():
+                import psutil
+                t0 = time.monotonic()
+                while True:
+                    tot = 0
+                    for p0 in procs:
+                        try:
+                            pp = psutil.Process(p0.pid)
+                            for q in [pp] + pp.children(recursive=True):
+                                tot += q.memory_info().rss
+                        except psutil.Error:
+                            pass
+                    rss.append((round(time.monotonic() - t0, 1), round(tot / 2**20, 1)))
+                    print(f"[http_load] t={rss[-1][0]}s server rss {rss[-1][1]} MiB", file=sys.stderr, flush=True)
+                    if rss_stop.wait(a.rss_every):
+                        return
+            if procs:
+                threading.Thread(target=_rss, daemon=True).start()
             r = subprocess.run([exe, host, port, str(a.rate), str(a.duration), str(a.procs), str(a.conns)] + extra,
                                capture_output=True, text=True, timeout=a.duration + 60)
             churn_stop.set()
+            rss_stop.set()
             st_end = None
             if api_url:                         # latency window closes with the load (before the drain)
                 with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
@@ -292,6 +319,9 @@ def main() -> None:
                                      "note": "latency: HTTP arrival (native ingress clock) -> GPU slot admission; "
                                              "latency_e2e: -> last generated token; window = the measured run"}
             out["mode"] = a.spawn or "url"
+            if rss:
+                out["server_rss_mib"] = {"every_s": a.rss_every, "first": rss[0][1], "last": rss[-1][1],
+                                         "max": max(v for _t, v in rss), "series": rss}
             if a.admin_churn > 0 and churn["ms"]:
                 ms = sorted(churn["ms"])
                 out["admin_churn"] = {"every_s": a.admin_churn, "calls": churn["calls"], "errors": churn["errors"],
