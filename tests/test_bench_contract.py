@@ -166,9 +166,14 @@ def test_bench_slo_search_backs_off_to_a_met_operating_point():
               "--gateway-only-s", "0", "--test-miss-above-util", "0.95"], timeout=420)
     s = d["slo_search"]
     assert s["util_tried"][0] == 0.98 and s["attempts"][0]["met"] is False
-    assert d["p99_target_met"] and s["value_util"] == 0.95 == d["config"]["util"]
+    # 0.95 is the first util the hook lets through; on a loaded host (the
+    # suite under xdist) the sim can genuinely miss there too and the search
+    # goes on down -- either way the value is the first met attempt's
+    u = s["value_util"]
+    assert d["p99_target_met"] and u <= 0.95 and u == d["config"]["util"]
+    assert s["attempts"][-1]["met"] and not any(t["met"] for t in s["attempts"][:-1])
     assert d["value"] == s["attempts"][-1]["value"] > 0
-    assert abs(d["offered_rate_per_gpu"] - 0.95 * d["calibrated_capacity_per_gpu"]) < 1.0
+    assert abs(d["offered_rate_per_gpu"] - u * d["calibrated_capacity_per_gpu"]) < 1.0
     assert d["requests_accounted"]["lost"] == 0
 
 
