@@ -118,3 +118,18 @@ def test_no_periodic_full_gc_by_default(monkeypatch):
         app._gc_maintenance(3600.0)
         assert calls["collect"] == want and calls["freeze"] == 1, (full, calls)
         app.stop()
+
+
+def test_message_index_unfiltered_page_matches_scan():
+    """GET /messages without filters reads only the page (a scan of the
+    200k-message index costs ~100 ms of interpreter time the serve loop
+    shares); the page and count match the filtered scan's semantics."""
+    from llm_message_queue_amd.gateway.app import MessageStore
+    from llm_message_queue_amd.models.message import Message
+    st = MessageStore(max_items=50)
+    for i in range(80):
+        st.put(Message(id=f"m{i}", content="x", priority=3, user_id="u"))
+    n, page = st.query(limit=7, offset=3)
+    n2, page2 = st.query(limit=7, offset=3, user_id="u")
+    assert n == n2 == 50 and [m.id for m in page] == [m.id for m in page2] == [f"m{i}" for i in range(33, 40)]
+    assert st.query(limit=5, offset=48)[1][-1].id == "m79" and st.query(limit=5, offset=60)[1] == []
