@@ -38,19 +38,39 @@ _REF_WAIT_NS = {1: 1_000_000_000, 2: 5_000_000_000, 3: 15_000_000_000, 4: 30_000
 
 
 class MessageStore:
-    """Bounded id -> Message index for GET /messages (stubs in the reference)."""
+    """Bounded id -> Message index for GET /messages (stubs in the reference).
+    Per-user and per-conversation sub-indexes (insertion-ordered like the
+    main one) keep filtered listings off a full scan."""
 
     def __init__(self, max_items: int = 200_000):
         self._d: "collections.OrderedDict[str, Message]" = collections.OrderedDict()
+        self._by: Dict[str, Dict[str, Dict[str, None]]] = {"user_id": {}, "conversation_id": {}}
         self._lock = threading.Lock()
         self.max_items = max_items
 
+    def _unindex(self, m: Message) -> None:
+        for f, idx in self._by.items():
+            k = getattr(m, f, "")
+            ids = idx.get(k) if k else None
+            if ids is not None:
+                ids.pop(m.id, None)
+                if not ids:
+                    del idx[k]
+
     def put(self, m: Message) -> None:
         with self._lock:
+            old = self._d.get(m.id)
+            if old is not None:
+                self._unindex(old)
             self._d[m.id] = m
             self._d.move_to_end(m.id)
+            for f, idx in self._by.items():
+                k = getattr(m, f, "")
+                if k:
+                    idx.setdefault(k, {})[m.id] = None
             while len(self._d) > self.max_items:
-                self._d.popitem(last=False)
+                _mid, ev = self._d.popitem(last=False)
+                self._unindex(ev)
 
     def get(self, mid: str) -> Optional[Message]:
         with self._lock:
@@ -62,19 +82,29 @@ class MessageStore:
 
     def remove(self, mid: str) -> Optional[Message]:
         with self._lock:
-            return self._d.pop(mid, None)
+            m = self._d.pop(mid, None)
+            if m is not None:
+                self._unindex(m)
+            return m
 
     def query(self, user_id: str = "", conversation_id: str = "", status: str = "", limit: int = 10,
               offset: int = 0) -> Tuple[int, List[Message]]:
         """Filtered page (oldest first) and the match count.  Unfiltered, only
-        the page is touched (the full index is 200k messages at serving
-        rates: a scan is ~100 ms of interpreter time the serve loop shares)."""
+        the page is touched; by user or conversation, only that sub-index (the
+        full index is 200k messages at serving rates: a scan is ~100 ms of
+        interpreter time the serve loop shares).  A status-only filter scans."""
+        offset, limit = max(0, offset), max(0, limit)
         if not (user_id or conversation_id or status):
             with self._lock:
-                return len(self._d), list(itertools.islice(self._d.values(), max(0, offset),
-                                                           max(0, offset) + max(0, limit)))
+                return len(self._d), list(itertools.islice(self._d.values(), offset, offset + limit))
         with self._lock:
-            items = list(self._d.values())
+            if user_id or conversation_id:
+                subs = [self._by[f].get(v, {}) for f, v in (("user_id", user_id), ("conversation_id", conversation_id))
+                        if v]
+                ids = min(subs, key=len)
+                items = [self._d[i] for i in ids if i in self._d]
+            else:
+                items = list(self._d.values())
         sel = [m for m in items if (not user_id or m.user_id == user_id)
                and (not conversation_id or m.conversation_id == conversation_id)
                and (not status or m.status == status)]

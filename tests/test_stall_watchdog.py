@@ -133,3 +133,32 @@ def test_message_index_unfiltered_page_matches_scan():
     n2, page2 = st.query(limit=7, offset=3, user_id="u")
     assert n == n2 == 50 and [m.id for m in page] == [m.id for m in page2] == [f"m{i}" for i in range(33, 40)]
     assert st.query(limit=5, offset=48)[1][-1].id == "m79" and st.query(limit=5, offset=60)[1] == []
+
+
+def test_message_index_filtered_queries_match_a_scan():
+    """The per-user / per-conversation sub-indexes give the same pages and
+    counts as a full scan through puts, re-puts, removals and evictions."""
+    import random
+    from llm_message_queue_amd.gateway.app import MessageStore
+    from llm_message_queue_amd.models.message import Message
+    rng = random.Random(5)
+    st = MessageStore(max_items=60)
+    for step in range(3000):
+        op = rng.random()
+        mid = f"m{rng.randrange(120)}"
+        if op < 0.6:
+            st.put(Message(id=mid, content="x", priority=3, user_id=f"u{rng.randrange(5)}",
+                           conversation_id=rng.choice(["", "c1", "c2", "c3"])))
+        elif op < 0.75:
+            st.remove(mid)
+        else:
+            u = rng.choice(["", "u0", "u1", "u3"])
+            c = rng.choice(["", "c1", "c2"])
+            s = rng.choice(["", "pending", "completed"])
+            off, lim = rng.randrange(0, 20), rng.randrange(0, 15)
+            allm = st.values()
+            want = [m for m in allm if (not u or m.user_id == u) and (not c or m.conversation_id == c)
+                    and (not s or m.status == s)]
+            n, page = st.query(user_id=u, conversation_id=c, status=s, limit=lim, offset=off)
+            assert n == len(want) and [m.id for m in page] == [m.id for m in want[off:off + lim]], step
+    assert len(st.values()) <= 60
