@@ -637,6 +637,22 @@ class HttpIngress {
   // api-gateway's fields ({"message": "Message accepted", "id"},
   // cmd/api-gateway/main.go:113), so clients of either binary read it
   void set_gateway_compat(bool on) { gateway_compat_ = on; }
+
+  // Health of the process behind the door (the serve loop's stall
+  // watchdog): while unhealthy, GET /health answers 503 with the reason, so
+  // probes replace a stalled rank instead of seeing it alive.
+  void set_health(bool ok, const std::string& reason) {
+    std::string r;
+    for (char c : reason) {                // the reason travels inside a JSON string
+      if (c == '"' || c == '\\') r += '\\';
+      if ((unsigned char)c >= 0x20) r += c;
+    }
+    {
+      std::lock_guard<std::mutex> g(health_mu_);
+      health_reason_ = r;
+    }
+    healthy_.store(ok, std::memory_order_release);
+  }
   void set_idle_timeout(double seconds) { idle_ns_.store(seconds > 0 ? (int64_t)(seconds * 1e9) : 0); }
 
  private:
@@ -1005,7 +1021,17 @@ class HttpIngress {
           }
         }
       } else if (method == "GET" && (path == "/health" || path == "/api/v1/health")) {
-        respond(cn, 200, "OK", "{\"status\":\"ok\",\"version\":\"1.0.0\",\"time\":\"" + rfc3339_now() + "\"}", keep);
+        if (healthy_.load(std::memory_order_acquire)) {
+          respond(cn, 200, "OK", "{\"status\":\"ok\",\"version\":\"1.0.0\",\"time\":\"" + rfc3339_now() + "\"}", keep);
+        } else {
+          std::string why;
+          {
+            std::lock_guard<std::mutex> g(health_mu_);
+            why = health_reason_;
+          }
+          respond(cn, 503, "Service Unavailable", "{\"status\":\"unhealthy\",\"reason\":\"" + why +
+                  "\",\"version\":\"1.0.0\",\"time\":\"" + rfc3339_now() + "\"}", keep);
+        }
       } else if (upstream_port_ > 0) {
         // handed to a proxy worker; the connection's later requests wait in
         // `in` until the answer is back (responses stay in request order)
@@ -1160,6 +1186,9 @@ class HttpIngress {
   bool pq_stop_ = false;
   int nthreads_;
   std::atomic<bool> running_{false};
+  std::atomic<bool> healthy_{true};
+  std::mutex health_mu_;
+  std::string health_reason_;
   std::vector<std::thread> th_;
   std::vector<int> lfds_;
   std::atomic<int64_t> accepted_{0}, rejected_full_{0}, bad_{0}, requests_{0}, conns_{0};
@@ -1186,6 +1215,7 @@ PYBIND11_MODULE(_ingress, m) {
       .def("set_upstream", &HttpIngress::set_upstream, py::arg("host"), py::arg("port"))
       .def("set_envelope", &HttpIngress::set_envelope)
       .def("set_gateway_compat", &HttpIngress::set_gateway_compat)
+      .def("set_health", &HttpIngress::set_health, py::arg("ok"), py::arg("reason") = "")
       .def("set_idle_timeout", &HttpIngress::set_idle_timeout, py::arg("seconds"));
   py::class_<llmq::Guard, std::shared_ptr<llmq::Guard>>(m, "Guard")
       .def(py::init<std::string, std::string, std::vector<std::string>, std::string, std::string, int64_t, bool,

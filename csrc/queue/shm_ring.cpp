@@ -57,8 +57,8 @@ static py::list a2a_mine(const ShmCollective& c) {
 PYBIND11_MODULE(_shmring, m) {
   m.doc() = "llm_message_queue_amd process-shared MPMC request ring (POSIX shm + robust mutex + futex)";
   py::class_<ShmRing>(m, "ShmRing")
-      .def(py::init<const std::string&, uint64_t, const std::string&>(), py::arg("name"),
-           py::arg("capacity") = 1 << 24, py::arg("mode") = "open")
+      .def(py::init<const std::string&, uint64_t, const std::string&, uint64_t>(), py::arg("name"),
+           py::arg("capacity") = 1 << 24, py::arg("mode") = "open", py::arg("gen") = 0)
       .def("push",
            [](ShmRing& r, py::bytes b, uint32_t tag) {
              std::string s = b;
@@ -92,6 +92,8 @@ PYBIND11_MODULE(_shmring, m) {
       .def("bytes_used", &ShmRing::bytes_used)
       .def_property_readonly("capacity", &ShmRing::capacity)
       .def_property_readonly("name", &ShmRing::name)
+      .def_property_readonly("generation", &ShmRing::generation)
+      .def_property_readonly("creator_pid", &ShmRing::creator_pid)
       .def("stats",
            [](ShmRing& r) {
              auto s = r.stats();

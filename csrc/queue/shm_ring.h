@@ -40,7 +40,7 @@
 namespace llmq {
 
 constexpr uint64_t kMagic = 0x4c4c4d5152494e47ull;   // "LLMQRING"
-constexpr uint32_t kVersion = 2;
+constexpr uint32_t kVersion = 3;   // 3: owner generation + creator pid in the header
 constexpr int kMaxConsumers = 64;     // consumer ids of the balanced share (pop `who`)
 constexpr uint32_t kWrap = 0xffffffffu;
 
@@ -49,6 +49,13 @@ struct alignas(64) Header {
   uint32_t version;
   uint32_t _pad0;
   uint64_t cap;
+  // owner generation: the job incarnation that created the ring (a nonce
+  // rank 0 broadcasts before any ring is opened, cli serve); an attach that
+  // expects a generation refuses a segment of another incarnation -- a job
+  // restarted under the same torchrun run id must never drain the dead
+  // incarnation's leftover records or its balanced-share ledger
+  uint64_t gen;
+  int64_t creator_pid;
   pthread_mutex_t mu;
   alignas(64) uint64_t head;      // producer offset (monotonic)
   uint64_t tail;                  // consumer offset (monotonic)
@@ -77,17 +84,19 @@ class ShmRing {
   // mode "create": new ring (replacing a stale segment of the same name);
   // "attach": an existing ring; "open": attach if it exists, else create
   // (the ring -- and any requests still in it -- outlives its processes).
-  ShmRing(const std::string& name, uint64_t capacity, const std::string& mode)
+  // gen != 0: "create" stamps it into the header, "attach" / "open" refuse a
+  // segment stamped with another generation (std::runtime_error "stale").
+  ShmRing(const std::string& name, uint64_t capacity, const std::string& mode, uint64_t gen = 0)
       : name_(name.empty() || name[0] != '/' ? "/" + name : name) {
     if (mode == "attach" || (mode.empty() && capacity == 0)) {
-      attach();
+      attach(gen);
     } else if (mode == "create" || mode.empty()) {
       shm_unlink(name_.c_str());
-      if (!create(capacity)) throw std::runtime_error("ShmRing create " + name_ + ": " + strerror(errno));
+      if (!create(capacity, gen)) throw std::runtime_error("ShmRing create " + name_ + ": " + strerror(errno));
     } else if (mode == "open") {
-      if (!create(capacity)) {
+      if (!create(capacity, gen)) {
         if (errno != EEXIST) throw std::runtime_error("ShmRing open " + name_ + ": " + strerror(errno));
-        attach();
+        attach(gen);
       }
     } else {
       throw std::invalid_argument("ShmRing mode must be create|attach|open");
@@ -205,6 +214,8 @@ class ShmRing {
   }
 
   uint64_t capacity() const { return h_ ? h_->cap : 0; }
+  uint64_t generation() const { return h_ ? h_->gen : 0; }
+  int64_t creator_pid() const { return h_ ? h_->creator_pid : 0; }
 
   // balanced-share ledger of consumers 0 .. n-1: records taken, plus any
   // deficit forgiven past kCatchUp (so >= what each actually took)
@@ -277,7 +288,7 @@ class ShmRing {
   }
 
   // false (errno set) if the segment already exists
-  bool create(uint64_t capacity) {
+  bool create(uint64_t capacity, uint64_t gen) {
     uint64_t cap = 4096;
     while (cap < capacity) cap <<= 1;
     int fd = shm_open(name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
@@ -291,6 +302,8 @@ class ShmRing {
     std::memset(static_cast<void*>(h_), 0, sizeof(Header));
     h_->version = kVersion;
     h_->cap = cap;
+    h_->gen = gen;
+    h_->creator_pid = (int64_t)getpid();
     pthread_mutexattr_t a;
     pthread_mutexattr_init(&a);
     pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
@@ -301,7 +314,7 @@ class ShmRing {
     return true;
   }
 
-  void attach() {
+  void attach(uint64_t gen) {
     int fd = -1;
     for (int i = 0; i < 200 && fd < 0; ++i) {             // creator may still be starting
       fd = shm_open(name_.c_str(), O_RDWR, 0600);
@@ -320,6 +333,12 @@ class ShmRing {
     if (h_->magic.load() != kMagic || h_->version != kVersion) {
       close();
       throw std::runtime_error("ShmRing " + name_ + " is not an initialised ring");
+    }
+    if (gen != 0 && h_->gen != gen) {
+      const uint64_t found = h_->gen;
+      close();
+      throw std::runtime_error("ShmRing " + name_ + " is stale: generation " + std::to_string(found) +
+                               ", expected " + std::to_string(gen));
     }
   }
 

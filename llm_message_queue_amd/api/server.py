@@ -205,6 +205,12 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None,
     @app.get("/health")
     @app.get("/api/v1/health")            # the path the reference's API docs use (docs/api.md:796)
     def health():
+        # a stalled or failing serve loop is NOT healthy: probes (k8s,
+        # the load balancer's URL checks) must see it and replace the process
+        ok, reason = G.health() if hasattr(G, "health") else (True, "")
+        if not ok:
+            return JSONResponse({"status": "unhealthy", "reason": reason, "version": VERSION,
+                                 "time": format_time(time.time_ns())}, status_code=503)
         return {"status": "ok", "version": VERSION, "time": format_time(time.time_ns())}
 
     @app.get("/metrics")
@@ -615,6 +621,26 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None,
     def list_dead_letter(limit: int = 1000):
         """The oldest ``limit`` dead letters of each GPU rank (``rank`` field)."""
         return {"items": G.dead_letters("list", str(max(1, min(int(limit), 5000))))}
+
+    @app.post("/api/v1/admin/faults")
+    async def inject_fault(request: Request):
+        """Failure drills (SURVEY.md §5 failure injection): inject faults
+        into this process's GPU backend -- ``{"fail_launch": n}`` (the next
+        n launches raise a HIP error), ``{"slow_ms": x}`` (every launch
+        stalls x ms; longer than ``server.stall_fatal_after`` drives the
+        stall watchdog to a fatal exit), ``{"drop_heartbeat": true}``; 0 /
+        false clears one.  403 unless ``server.fault_injection``."""
+        if not G.cfg.server.fault_injection:
+            return _err(403, "fault injection is disabled (server.fault_injection)")
+        eng = getattr(G, "engine", None)
+        if eng is None or not hasattr(eng, "inject"):
+            return _err(409, "no GPU backend in this process")
+        try:
+            body = await _json(request)
+            eng.inject(**dict(body))
+        except (ValueError, TypeError) as e:
+            return _err(400, f"bad fault: {e}")
+        return {"status": "injected", "faults": dict(eng.fault)}
 
     @app.get("/api/v1/config")
     def get_config():

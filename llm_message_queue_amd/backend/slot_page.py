@@ -48,6 +48,16 @@ class SlotPage:
         self._registered_ptr: Optional[int] = None
         self.owner = create
 
+    def unlink_name(self) -> None:
+        """Drop the page's /dev/shm name, keeping the mapping (a serving job
+        whose readers all hold the page object: nothing is left behind if the
+        process is SIGKILLed)."""
+        if self.owner:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
     def host_ptr(self) -> int:
         return self.words.ctypes.data
 

@@ -40,13 +40,13 @@ def _load_cfg(path):
     return load_config(path)
 
 
-def _build_engine(cfg, model: str, device):
+def _build_engine(cfg, model: str, device, job: str = ""):
     import torch
     from ..backend.engine import BackendEngine
     from ..backend.slot_page import SlotPage
     from ..models.llama_stub import LlamaConfig
     rank = int(os.environ.get("RANK", "0"))
-    page = SlotPage(f"serve{os.environ.get('TORCHELASTIC_RUN_ID', os.getpid())}", rank)
+    page = SlotPage(f"serve{job or os.getpid()}", rank)
     mcfg = LlamaConfig.by_name(model)
     slots = fit_slots(mcfg, cfg.gpu.slots_per_gpu, cfg.backend.max_ctx, cfg.gpu.hbm_reserve_gb,
                       torch.cuda.get_device_properties(device).total_memory)
@@ -73,7 +73,7 @@ def fit_slots(mcfg, slots: int, max_ctx: int, reserve_gb: float, total_bytes: in
     return slots
 
 
-def _build_cpu_engine(cfg, sim_gpu: str = ""):
+def _build_cpu_engine(cfg, sim_gpu: str = "", job: str = ""):
     """``--cpu-ranks``: a tiny Llama-shaped engine on the CPU reference ops
     (the multi-rank control flow without a GPU; never a measurement).  With
     ``--sim-gpu SPEEDS`` each rank runs a SimEngine instead: the engine's
@@ -84,7 +84,7 @@ def _build_cpu_engine(cfg, sim_gpu: str = ""):
     from ..backend.slot_page import SlotPage
     from ..models.llama_stub import LlamaConfig
     rank = int(os.environ.get("RANK", "0"))
-    page = SlotPage(f"serve{os.environ.get('TORCHELASTIC_RUN_ID', os.getpid())}", rank)
+    page = SlotPage(f"serve{job or os.getpid()}", rank)
     if sim_gpu:
         from ..backend.sim_engine import SimEngine
         speeds = [float(x) for x in sim_gpu.split(",")]
@@ -166,30 +166,45 @@ def cmd_serve(a, role: str = "serve") -> int:
         # CPU rehearsal of the multi-GPU job: gloo data plane, the same
         # control plane, tiny reference-op engines (tests / CI)
         comm = init_from_env(backend="gloo", control=cfg.gpu.control_plane)
+    # every node-shared segment of this job INCARNATION is named by a token
+    # no earlier job or restart can share (run id + restart count + a nonce
+    # rank 0 broadcasts) and stamped with its generation
+    from ..parallel.comm import job_token
+    multi = comm is not None and comm.world > 1
+    job, gen = job_token(comm if multi else None)
     engine = page = None
     if use_gpu and role in ("serve", "queue-manager"):
         local = local_device_index()
         torch.cuda.set_device(local)
-        engine, page = _build_engine(cfg, a.model, torch.device("cuda", local))
+        engine, page = _build_engine(cfg, a.model, torch.device("cuda", local), job)
         engine.warm_shapes()      # cold-start GEMM shapes before the first request (idle -> busy)
     elif cpu_ranks and role in ("serve", "queue-manager"):
-        engine, page = _build_cpu_engine(cfg, getattr(a, "sim_gpu", ""))
+        engine, page = _build_cpu_engine(cfg, getattr(a, "sim_gpu", ""), job)
+    if page is not None:
+        page.unlink_name()        # read through this mapping only; a SIGKILL leaves no file behind
     ring, app_role = None, "serve"
     # the C++ front door fronts every `serve` with a backend -- one GPU or a
     # whole node (the Python ASGI stack tops out at ~2k req/s for POST
     # /api/v1/messages); `server.front_door: python` keeps uvicorn on the port
     front = role == "serve" and engine is not None and cfg.server.front_door == "native"
-    job = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT") or str(os.getpid())
     conv_ring = None
     if front:
         # the front door: ONE shared request ring every rank drains
         # (MPMC), plus rank 0's ring for conversation turns (rank 0 owns
-        # conversation state); the C++ ingress on rank 0 feeds both
+        # conversation state); the C++ ingress on rank 0 feeds both.  The
+        # rings belong to this job incarnation: rank 0 creates them (stamped
+        # with the generation), the others attach after a barrier and refuse
+        # a ring of any other generation; once rank 0's ingress has mapped
+        # them too their names are dropped (nothing survives a SIGKILL)
         from ..gateway.shm_bridge import RingPair
         shared = f"{a.ring or cfg.server.shared_ring}-{job}"
-        ring = RingPair(shared, cfg.server.shared_ring_bytes, "open")
         if rank == 0:
-            conv_ring = RingPair(f"{shared}-conv", cfg.server.shared_ring_bytes, "open")
+            ring = RingPair(shared, cfg.server.shared_ring_bytes, "create", gen)
+            conv_ring = RingPair(f"{shared}-conv", cfg.server.shared_ring_bytes, "create", gen)
+        if multi:
+            comm.barrier()
+        if rank != 0:
+            ring = RingPair(shared, 0, "attach", gen)
         app_role = "rank"
     elif role in ("api-gateway", "queue-manager") and not a.no_ring:
         # the split deployment shares ONE request queue through shared memory (D14)
@@ -205,7 +220,8 @@ def cmd_serve(a, role: str = "serve") -> int:
     peered = front or (role == "queue-manager" and ring is not None and comm is not None and comm.world > 1)
     if peered:
         from ..gateway.peers import PeerDirectory
-        gapp.peers = PeerDirectory(ring.name, rank, comm.world if comm is not None else 1, handler=gapp.peer_op)
+        gapp.peers = PeerDirectory(ring.name, rank, comm.world if comm is not None else 1, handler=gapp.peer_op,
+                                   comm=comm if multi else None, gen=gen)
     if engine is not None:
         # every rank's balancer lists EVERY GPU of the job (its own bound to
         # the zero-copy load page): the multi-GPU planner reads the view of
@@ -221,14 +237,25 @@ def cmd_serve(a, role: str = "serve") -> int:
     if page is not None:
         gapp.start_telemetry({rank: page})
     gapp.start()
+    print(json.dumps({"event": "rank", "rank": rank, "pid": os.getpid(), "job": job,
+                      "restart": int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))}), flush=True)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
 
-    def _watch_fatal():            # a lost peer rank ends this process too
+    def _watch_fatal():            # a lost peer rank / a stalled loop ends this process too
         while not stop.is_set():
             if gapp.fatal is not None:
+                print(json.dumps({"event": "fatal", "rank": rank, "error": str(gapp.fatal)}), flush=True)
                 stop.set()
+                # the orderly shutdown below joins threads; a thread stuck in
+                # whatever stalled the loop must not keep the process alive:
+                # leave with the failure status regardless after a grace period
+                # (os._exit, never an exec -- the launcher starts the new one)
+                t = threading.Timer(float(os.environ.get("LLMQ_FATAL_EXIT_GRACE_S", "20")),
+                                    lambda: os._exit(3))
+                t.daemon = True
+                t.start()
             stop.wait(0.2)
     threading.Thread(target=_watch_fatal, daemon=True).start()
     ingress = None
@@ -260,6 +287,8 @@ def cmd_serve(a, role: str = "serve") -> int:
                                     conv_ring=f"{ring.name}-conv", upstream=(api_host, api_port))
             port = ingress.start()
             gapp.front_door = ingress
+            for r in (ring, conv_ring):           # every process of the job has them mapped now
+                r.unlink_names()
         print(json.dumps({"event": "listening", "host": cfg.server.host, "port": port,
                           "gpu": use_gpu, "role": role, "world": world,
                           "front_door": "native" if front else "python", "api_port": api_port}), flush=True)
@@ -291,7 +320,6 @@ def cmd_serve(a, role: str = "serve") -> int:
             if r is not None:
                 r.close(unlink=rank == 0)
     if gapp.fatal is not None:
-        print(json.dumps({"event": "fatal", "error": str(gapp.fatal)}), flush=True)
         return 3
     return 0
 

@@ -46,6 +46,11 @@ class NativeIngress:
         stalled / slowloris senders); 0 = never.  Default 60 s."""
         self._k.set_idle_timeout(float(seconds))
 
+    def set_health(self, ok: bool, reason: str = "") -> None:
+        """``GET /health`` on the door answers 503 (with ``reason``) while
+        not ok -- the serve loop's stall watchdog drives it."""
+        self._k.set_health(bool(ok), str(reason))
+
     def start(self) -> int:
         """Start listening; returns the bound port (useful with port 0)."""
         self.port = self._k.start()

@@ -47,9 +47,15 @@ class PeerDirectory:
     REPLY_RING = 4 << 20             # per-peer reply ring (>= 2 pages in flight plus slack)
     ANSWER_MAX = 256 << 20           # larger answers are replaced by an explicit error
 
-    def __init__(self, name: str, rank: int, world: int, handler: Optional[Callable[[str, list], Any]] = None):
+    def __init__(self, name: str, rank: int, world: int, handler: Optional[Callable[[str, list], Any]] = None,
+                 comm=None, gen: int = 0):
         """``handler(op, args)`` answers a query on ranks > 0 (the app's
-        local store); rank 0 asks with ``ask``."""
+        local store); rank 0 asks with ``ask``.  With ``comm`` (every rank
+        constructs the directory at the same point): rank 0 CREATES the rings
+        stamped with the job generation ``gen``, a barrier, then the peers
+        attach (refusing a ring of another generation) and rank 0 drops the
+        names -- nothing of this job survives a SIGKILL in /dev/shm.  Without
+        ``comm`` every rank opens the rings by name (tests, one process)."""
         R = _native.shmring().ShmRing
         self.rank, self.world, self.name = rank, world, name
         self.handler = handler
@@ -57,14 +63,25 @@ class PeerDirectory:
         self._thread: Optional[threading.Thread] = None
         self.asked = self.answered = self.timeouts = self.dropped = self.missing_total = 0
         self.last_missing: List[int] = []
+        coll = comm is not None and world > 1
         if rank == 0:
-            self.qrings = {r: R(f"llmq-{name}-q{r}", 1 << 20, "open") for r in range(1, world)}
-            self.replies = {r: R(f"llmq-{name}-qrep{r}", self.REPLY_RING, "open") for r in range(1, world)}
+            mode = "create" if coll else "open"
+            self.qrings = {r: R(f"llmq-{name}-q{r}", 1 << 20, mode, gen) for r in range(1, world)}
+            self.replies = {r: R(f"llmq-{name}-qrep{r}", self.REPLY_RING, mode, gen) for r in range(1, world)}
             self._lock = threading.Lock()
             self._qid = 0
-        else:
-            self.qring = R(f"llmq-{name}-q{rank}", 1 << 20, "open")
-            self.reply = R(f"llmq-{name}-qrep{rank}", self.REPLY_RING, "open")
+        if coll:
+            comm.barrier()                             # rank 0's rings exist
+        if rank != 0:
+            mode = "attach" if coll else "open"
+            self.qring = R(f"llmq-{name}-q{rank}", 1 << 20, mode, gen)
+            self.reply = R(f"llmq-{name}-qrep{rank}", self.REPLY_RING, mode, gen)
+        if coll:
+            comm.barrier()                             # every peer mapped them
+            if rank == 0:
+                for r in list(self.qrings.values()) + list(self.replies.values()):
+                    r.unlink()
+        if rank != 0:
             self._thread = threading.Thread(target=self._serve, name="peer-queries", daemon=True)
             self._thread.start()
 

@@ -80,11 +80,20 @@ def decode_event(b: bytes) -> dict:
 class RingPair:
     """The request ring and the event ring of one gateway deployment."""
 
-    def __init__(self, name: str, capacity: int = 64 << 20, mode: str = "open"):
+    def __init__(self, name: str, capacity: int = 64 << 20, mode: str = "open", gen: int = 0):
+        """``gen`` (job generation, ``parallel.comm.job_token``): "create"
+        stamps it, "attach" refuses a ring of another generation."""
         R = _native.shmring().ShmRing
         self.name = name
-        self.requests = R(f"llmq-{name}-req", capacity, mode)
-        self.events = R(f"llmq-{name}-evt", max(capacity // 4, 1 << 20), mode)
+        self.requests = R(f"llmq-{name}-req", capacity, mode, gen)
+        self.events = R(f"llmq-{name}-evt", max(capacity // 4, 1 << 20), mode, gen)
+
+    def unlink_names(self) -> None:
+        """Remove the rings' names once every process of the job has mapped
+        them (the mappings stay valid): a job that is SIGKILLed then leaves
+        nothing in /dev/shm for a later job to find."""
+        for r in (self.requests, self.events):
+            r.unlink()
 
     # ingress side
     def put_messages(self, msgs: Sequence[Message]) -> int:

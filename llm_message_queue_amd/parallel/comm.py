@@ -419,6 +419,29 @@ class ShmComm(Comm):
         self.data.warm_data_plane()
 
 
+def job_token(comm: Optional[Comm] = None):
+    """``(token, generation)`` naming THIS job incarnation's node-shared
+    segments (front-door rings, peer query rings, load pages).
+
+    ``torch.distributed.run`` with a static rendezvous gives every launch the
+    run id ``"none"``, and a ``--max-restarts`` restart keeps the run id of
+    the incarnation it replaces, so names built from the run id alone let a
+    new job re-attach a dead job's segments -- leftover records, a stale
+    balanced-share ledger (lead a).  The token adds the
+    restart count and a random nonce that rank 0 draws and broadcasts over
+    the control plane before any segment is opened; the nonce is also the
+    generation ``ShmRing`` stamps into (and checks against) its header."""
+    import os
+    import re
+    run = os.environ.get("TORCHELASTIC_RUN_ID") or "solo"
+    restart = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    nonce = (int.from_bytes(os.urandom(8), "little") & ((1 << 62) - 1)) | 1
+    if comm is not None and comm.world > 1:
+        nonce = int(comm.broadcast_i64(np.array([nonce], dtype=np.int64), root=0)[0])
+    safe = re.sub(r"[^A-Za-z0-9_.-]", "_", run)[:32]
+    return f"{safe}.{restart}.{nonce:x}", nonce
+
+
 def single_node() -> bool:
     """Every rank of the job on this node (torchrun's LOCAL_WORLD_SIZE)."""
     import os

@@ -1,27 +1,73 @@
 """Serve-loop stall watchdog (``server.stall_dump_after``)."""
 
 
-def test_stall_watchdog_dumps_stacks_once(capfd):
-    """``server.stall_dump_after``: no tick while requests wait -> one error
-    log and every thread's stack on stderr (what a hung rank was doing)."""
+def _watchdog_app(dump_s, fatal_s, pending=3):
     import threading
-    import time
     from types import SimpleNamespace
     from llm_message_queue_amd.gateway.app import GatewayApp
     from llm_message_queue_amd.utils.config import default_config
     cfg = default_config()
-    cfg.server.stall_dump_after = 200_000_000          # 0.2 s
+    cfg.server.stall_dump_after = int(dump_s * 1e9)
+    cfg.server.stall_fatal_after = int(fatal_s * 1e9)
     logged = []
-    gw = SimpleNamespace(counters={"ticks": 7}, pending=lambda: 3, engine=None, rank=0)
-    app = SimpleNamespace(gateway=gw, cfg=cfg, _stop=threading.Event(),
-                          log=SimpleNamespace(error=lambda msg, **kw: logged.append((msg, kw))))
+    door = []
+
+    class App(SimpleNamespace):
+        _set_stalled = GatewayApp._set_stalled
+        health = GatewayApp.health
+
+    gw = SimpleNamespace(counters={"ticks": 7}, pending=lambda: pending, inbox_size=lambda: 0,
+                         preprocessing=lambda: 0, engine=None, rank=0)
+    app = App(gateway=gw, cfg=cfg, _stop=threading.Event(), stalled="", fatal=None,
+              front_door=SimpleNamespace(set_health=lambda ok, reason="": door.append((ok, reason))),
+              log=SimpleNamespace(error=lambda msg, **kw: logged.append((msg, kw))))
     th = threading.Thread(target=GatewayApp._stall_watchdog, args=(app,), daemon=True)
+    return app, th, logged, door
+
+
+def test_stall_watchdog_dumps_stacks_once(capfd):
+    """``server.stall_dump_after``: no tick while requests wait -> one error
+    log and every thread's stack on stderr (what a hung rank was doing), and
+    /health (the app's and the C++ front door's) reports the stall."""
+    import time
+    app, th, logged, door = _watchdog_app(0.2, 0)
+    th.start()
+    time.sleep(0.8)
+    assert app.health()[0] is False and "stalled" in app.health()[1]
+    assert door and door[-1][0] is False
+    app.gateway.counters["ticks"] += 1                 # ticks resume: healthy again
+    time.sleep(0.12)                                   # (< stall_dump_after: not stalled anew yet)
+    assert app.health() == (True, "") and door[-1] == (True, "")
+    app._stop.set()
+    th.join(2)
+    assert len(logged) >= 1 and logged[0][1]["waiting"] == 3
+    assert app.fatal is None                           # stall_fatal_after 0: never fatal
+    assert "_stall_watchdog" in capfd.readouterr().err   # the dump names the watchdog's own frame
+
+
+def test_stall_watchdog_fatal_after_threshold():
+    """``server.stall_fatal_after``: a stall that lasts is fatal -- the app
+    records it (cli serve exits non-zero for a restart) and stops."""
+    import time
+    app, th, logged, _door = _watchdog_app(0.1, 0.5)
+    t0 = time.monotonic()
+    th.start()
+    th.join(5)
+    assert not th.is_alive() and 0.4 < time.monotonic() - t0 < 3
+    assert isinstance(app.fatal, RuntimeError) and "stall_fatal_after" in str(app.fatal)
+    assert app._stop.is_set() and app.health()[0] is False
+    assert [m for m, _ in logged][-1].startswith("serve loop stall is fatal")
+
+
+def test_stall_watchdog_ignores_an_idle_loop():
+    """No request waiting: an idle loop that sleeps is no stall."""
+    import time
+    app, th, logged, _door = _watchdog_app(0.1, 0.3, pending=0)
     th.start()
     time.sleep(0.8)
     app._stop.set()
     th.join(2)
-    assert len(logged) == 1 and logged[0][1]["waiting"] == 3
-    assert "_stall_watchdog" in capfd.readouterr().err   # the dump names the watchdog's own frame
+    assert app.fatal is None and not logged and app.health() == (True, "")
 
 
 def test_engine_step_timeout_raises_backend_hung():
