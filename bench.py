@@ -58,6 +58,9 @@ def parse(argv=None):
     ap.add_argument("--token-budget-by-rank", default="",
                     help="lock-step experiments: per-rank token budget overrides, e.g. '1:2048' (rank 1 takes "
                          "half-size steps)")
+    ap.add_argument("--realtime-step-tokens", type=int, default=0,
+                    help="cap a step at this many tokens while a realtime request is in the batch (A/B of "
+                         "backend.realtime_step_tokens; 0 = off)")
     ap.add_argument("--gen-tokens", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=2, help="forward steps queued ahead on the GPU")
     ap.add_argument("--aging-ms", default="50,100,150,200",
@@ -73,6 +76,14 @@ def parse(argv=None):
     ap.add_argument("--slo-backoff", default="0.98,0.95,0.9,0.85,0.75",
                     help="utilisations re-served (in order, same process) when the window at --util misses the "
                          "operating point; value = req/s at the highest one that held it (0 if none did)")
+    ap.add_argument("--slo-climb", default="1.0,1.02,1.04",
+                    help="utilisations tried next (in order, same process) while the window at --util and every "
+                         "later one HOLD the operating point; the headline is the best window that held it.  '' = "
+                         "no climb (VERDICT r4 weak #4: a search that only backs off caps the headline below what "
+                         "the SLO allows)")
+    ap.add_argument("--slo-budget-s", type=float, default=150.0,
+                    help="wall-time bound of the SLO search: no further window starts once the search has used "
+                         "this long minus one window's duration")
     ap.add_argument("--test-miss-above-util", type=float, default=0.0, help=argparse.SUPPRESS)
     ap.add_argument("--steady-ticks", type=int, default=-1,
                     help="untimed serving ticks at the offered rate before the timed window, so it starts in "
@@ -108,8 +119,13 @@ def parse(argv=None):
                          "forward as a simulated device clock) at the serving config's slots / token budget -- "
                          "for studying multi-GPU dynamics (lock-step vs GPU speed spread) without the GPUs")
     ap.add_argument("--pin-cpu", action="store_true",
-                    help="pin rank r to CPU core r (mod the core count) -- CPU-rehearsal hygiene: separates "
-                         "scheduler migrations / contention from design costs in --cpu-dry-run --sim-gpu runs")
+                    help="with --cpu-dry-run: pin rank r to CPU core r (mod the core count) -- CPU-rehearsal "
+                         "hygiene for --sim-gpu runs; on GPUs: the same as --cpu-bind gpu")
+    ap.add_argument("--cpu-bind", default="auto", choices=["auto", "gpu", "core", "off"],
+                    help="host placement of each rank (parallel/placement.py): gpu = the physical cores of its "
+                         "GPU's socket (sysfs local_cpulist), split evenly among the ranks on that socket, for "
+                         "every thread of the rank and its front-door feeder; auto = gpu when the job has more "
+                         "than one rank (a one-GPU run stays as launched); core = rank r -> core r; off")
     ap.add_argument("--no-extra-steps", action="store_true",
                     help="multi-rank A/B: never launch an extra local forward while the peers are still "
                          "behind at the per-tick exchange (pure lock-step)")
@@ -212,7 +228,7 @@ def main(argv=None) -> int:
         return 3
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if a.pin_cpu and hasattr(os, "sched_setaffinity"):
+    if a.pin_cpu and a.cpu_dry_run and hasattr(os, "sched_setaffinity"):
         cores = sorted(os.sched_getaffinity(0))
         os.sched_setaffinity(0, {cores[int(os.environ.get("LOCAL_RANK", rank)) % len(cores)]})
     # rank 0 starts the front-door feeder process before anything here
@@ -248,9 +264,14 @@ def main(argv=None) -> int:
         local = local_device_index()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
+        # every thread of this rank (and rank 0's feeder process) on its GPU's
+        # socket, before the serving threads start (they inherit it)
+        from llm_message_queue_amd.parallel.placement import bind_rank
+        binding = bind_rank("gpu" if a.pin_cpu else a.cpu_bind,
+                            extra_pids=[door.proc.pid] if door is not None and door.proc is not None else ())
         comm = init_from_env(control=a.control_plane)
     comm_kind = "solo" if world == 1 else str(getattr(comm, "backend", a.control_plane))
-    evidence = comm_evidence(comm, dev, world, dry)
+    evidence = comm_evidence(comm, dev, world, dry, binding=None if dry else binding)
 
     def dsync():
         if not dry:
@@ -293,7 +314,7 @@ def main(argv=None) -> int:
                                fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
                                fused_head=False if a.no_fused_head else None,
                                fused_resid=True if a.fused_resid else None,
-                               prune_last=not a.no_prune_last)
+                               prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -557,16 +578,42 @@ def main(argv=None) -> int:
     # reports the highest one that held the SLO.  Every rank takes the same
     # decision (the latency summary is all-gathered), so the collective
     # counts stay aligned.
-    utils = [a.util] + [u for u in (float(x) for x in a.slo_backoff.split(",") if x) if u < a.util]
+    # Both directions: a first window that holds the SLO climbs through
+    # --slo-climb while every window keeps holding it; one that misses backs
+    # off through --slo-backoff.  The headline is the best window that held
+    # it (its value is still capped by what was dispatched AND what arrived
+    # in the window).  The decision inputs are all-gathered, so every rank
+    # runs the same windows.
+    backoff = [u for u in (float(x) for x in a.slo_backoff.split(",") if x) if u < a.util]
+    climb = [u for u in (float(x) for x in a.slo_climb.split(",") if x) if u > a.util]
     tried = []
-    res = None
-    for k, u in enumerate(utils):
+    best = res = None
+    t_search = time.monotonic()
+    utils = [a.util]
+    k = 0
+    while utils:
+        u = utils.pop(0)
+        t_w = time.monotonic()
         res = window(u, k)
+        k += 1
         tried.append({"util": round(u, 4), "value": round(res["value"], 2), "met": res["met"],
                       "p99_ms": round(res["lat"]["p99_ms"], 3),
-                      "p99_by_tier_ms": [round(x, 3) for x in res["lat"]["p99_by_tier_ms"]]})
-        if res["met"]:
+                      "p99_by_tier_ms": [round(x, 3) for x in res["lat"]["p99_by_tier_ms"]],
+                      "p99_e2e_by_tier_ms": [round(x, 3) for x in res["lat_done"]["p99_by_tier_ms"]],
+                      "window_s": round(time.monotonic() - t_w, 2)})
+        if res["met"] and (best is None or res["value"] > best["value"]):
+            best = res
+        if k == 1:
+            up = bool(res["met"])
+            utils = list(climb) if up else list(backoff)
+        elif res["met"] != up:
+            break                         # climbed past the knee / backed off into the SLO
+        # bounded wall time: another window must fit (the slowest one so far)
+        over = time.monotonic() - t_search + max(t["window_s"] for t in tried) > a.slo_budget_s
+        if int(comm.all_gather_i64(np.array([int(over)], dtype=np.int64)).max()):
             break
+    if best is not None:
+        res = best
     gc.enable()
     if door is not None:
         comm.barrier()
@@ -576,7 +623,8 @@ def main(argv=None) -> int:
     acct = res["acct"]
     value = res["value"] if res["met"] else 0.0
     slo = {"util_tried": [t["util"] for t in tried], "attempts": tried,
-           "value_util": round(res["util"], 4) if res["met"] else None}
+           "value_util": round(res["util"], 4) if res["met"] else None,
+           "search_s": round(time.monotonic() - t_search, 1), "directions": "climb + backoff"}
     if not res["met"]:
         slo["reason"] = (f"no utilisation in {slo['util_tried']} held p99 <= {P99_TARGET_MS} ms (all tiers) and "
                          f"realtime p99 <= {REALTIME_P99_TARGET_MS} ms; value is 0 by construction")
@@ -601,6 +649,7 @@ def main(argv=None) -> int:
                    "token_budget_by_rank": a.token_budget_by_rank or None,
                    "sim_gpu": a.sim_gpu or None, "extra_steps": not a.no_extra_steps,
                    "control_plane": comm_kind, "token_budget": a.token_budget,
+                   "realtime_step_tokens": a.realtime_step_tokens,
                    "gen_tokens": a.gen_tokens, "prompt_cap": a.prompt_cap, "inflight": a.inflight,
                    "aging_ms": a.aging_ms, "util": round(res["util"], 4),
                    "classifier": not a.no_classifier, "residual_in_gemm": not a.no_residual_gemm,
@@ -610,6 +659,9 @@ def main(argv=None) -> int:
                    "fused_head": bool(engine.model.fused_head),
                    "fused_resid": bool(engine.model.fused_resid),
                    "prune_last": bool(getattr(engine.model, "prune_last", False))},
+        # realtime tier, arrival -> LAST generated token (the 8B backend's 4
+        # forwards included); the headline's clock is arrival -> dispatch
+        "realtime_p99_e2e_ms": round(lat_done["p99_by_tier_ms"][0], 3),
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),
         "p99_enqueue_to_dispatch_ms": round(lat["p99_enq_ms"], 3),

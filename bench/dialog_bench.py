@@ -64,6 +64,9 @@ def parse(argv=None):
     ap.add_argument("--sim-gpu", default="",
                     help="with --cpu-dry-run: per-rank relative GPU speeds (SimEngine at the serving config)")
     ap.add_argument("--control-plane", default="shm", choices=["shm", "gloo", "nccl"])
+    ap.add_argument("--cpu-bind", default="auto", choices=["auto", "gpu", "core", "off"],
+                    help="host placement of each rank (parallel/placement.py; auto = its GPU's socket cores "
+                         "when the job has more than one rank)")
     return ap.parse_args(argv)
 
 
@@ -104,8 +107,10 @@ def main(argv=None) -> int:
         local = local_device_index()
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
+        from llm_message_queue_amd.parallel.placement import bind_rank
+        binding = bind_rank(a.cpu_bind)              # this rank's threads on its GPU's socket
         comm = init_from_env(control=a.control_plane)
-    evidence = comm_evidence(comm, dev, world, dry)
+    evidence = comm_evidence(comm, dev, world, dry, binding=None if dry else binding)
 
     def dsync():
         if not dry:

@@ -301,15 +301,19 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None,
 
     @app.delete("/api/v1/messages/{mid}")
     def delete_message(mid: str):
+        # queued: removed from its queue; running on a GPU: aborted there
+        # (its batch slot freed), on whichever rank popped it
         m = G.messages.get(mid)
         if m is None:
             res = G.peers.first("remove", [mid]) if G.peers is not None else None
             if isinstance(res, dict):
-                return {"status": "deleted", "message_id": mid, "dequeued": bool(res.get("dequeued"))}
+                return {"status": "deleted", "message_id": mid, "dequeued": bool(res.get("dequeued")),
+                        "cancelled": bool(res.get("cancelled"))}
             return _err(404, "Message not found")
         removed = m.queue_name and G.standard.has_queue(m.queue_name) and G.standard.remove_message(m.queue_name, m)
+        cancelled = "" if removed else (G.cancel_inflight(m) if hasattr(G, "cancel_inflight") else "")
         G.messages.remove(mid)
-        return {"status": "deleted", "message_id": mid, "dequeued": bool(removed)}
+        return {"status": "deleted", "message_id": mid, "dequeued": bool(removed), "cancelled": bool(cancelled)}
 
     # ------------------------------------------------------------------ conversations
     @app.post("/api/v1/conversations")

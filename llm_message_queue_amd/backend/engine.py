@@ -58,6 +58,8 @@ class Request:
     conv: int = -1                # conversation key: its KV stays resident in the slot between turns
     reused: int = 0               # context tokens served from the resident KV (not re-prefilled)
     history: Optional[np.ndarray] = None   # earlier dialog tokens, prefilled only if not resident
+    timeout_ns: int = 0           # processing timeout of this attempt (0: none); the deadline starts at admission
+    deadline_ns: int = 0          # admitted_ns + timeout_ns (monotonic), set by ``admit``
 
 
 @dataclass
@@ -99,7 +101,8 @@ class BackendEngine:
                  token_budget: int = 2048, device="cuda", impl: str = "hip", seed: int = 0,
                  page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True,
                  split_qkv: bool = False, fused_mlp=None, fused_qkv=None, row_scale_norm: bool = True,
-                 fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0):
+                 fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
+                 realtime_step_tokens: int = 0):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
         self.step_timeout_s = float(step_timeout_s)
@@ -108,6 +111,13 @@ class BackendEngine:
         # every generating slot gets its decode token each step (the on-device
         # token gather reads the previous step's output only)
         self.token_budget = max(token_budget, slots)
+        # realtime step cap (``backend.realtime_step_tokens``, 0 = off): while
+        # a realtime-lane request (tier < fast_tiers) is in the batch, a step
+        # carries at most this many tokens (never fewer than its decode rows),
+        # so the 4 forwards a realtime request needs finish sooner -- at the
+        # price of the smaller steps' GEMM efficiency for everyone in them
+        # (measured: profiles/r5_step_budget_sweep_1gpu.jsonl)
+        self.rt_step_tokens = int(realtime_step_tokens)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.async_device = self.cuda          # forwards run asynchronously (a GPU stream)
@@ -143,6 +153,14 @@ class BackendEngine:
         self.s_out_idx = np.zeros(slots, dtype=np.int64)    # row of my last token in the step output
         self.s_out_step = np.full(slots, -2, dtype=np.int64)
         self.s_active = np.zeros(slots, dtype=bool)
+        self.s_tier = np.zeros(slots, dtype=np.int64)
+        # processing deadline per slot (monotonic ns, 0 = none): a request
+        # still running past it is aborted by ``expire`` (the reference runs
+        # every message under context.WithTimeout(msg.Timeout),
+        # `internal/priorityqueue/worker.go:162-188`)
+        self.s_deadline = np.zeros(slots, dtype=np.int64)
+        self.expired_total = 0
+        self.cancelled_total = 0
         self._admit_seq = 0
         self._mean_plen = 16.0                              # EMA of admitted prompt lengths
         # realtime lane: requests of tiers < fast_tiers are prefilled ahead of
@@ -225,7 +243,7 @@ class BackendEngine:
             return 0
         act = self.s_active
         pending = int((self.s_plen[act] - self.s_pref[act]).sum())
-        head = self.token_budget - int(act.sum()) - pending
+        head = self.step_budget() - int(act.sum()) - pending
         if head <= 0:
             return 0
         # round UP: the last admitted prompt may spill into the following step
@@ -315,7 +333,20 @@ class BackendEngine:
         if not act.any():
             return 0
         plen, pref = self.s_plen[act], self.s_pref[act]
-        return min(self.token_budget, int((pref >= plen).sum()) + int((plen - pref).clip(min=0).sum()))
+        return min(self.step_budget(), int((pref >= plen).sum()) + int((plen - pref).clip(min=0).sum()))
+
+    def step_budget(self) -> int:
+        """Tokens the next step may carry: ``token_budget``, or the realtime
+        cap while a realtime-lane request is active (at least one more than
+        the decode rows, which every step must carry)."""
+        cap = self.rt_step_tokens
+        if cap <= 0 or cap >= self.token_budget or not self.active:
+            return self.token_budget
+        act = self.s_active
+        if not (act & (self.s_tier < self.fast_tiers)).any():
+            return self.token_budget
+        dec = int((self.s_pref[act] >= self.s_plen[act]).sum())
+        return max(cap, dec + 1)
 
     def lane_capacity(self) -> int:
         """Slots a realtime request may take beyond ``admit_capacity``: every
@@ -361,6 +392,8 @@ class BackendEngine:
             r.generated = 0
             r.out_idx = r.out_step = -1
             r.admitted_ns = now
+            r.deadline_ns = now + int(r.timeout_ns) if r.timeout_ns > 0 else 0
+            self.s_deadline[s] = r.deadline_ns
             self.active[s] = r
             n = len(r.prompt)
             self.s_prompt[s, base:base + n] = r.prompt
@@ -372,10 +405,60 @@ class BackendEngine:
             self.s_seq[s] = self._admit_seq - (1 << 48 if 0 <= r.tier < self.fast_tiers else 0)
             self._admit_seq += 1
             self.s_active[s] = True
+            self.s_tier[s] = r.tier
             self.s_conv[s] = r.conv
             self.kv_reused_tokens += base
             self._mean_plen += 0.01 * (n - self._mean_plen)
             out.append(r)
+        return out
+
+    # ------------------------------------------------------------------ abort (timeout / cancel)
+    def _abort_slots(self, slots) -> List[Request]:
+        """Take the active requests of ``slots`` out of the batch: their slots
+        return to the free list for the NEXT launch.  Steps already queued on
+        the GPU still compute their rows; a request admitted into the slot
+        afterwards is prefilled by a later step on the same stream, so stream
+        order keeps it from reading anything the aborted request wrote.  The
+        aborted turn's KV is partial, so it is never parked for reuse."""
+        out = []
+        for s in slots:
+            s = int(s)
+            r = self.active.pop(s, None)
+            if r is None:
+                continue
+            self.s_active[s] = False
+            self.s_deadline[s] = 0
+            self.s_conv[s] = -1
+            self.s_cached[s] = 0
+            self.free.append(s)                # reused first (``_take_slot`` pops from the end)
+            out.append(r)
+        return out
+
+    def expire(self, now_ns: Optional[int] = None) -> List[Request]:
+        """Abort every active request whose processing deadline
+        (``Request.timeout_ns`` after admission) has passed; returns them so
+        the caller can retry or dead-letter them.  Requests whose last token
+        is already launched completed at that launch and are not touched."""
+        if not self.active:
+            return []
+        now = time.monotonic_ns() if now_ns is None else int(now_ns)
+        d = self.s_deadline
+        hit = np.flatnonzero(self.s_active & (d > 0) & (d < now))
+        if not len(hit):
+            return []
+        out = self._abort_slots(hit)
+        self.expired_total += len(out)
+        return out
+
+    def cancel(self, req_ids: Sequence[int]) -> List[Request]:
+        """Abort the active requests with these ids (``DELETE
+        /api/v1/messages/{id}`` on a request in flight); returns the ones
+        found (a request that completed or was never admitted is not)."""
+        want = {int(x) for x in req_ids}
+        if not want or not self.active:
+            return []
+        out = self._abort_slots([s for s, r in self.active.items() if r.req_id in want])
+        self.cancelled_total += len(out)
         return out
 
     # ------------------------------------------------------------------ step
@@ -395,7 +478,7 @@ class BackendEngine:
         if len(pre):
             pre = pre[np.argsort(self.s_seq[pre], kind="stable")]
         rem = self.s_plen[pre] - self.s_pref[pre]
-        budget = self.token_budget - D
+        budget = self.step_budget() - D
         before = np.cumsum(rem) - rem
         take = np.clip(budget - before, 0, rem)
         keep = take > 0
@@ -525,6 +608,7 @@ class BackendEngine:
         self._prev_out = None
         self.active.clear()
         self.s_active[:] = False
+        self.s_deadline[:] = 0
         self.conv_lru.clear()
         self._importing.clear()
         self.s_conv[:] = -1

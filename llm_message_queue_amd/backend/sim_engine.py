@@ -29,17 +29,26 @@ SIM_MODEL = LlamaConfig(vocab=512, dim=64, layers=1, heads=2, kv_heads=1, ffn=12
 
 
 class _SimEvent:
-    """End of one simulated step (monotonic ns)."""
+    """End of one simulated step (monotonic ns, or a ``VirtualClock``'s)."""
 
-    __slots__ = ("start_ns", "due_ns")
+    __slots__ = ("start_ns", "due_ns", "clock")
 
-    def __init__(self, start_ns: int, due_ns: int):
-        self.start_ns, self.due_ns = start_ns, due_ns
+    def __init__(self, start_ns: int, due_ns: int, clock=None):
+        self.start_ns, self.due_ns, self.clock = start_ns, due_ns, clock
 
     def query(self) -> bool:
-        return time.monotonic_ns() >= self.due_ns
+        c = self.clock
+        if c is None:
+            return time.monotonic_ns() >= self.due_ns
+        if c.now_ns() >= self.due_ns:
+            return True
+        c.poll()                                  # the host's poll interval passes
+        return c.now_ns() >= self.due_ns
 
     def synchronize(self) -> None:
+        if self.clock is not None:
+            self.clock.advance_to(self.due_ns)
+            return
         d = self.due_ns - time.monotonic_ns()
         if d > 0:
             time.sleep(d / 1e9)
@@ -56,7 +65,9 @@ class _SimStart:
 class SimEngine(BackendEngine):
     def __init__(self, *, speed: float = 1.0, tile_ms: float = 2.5, base_ms: float = 1.5,
                  slots: int = 1536, max_ctx: int = 512, token_budget: int = 4096, max_inflight: int = 2,
-                 page=None, gpu_index: int = 0, seed: int = 0):
+                 page=None, gpu_index: int = 0, seed: int = 0, clock=None):
+        """``clock``: a ``parallel.comm.VirtualClock`` (deterministic tests:
+        the device runs in simulated time); None = wall time."""
         super().__init__(SIM_MODEL, slots=slots, max_ctx=max_ctx, token_budget=token_budget, device="cpu",
                          impl="ref", seed=seed, page=page, gpu_index=gpu_index, max_inflight=max_inflight)
         if speed <= 0:
@@ -64,6 +75,7 @@ class SimEngine(BackendEngine):
         self.speed = float(speed)
         self.tile_ms, self.base_ms = float(tile_ms), float(base_ms)
         self._dev_free_ns = 0
+        self.clock = clock
         self.async_device = True                   # the simulated device runs steps asynchronously
         self.model.forward = self._forward          # the host never computes a forward
 
@@ -80,11 +92,14 @@ class SimEngine(BackendEngine):
     def _start_event(self):
         return _SimStart() if self.time_steps else None
 
+    def _now(self) -> int:
+        return self.clock.now_ns() if self.clock is not None else time.monotonic_ns()
+
     def _end_event(self, T: int, timing: bool):
-        now = time.monotonic_ns()
+        now = self._now()
         start = max(now, self._dev_free_ns)
         self._dev_free_ns = start + int(self.step_ms(T) * 1e6)
-        return _SimEvent(start, self._dev_free_ns)
+        return _SimEvent(start, self._dev_free_ns, self.clock)
 
     def device_idle(self) -> bool:
-        return time.monotonic_ns() >= self._dev_free_ns
+        return self._now() >= self._dev_free_ns

@@ -52,7 +52,8 @@ def _build_engine(cfg, model: str, device, job: str = ""):
                       torch.cuda.get_device_properties(device).total_memory)
     return BackendEngine(mcfg, slots=slots, max_ctx=cfg.backend.max_ctx,
                          token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank,
-                         step_timeout_s=cfg.backend.step_timeout / 1e9), page
+                         step_timeout_s=cfg.backend.step_timeout / 1e9,
+                         realtime_step_tokens=cfg.backend.realtime_step_tokens), page
 
 
 def fit_slots(mcfg, slots: int, max_ctx: int, reserve_gb: float, total_bytes: int) -> int:
@@ -176,6 +177,11 @@ def cmd_serve(a, role: str = "serve") -> int:
     if use_gpu and role in ("serve", "queue-manager"):
         local = local_device_index()
         torch.cuda.set_device(local)
+        from ..parallel.placement import bind_rank
+        binding = bind_rank(cfg.gpu.cpu_bind)    # before the serving threads start (they inherit it)
+        if binding.get("cpus"):
+            print(json.dumps({"event": "cpu_binding", "rank": rank, **{k: v for k, v in binding.items()
+                                                                       if k != "shared_with"}}), flush=True)
         engine, page = _build_engine(cfg, a.model, torch.device("cuda", local), job)
         engine.warm_shapes()      # cold-start GEMM shapes before the first request (idle -> busy)
     elif cpu_ranks and role in ("serve", "queue-manager"):

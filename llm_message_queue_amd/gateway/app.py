@@ -339,7 +339,7 @@ class GatewayApp:
         gateway's health (unhealthy evacuates the backend, healthy re-admits)."""
         self.lb.update_endpoint_status(eid, status)
         if self.engine is not None and eid == f"gpu{self.gateway.rank}":
-            self.gateway.set_healthy(status == "healthy", f"operator set {status}")
+            self.gateway.set_healthy(status == "healthy", f"operator set {status}", failure=False)
 
     def _gpu_unhealthy(self, gpu: int, reason: str) -> None:
         """Telemetry callback (ECC / amd-smi failure)."""
@@ -545,7 +545,7 @@ class GatewayApp:
                 return False
             removed = bool(m.queue_name and self.standard.has_queue(m.queue_name)
                            and self.standard.remove_message(m.queue_name, m))
-            return {"dequeued": removed}
+            return {"dequeued": removed, "cancelled": bool(not removed and self.cancel_inflight(m))}
         if op == "stats":
             return self._rank_stats()
         if op == "reset_latency":
@@ -604,6 +604,18 @@ class GatewayApp:
             got = self.peers.first("dlq", [action, mid])
             return got if got is not None else False
         return res
+
+    def cancel_inflight(self, m: Message, timeout_s: float = 1.5) -> str:
+        """Abort ``m`` if it runs on a GPU (``DELETE /api/v1/messages/{id}``
+        on a dispatched request): "cancelled" (aborted on this rank's GPU,
+        its slot freed), "forwarded" (the GPU running it was told to abort it
+        at the next exchange) or "" (not in flight from here)."""
+        if self.engine is None or m.status != MessageStatus.PROCESSING:
+            return ""
+        try:
+            return self.gateway.request_cancel(m).result(timeout=timeout_s)
+        except Exception:                      # noqa: BLE001 -- serve loop busy / stopping: not cancelled
+            return ""
 
     def _dequeue_local(self, queue_type: str, mid: str) -> bool:
         mgr = self.factory.get_queue_manager(queue_type)

@@ -156,8 +156,13 @@ class StageRecorder:
 # --------------------------------------------------------------------------- descriptors
 K_DISPATCH, K_DONE, K_FAIL = 1, 2, 3     # K_FAIL: an evacuating backend hands a request back
 K_MIGRATE = 4       # [kind, conv lo/hi, dest]: to a conversation's home GPU -- send its KV to dest this tick
-DESC_HDR = 16       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
-#                    dialog history length, decision - enq (us)]; flags = (home GPU + 1) | KV_MIGRATE
+# a backend aborted a request in flight: its processing deadline passed /
+# its origin cancelled it (completion-record layout, owed like K_DONE)
+K_TIMEOUT, K_CANCELLED = 5, 6
+K_CANCEL = 7        # [kind, handle lo/hi, origin]: origin -> the GPU running its request: abort it
+DESC_HDR = 17       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
+#                    dialog history length, decision - enq (us), processing timeout (ms)];
+#                    flags = (home GPU + 1) | KV_MIGRATE
 KV_MIGRATE = 1 << 8     # descriptor flag: hold the turn until its KV arrives from the home GPU
 
 
@@ -275,7 +280,24 @@ class Gateway:
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
                          "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0, "realtime_local": 0,
-                         "extra_steps": 0, "extra_admitted": 0, "retried": 0, "retry_exhausted": 0}
+                         "extra_steps": 0, "extra_admitted": 0, "retried": 0, "retry_exhausted": 0,
+                         "inflight_timeout": 0, "cancelled": 0}
+        # In-flight processing timeout: the reference runs every message under
+        # context.WithTimeout(msg.Timeout) and retries / dead-letters it on
+        # expiry (`internal/priorityqueue/worker.go:162-188, 202-239`).  Here a
+        # request's attempt gets ``Message.timeout`` (30 s default, D16) from
+        # its admission into a GPU slot; the engine aborts it past that (slot
+        # freed for the next admission) and it takes the retry path.
+        # ``queue.inflight_timeout`` off: admitted requests always run out.
+        self.inflight_timeout = bool(getattr(q, "inflight_timeout", True))
+        self._expire_next_ns = 0
+        # cancellation of a request in flight (DELETE /api/v1/messages/{id}):
+        # API / peer threads queue (message, Future); the serve loop aborts it
+        # on its own GPU or sends K_CANCEL to the GPU running it
+        self._cancel_lock = threading.Lock()
+        self._cancel_req: List[Tuple[Message, object]] = []
+        self._cancel_out: Dict[int, List[int]] = {}     # dest GPU -> handles to abort there
+        self._cancel_pub: Dict[int, List[int]] = {}     # ... announced in this tick's load vector
         # overload shedding (expire_queued) -> dead-letter queue
         self.shed_expired = bool(getattr(q, "shed_expired", True))
         # realtime lane (tier 0 admitted past the step's prefill headroom and
@@ -517,7 +539,10 @@ class Gateway:
         ck = conv_key(m.conversation_id) if self.kv_residency else -1
         hist = self.conv_hist.get(m.conversation_id) if m.conversation_id else None
         return Request(req_id=m.handle, prompt=p, gen_tokens=self.gen_tokens, tier=tier, meta=m, conv=ck,
-                       history=hist)
+                       history=hist, timeout_ns=self._timeout_ns(m))
+
+    def _timeout_ns(self, m: Message) -> int:
+        return int(m.timeout) if (self.inflight_timeout and m.timeout and m.timeout > 0) else 0
 
     def _remember_dialog(self, m: Message, gpu: int) -> None:
         """Completion of a conversation turn: its home GPU (KV residency) and
@@ -610,7 +635,9 @@ class Gateway:
 
     @staticmethod
     def _expired(m: Message, now: int) -> bool:
-        t0 = m.arrival_ns or m.enqueued_at
+        # a retried request (backend failure, processing timeout) gets a fresh
+        # queue deadline from its requeue: its first deadline has passed
+        t0 = (m.enqueued_at if m.retry_count > 0 else 0) or m.arrival_ns or m.enqueued_at
         return bool(m.timeout > 0 and t0 and now - t0 > m.timeout)
 
     def _shed(self, out: List[Message]) -> None:
@@ -851,6 +878,9 @@ class Gateway:
         free = max(0, eng.admit_capacity() - held) if up else 0
         slots_free = max(0, eng.lane_capacity() - held) if (up and self.realtime_lane) else free
         if W > 1:
+            # cancels for requests running on other GPUs: announced now (row
+            # counts in L_MIGC), sent in this tick's all_to_all
+            self._cancel_pub, self._cancel_out = self._cancel_out, {}
             # EWMA (alpha 0.25) of own enqueues per tick -> this tick's reserve
             a = 0.25
             self._enq_ewma = [(1 - a) * e + a * n for e, n in zip(self._enq_ewma, self._enq_tick)]
@@ -884,7 +914,8 @@ class Gateway:
             slots_free=slots_free, slots_total=eng.slots if eng is not None else 0,
             exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
             weights=self._weights(),
-            migrate_rows=[sum(1 for _, h, _ in self._mig_out if h == j and j != self.rank) for j in range(W)],
+            migrate_rows=[sum(1 for _, h, _ in self._mig_out if h == j and j != self.rank)
+                          + (len(self._cancel_pub.get(j, ())) if j != self.rank else 0) for j in range(W)],
             migrate_busy=bool(self._mig_out) or bool(self._await_kv),
             kv_tokens=kv_tok, kv_capacity=kv_cap)
 
@@ -994,11 +1025,19 @@ class Gateway:
             if rows and self.lb is not None:
                 self.lb.note_dispatch(f"gpu{j}", len(rows))
             mig_rows = [(c, d) for c, h, d in orders_prev if h == j] if j != me else []
-            if mig_rows:
-                extra = np.zeros((len(mig_rows), width), dtype=np.int32)
-                extra[:, 0] = K_MIGRATE
-                _put64(extra, 1, [c for c, _d in mig_rows])
-                extra[:, 3] = [d for _c, d in mig_rows]
+            can = self._cancel_pub.get(j, []) if j != me else []
+            if mig_rows or can:
+                extra = np.zeros((len(mig_rows) + len(can), width), dtype=np.int32)
+                nm = len(mig_rows)
+                if nm:
+                    extra[:nm, 0] = K_MIGRATE
+                    _put64(extra[:nm], 1, [c for c, _d in mig_rows])
+                    extra[:nm, 3] = [d for _c, d in mig_rows]
+                if can:
+                    ec = extra[nm:]
+                    ec[:, 0] = K_CANCEL
+                    _put64(ec, 1, can)
+                    ec[:, 3] = me
             recs = self._done_owed[j]
             if recs:
                 # completion records: (handle, tier, admitted ns, done ns, kind)
@@ -1011,12 +1050,13 @@ class Gateway:
                 _put64(d, 5, a[:, 2])
                 _put64(d, 7, a[:, 3])
             self._done_owed[j] = []
-            send.append(np.concatenate([buf, extra]) if mig_rows else buf)
+            send.append(np.concatenate([buf, extra]) if (mig_rows or can) else buf)
             if j != me:
                 self.counters["remote_sent"] += len(rows)
         recv_counts = [int(quota[i, me].sum()) + int(loads[i, planner.L_DONE + me])
                        + int(loads[i, planner.L_MIGC + me]) if i != me else 0 for i in range(W)]
         send[me] = np.zeros((0, width), dtype=np.int32)
+        self._cancel_pub = {}
         tc0 = time.perf_counter_ns()
         pend = self.comm.all_to_all_rows_async(send, recv_counts, width)
         self._overlap(pend)
@@ -1051,6 +1091,11 @@ class Gateway:
                 self._remote_done_rows(done)
             for row in g[kinds == K_FAIL]:
                 self._remote_fail(row)
+            for row in g[(kinds == K_TIMEOUT) | (kinds == K_CANCELLED)]:
+                self._remote_abort(row)
+            can = g[kinds == K_CANCEL]
+            if len(can):
+                self._cancel_foreign(src, _get64(can, 1))
             mig = g[kinds == K_MIGRATE]
             if len(mig):
                 src_orders.extend((int(c), me, int(d)) for c, d in zip(_get64(mig, 1), mig[:, 3]))
@@ -1256,6 +1301,7 @@ class Gateway:
             # records the decision -> admission hand-off stage)
             small[k, 4] = min(0x7FFFFFFF, max(0, (m.popped_ns - m.enqueued_at) // 1000)) \
                 if (m.popped_ns and m.enqueued_at) else 0
+            small[k, 5] = min(0x7FFFFFFF, self._timeout_ns(m) // 1_000_000)
         buf[:, 0] = K_DISPATCH
         _put64(buf, 1, v[:, 0])
         buf[:, 3] = origin
@@ -1268,6 +1314,7 @@ class Gateway:
         _put64(buf, 12, v[:, 3])
         buf[:, 14] = small[:, 3]
         buf[:, 15] = small[:, 4]
+        buf[:, 16] = small[:, 5]
         for k, p in enumerate(prompts):
             if len(p):
                 buf[k, DESC_HDR:DESC_HDR + len(p)] = p.view(np.int32)
@@ -1278,16 +1325,18 @@ class Gateway:
         handle, arrival, enq, ck = _get64(rows, 1), _get64(rows, 5), _get64(rows, 7), _get64(rows, 12)
         dec = enq + rows[:, 15].astype(np.int64) * 1000
         out = []
-        for k, (h, a, e, c, d, origin, tier, gen, plen, hl) in enumerate(zip(
+        for k, (h, a, e, c, d, origin, tier, gen, plen, hl, to_ms) in enumerate(zip(
                 handle.tolist(), arrival.tolist(), enq.tolist(), ck.tolist(), dec.tolist(), rows[:, 3].tolist(),
-                rows[:, 4].tolist(), rows[:, 9].tolist(), rows[:, 10].tolist(), rows[:, 14].tolist())):
+                rows[:, 4].tolist(), rows[:, 9].tolist(), rows[:, 10].tolist(), rows[:, 14].tolist(),
+                rows[:, 16].tolist())):
             self._next_req += 1
             # a non-resident turn replays its dialog: the origin router holds
             # the history, the descriptor carries its length (the replay's
             # prefill cost; generated tokens are placeholders there as well)
             out.append(Request(req_id=self._next_req, prompt=rows[k, DESC_HDR:DESC_HDR + max(1, plen)].copy(),
                                gen_tokens=gen, tier=tier, meta=(origin, h, tier, a, e, d), conv=c,
-                               history=np.zeros(hl, dtype=np.int32) if hl > 0 else None))
+                               history=np.zeros(hl, dtype=np.int32) if hl > 0 else None,
+                               timeout_ns=int(to_ms) * 1_000_000))
         return out
 
     def _remote_done_rows(self, rows: np.ndarray) -> None:
@@ -1308,8 +1357,109 @@ class Gateway:
         if m is None:
             return
         self.inflight_by_tier[m.tier] -= 1
+        if self.lb is not None and m.endpoint_id:
+            self.lb.release_endpoint(m.endpoint_id, 0, True)     # (note_dispatch counted it)
         self._retry(m, "backend evacuated the request")
         self.counters["handed_back"] += 1
+
+    def _remote_abort(self, row: np.ndarray) -> None:
+        """K_TIMEOUT / K_CANCELLED: the GPU running my request aborted it."""
+        r1 = row.reshape(1, -1)
+        m = self.remote_out.pop(int(_get64(r1, 1)[0]), None)
+        if m is None:
+            return
+        self.inflight_by_tier[m.tier] -= 1
+        self._abort_local(m, int(row[0]), max(0, int(_get64(r1, 7)[0] - _get64(r1, 5)[0])))
+
+    # ------------------------------------------------------------------ in-flight timeout / cancel
+    EXPIRE_EVERY_NS = 5_000_000      # deadline scan period (a vectorised pass over the slots)
+
+    def _expire_inflight(self) -> None:
+        """Abort this GPU's requests whose processing deadline passed."""
+        eng = self.engine
+        if eng is None or not self.inflight_timeout or not hasattr(eng, "expire"):
+            return
+        now = time.monotonic_ns()
+        if now < self._expire_next_ns:
+            return
+        self._expire_next_ns = now + self.EXPIRE_EVERY_NS
+        for r in eng.expire(now):
+            self._aborted(r, K_TIMEOUT, now)
+
+    def _aborted(self, r: Request, kind: int, now: int) -> None:
+        """My engine aborted ``r`` (processing timeout / cancel): my own
+        message takes the timeout / cancel path here; a foreign one is
+        reported to its origin router with the next completion records."""
+        if isinstance(r.meta, Message):
+            m = r.meta
+            self.local.pop(m.handle, None)
+            if 0 <= r.tier < len(self.inflight_by_tier):
+                self.inflight_by_tier[r.tier] -= 1
+            self._abort_local(m, kind, max(0, now - r.admitted_ns))
+        else:
+            origin, handle, tier = self.foreign.pop(r.req_id)
+            self._done_owed[origin].append((handle, tier, r.admitted_ns, now, kind))
+
+    def _abort_local(self, m: Message, kind: int, ran_ns: int) -> None:
+        """One of my messages was aborted on the GPU that ran it: a processing
+        timeout is a failure (retry with backoff, dead-letter when retries
+        are spent -- the reference's handleFailure); a cancel ends it."""
+        if self.lb is not None and m.endpoint_id:
+            self.lb.release_endpoint(m.endpoint_id, ran_ns, kind == K_TIMEOUT)
+        if isinstance(m.metadata, dict):
+            m.metadata["last_error"] = "processing timeout" if kind == K_TIMEOUT else "cancelled"
+        if kind == K_TIMEOUT:
+            self.counters["inflight_timeout"] += 1
+            if self.metrics is not None:
+                self.metrics.requests_rejected.labels("processing_timeout").inc()
+            self._retry(m, f"processing timeout ({m.timeout / 1e9:.3g} s)")
+            return
+        self.counters["cancelled"] += 1
+        m.status = MessageStatus.CANCELLED
+        m.updated_at = time.time_ns()
+        self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
+
+    def request_cancel(self, m: Message):
+        """Any thread: cancel ``m`` if it runs on a GPU.  Returns a Future the
+        serve loop resolves with "cancelled" (aborted on this rank's GPU),
+        "forwarded" (K_CANCEL sent to the GPU running it, which reports the
+        abort back) or "" (not in flight from this router)."""
+        from concurrent.futures import Future
+        f: Future = Future()
+        with self._cancel_lock:
+            self._cancel_req.append((m, f))
+        return f
+
+    def _process_cancels(self) -> None:
+        if not self._cancel_req:
+            return
+        with self._cancel_lock:
+            reqs, self._cancel_req = self._cancel_req, []
+        now = time.monotonic_ns()
+        for m, f in reqs:
+            res = ""
+            if m.handle in self.local and self.engine is not None:
+                got = self.engine.cancel([m.handle])
+                for r in got:
+                    self._aborted(r, K_CANCELLED, now)
+                res = "cancelled" if got else ""
+            elif m.handle in self.remote_out and str(m.endpoint_id).startswith("gpu"):
+                j = int(m.endpoint_id[3:])
+                if 0 <= j < self.world and j != self.rank:
+                    self._cancel_out.setdefault(j, []).append(m.handle)
+                    res = "forwarded"
+            if not f.done():
+                f.set_result(res)
+
+    def _cancel_foreign(self, origin: int, handles) -> None:
+        """K_CANCEL rows from ``origin``: abort those of its requests my GPU
+        is running (one that already completed is reported done as usual)."""
+        hs = {int(h) for h in handles}
+        ids = [rid for rid, (o, h, _t) in self.foreign.items() if o == origin and h in hs]
+        if ids and self.engine is not None:
+            now = time.monotonic_ns()
+            for r in self.engine.cancel(ids):
+                self._aborted(r, K_CANCELLED, now)
 
     def attach_retry_queue(self, delayed, backoff=None) -> None:
         """Route backend-failure retries through ``delayed`` (a
@@ -1327,8 +1477,10 @@ class Gateway:
         if self.retry_queue is None:
             self._requeue(m)
             return
-        m.retry_count += 1
-        if m.retry_count > self.retry_backoff.max_retries():
+        # the reference's handleFailure (`worker.go:202-239`): retry while
+        # RetryCount < MaxRetries (counting this retry), else dead-letter with
+        # RetryCount == MaxRetries (the count was one too high)
+        if m.retry_count >= self.retry_backoff.max_retries():
             m.status = MessageStatus.FAILED
             m.endpoint_id = ""
             self.counters["retry_exhausted"] += 1
@@ -1339,6 +1491,7 @@ class Gateway:
                 except QueueError:
                     self.log.warning("dead-letter queue full; failed request dropped", message_id=m.id)
             return
+        m.retry_count += 1
         m.status = MessageStatus.PENDING
         m.endpoint_id = ""
         m.dispatched_at = 0
@@ -1378,15 +1531,19 @@ class Gateway:
             self._pin(m, +1)
 
     # ------------------------------------------------------------------ health
-    def set_healthy(self, healthy: bool, reason: str = "") -> int:
+    def set_healthy(self, healthy: bool, reason: str = "", failure: bool = True) -> int:
         """Mark this rank's GPU (un)healthy.  Going unhealthy evacuates the
         backend: local requests are re-queued here (the planner then places
         them on healthy GPUs), foreign ones are handed back to their origin
-        router (K_FAIL).  Returns the number of evacuated requests."""
+        router (K_FAIL).  ``failure``: the GPU failed (backend error, ECC,
+        telemetry) -- the requests it was running take the retry path
+        (backoff, retry count, dead letter when spent); an operator's drain
+        (``failure`` False) requeues them at once, untouched.  Returns the
+        number of evacuated requests."""
         with self._tick_lock:
-            return self._set_healthy(healthy, reason)
+            return self._set_healthy(healthy, reason, failure)
 
-    def _set_healthy(self, healthy: bool, reason: str) -> int:
+    def _set_healthy(self, healthy: bool, reason: str, failure: bool = True) -> int:
         was = self.healthy
         self.healthy, self.health_reason = bool(healthy), ("" if healthy else reason)
         if healthy or not was or self.engine is None:
@@ -1400,7 +1557,9 @@ class Gateway:
         for r in held:                                  # turns waiting for a KV that will not be used here
             n += 1
             if isinstance(r.meta, Message):
-                self._retry(r.meta, reason)
+                # never launched on this GPU: nothing failed for it -- back
+                # into its tier at once, no retry spent
+                self._requeue(r.meta)
             else:
                 origin, handle, tier = r.meta[:3]
                 self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
@@ -1418,7 +1577,10 @@ class Gateway:
                     self.inflight_by_tier[r.tier] -= 1
                 if m.metadata and m.metadata.get("home_gpu") == self.rank:
                     del m.metadata["home_gpu"]
-                self._retry(m, reason)
+                if failure:
+                    self._retry(m, reason)
+                else:
+                    self._requeue(m)
             else:
                 origin, handle, tier = self.foreign.pop(r.req_id)
                 self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
@@ -1723,6 +1885,8 @@ class Gateway:
     def _tick(self, pump=None):
         self._pump = pump
         self._drain_retries()
+        self._process_cancels()
+        self._expire_inflight()
         res = None
         pc = time.perf_counter_ns
         ht = self.host_ns

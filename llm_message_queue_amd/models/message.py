@@ -109,7 +109,8 @@ class MessageStatus:
     COMPLETED = "completed"
     FAILED = "failed"
     TIMEOUT = "timeout"
-    ALL = ("pending", "processing", "completed", "failed", "timeout")
+    CANCELLED = "cancelled"      # DELETE /api/v1/messages/{id} aborted it in flight
+    ALL = ("pending", "processing", "completed", "failed", "timeout", "cancelled")
 
 
 class ConversationState:

@@ -186,6 +186,12 @@ class QueueConfig:
     # when the next step's prefill headroom is spoken for, and is prefilled
     # first in that step (docs/architecture.md:233 "realtime < 100 ms")
     realtime_lane: bool = True
+    # in-flight processing timeout: a request still running on a GPU
+    # ``timeout`` (30 s default) after its admission is aborted (slot freed)
+    # and retried with backoff / dead-lettered when retries are spent -- the
+    # reference's context.WithTimeout + handleFailure (worker.go:162-239).
+    # False: an admitted request always runs to completion.
+    inflight_timeout: bool = True
 
 
 @dataclass
@@ -274,6 +280,11 @@ class GPUConfig:
     hbm_reserve_gb: float = 16.0
     telemetry_period_ms: int = 20
     comm_backend: str = "nccl"        # RCCL on ROCm; "gloo" for CPU tests
+    # host placement of each rank (parallel/placement.py): "gpu" binds every
+    # thread of the rank to the physical cores of its GPU's socket (sysfs
+    # local_cpulist, split among the ranks on that socket); "auto" does so
+    # when the job has more than one rank; "core" = rank r -> core r; "off"
+    cpu_bind: str = "auto"
     control_plane: str = "shm"        # per-tick load/descriptor exchange: shm (node-local shared memory;
                                       # gloo when ranks span nodes), gloo (host TCP) or nccl (RCCL)
     # move a conversation's KV to the GPU its next turn is placed on (RCCL
@@ -295,6 +306,12 @@ class BackendConfig:
     gen_tokens: int = 4                # decode steps per request
     dtype: str = "bf16"
     token_budget: int = 4096           # max tokens per forward step (prefill chunking)
+    # cap a step at this many tokens while a realtime request is in the batch
+    # (0 = off).  Under continuous realtime traffic it acts like a smaller
+    # token_budget: on one MI355X a 1024-token step brings realtime
+    # arrival -> last token p99 from ~270 ms to ~100 ms for ~29 % fewer
+    # requests/s (profiles/r5_step_budget_sweep_1gpu.jsonl), so it is off
+    realtime_step_tokens: int = 0
     # a forward still incomplete this long after launch = a hung GPU: the
     # serve loop stops with a failure status (BackendHung) so the launcher
     # restarts the job; 0 waits forever
@@ -492,6 +509,8 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("gpu.hbm_reserve_gb must be >= 0 and gpu.rebalance_interval_ms > 0")
     if cfg.gpu.comm_backend not in ("nccl", "gloo"):
         raise ConfigError("gpu.comm_backend must be nccl (RCCL) or gloo")
+    if cfg.gpu.cpu_bind not in ("auto", "gpu", "core", "off"):
+        raise ConfigError("gpu.cpu_bind must be auto, gpu, core or off")
     q = cfg.queue
     for name in ("monitor_interval", "cleanup_interval"):
         if getattr(q, name) <= 0:

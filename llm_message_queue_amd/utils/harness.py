@@ -13,15 +13,28 @@ import time
 import numpy as np
 
 
-def comm_evidence(comm, dev, world: int, dry: bool) -> dict:
+def comm_evidence(comm, dev, world: int, dry: bool, binding: dict = None) -> dict:
     """Proof of what the job ran on, gathered from every rank: data-plane
     backend, per-rank HIP device index and PCI address (distinct unless the
-    ranks were wrapped onto fewer GPUs), and one timed all_reduce on the data
-    plane (64 MiB on RCCL; 8 MiB on the CPU rehearsal's gloo)."""
+    ranks were wrapped onto fewer GPUs), each rank's host CPU binding
+    (``parallel.placement``: NUMA node and cores of its GPU's socket), and
+    one timed all_reduce on the data plane (64 MiB on RCCL; 8 MiB on the CPU
+    rehearsal's gloo)."""
     import torch
     from ..parallel.comm import gpus_oversubscribed
     ev = {"world": world, "control_plane": "solo" if world == 1 else str(getattr(comm, "backend", "?")),
           "data_backend": "none", "oversubscribed": False}
+    if binding is not None:
+        from ..parallel.placement import parse_cpulist
+        cpus = parse_cpulist(str(binding.get("cpus") or ""))
+        row = np.array([int(binding.get("numa_node", -1)), len(cpus), cpus[0] if cpus else -1,
+                        cpus[-1] if cpus else -1, int(binding.get("bound_threads", 0))], dtype=np.int64)
+        g = comm.all_gather_i64(row)
+        ev["cpu_binding"] = {"mode": binding.get("mode"), "source": binding.get("source", ""),
+                             "rank0_cpus": binding.get("cpus", ""),
+                             "by_rank": [{"rank": r, "numa_node": int(x[0]), "ncpus": int(x[1]),
+                                          "first_cpu": int(x[2]), "last_cpu": int(x[3]),
+                                          "threads_bound": int(x[4])} for r, x in enumerate(g.tolist())]}
     if dev.type == "cuda":
         p = torch.cuda.get_device_properties(dev)
         mine = [int(dev.index), int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)]

@@ -43,7 +43,9 @@ def test_bench_single_rank_dry_run():
     # the reported window's rate = min(dispatched, arrived) per second: never
     # above the rate the offered load actually arrived at; value is that rate
     # when the window held the operating point and 0 otherwise (SLO search)
-    w = d["slo_search"]["attempts"][-1]["value"]
+    # (the reported window: the best attempt that held the SLO, else the last)
+    att = d["slo_search"]["attempts"]
+    w = next((t for t in att if t["met"] and t["util"] == d["config"]["util"]), att[-1])["value"]
     assert w <= d["dispatch_rate_in_window"] + 1e-6
     assert w <= d["arrival_rate_in_window"] + 1e-6
     assert abs(w - min(d["dispatch_rate_in_window"], d["arrival_rate_in_window"])) < 0.02
@@ -66,7 +68,7 @@ def test_bench_four_ranks_torchrun_dry_run():
     slo = d["slo_search"]
     assert all(a["value"] > 0 for a in slo["attempts"])
     met = [a["value"] for a in slo["attempts"] if a["met"]]
-    assert d["value"] == (met[0] if met else 0.0)
+    assert d["value"] == (max(met) if met else 0.0)
     assert met or "reason" in slo
     # the secondary null-backend phase runs multi-rank too (the driver's 8-GPU run does it)
     assert d["gateway_only"]["requests_per_s"] > 0
@@ -175,6 +177,25 @@ def test_bench_slo_search_backs_off_to_a_met_operating_point():
     assert d["value"] == s["attempts"][-1]["value"] > 0
     assert abs(d["offered_rate_per_gpu"] - u * d["calibrated_capacity_per_gpu"]) < 1.0
     assert d["requests_accounted"]["lost"] == 0
+
+
+def test_bench_slo_search_climbs_while_the_slo_holds():
+    """the search climbs too.  The first window (0.98)
+    holds the SLO, so 1.0, 1.02, ... are served while it keeps holding (the
+    test hook makes every util above 1.01 miss); the headline is the best
+    window that held it, and every attempt is listed."""
+    d = _run([sys.executable, "bench.py", "--cpu-dry-run", "--sim-gpu", "1", "--steps", "20", "--warmup", "2",
+              "--gateway-only-s", "0", "--test-miss-above-util", "1.01"], timeout=420)
+    s = d["slo_search"]
+    met = [t for t in s["attempts"] if t["met"]]
+    if not s["attempts"][0]["met"]:                 # a loaded host missed at 0.98: the back-off path ran
+        assert s["util_tried"][1] < 0.98
+        return
+    assert s["util_tried"][:3] == [0.98, 1.0, 1.02] and s["attempts"][2]["met"] is False
+    assert len(s["util_tried"]) == 3                # stopped at the first miss above the knee
+    best = max(met, key=lambda t: t["value"])
+    assert d["value"] == best["value"] > 0 and s["value_util"] == best["util"] == d["config"]["util"]
+    assert d["p99_target_met"] and s["search_s"] > 0 and d["requests_accounted"]["lost"] == 0
 
 
 def test_overload_bench_multirank_sheds_low_tiers_parks_and_unparks():

@@ -226,7 +226,7 @@ def test_every_removal_of_a_queued_turn_releases_its_pin():
 
     queued("a")
     assert gw.pinned[1].sum() == 1
-    assert app.peer_op("remove", ["a"]) == {"dequeued": True}           # peer 'remove'
+    assert app.peer_op("remove", ["a"]) == {"dequeued": True, "cancelled": False}   # peer 'remove'
     assert gw.pinned.sum() == 0
     queued("b")
     assert app.peer_op("dequeue", ["standard", "b"]) is True            # peer 'dequeue'

@@ -59,5 +59,7 @@ def test_retries_exhausted_go_to_the_dead_letter_queue():
     gw.set_healthy(False, "fault 2")            # second failure: retries (1) spent
     assert gw.counters["retry_exhausted"] == 3 and dlq.size() == 3
     items = dlq.get_all()
-    assert all("retries exhausted" in it.fail_reason and it.retry_count == 2 for it in items)
+    # dead-lettered with RetryCount == MaxRetries, as the reference's
+    # handleFailure (worker.go:210) -- not incremented on that path
+    assert all("retries exhausted" in it.fail_reason and it.retry_count == 1 for it in items)
     assert gw.retrying() == 0 and gw.pending() == 0

@@ -54,15 +54,20 @@ class Server:
     """A ``cli serve`` process (optionally under torchrun) whose stdout JSON
     events are collected by a reader thread."""
 
-    def __init__(self, args, env_extra=None, torchrun=0, mport=0, restarts=0):
+    def __init__(self, args, env_extra=None, torchrun=0, mport=0, restarts=0, standalone=False):
         self.port = _port()
         env = dict(os.environ, LLMQ_LOGGING__LEVEL="warning", OMP_NUM_THREADS="1", **(env_extra or {}))
         cmd = [sys.executable, "-m", "llm_message_queue_amd.cli", "serve", "--cpu-ranks", "--port", str(self.port),
                "--host", "127.0.0.1"] + list(args)
         if torchrun:
-            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={torchrun}",
-                   "--master-addr=127.0.0.1", f"--master-port={mport or _port()}",
-                   f"--max-restarts={restarts}"] + cmd[1:]
+            # static rendezvous (run id "none", as the round-4 HTTP runs), or
+            # --standalone: the c10d rendezvous deployments use, whose restart
+            # rounds re-rendezvous (gloo under a static one can read the dead
+            # incarnation's addresses from the store on restart)
+            rdzv = (["--standalone", "--local-addr=127.0.0.1"] if standalone else
+                    ["--master-addr=127.0.0.1", f"--master-port={mport or _port()}"])
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={torchrun}"] \
+                + rdzv + [f"--max-restarts={restarts}"] + cmd[1:]
         self.proc = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                      text=True, start_new_session=True)
         self.events, self.err = [], []
@@ -95,7 +100,7 @@ class Server:
                 if self.proc.poll() is not None:
                     break
                 self._cv.wait(0.5)
-        tail = "".join(self.err[-40:])
+        tail = "".join(self.err[-120:])
         raise AssertionError(f"server event not seen (rc={self.proc.poll()}); stderr tail:\n{tail}")
 
     def ranks(self, n, restart=0, timeout=180):
@@ -238,7 +243,7 @@ def test_restart_after_peer_lost_gets_a_fresh_incarnation():
     and serves every request."""
     env = {"LLMQ_SERVER__FAULT_INJECTION": "true", "LLMQ_COLLECTIVE_TIMEOUT_S": "4",
            "LLMQ_SERVER__STALL_FATAL_AFTER": "0", "LLMQ_FATAL_EXIT_GRACE_S": "5"}
-    s = Server([], env_extra=env, torchrun=2, restarts=1)
+    s = Server([], env_extra=env, torchrun=2, restarts=1, standalone=True)
     try:
         r0 = s.ranks(2, restart=0)
         s.wait_for(lambda e: e.get("event") == "listening")
@@ -246,8 +251,9 @@ def test_restart_after_peer_lost_gets_a_fresh_incarnation():
         assert st == 200 and r["faults"] == {"slow_ms": 20000}, r
         s.post_all(5, "x")
         r1 = s.ranks(2, restart=1, timeout=240)
-        assert r1[0]["job"] == r1[1]["job"] and r1[0]["job"].startswith("none.1.")
-        assert r1[0]["job"] != r0[0]["job"]
+        run0, rs0, n0 = r0[0]["job"].split(".")
+        run1, rs1, n1 = r1[0]["job"].split(".")
+        assert r1[0]["job"] == r1[1]["job"] and (rs0, rs1) == ("0", "1") and n1 != n0
         fatal = [e for e in s.events if e.get("event") == "fatal"]
         assert fatal and any("control" in e["error"] or "did not reach" in e["error"] or "rank" in e["error"]
                              for e in fatal), fatal

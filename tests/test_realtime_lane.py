@@ -89,3 +89,29 @@ def test_realtime_lane_off_waits_for_headroom():
 @pytest.mark.gpu
 def test_realtime_lane_gpu():
     _check_lane(torch.device("cuda", 0), "hip")
+
+
+def test_realtime_step_cap_shrinks_steps_only_while_realtime_runs():
+    """``backend.realtime_step_tokens``: a step carries at most the cap while
+    a realtime-lane request is in the batch (never fewer than its decode
+    rows + 1), the full token budget otherwise; admission headroom follows."""
+    import numpy as np
+    from llm_message_queue_amd.backend.engine import BackendEngine, Request
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig
+    eng = BackendEngine(LlamaConfig.tiny(), slots=16, max_ctx=256, token_budget=200, device="cpu", impl="ref",
+                        realtime_step_tokens=40)
+    eng.admit([Request(1, np.arange(150, dtype=np.int32) % 50, gen_tokens=3, tier=2)])
+    assert eng.step_budget() == 200
+    eng.admit([Request(2, np.arange(10, dtype=np.int32), gen_tokens=3, tier=0)])
+    assert eng.step_budget() == 40 and eng.admit_capacity() <= 1
+    eng.launch()
+    assert eng.finish(block=True).tokens == 40              # realtime prefill first, then 30 bulk tokens
+    steps = []
+    while eng.active:
+        eng.launch()
+        steps.append(eng.finish(block=True).tokens)
+    # realtime done after 3 capped steps in all; the bulk prompt then runs at the full budget
+    assert max(steps) <= 200 and steps[0] == 40 and 40 < max(steps)
+    off = BackendEngine(LlamaConfig.tiny(), slots=16, max_ctx=256, token_budget=200, device="cpu", impl="ref")
+    off.admit([Request(2, np.arange(10, dtype=np.int32), gen_tokens=3, tier=0)])
+    assert off.step_budget() == 200
