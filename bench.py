@@ -531,6 +531,10 @@ def main(argv=None) -> int:
         elapsed = agg[:, 0].max() / 1e9
         lockstep = lockstep_report(gw, engine, comm, elapsed)
         lockstep["ingested_by_rank"] = [int(v) for v in agg[:, 3].tolist()]   # requests each rank preprocessed
+        # ... over the whole attempt (steady phase + timed window + drain): the
+        # front door's balanced ring share evens THIS out (rank0 ingress)
+        lockstep["ingested_total_by_rank"] = [int(v) for v in comm.all_gather_i64(
+            np.array([gw.counters["submitted"] - c0["submitted"]], dtype=np.int64))[:, 0].tolist()]
         # extra forwards a rank launched while its peers were behind (Gateway._extra_local_step)
         lockstep["extra_steps_by_rank"] = [int(v) for v in
                                            comm.all_gather_i64(np.array([extra_local], dtype=np.int64))[:, 0].tolist()]

@@ -155,6 +155,29 @@ class NamedQueue {
     }
     return nullptr;
   }
+  // Oldest non-skipped item from a scan cursor (bucket, index) that only
+  // moves forward: everything before it is known to be skipped.  Within one
+  // pop_tiers call skipped items stay skipped and the queue is locked, so
+  // each skipped handle is looked at once per call instead of once per
+  // popped item (the full rescan made a pop O(count x skipped)).
+  // After take_locked() at the returned position the next item shifts into
+  // it, so the cursor stays valid.
+  struct Cursor {
+    size_t b = 0, k = 0;
+  };
+  const Item* find_front_locked(const std::vector<int64_t>& skip, Cursor* c, size_t* bi, size_t* ii) const {
+    for (; c->b < buckets_.size(); ++c->b, c->k = 0) {
+      const auto& r = buckets_[c->b].ring;
+      for (; c->k < r.size(); ++c->k) {
+        if (!skipped(skip, r[c->k].handle)) {
+          *bi = c->b;
+          *ii = c->k;
+          return &r[c->k];
+        }
+      }
+    }
+    return nullptr;
+  }
   void take_locked(size_t bi, size_t ii, Item* out, int64_t now) {
     auto& r = buckets_[bi].ring;
     *out = r[ii];
@@ -379,18 +402,19 @@ class MultiLevelQueue {
                                     const std::vector<int64_t>& lifo_ns, const std::vector<int64_t>& skip,
                                     int64_t now) {
     const size_t T = qs.size();
+    std::vector<NamedQueue::Cursor> cur(T);          // per tier, for the whole call
     while ((int64_t)hs.size() < count) {
       int pick = -1;
       size_t bi = 0, ii = 0;
       const Item* h = nullptr;
       for (size_t i = 0; i < T && pick < 0; ++i) {
         if (!qs[i] || budget[i] == 0 || aging_ns[i] <= 0) continue;
-        const Item* c = qs[i]->find_locked(skip, false, &bi, &ii);
+        const Item* c = qs[i]->find_front_locked(skip, &cur[i], &bi, &ii);
         if (c && now - c->enq_ns > aging_ns[i]) pick = (int)i, h = c;
       }
       for (size_t i = 0; i < T && pick < 0; ++i) {
         if (!qs[i] || budget[i] == 0) continue;
-        const Item* c = qs[i]->find_locked(skip, false, &bi, &ii);
+        const Item* c = qs[i]->find_front_locked(skip, &cur[i], &bi, &ii);
         if (c) pick = (int)i, h = c;
       }
       if (pick < 0) break;

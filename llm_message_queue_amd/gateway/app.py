@@ -42,35 +42,43 @@ class MessageStore:
     Per-user and per-conversation sub-indexes (insertion-ordered like the
     main one) keep filtered listings off a full scan."""
 
+    _FIELDS = ("user_id", "conversation_id")
+
     def __init__(self, max_items: int = 200_000):
         self._d: "collections.OrderedDict[str, Message]" = collections.OrderedDict()
-        self._by: Dict[str, Dict[str, Dict[str, None]]] = {"user_id": {}, "conversation_id": {}}
+        self._by: Dict[str, Dict[str, Dict[str, None]]] = {f: {} for f in self._FIELDS}
+        # the keys each id is indexed under: a message re-put after its
+        # user_id / conversation_id changed is unindexed from the keys it was
+        # filed under, not from its live attributes (ADVICE r4)
+        self._keys: Dict[str, Tuple[str, ...]] = {}
         self._lock = threading.Lock()
         self.max_items = max_items
 
-    def _unindex(self, m: Message) -> None:
-        for f, idx in self._by.items():
-            k = getattr(m, f, "")
+    def _unindex(self, mid: str) -> None:
+        keys = self._keys.pop(mid, None)
+        if keys is None:
+            return
+        for f, k in zip(self._FIELDS, keys):
+            idx = self._by[f]
             ids = idx.get(k) if k else None
             if ids is not None:
-                ids.pop(m.id, None)
+                ids.pop(mid, None)
                 if not ids:
                     del idx[k]
 
     def put(self, m: Message) -> None:
         with self._lock:
-            old = self._d.get(m.id)
-            if old is not None:
-                self._unindex(old)
+            self._unindex(m.id)
             self._d[m.id] = m
             self._d.move_to_end(m.id)
-            for f, idx in self._by.items():
-                k = getattr(m, f, "")
+            keys = tuple(getattr(m, f, "") or "" for f in self._FIELDS)
+            self._keys[m.id] = keys
+            for f, k in zip(self._FIELDS, keys):
                 if k:
-                    idx.setdefault(k, {})[m.id] = None
+                    self._by[f].setdefault(k, {})[m.id] = None
             while len(self._d) > self.max_items:
-                _mid, ev = self._d.popitem(last=False)
-                self._unindex(ev)
+                mid, _ev = self._d.popitem(last=False)
+                self._unindex(mid)
 
     def get(self, mid: str) -> Optional[Message]:
         with self._lock:
@@ -84,7 +92,7 @@ class MessageStore:
         with self._lock:
             m = self._d.pop(mid, None)
             if m is not None:
-                self._unindex(m)
+                self._unindex(mid)
             return m
 
     def query(self, user_id: str = "", conversation_id: str = "", status: str = "", limit: int = 10,

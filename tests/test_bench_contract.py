@@ -96,6 +96,12 @@ def test_bench_rank0_ingress_world4_dry_run():
     d = _rank0_ingress(4)
     ing = d["lockstep"]["ingested_by_rank"]
     assert len(ing) == 4 and min(ing) > 0, ing
+    # (every rank took part over the whole attempt too; the even split of the
+    # balanced share needs consumers that poll continuously -- cli serve's
+    # ring threads -- and is pinned in test_multirank_serve.py, while these
+    # dry-run pumps poll once per 20 ms tick)
+    tot = d["lockstep"]["ingested_total_by_rank"]
+    assert d["config"]["door_share"] == "fair" and min(tot) > 0, tot
 
 
 def test_bench_rank0_funnel_world4_dry_run():

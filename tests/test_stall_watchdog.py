@@ -208,3 +208,22 @@ def test_message_index_filtered_queries_match_a_scan():
             n, page = st.query(user_id=u, conversation_id=c, status=s, limit=lim, offset=off)
             assert n == len(want) and [m.id for m in page] == [m.id for m in want[off:off + lim]], step
     assert len(st.values()) <= 60
+
+
+def test_message_index_reput_after_key_change_does_not_leak():
+    """the same Message object re-put after its user_id changed
+    leaves nothing under the old key (the index remembers where it filed it)."""
+    from llm_message_queue_amd.gateway.app import MessageStore
+    from llm_message_queue_amd.models.message import Message
+    st = MessageStore(max_items=10)
+    m = Message(id="m1", content="x", priority=3, user_id="alice", conversation_id="c1")
+    st.put(m)
+    m.user_id, m.conversation_id = "bob", ""
+    st.put(m)
+    assert "alice" not in st._by["user_id"] and "c1" not in st._by["conversation_id"]
+    assert st.query(user_id="bob")[0] == 1 and st.query(user_id="alice")[0] == 0
+    st.remove("m1")
+    assert not st._by["user_id"] and not st._keys
+    for i in range(30):                                   # eviction unindexes too
+        st.put(Message(id=f"e{i}", content="x", priority=3, user_id=f"u{i}"))
+    assert len(st._keys) == 10 and len(st._by["user_id"]) == 10
