@@ -35,6 +35,7 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
     ap.add_argument("--text-batches", default="4096", help="preprocess batch sizes (messages), comma-separated")
+    ap.add_argument("--summ-convs", default="64", help="summarise: conversations per batch (8 evicted turns each)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -137,6 +138,20 @@ def main() -> None:
         sl = torch.randint(0, S, (T,), dtype=torch.int32, device=dev)
         ms = timeit(lambda: ops.rope_kv(qkv, p, sl, cos, sin, Hq, Hkv, kc2, vc2), a.reps)
         rec("rope_kv_T4096", ms, GBps=round(T * (Hq + 2 * Hkv) * 128 * 2 * 2 / ms / 1e6, 1))
+    # --- conversation summarise-on-evict (N5): the text pipeline's pooled
+    # embeddings -> summarise_project (segmented mean + MFMA projection +
+    # running-summary blend) and the salient-token top-k, per batch of
+    # conversations evicting 8 turns each
+    if not want or "summarise" in want:
+        from llm_message_queue_amd.conversation.summarise import SummaryEngine
+        from llm_message_queue_amd.utils.config import default_config
+        eng = SummaryEngine(default_config().preprocessor, device="cuda", k=8, alpha=0.8, dim=256)
+        turns = [m.content for m in Workload(seed=3).make(8 * 512)]
+        for nc in (int(x) for x in a.summ_convs.split(",")):
+            groups = [(None if c % 2 else np.full(256, 0.1, dtype=np.float32), turns[8 * c:8 * c + 8])
+                      for c in range(nc)]
+            ms = timeit(lambda: eng.summarise(groups), max(5, a.reps // 5))
+            rec(f"summarise_{nc}convs", ms, us_per_conv=round(ms * 1e3 / nc, 2), turns=8 * nc)
     print(json.dumps({"summary": out}))
 
 
