@@ -249,8 +249,17 @@ def cmd_serve(a, role: str = "serve") -> int:
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
 
+    # under torchrun the launcher is our parent: if it dies (SIGKILLed) the
+    # ranks -- each in a session of its own -- would live on, holding their
+    # GPU and port, so a rank whose launcher is gone stops like on SIGTERM
+    launcher = os.getppid() if os.environ.get("TORCHELASTIC_RUN_ID") else 0
+
     def _watch_fatal():            # a lost peer rank / a stalled loop ends this process too
         while not stop.is_set():
+            if launcher and os.getppid() != launcher:
+                print(json.dumps({"event": "launcher_gone", "rank": rank}), flush=True)
+                stop.set()
+                break
             if gapp.fatal is not None:
                 print(json.dumps({"event": "fatal", "rank": rank, "error": str(gapp.fatal)}), flush=True)
                 stop.set()

@@ -1,0 +1,118 @@
+"""Latency histograms of the gateway data path: per-tier arrival -> dispatch
+and enqueue -> dispatch (``LatencyRecorder``), and where a request's arrival
+-> admission time goes, stage by stage (``StageRecorder``).  Log-binned
+int64 histograms, so every rank's can be summed over the control plane."""
+from __future__ import annotations
+
+import numpy as np
+
+# --------------------------------------------------------------------------- latency histogram
+_HBINS = 2400
+_HMIN_NS = 1_000.0            # 1 us
+_HDECADES = 8.0               # .. 100 s
+
+
+def _hbin(ns: np.ndarray) -> np.ndarray:
+    x = np.log10(np.maximum(ns, _HMIN_NS) / _HMIN_NS) / _HDECADES * _HBINS
+    return np.minimum(x.astype(np.int64), _HBINS - 1)
+
+
+def hist_percentile(h: np.ndarray, q: float) -> float:
+    """Upper edge (ns) of the bin holding quantile q."""
+    tot = int(h.sum())
+    if tot == 0:
+        return 0.0
+    k = int(np.searchsorted(np.cumsum(h), q * tot, side="left"))
+    return _HMIN_NS * 10 ** ((k + 1) / _HBINS * _HDECADES)
+
+
+class LatencyRecorder:
+    """Per-tier arrival->dispatch and enqueue->dispatch latency histograms."""
+
+    def __init__(self, ntiers: int = 4):
+        self.ntiers = ntiers
+        self.reset()
+
+    def reset(self):
+        self.arr = np.zeros((self.ntiers + 1, _HBINS), dtype=np.int64)   # last row = all tiers
+        self.enq = np.zeros((self.ntiers + 1, _HBINS), dtype=np.int64)
+        self.count = 0
+
+    def record(self, tiers: np.ndarray, arr_ns: np.ndarray, enq_ns: np.ndarray) -> None:
+        if len(tiers) == 0:
+            return
+        ba, be = _hbin(arr_ns), _hbin(enq_ns)
+        for t in range(self.ntiers):
+            m = tiers == t
+            if m.any():
+                np.add.at(self.arr[t], ba[m], 1)
+                np.add.at(self.enq[t], be[m], 1)
+        np.add.at(self.arr[self.ntiers], ba, 1)
+        np.add.at(self.enq[self.ntiers], be, 1)
+        self.count += len(tiers)
+
+    def summary(self, arr=None, enq=None) -> dict:
+        arr = self.arr if arr is None else arr
+        enq = self.enq if enq is None else enq
+        out = {"count": int(arr[self.ntiers].sum())}
+        for q, name in ((0.5, "p50"), (0.99, "p99")):
+            out[f"{name}_ms"] = hist_percentile(arr[self.ntiers], q) / 1e6
+            out[f"{name}_enq_ms"] = hist_percentile(enq[self.ntiers], q) / 1e6
+        out["p99_by_tier_ms"] = [hist_percentile(arr[t], 0.99) / 1e6 for t in range(self.ntiers)]
+        out["count_by_tier"] = [int(arr[t].sum()) for t in range(self.ntiers)]
+        return out
+
+
+# Where a request's arrival -> admission time goes (multi-rank attribution,
+# VERDICT r3 next #1): arrival -> handed to this rank's gateway (the front
+# door's hop: rank 0 -> a shared-memory ring -> the rank's pump); -> taken
+# from the inbox into a preprocess batch; preprocess + queue push; queue wait
+# until a dispatch decision pops it; decision -> admitted into a backend
+# slot (0 on the own GPU; the descriptor's trip through the all_to_all for
+# another rank's GPU).
+STAGES = ("ingress", "inbox", "preprocess", "queue", "handoff")
+# how the request got its slot: realtime lane between collectives; own-GPU
+# admission between collectives (extra step / leftover headroom); the
+# tick's plan on the own GPU; the plan on another rank's GPU
+PATHS = ("lane", "own", "plan_local", "plan_remote")
+P_LANE, P_OWN, P_PLAN_LOCAL, P_PLAN_REMOTE = range(4)
+
+
+class StageRecorder:
+    """Per-stage, per-tier latency histograms (``STAGES``) and per-path,
+    per-tier admission counts (``PATHS``)."""
+
+    def __init__(self, ntiers: int = 4):
+        self.ntiers = ntiers
+        self.reset()
+
+    def reset(self):
+        self.h = np.zeros((len(STAGES), self.ntiers + 1, _HBINS), dtype=np.int64)
+        self.paths = np.zeros((len(PATHS), self.ntiers), dtype=np.int64)
+
+    def record(self, stage: int, tiers: np.ndarray, ns: np.ndarray) -> None:
+        if len(tiers) == 0:
+            return
+        b = _hbin(np.maximum(np.asarray(ns, dtype=np.int64), 0))
+        tiers = np.asarray(tiers, dtype=np.int64)
+        for t in range(self.ntiers):
+            m = tiers == t
+            if m.any():
+                np.add.at(self.h[stage, t], b[m], 1)
+        np.add.at(self.h[stage, self.ntiers], b, 1)
+
+    def count(self, path: int, tiers) -> None:
+        for t in tiers:
+            if 0 <= t < self.ntiers:
+                self.paths[path, t] += 1
+
+    @staticmethod
+    def summary(h: np.ndarray, paths: np.ndarray) -> dict:
+        """``h`` [stages, tiers+1, bins], ``paths`` [paths, tiers] -> JSON
+        (p50 / p99 ms per stage: one value per tier, then all tiers)."""
+        out = {}
+        for s, name in enumerate(STAGES):
+            out[name] = {q: [round(hist_percentile(h[s, t], p) / 1e6, 3) for t in range(h.shape[1])]
+                         for q, p in (("p50_ms", 0.5), ("p99_ms", 0.99))}
+        out["admitted_by_path"] = {name: [int(x) for x in paths[k]] for k, name in enumerate(PATHS)}
+        return out

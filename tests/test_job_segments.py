@@ -134,6 +134,15 @@ class Server:
         return len(done)
 
     def stop(self, sig=signal.SIGTERM):
+        # torchrun's workers run in sessions of their own: signal them by pid
+        # too (a SIGKILL of the launcher alone would leave them running)
+        pids = {int(e["pid"]) for e in self.events if e.get("event") == "rank" and "pid" in e}
+        if sig == signal.SIGKILL:
+            for pid in pids:
+                try:
+                    os.kill(pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
         try:
             os.killpg(self.proc.pid, sig)
             self.proc.wait(timeout=60)
@@ -143,6 +152,19 @@ class Server:
             except ProcessLookupError:
                 pass
             self.proc.wait(timeout=10)
+        deadline = time.time() + 30
+        for pid in pids:                               # nothing of the job outlives the test
+            while time.time() < deadline:
+                try:
+                    os.kill(pid, 0)
+                except ProcessLookupError:
+                    break
+                time.sleep(0.2)
+            else:
+                try:
+                    os.kill(pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
 
 
 def test_ring_generation_refuses_a_stale_segment():
@@ -215,6 +237,7 @@ def test_sigkilled_job_leaves_nothing_and_next_job_completes_every_request():
         a.stop(signal.SIGKILL)
     leaked = [n for n in _shm_names() - before if tok_a in n]
     assert leaked == [], leaked
+    assert a.proc.poll() is not None
     # a stale ring under the round-4 name (run id only) with a leftover record
     R = _native.shmring().ShmRing
     stale = R("llmq-default-none-req", 1 << 16, "open", 0)
@@ -317,3 +340,27 @@ def test_fault_injection_is_off_by_default():
         assert c.post("/api/v1/admin/faults", json={"slow_ms": 5}).status_code == 409   # no backend here
     finally:
         app.stop()
+
+
+def test_ranks_exit_when_their_launcher_dies():
+    """torchrun's workers run in sessions of their own, so SIGKILLing the
+    launcher used to leave the ranks serving (holding GPU and port) forever;
+    a rank now notices its launcher is gone and stops."""
+    s = Server([], torchrun=2)
+    try:
+        rk = s.ranks(2)
+        s.wait_for(lambda e: e.get("event") == "listening")
+        os.killpg(s.proc.pid, signal.SIGKILL)              # the launcher only
+        s.proc.wait(timeout=10)
+        deadline = time.time() + 40
+        alive = {int(e["pid"]) for e in rk}
+        while alive and time.time() < deadline:
+            for pid in list(alive):
+                try:
+                    os.kill(pid, 0)
+                except ProcessLookupError:
+                    alive.discard(pid)
+            time.sleep(0.3)
+        assert not alive, f"ranks {alive} outlived their launcher"
+    finally:
+        s.stop(signal.SIGKILL)
