@@ -175,7 +175,9 @@ def main():
                 x = torch.randn(T, K, device=dev).to(torch.bfloat16)
                 y = torch.randn(T, N, device=dev).to(torch.bfloat16)
                 fns = {"hipblaslt_resid": lambda: y.addmm_(x, w.t()),
-                       "hip_resid": lambda: G.gemm_residual(x, w, y)}
+                       "hip_resid": lambda: G.gemm_residual(x, w, y),
+                       "hip_resid_lds": lambda: G._launch(x, w, y, G.EPI_RESID_LDS),
+                       "hip_plain": lambda: G.gemm(x, w, out=y)}
                 for f in fns.values():
                     f()
                 res = {k: [] for k in fns}

@@ -57,7 +57,8 @@ constexpr int GM_BUF_BYTES = 4 * GM_HALF_BYTES;    // A0 A1 B0 B1
 constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
 constexpr int GM_GROUP_M = 8;                    // default M-tiles per block-order group
 
-enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4, GM_EPI_RESID = 5 };
+enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4, GM_EPI_RESID = 5,
+       GM_EPI_RESID_LDS = 6 };
 
 // GM_EPI_ARGMAX: the LM head's greedy sampling as the epilogue -- no [M][N]
 // logits tensor.  Each tile writes, per row, the max over its 256 columns and
@@ -634,6 +635,52 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         GM_LGKM(0);
         __builtin_amdgcn_wave_barrier();
       }
+  } else if (EPI == GM_EPI_RESID_LDS) {
+    // The residual tile staged by DMA instead of through registers: the
+    // wave's 128 x 64 bf16 block of C lands in its 16 KiB of LDS (16
+    // buffer_load ... lds of 16 B per lane, row-major, the plain epilogue's
+    // layout; rows >= M read 0 off the buffer descriptor), each lane adds its
+    // fp32 accumulators in place (one rounding of the sum) and the block
+    // leaves with the plain epilogue's 16-B coalesced stores.  Against the
+    // four-pass fp32 staging (GM_EPI_RESID): half the global instructions
+    // (16-B instead of 8-B loads and stores), no fp32 LDS round trip, one
+    // wave barrier instead of eight.
+    uint8_t* cw = smem + w * 16384;
+    const int col0 = tn * GM_BN + wc * 64;
+    const __amdgpu_buffer_rsrc_t rsc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (uint32_t)M * (uint32_t)N * 2u, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {                 // LDS bytes [i KiB, i+1 KiB): rows 8i .. 8i+7
+      const int r = i * 8 + (lane >> 3), c = lane & 7;
+      const uint32_t vo = ((uint32_t)(row0 + r) * (uint32_t)N + (uint32_t)(col0 + c * 8)) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, (gm_lds_ptr)(cw + i * 1024), 16, vo, 0, 0, 0);
+    }
+    GM_VMCNT(0);
+    __builtin_amdgcn_wave_barrier();
+    uint16_t* o = reinterpret_cast<uint16_t*>(cw);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int at = (mh * 64 + m * 16 + fq * 4 + j) * 64 + nh * 32 + n * 16 + fr;
+              o[at] = gm_f2bf(__uint_as_float((uint32_t)o[at] << 16) + acc[mh][m][nh][n][j]);
+            }
+    GM_LGKM(0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int qd = it * 64 + lane;               // row qd/8, chunk qd%8
+      const int r = qd >> 3, cb = qd & 7;
+      const int grow = row0 + r;
+      const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(cw + r * 128 + cb * 16);
+      if (grow < M) *reinterpret_cast<gm_u32x4*>(C + (int64_t)grow * N + col0 + cb * 8) = v;
+    }
   } else if (EPI == GM_EPI_SWIGLU) {
     // wave w: 128 rows x 32 features bf16 = 8 KiB at w * 8 KiB
     uint16_t* o = reinterpret_cast<uint16_t*>(smem + w * 8192);

@@ -234,6 +234,9 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
                                rsp);
   else if (epi == GM_EPI_RESID)                    // C += A·Wᵀ in place (no row scales)
     launch_gemm<GM_EPI_RESID>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
+  else if (epi == GM_EPI_RESID_LDS)                // the same, residual tile staged by DMA (A/B)
+    launch_gemm<GM_EPI_RESID_LDS>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
+                                  group_m);
   else if (epi == GM_EPI_STORE + 16)
     launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_STORE + 32)

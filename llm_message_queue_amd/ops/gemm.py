@@ -24,6 +24,7 @@ from .. import _native
 EPI_STORE = 0
 EPI_SWIGLU = 2
 EPI_RESID = 5
+EPI_RESID_LDS = 6   # A/B: residual tile staged into LDS by DMA, added in place
 TILE_N = 256
 SWIGLU_HALF = 32   # per-wave gate/up split (a wave owns 64 output columns)
 

@@ -178,6 +178,9 @@ def torch_rank_pci(local_world: int) -> List[str]:
     return out
 
 
+MIN_AUTO_CPUS = 4
+
+
 def bind_rank(mode: str = "auto", extra_pids: Sequence[int] = (), sysfs: str = "/sys",
               world: Optional[int] = None) -> Dict[str, object]:
     """Bind this rank (and ``extra_pids``, e.g. its front-door feeder) to its
@@ -203,6 +206,12 @@ def bind_rank(mode: str = "auto", extra_pids: Sequence[int] = (), sysfs: str = "
         except Exception as e:                 # noqa: BLE001 -- placement is an optimisation, never fatal
             return {"mode": mode, "cpus": "", "bound_threads": 0, "source": f"error: {e}"}
         cpus = list(plan.get("cpus") or [])
+        if mode == "auto" and 0 < len(cpus) < MIN_AUTO_CPUS:
+            # a rank's serve loop, ring / ingest / peer threads and the
+            # preprocess host work need a few cores: a cpuset that leaves it
+            # fewer is better shared than split (explicit "gpu" still binds)
+            plan = dict(plan, source=f"{plan.get('source')}: only {len(cpus)} CPUs for this rank, left unbound")
+            cpus = []
     n = apply_binding(cpus, [0] + [int(p) for p in extra_pids]) if cpus else 0
     out = dict(plan, mode=mode, cpus=format_cpulist(cpus), bound_threads=n)
     return out

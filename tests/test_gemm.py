@@ -233,10 +233,13 @@ def test_serving_shapes_match_fp32():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("epi", ["regs", "lds"])
 @pytest.mark.parametrize("T,K", [(1, 512), (37, 4096), (300, 1024), (4041, 4096), (4041, 14336)])
-def test_gemm_residual_matches_fp32(T, K):
-    """res += x·wᵀ in place (GM_EPI_RESID, the o / down projections): against
-    the fp32 sum rounded once; rows past M of a larger buffer untouched."""
+def test_gemm_residual_matches_fp32(T, K, epi):
+    """res += x·wᵀ in place (the o / down projections; "regs" = GM_EPI_RESID,
+    the residual tile through registers; "lds" = GM_EPI_RESID_LDS, staged by
+    DMA): against the fp32 sum rounded once; rows past M of a larger buffer
+    untouched."""
     N = 4096 if T == 4041 else 1024
     x, w = _rand(T, K, N, seed=300 + T)
     g = torch.Generator(device=DEV).manual_seed(T)
@@ -244,7 +247,10 @@ def test_gemm_residual_matches_fp32(T, K):
     big[:T] = torch.randn(T, N, generator=g, device=DEV).to(torch.bfloat16)
     res0 = big[:T].float().clone()
     ref = res0 + x.float() @ w.float().t()
-    G.gemm_residual(x, w, big[:T])
+    if epi == "regs":
+        G.gemm_residual(x, w, big[:T])
+    else:
+        G._launch(x, w, big[:T], G.EPI_RESID_LDS)
     err = (big[:T].float() - ref).abs().max().item()
     assert err <= 0.01 * ref.abs().max().item() + 1e-3, err
     assert (big[T:] == 3.0).all()
