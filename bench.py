@@ -99,6 +99,9 @@ def parse(argv=None):
                     help="LM head on hipBLASLt + torch.argmax instead of the GEMM with the argmax epilogue")
     ap.add_argument("--fused-resid", action="store_true",
                     help="A/B: o / down projections on the hand-written residual-add GEMM epilogue (default hipBLASLt beta = 1)")
+    ap.add_argument("--resid-epi", default="regs", choices=["regs", "lds", "pre"],
+                    help="with --fused-resid: the residual tile through registers (GM_EPI_RESID) or staged into "
+                         "LDS by DMA (GM_EPI_RESID_LDS) -- A/B")
     ap.add_argument("--no-fused-qkv", action="store_true",
                     help="qkv on hipBLASLt + rope_kv instead of the GEMM with the RoPE/KV epilogue (A/B)")
     ap.add_argument("--no-fused-mlp", action="store_true",
@@ -250,6 +253,9 @@ def main(argv=None) -> int:
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dry = a.cpu_dry_run
+    if a.resid_epi != "regs":
+        from llm_message_queue_amd.ops import gemm as _G
+        _G.RESID_EPI = _G.EPI_RESID_LDS if a.resid_epi == "lds" else _G.EPI_RESID_PRE
     if dry:
         # CPU rehearsal of the exact control flow (collectives, tick counts,
         # reductions) with a tiny model and gloo -- never a measurement
@@ -661,7 +667,7 @@ def main(argv=None) -> int:
                    "fused_qkv": bool(engine.model.fused_qkv),
                    "row_scale_norm": bool(engine.model.row_scale_norm),
                    "fused_head": bool(engine.model.fused_head),
-                   "fused_resid": bool(engine.model.fused_resid),
+                   "fused_resid": bool(engine.model.fused_resid), "resid_epi": a.resid_epi,
                    "prune_last": bool(getattr(engine.model, "prune_last", False))},
         # realtime tier, arrival -> LAST generated token (the 8B backend's 4
         # forwards included); the headline's clock is arrival -> dispatch

@@ -177,6 +177,7 @@ def main():
                 fns = {"hipblaslt_resid": lambda: y.addmm_(x, w.t()),
                        "hip_resid": lambda: G.gemm_residual(x, w, y),
                        "hip_resid_lds": lambda: G._launch(x, w, y, G.EPI_RESID_LDS),
+                       "hip_resid_pre": lambda: G._launch(x, w, y, G.EPI_RESID_PRE),
                        "hip_plain": lambda: G.gemm(x, w, out=y)}
                 for f in fns.values():
                     f()

@@ -58,7 +58,14 @@ constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
 constexpr int GM_GROUP_M = 8;                    // default M-tiles per block-order group
 
 enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4, GM_EPI_RESID = 5,
-       GM_EPI_RESID_LDS = 6 };
+       GM_EPI_RESID_LDS = 6, GM_EPI_RESID_PRE = 7 };
+// GM_EPI_RESID_PRE: GM_EPI_RESID_LDS whose first quarter of the residual tile
+// (rows 0-31 of every wave's 128 x 64 block) is fetched into the 32 KiB of
+// LDS gfx950 has beyond the operand buffers at kernel start, so it is in LDS
+// long before the epilogue; the launch asks for 160 KiB.
+constexpr int GM_LDS_SPARE = 32768;
+template <int EPI>
+constexpr int gm_lds_bytes() { return EPI == GM_EPI_RESID_PRE ? GM_LDS_BYTES + GM_LDS_SPARE : GM_LDS_BYTES; }
 
 // GM_EPI_ARGMAX: the LM head's greedy sampling as the epilogue -- no [M][N]
 // logits tensor.  Each tile writes, per row, the max over its 256 columns and
@@ -152,6 +159,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp,
     const GmArgmax am) {
   extern __shared__ __align__(16) uint8_t smem[];
+  static_assert(EPI != GM_EPI_RESID_PRE || SCHED >= 1, "the residual prefetch is issued by the SCHED >= 1 prologue");
 
   const int tiles_m = (M + GM_BM - 1) / GM_BM;
   const int tiles_n = N / GM_BN;
@@ -314,6 +322,20 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     // 8/4/8/4 fragment reads per phase instead of 12/4/8/0.  Stage order per
     // buffer is B0, A0, B1, A1; every restage is >= 2 phases after the
     // half-tile's last read (safe with the wave-row stagger).
+    if constexpr (EPI == GM_EPI_RESID_PRE) {
+      // the residual rows 0-31 of this wave's output block -> spare LDS; the
+      // prologue's counted vmcnt waits retire them with the first half-tiles
+      const int col0p = tn * GM_BN + wc * 64, row0p = tm * GM_BM + wr * 128;
+      const __amdgpu_buffer_rsrc_t rsp =
+          __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (uint32_t)M * (uint32_t)N * 2u, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = i * 8 + (lane >> 3), c = lane & 7;
+        const uint32_t vo = ((uint32_t)(row0p + r) * (uint32_t)N + (uint32_t)(col0p + c * 8)) * 2u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsp, (gm_lds_ptr)(smem + GM_LDS_BYTES + w * 4096 + i * 1024), 16,
+                                                 vo, 0, 0, 0);
+      }
+    }
     GM_STAGE(0, GM_B0, 0);
     GM_STAGE(0, GM_A0, 0);
     GM_STAGE(0, GM_B1, 0);
@@ -635,7 +657,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         GM_LGKM(0);
         __builtin_amdgcn_wave_barrier();
       }
-  } else if (EPI == GM_EPI_RESID_LDS) {
+  } else if (EPI == GM_EPI_RESID_LDS || EPI == GM_EPI_RESID_PRE) {
     // The residual tile staged by DMA instead of through registers: the
     // wave's 128 x 64 bf16 block of C lands in its 16 KiB of LDS (16
     // buffer_load ... lds of 16 B per lane, row-major, the plain epilogue's
@@ -645,19 +667,23 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     // four-pass fp32 staging (GM_EPI_RESID): half the global instructions
     // (16-B instead of 8-B loads and stores), no fp32 LDS round trip, one
     // wave barrier instead of eight.
+    // (GM_EPI_RESID_PRE: rows 0-31 are already in the spare LDS, loaded at
+    // kernel start; rows r < 32 are exactly mh = 0, m < 2 / it < 4 below)
+    constexpr int kPre = EPI == GM_EPI_RESID_PRE ? 4 : 0;
     uint8_t* cw = smem + w * 16384;
+    uint8_t* cpre = smem + GM_LDS_BYTES + w * 4096;
+    auto rowp = [&](int r) -> uint8_t* { return (kPre && r < 32) ? cpre + r * 128 : cw + r * 128; };
     const int col0 = tn * GM_BN + wc * 64;
     const __amdgpu_buffer_rsrc_t rsc =
         __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (uint32_t)M * (uint32_t)N * 2u, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {                 // LDS bytes [i KiB, i+1 KiB): rows 8i .. 8i+7
+    for (int i = kPre; i < 16; ++i) {              // LDS bytes [i KiB, i+1 KiB): rows 8i .. 8i+7
       const int r = i * 8 + (lane >> 3), c = lane & 7;
       const uint32_t vo = ((uint32_t)(row0 + r) * (uint32_t)N + (uint32_t)(col0 + c * 8)) * 2u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsc, (gm_lds_ptr)(cw + i * 1024), 16, vo, 0, 0, 0);
     }
     GM_VMCNT(0);
     __builtin_amdgcn_wave_barrier();
-    uint16_t* o = reinterpret_cast<uint16_t*>(cw);
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
@@ -668,8 +694,9 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
           for (int n = 0; n < 2; ++n)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const int at = (mh * 64 + m * 16 + fq * 4 + j) * 64 + nh * 32 + n * 16 + fr;
-              o[at] = gm_f2bf(__uint_as_float((uint32_t)o[at] << 16) + acc[mh][m][nh][n][j]);
+              const int r = mh * 64 + m * 16 + fq * 4 + j;
+              uint16_t* e = reinterpret_cast<uint16_t*>(rowp(r) + (nh * 32 + n * 16 + fr) * 2);
+              *e = gm_f2bf(__uint_as_float((uint32_t)*e << 16) + acc[mh][m][nh][n][j]);
             }
     GM_LGKM(0);
     __builtin_amdgcn_wave_barrier();
@@ -678,7 +705,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
       const int qd = it * 64 + lane;               // row qd/8, chunk qd%8
       const int r = qd >> 3, cb = qd & 7;
       const int grow = row0 + r;
-      const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(cw + r * 128 + cb * 16);
+      const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(rowp(r) + cb * 16);
       if (grow < M) *reinterpret_cast<gm_u32x4*>(C + (int64_t)grow * N + col0 + cb * 8) = v;
     }
   } else if (EPI == GM_EPI_SWIGLU) {

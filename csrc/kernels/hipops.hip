@@ -204,12 +204,13 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, GM_LDS_BYTES));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, gm_lds_bytes<EPI>()));
     attr = true;
   }
   const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
   const int grid = sp.ws ? sp.full + 2 * (tiles - sp.full) : tiles;
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(grid), dim3(GM_THREADS), GM_LDS_BYTES, st, a, w, c,
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(grid), dim3(GM_THREADS), gm_lds_bytes<EPI>(), st,
+                     a, w, c,
                      M, N, K, group_m, rs, rp, sp, am);
 }
 
@@ -236,6 +237,9 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
     launch_gemm<GM_EPI_RESID>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_RESID_LDS)                // the same, residual tile staged by DMA (A/B)
     launch_gemm<GM_EPI_RESID_LDS>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
+                                  group_m);
+  else if (epi == GM_EPI_RESID_PRE)                // ... with its first quarter prefetched at start (A/B)
+    launch_gemm<GM_EPI_RESID_PRE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
                                   group_m);
   else if (epi == GM_EPI_STORE + 16)
     launch_gemm<GM_EPI_STORE, true, 0>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);

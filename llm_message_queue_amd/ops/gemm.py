@@ -25,6 +25,9 @@ EPI_STORE = 0
 EPI_SWIGLU = 2
 EPI_RESID = 5
 EPI_RESID_LDS = 6   # A/B: residual tile staged into LDS by DMA, added in place
+EPI_RESID_PRE = 7   # A/B: ... its first quarter fetched into spare LDS at kernel start
+# which residual epilogue ``gemm_residual`` launches (bench.py --resid-epi)
+RESID_EPI = EPI_RESID
 TILE_N = 256
 SWIGLU_HALF = 32   # per-wave gate/up split (a wave owns 64 output columns)
 
@@ -147,7 +150,7 @@ def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor) -> torch.
     _check(res, "res")
     if res.shape != (x.shape[0], w.shape[0]):
         raise ValueError("gemm_residual: res shape mismatch")
-    return _launch(x, w, res, EPI_RESID)
+    return _launch(x, w, res, RESID_EPI)
 
 
 def residual_tiles_ok(M: int, N: int, cus: int, min_fill: float = 0.97) -> bool:

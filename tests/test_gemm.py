@@ -233,7 +233,7 @@ def test_serving_shapes_match_fp32():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("epi", ["regs", "lds"])
+@pytest.mark.parametrize("epi", ["regs", "lds", "pre"])
 @pytest.mark.parametrize("T,K", [(1, 512), (37, 4096), (300, 1024), (4041, 4096), (4041, 14336)])
 def test_gemm_residual_matches_fp32(T, K, epi):
     """res += x·wᵀ in place (the o / down projections; "regs" = GM_EPI_RESID,
@@ -250,7 +250,7 @@ def test_gemm_residual_matches_fp32(T, K, epi):
     if epi == "regs":
         G.gemm_residual(x, w, big[:T])
     else:
-        G._launch(x, w, big[:T], G.EPI_RESID_LDS)
+        G._launch(x, w, big[:T], G.EPI_RESID_LDS if epi == "lds" else G.EPI_RESID_PRE)
     err = (big[:T].float() - ref).abs().max().item()
     assert err <= 0.01 * ref.abs().max().item() + 1e-3, err
     assert (big[T:] == 3.0).all()
