@@ -258,7 +258,8 @@ def test_sigkilled_job_leaves_nothing_and_next_job_completes_every_request():
     assert not [n for n in _shm_names() - before if rb[0]["job"] in n]
 
 
-def test_restart_after_peer_lost_gets_a_fresh_incarnation():
+@pytest.mark.parametrize("standalone", [True, False])
+def test_restart_after_peer_lost_gets_a_fresh_incarnation(standalone):
     """``torchrun --max-restarts 1``: rank 0's backend stalls (injected), so
     rank 1 loses its peer at the control-plane collective (``PeerLost``) and
     exits non-zero; torchrun restarts the group.  The new incarnation has its
@@ -266,7 +267,7 @@ def test_restart_after_peer_lost_gets_a_fresh_incarnation():
     and serves every request."""
     env = {"LLMQ_SERVER__FAULT_INJECTION": "true", "LLMQ_COLLECTIVE_TIMEOUT_S": "4",
            "LLMQ_SERVER__STALL_FATAL_AFTER": "0", "LLMQ_FATAL_EXIT_GRACE_S": "5"}
-    s = Server([], env_extra=env, torchrun=2, restarts=1, standalone=True)
+    s = Server([], env_extra=env, torchrun=2, restarts=1, standalone=standalone)
     try:
         r0 = s.ranks(2, restart=0)
         s.wait_for(lambda e: e.get("event") == "listening")
