@@ -5,19 +5,11 @@ load), and the extra local forward a faster GPU takes while its peers are
 behind.  Serve-loop only."""
 from __future__ import annotations
 
-import threading  # noqa: F401
 import time
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+from typing import Sequence
 
-import numpy as np
-
-from ..backend.engine import Request  # noqa: F401
-from ..models.message import Message, MessageStatus  # noqa: F401
-from ..parallel import planner  # noqa: F401
-from ..queue.core import QueueError  # noqa: F401
-from .descriptors import (K_CANCEL, K_CANCELLED, K_DONE, K_FAIL, K_TIMEOUT, _get64, _put64,  # noqa: F401
-                          conv_key)
-from .latency import P_LANE, P_OWN  # noqa: F401
+from ..models.message import Message, MessageStatus
+from .latency import P_LANE, P_OWN
 
 
 class OwnAdmissionMixin:

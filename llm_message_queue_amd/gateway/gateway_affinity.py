@@ -9,19 +9,14 @@ and ``_skip_away`` hold ``_pin_lock``; everything else runs on the serve
 loop."""
 from __future__ import annotations
 
-import threading  # noqa: F401
-import time
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+from typing import Dict, List, Tuple
 
 import numpy as np
 
-from ..backend.engine import Request  # noqa: F401
-from ..models.message import Message, MessageStatus  # noqa: F401
-from ..parallel import planner  # noqa: F401
-from ..queue.core import QueueError  # noqa: F401
-from .descriptors import (K_CANCEL, K_CANCELLED, K_DONE, K_FAIL, K_TIMEOUT, _get64, _put64,  # noqa: F401
-                          conv_key)
-from .latency import P_LANE, P_OWN  # noqa: F401
+from ..backend.engine import Request
+from ..models.message import Message
+from ..parallel import planner
+from .descriptors import conv_key
 
 
 class AffinityMixin:
