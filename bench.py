@@ -98,10 +98,13 @@ def parse(argv=None):
     ap.add_argument("--no-fused-head", action="store_true",
                     help="LM head on hipBLASLt + torch.argmax instead of the GEMM with the argmax epilogue")
     ap.add_argument("--fused-resid", action="store_true",
-                    help="A/B: o / down projections on the hand-written residual-add GEMM epilogue (default hipBLASLt beta = 1)")
-    ap.add_argument("--resid-epi", default="regs", choices=["regs", "lds", "pre"],
-                    help="with --fused-resid: the residual tile through registers (GM_EPI_RESID) or staged into "
-                         "LDS by DMA (GM_EPI_RESID_LDS) -- A/B")
+                    help="o / down projections on the hand-written residual-add GEMM epilogue (the default; "
+                         "kept for the A/B scripts)")
+    ap.add_argument("--no-fused-resid", action="store_true",
+                    help="A/B: o / down projections on hipBLASLt beta = 1")
+    ap.add_argument("--resid-epi", default="lds", choices=["regs", "lds", "pre"],
+                    help="the fused residual tile through registers (GM_EPI_RESID), staged into LDS by DMA "
+                         "(GM_EPI_RESID_LDS, default) or with its first quarter prefetched (GM_EPI_RESID_PRE)")
     ap.add_argument("--no-fused-qkv", action="store_true",
                     help="qkv on hipBLASLt + rope_kv instead of the GEMM with the RoPE/KV epilogue (A/B)")
     ap.add_argument("--no-fused-mlp", action="store_true",
@@ -253,9 +256,8 @@ def main(argv=None) -> int:
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dry = a.cpu_dry_run
-    if a.resid_epi != "regs":
-        from llm_message_queue_amd.ops import gemm as _G
-        _G.RESID_EPI = _G.EPI_RESID_LDS if a.resid_epi == "lds" else _G.EPI_RESID_PRE
+    from llm_message_queue_amd.ops import gemm as _G
+    _G.RESID_EPI = {"regs": _G.EPI_RESID, "lds": _G.EPI_RESID_LDS, "pre": _G.EPI_RESID_PRE}[a.resid_epi]
     if dry:
         # CPU rehearsal of the exact control flow (collectives, tick counts,
         # reductions) with a tiny model and gloo -- never a measurement
@@ -319,7 +321,7 @@ def main(argv=None) -> int:
                                fused_mlp=False if a.no_fused_mlp else None,
                                fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
                                fused_head=False if a.no_fused_head else None,
-                               fused_resid=True if a.fused_resid else None,
+                               fused_resid=False if a.no_fused_resid else None,
                                prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer

@@ -165,9 +165,11 @@ static void summarise_project(uintptr_t pooled, uintptr_t seg_off, int C, uintpt
                               uintptr_t state, uintptr_t first_flag, int H, int DS, uintptr_t stream) {
   require(H == SM_H && DS == SM_DS, "summarise expects H=1024, DS=256");
   if (C == 0) return;
-  hipLaunchKernelGGL(summarise_project_kernel, dim3((C + SM_ROWS - 1) / SM_ROWS), dim3(256), 0, S(stream),
-                     P<const float>(pooled), P<const int32_t>(seg_off), C, P<const uint16_t>(Pt), alpha,
-                     P<float>(state), P<int32_t>(first_flag));
+  // (16-conversation row block, 64-column block): 4 blocks per 16 conversations
+  const dim3 grid((C + SM_ROWS - 1) / SM_ROWS, SM_DS / SM_NB);
+  hipLaunchKernelGGL(summarise_project_kernel, grid, dim3(256), 0, S(stream), P<const float>(pooled),
+                     P<const int32_t>(seg_off), C,
+                     P<const uint16_t>(Pt), alpha, P<float>(state), P<int32_t>(first_flag));
   check_launch();
 }
 
@@ -433,7 +435,7 @@ static void kv_move(uintptr_t table, int layers, int slots, int slot, int n, int
   require(slot >= 0 && slot < slots, "kv_move: slot out of range");
   require(n > 0 && n <= max_ctx, "kv_move: token count out of range");
   require(table != 0 && buf != 0 && buf % 16 == 0, "kv_move: null or misaligned buffer");
-  const dim3 grid(layers * 2 * hkv);
+  const dim3 grid(layers * 2 * hkv, (n * 16 + KV_CHUNK - 1) / KV_CHUNK);   // (run, chunk of the run)
   if (pack)
     hipLaunchKernelGGL(kv_move_kernel<true>, grid, dim3(256), 0, S(stream), P<const uint64_t>(table), layers, slot,
                        n, max_ctx, hkv, P<uint4>(buf));

@@ -8,9 +8,14 @@
 // n x 256 bytes.  Buffer layout: [layer][k|v][kv_head][n][128] -- the wire
 // format RCCL sends between GPUs (llm_message_queue_amd/parallel/migration.py).
 //
-// Grid: one 256-thread workgroup per (layer, k|v, kv head) run: 32 x 2 x 8 =
-// 512 workgroups for Llama-3-8B (two per CU on 256 CUs), 16-byte vector
-// loads/stores, a pure HBM stream (n = 512 tokens: 64 MiB moved per launch).
+// Grid: (layer, k|v, kv head) run x 32 KiB chunks of the run: each 256-thread
+// workgroup moves KV_UNROLL x 16 B per thread with all KV_UNROLL loads in
+// flight before the first store, non-temporal both ways (touched once).  The
+// round-4 form (one workgroup per run, a load -> store chain of one 16-byte
+// vector per thread per iteration: ~2 MiB in flight chip-wide) moved 4.37
+// TB/s beyond the 256 MiB Infinity Cache against a plain copy's 5.04 TB/s
+// (profiles/r5_preprocess_kernels_pmc.md); at 512 tokens this grid is 2048
+// workgroups with 32 MiB in flight.
 // The per-layer base pointers come from a device table [2 L] (k0..kL-1,
 // v0..vL-1) built once by the migrator.
 #pragma once
@@ -18,6 +23,10 @@
 #include <stdint.h>
 
 namespace llmq {
+
+constexpr int KV_UNROLL = 8;
+constexpr int KV_CHUNK = 256 * KV_UNROLL;   // 16-byte vectors per workgroup
+typedef unsigned int kv_u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool PACK>
 __global__ __launch_bounds__(256) void kv_move_kernel(const uint64_t* __restrict__ table, int layers, int slot,
@@ -27,15 +36,23 @@ __global__ __launch_bounds__(256) void kv_move_kernel(const uint64_t* __restrict
   const int lk = seg / hkv;
   const int layer = lk >> 1, kv = lk & 1;
   uint4* cache = reinterpret_cast<uint4*>(table[kv * layers + layer]);
-  // 128 bf16 per position = 256 B = 16 uint4
-  uint4* c = cache + ((size_t)slot * hkv + h) * (size_t)max_ctx * 16;
-  uint4* b = buf + (size_t)seg * (size_t)n * 16;
+  // 128 bf16 per position = 256 B = 16 vectors
+  kv_u32x4* c = reinterpret_cast<kv_u32x4*>(cache + ((size_t)slot * hkv + h) * (size_t)max_ctx * 16);
+  kv_u32x4* b = reinterpret_cast<kv_u32x4*>(buf + (size_t)seg * (size_t)n * 16);
+  const kv_u32x4* src = PACK ? c : b;
+  kv_u32x4* dst = PACK ? b : c;
   const int nv = n * 16;
-  for (int i = threadIdx.x; i < nv; i += 256) {
-    if (PACK)
-      b[i] = c[i];
-    else
-      c[i] = b[i];
+  const int i0 = blockIdx.y * KV_CHUNK + threadIdx.x;
+  kv_u32x4 v[KV_UNROLL];
+#pragma unroll
+  for (int u = 0; u < KV_UNROLL; ++u) {
+    const int i = i0 + u * 256;
+    if (i < nv) v[u] = __builtin_nontemporal_load(src + i);
+  }
+#pragma unroll
+  for (int u = 0; u < KV_UNROLL; ++u) {
+    const int i = i0 + u * 256;
+    if (i < nv) __builtin_nontemporal_store(v[u], dst + i);
   }
 }
 

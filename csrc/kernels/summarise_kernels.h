@@ -13,11 +13,25 @@
 // plus a salient-token list: the top-k token hashes of the evicted messages
 // by frequency (stop words excluded), ties broken by first occurrence.
 //
-// summarise_project_kernel: one workgroup = 16 conversations x 256 outputs;
-// the 16 mean rows are built in LDS as bf16 (32 KiB, chunk-swizzled like
-// embed_pool's A tile) and each wave computes 64 output columns with
-// v_mfma_f32_16x16x32_bf16 over K = 1024 (32 k-steps); P is stored
-// transposed (Pt[DS][H]) so B fragments are 16 contiguous bytes.
+// summarise_project_kernel (round 5; profiles/r5_preprocess_kernels_pmc.md):
+// one workgroup = 16 conversations x 64 output columns (grid.y = DS / 64),
+// its 4 waves split K = 1024 into quarters.  The round-4 form (one block per
+// 16 conversations, every lane a serial chain of 8 x n_msgs dependent loads,
+// then 32 k-steps each waiting on its own B load, 2-byte LDS stores) took a
+// flat 43 us at 16..256 conversations with 60 % LDS bank conflicts:
+//   * all 32 B fragments of a wave's 8 k-steps x 4 column tiles are issued at
+//     kernel entry (Pt is 512 KiB, L2-resident), overlapping the mean pass;
+//   * the mean pass walks the 16 conversations' messages -- one contiguous
+//     run of pooled rows -- as ONE flat loop, 8 messages per round with the 8
+//     float4 loads in flight together; conversation boundaries are uniform
+//     (every lane handles the same message), and a finished row's mean goes
+//     to LDS as 4 packed bf16 (8-byte stores, chunk-swizzled), so the
+//     summation order per element is the old one (m ascending) and the means
+//     are bit-identical;
+//   * v_mfma_f32_16x16x32_bf16 over the wave's 8 k-steps, then the four
+//     K-quarter partials meet in LDS (stride-68 rows, conflict-free) and the
+//     EMA update is a float4 per thread.
+// P is stored transposed (Pt[DS][H]) so B fragments are 16 contiguous bytes.
 
 #pragma once
 #include <hip/hip_runtime.h>
@@ -38,67 +52,134 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
   return (uint16_t)(u >> 16);
 }
 
+constexpr int SM_NB = 64;                 // output columns per block
+constexpr int SM_KQ = SM_H / 4;           // K per wave
+constexpr int SM_RED = SM_NB + 4;         // reduction row stride (floats)
+
 __global__ void __launch_bounds__(256)
 summarise_project_kernel(const float* __restrict__ pooled, const int32_t* __restrict__ seg_off, int C,
                          const uint16_t* __restrict__ Pt, float alpha, float* __restrict__ state,
                          int32_t* __restrict__ first_flag) {
-  __shared__ __align__(16) uint16_t Am[SM_ROWS * SM_H];  // 32 KiB
+  __shared__ __align__(16) uint16_t Am[4][SM_ROWS * SM_KQ];       // per wave: 16 rows x its K quarter (8 KiB)
+  __shared__ __align__(16) float red[4][SM_ROWS * SM_RED];        // K-quarter partials (17 KiB)
+  __shared__ int32_t bnd[SM_ROWS + 1];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
   const int c0 = blockIdx.x * SM_ROWS;
+  const int n0 = blockIdx.y * SM_NB;
+  const int kq = wv * SM_KQ;
+  const int fr = lane & 15, fq = lane >> 4;
 
-  // ---- segment means -> bf16 rows (chunk ^ (row & 15) swizzle, 8 bf16 per chunk)
-  for (int idx = tid; idx < SM_ROWS * (SM_H / 8); idx += 256) {
-    const int r = idx / (SM_H / 8);
-    const int ch = idx % (SM_H / 8);
-    const int c = c0 + r;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (c < C) {
-      const int a = seg_off[c], b = seg_off[c + 1];
-      for (int m = a; m < b; ++m) {
-        const float4 x0 = *reinterpret_cast<const float4*>(pooled + (int64_t)m * SM_H + ch * 8);
-        const float4 x1 = *reinterpret_cast<const float4*>(pooled + (int64_t)m * SM_H + ch * 8 + 4);
-        v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
-        v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
-      }
-      const float inv = (b > a) ? 1.0f / (float)(b - a) : 0.f;
+  // B fragments of all 8 k-steps x 4 column tiles, in flight during the means
+  bf16x8 bfr[SM_KQ / 32][4];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] *= inv;
-    }
-    uint16_t* dst = Am + r * SM_H + ((ch ^ (r & 15)) * 8);
+  for (int ks = 0; ks < SM_KQ / 32; ++ks)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dst[k] = f32_to_bf16_rne(v[k]);
-  }
+    for (int j = 0; j < 4; ++j)
+      bfr[ks][j] = *reinterpret_cast<const bf16x8*>(Pt + (int64_t)(n0 + j * 16 + fr) * SM_H + kq + ks * 32 + fq * 8);
+
+  if (tid <= SM_ROWS) bnd[tid] = seg_off[min(c0 + tid, C)];
   __syncthreads();
 
-  const int fr = lane & 15, fq = lane >> 4;
-  f32x4 acc[4];
+  // ---- segment means of this wave's K quarter: lane = 4 columns
+  uint16_t* A = Am[wv];
+  const int col4 = lane * 4;
+  int r = 0;                                         // current row (uniform)
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto flush = [&](int row) {                        // mean of row -> bf16 into the swizzled tile
+    const int n = bnd[row + 1] - bnd[row];
+    const float inv = n > 0 ? 1.0f / (float)n : 0.f;
+    const uint32_t lo = (uint32_t)f32_to_bf16_rne(acc.x * inv) | ((uint32_t)f32_to_bf16_rne(acc.y * inv) << 16);
+    const uint32_t hi = (uint32_t)f32_to_bf16_rne(acc.z * inv) | ((uint32_t)f32_to_bf16_rne(acc.w * inv) << 16);
+    const int ch = (col4 >> 3) ^ (row & 15);         // 16-byte chunk, swizzled
+    *reinterpret_cast<uint2*>(A + row * SM_KQ + ch * 8 + (col4 & 7)) = make_uint2(lo, hi);
+    acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const int M0 = bnd[0], M1 = bnd[SM_ROWS];
+  for (int m = M0; m < M1; m += 8) {
+    float4 x[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int ks = 0; ks < SM_H / 32; ++ks) {
-    const int ch = ks * 4 + fq;
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(Am + fr * SM_H + ((ch ^ fr) * 8));
+    for (int u = 0; u < 8; ++u)
+      x[u] = (m + u < M1) ? *reinterpret_cast<const float4*>(pooled + (int64_t)(m + u) * SM_H + kq + col4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = wv * 64 + j * 16 + fr;
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(Pt + (int64_t)col * SM_H + ks * 32 + fq * 8);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[j], 0, 0, 0);
+    for (int u = 0; u < 8; ++u) {
+      if (m + u >= M1) break;                        // uniform
+      while (m + u >= bnd[r + 1]) flush(r++);        // uniform: rows ending before message m + u
+      acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
     }
   }
-  // ---- EMA update: C map row = 4*fq + k, col = fr
+  while (r < SM_ROWS) flush(r++);                    // the last row, empty rows, rows past C
+  __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): the tile is written
+  __builtin_amdgcn_wave_barrier();
+
+  // ---- this wave's K quarter: 8 k-steps x 4 column tiles
+  f32x4 pacc[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = wv * 64 + j * 16 + fr;
+  for (int j = 0; j < 4; ++j) pacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = c0 + fq * 4 + k;
-      if (c < C) {
-        float* s = state + (int64_t)c * SM_DS + col;
-        // a conversation's first summary takes the projection as-is
-        *s = first_flag[c] ? acc[j][k] : alpha * (*s) + (1.0f - alpha) * acc[j][k];
-      }
+  for (int ks = 0; ks < SM_KQ / 32; ++ks) {
+    const int ch = ks * 4 + fq;
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + fr * SM_KQ + ((ch ^ fr) * 8));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[ks][j], pacc[j], 0, 0, 0);
+  }
+  // C map: row 4 fq + k, column j * 16 + fr
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[wv][(fq * 4 + k) * SM_RED + j * 16 + fr] = pacc[j][k];
+  __syncthreads();
+
+  // ---- K-quarter sum + EMA: thread = 4 columns of one row
+  const int row = tid >> 4, cc = (tid & 15) * 4;
+  const int c = c0 + row;
+  if (c < C) {
+    float4 p = *reinterpret_cast<const float4*>(&red[0][row * SM_RED + cc]);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 q = *reinterpret_cast<const float4*>(&red[w][row * SM_RED + cc]);
+      p.x += q.x; p.y += q.y; p.z += q.z; p.w += q.w;
     }
+    float4* sp = reinterpret_cast<float4*>(state + (int64_t)c * SM_DS + n0 + cc);
+    if (first_flag[c]) {                             // a conversation's first summary takes the projection
+      *sp = p;
+    } else {
+      const float4 o = *sp;
+      const float b = 1.0f - alpha;
+      *sp = make_float4(alpha * o.x + b * p.x, alpha * o.y + b * p.y, alpha * o.z + b * p.z, alpha * o.w + b * p.w);
+    }
+  }
+}
+
+// One round of a wave argmax over the lanes' NV scores each: returns the
+// winner's score ws (0: nothing left) and index_of(its slot) in wi; the
+// owner lane retires it.  Scores are unique, so exactly one lane owns it.
+template <int NV, typename F>
+__device__ __forceinline__ void sal_wave_pick(uint64_t (&v)[NV], F index_of, int lane, uint64_t& ws, int& wi) {
+  uint64_t bs = 0ull;
+  int be = -1;
+#pragma unroll
+  for (int e = 0; e < NV; ++e)
+    if (v[e] > bs) { bs = v[e]; be = e; }
+  uint64_t gs = bs;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(gs, off, 64);
+    if (o > gs) gs = o;
+  }
+  ws = gs;
+  wi = -1;
+  if (gs == 0ull) return;                              // uniform
+  const uint64_t mine = __ballot(be >= 0 && bs == gs);
+  const int owner = (int)__builtin_ctzll(mine);
+  const int idx = be >= 0 ? index_of(be) : -1;
+  wi = __shfl(idx, owner, 64);
+  if (lane == owner) {
+#pragma unroll
+    for (int e = 0; e < NV; ++e)
+      if (e == be) v[e] = 0ull;
   }
 }
 
@@ -114,8 +195,6 @@ salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* _
   __shared__ int overflow;  // a token found no table slot (> SAL_TABLE distinct): result is partial
   __shared__ int32_t cnt[SAL_TABLE];
   __shared__ int32_t first[SAL_TABLE];
-  __shared__ uint64_t best_s[4];
-  __shared__ int32_t best_i[4];
   const int tid = threadIdx.x;
   const int c = blockIdx.x;
   for (int i = tid; i < SAL_TABLE; i += 256) { key[i] = 0u; cnt[i] = 0; first[i] = 0x7FFFFFFF; }
@@ -148,38 +227,50 @@ salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* _
     ord += n;
   }
   __syncthreads();
-  // K rounds of block argmax over (count desc, first asc)
+  // ---- selection by (count desc, first occurrence asc); scores are unique
+  // (distinct tokens have distinct first positions).  Round 4 ran K rounds of
+  // a block-wide argmax, two barriers each (a flat ~26 us); here each wave
+  // takes the top K of its 512 table entries from registers with shuffles
+  // alone, then wave 0 merges the 4 K candidates the same way: 2 barriers.
+  __shared__ uint64_t cand_s[4][64];
+  __shared__ int32_t cand_i[4][64];
+  const int lane = tid & 63, wv = tid >> 6;
+  constexpr int PER = SAL_TABLE / 256;               // entries per lane
+  uint64_t sc[PER];
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int i = wv * (SAL_TABLE / 4) + e * 64 + lane;
+    sc[e] = cnt[i] > 0 ? (((uint64_t)(uint32_t)cnt[i] << 32) | (uint32_t)(0x7FFFFFFF - first[i])) : 0ull;
+  }
   for (int k = 0; k < K; ++k) {
-    uint64_t bs = 0ull;
-    int bi = -1;
-    for (int i = tid; i < SAL_TABLE; i += 256) {
-      if (cnt[i] > 0) {
-        const uint64_t s = ((uint64_t)(uint32_t)cnt[i] << 32) | (uint32_t)(0x7FFFFFFF - first[i]);
-        if (s > bs) { bs = s; bi = i; }
+    uint64_t ws;
+    int wi;
+    sal_wave_pick(sc, [&](int e) { return wv * (SAL_TABLE / 4) + e * 64 + lane; }, lane, ws, wi);
+    if (lane == 0) { cand_s[wv][k] = ws; cand_i[wv][k] = wi; }
+    if (ws == 0ull) {
+      for (int kk = k + 1 + lane; kk < K; kk += 64) { cand_s[wv][kk] = 0ull; cand_i[wv][kk] = -1; }
+      break;
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    uint64_t cs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cs[q] = lane < K ? cand_s[q][lane] : 0ull;   // candidate (wave q, rank lane)
+    for (int k = 0; k < K; ++k) {
+      uint64_t ws;
+      int wi;
+      sal_wave_pick(cs, [&](int q) { return cand_i[q][lane]; }, lane, ws, wi);
+      if (lane == 0) {
+        if (ws != 0ull && wi >= 0) {
+          out_hash[(int64_t)c * K + k] = key[wi];
+          out_cnt[(int64_t)c * K + k] = (int32_t)(ws >> 32);
+        } else {
+          out_hash[(int64_t)c * K + k] = 0u;
+          out_cnt[(int64_t)c * K + k] = 0;
+        }
       }
     }
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint64_t os = __shfl_xor(bs, off, 64);
-      const int oi = __shfl_xor(bi, off, 64);
-      if (os > bs) { bs = os; bi = oi; }
-    }
-    if ((tid & 63) == 0) { best_s[tid >> 6] = bs; best_i[tid >> 6] = bi; }
-    __syncthreads();
-    if (tid == 0) {
-      uint64_t s = best_s[0];
-      int i = best_i[0];
-      for (int w = 1; w < 4; ++w)
-        if (best_s[w] > s) { s = best_s[w]; i = best_i[w]; }
-      if (i >= 0 && s > 0ull) {
-        out_hash[(int64_t)c * K + k] = key[i];
-        out_cnt[(int64_t)c * K + k] = cnt[i];
-        cnt[i] = 0;
-      } else {
-        out_hash[(int64_t)c * K + k] = 0u;
-        out_cnt[(int64_t)c * K + k] = 0;
-      }
-    }
-    __syncthreads();
   }
   // the host recomputes a flagged conversation exactly (never a silently
   // truncated top-k)

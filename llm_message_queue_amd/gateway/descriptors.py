@@ -12,6 +12,9 @@ K_MIGRATE = 4       # [kind, conv lo/hi, dest]: to a conversation's home GPU -- 
 # a backend aborted a request in flight: its processing deadline passed /
 # its origin cancelled it (completion-record layout, owed like K_DONE)
 K_TIMEOUT, K_CANCELLED = 5, 6
+# K_FAIL's admitted field: the backend failed while running the request
+# (the origin retries with backoff) / it never ran there (requeued as is)
+FAIL_UNTOUCHED, FAIL_FAILED = 0, 1
 K_CANCEL = 7        # [kind, handle lo/hi, origin]: origin -> the GPU running its request: abort it
 DESC_HDR = 17       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
 #                    dialog history length, decision - enq (us), processing timeout (ms)];

@@ -20,7 +20,7 @@ import numpy as np
 from ..backend.engine import Request
 from ..models.message import Message, MessageStatus
 from ..queue.core import QueueError
-from .descriptors import K_CANCELLED, K_FAIL, K_TIMEOUT, _get64
+from .descriptors import FAIL_FAILED, FAIL_UNTOUCHED, K_CANCELLED, K_FAIL, K_TIMEOUT, _get64
 
 
 class FailureMixin:
@@ -77,15 +77,24 @@ class FailureMixin:
                     self.on_expire(m)
 
     def _remote_fail(self, row: np.ndarray) -> None:
-        """The backend my request was sent to evacuated it: queue it again."""
-        handle = int(_get64(row.reshape(1, -1), 1)[0])
+        """The backend my request was sent to handed it back (K_FAIL).  The
+        record's admitted field is 1 when that backend failed while running
+        it: the retry path (backoff, retry count, dead letter).  0: it never
+        ran there (a held turn, an over-committed plan, an operator's drain):
+        back into its tier at once, no retry spent."""
+        r1 = row.reshape(1, -1)
+        handle = int(_get64(r1, 1)[0])
         m = self.remote_out.pop(handle, None)
         if m is None:
             return
+        failed = int(_get64(r1, 5)[0]) == FAIL_FAILED
         self.inflight_by_tier[m.tier] -= 1
         if self.lb is not None and m.endpoint_id:
-            self.lb.release_endpoint(m.endpoint_id, 0, True)     # (note_dispatch counted it)
-        self._retry(m, "backend evacuated the request")
+            self.lb.release_endpoint(m.endpoint_id, 0, failed)   # (note_dispatch counted it)
+        if failed:
+            self._retry(m, "backend failed while running the request")
+        else:
+            self._requeue(m)
         self.counters["handed_back"] += 1
 
     def _remote_abort(self, row: np.ndarray) -> None:
@@ -288,7 +297,7 @@ class FailureMixin:
                 self._requeue(r.meta)
             else:
                 origin, handle, tier = r.meta[:3]
-                self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
+                self._done_owed[origin].append((handle, tier, FAIL_UNTOUCHED, 0, K_FAIL))
         if self.migrator is not None:
             # imports still landing on the side stream write into reserved
             # slots that abort_all hands back to the free list: the next
@@ -309,6 +318,7 @@ class FailureMixin:
                     self._requeue(m)
             else:
                 origin, handle, tier = self.foreign.pop(r.req_id)
-                self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
+                self._done_owed[origin].append((handle, tier, FAIL_FAILED if failure else FAIL_UNTOUCHED,
+                                                0, K_FAIL))
         self.counters["evacuated"] += n
         return n

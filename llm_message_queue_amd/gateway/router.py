@@ -41,8 +41,8 @@ from ..utils.logging import get_logger
 
 NS = 1_000_000_000
 
-from .descriptors import (DESC_HDR, K_CANCEL, K_CANCELLED, K_DISPATCH, K_DONE, K_FAIL, K_MIGRATE,  # noqa: F401
-                          K_TIMEOUT, KV_MIGRATE, _get64, _put64, conv_key)
+from .descriptors import (DESC_HDR, FAIL_UNTOUCHED, K_CANCEL, K_CANCELLED, K_DISPATCH, K_DONE,  # noqa: F401
+                          K_FAIL, K_MIGRATE, K_TIMEOUT, KV_MIGRATE, _get64, _put64, conv_key)
 from .latency import (PATHS, P_LANE, P_OWN, P_PLAN_LOCAL, P_PLAN_REMOTE, STAGES, LatencyRecorder,  # noqa: F401
                       StageRecorder, _hbin, hist_percentile)
 from .gateway_admission import OwnAdmissionMixin
@@ -772,7 +772,7 @@ class Gateway(FailureMixin, AffinityMixin, ResourceMixin, OwnAdmissionMixin):
                     self._requeue(r.meta)
                 else:
                     origin, handle, tier = r.meta[:3]
-                    self._done_owed[origin].append((handle, tier, 0, 0, K_FAIL))
+                    self._done_owed[origin].append((handle, tier, FAIL_UNTOUCHED, 0, K_FAIL))
         self.counters["dispatched"] += len(admitted)
         # requests enqueued while this rank waited at the collectives: into
         # the capacity the plan left on the own GPU now, not a tick later

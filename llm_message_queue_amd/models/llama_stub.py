@@ -112,14 +112,15 @@ class LlamaStub:
         # [rows][vocab] logits) when the step samples >= 256 rows
         self.fused_head = (impl == "hip") if fused_head is None else bool(fused_head)
         # o / down projections into the residual on the hand-written kernel
-        # (GM_EPI_RESID) when its 256x256 tiles fill whole waves of the chip
+        # (ops.gemm.RESID_EPI: the residual tile staged into LDS by DMA and
+        # added in place) when its 256x256 tiles fill whole waves of the chip
         # (the saturated serving step: T ~ 4,040 -> 256 tiles); hipBLASLt's
         # beta = 1 stream-K kernel otherwise (ops.gemm.residual_tiles_ok).
-        # Off by default: at parity with hipBLASLt (down 0.306 vs 0.305 ms,
-        # o 0.0997 vs 0.0980 ms at T = 4041, profiles/r2_gemm_resid_ab.jsonl)
-        # -- with one wave of tiles every block reads and writes its residual
-        # tile at the same moment, so the 66 MB round trip is exposed in both.
-        self.fused_resid = False if fused_resid is None else bool(fused_resid)
+        # Default since round 5: faster than hipBLASLt in isolation (o 94.8 vs
+        # 95.3 us, down 299.7 vs 304.3 us at T = 4041,
+        # profiles/r5_resid_ab_1gpu.jsonl) and >= it in the serving A/B
+        # (profiles/r5_resid_serving_ab_1gpu.jsonl).
+        self.fused_resid = (impl == "hip") if fused_resid is None else bool(fused_resid)
         self._cus = G._cu_count(self.device) if (self.fused_resid and self.device.type == "cuda") else 0
         # fused paths take the raw residual rows + a per-row RMSNorm scale
         # (True) or an rmsnorm'd copy of the rows (False, A/B)

@@ -23,11 +23,11 @@ from .. import _native
 
 EPI_STORE = 0
 EPI_SWIGLU = 2
-EPI_RESID = 5
-EPI_RESID_LDS = 6   # A/B: residual tile staged into LDS by DMA, added in place
+EPI_RESID = 5       # A/B: residual tile read into registers in the epilogue
+EPI_RESID_LDS = 6   # residual tile staged into LDS by DMA, added in place (default)
 EPI_RESID_PRE = 7   # A/B: ... its first quarter fetched into spare LDS at kernel start
 # which residual epilogue ``gemm_residual`` launches (bench.py --resid-epi)
-RESID_EPI = EPI_RESID
+RESID_EPI = EPI_RESID_LDS
 TILE_N = 256
 SWIGLU_HALF = 32   # per-wave gate/up split (a wave owns 64 output columns)
 

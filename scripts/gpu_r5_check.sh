@@ -19,6 +19,7 @@ if [ -z "${SKIP_BENCH:-}" ]; then
   python -c "import json;d=json.loads(open('gpurun_out/r5_bench.json').read().strip().splitlines()[-1]);print('bench', d['value'], d['p99_by_tier_ms'], d['p99_e2e_by_tier_ms'], d['slo_search']['util_tried'])"
 fi
 i=0
+[ -n "${SKIP_HTTP:-}" ] && exit 0
 for V in ${VARIANTS:-1:5300:--bench-config 2:5000:--bench-config}; do
   IFS=: read -r RANKS RATE EXTRA <<< "$V"
   i=$((i + 1))

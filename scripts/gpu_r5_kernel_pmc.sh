@@ -32,4 +32,4 @@ for C in ${CONVS:-16 64 256}; do
   pass summ${C}_write "${A[@]}" -- WRITE_SIZE || exit 1
 done
 timeout -k 10 180 python3 bench/kv_move_bench.py > $D/kv_move.json 2> $D/kv_move.err || { echo "kv_move failed"; tail -5 $D/kv_move.err; exit 1; }
-python3 -c "import json;d=json.load(open('$D/kv_move.json'));print(d.get('beyond_cache'), d.get('torch_copy_64MiB_GBps'))"
+grep '^{' $D/kv_move.json | python3 -c "import json,sys;d=json.loads(sys.stdin.readline());print(d.get('beyond_cache'))"

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-5 kernel rework check: summarise_project (K-split, flat mean pass),
+# salient_topk (wave-level top-K), kv_move (chunked, 8 loads in flight,
+# non-temporal): numerics tests, then standalone timing, one PMC pass of
+# each summarise configuration (LDS + MFMA counters) and kv_move beyond the
+# Infinity Cache.  Every GPU step bounded; the chain stops at the first failure.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+D=gpurun_out/r5_k2
+mkdir -p $D
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+  tests/test_gpu_kernels.py tests/test_gpu_migration.py -k "summar or salient or kv_move or summary" \
+  > $D/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $D/pytest.log; exit 1; }
+tail -2 $D/pytest.log
+for C in ${CONVS:-16 64 256}; do
+  A=(--only summarise --summ-convs $C --reps 20)
+  timeout -k 5 120 python3 bench/kernel_bench.py "${A[@]}" > $D/time_summ_$C.log 2>&1 || exit 1
+  grep '^{"kernel' $D/time_summ_$C.log
+  timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES \
+    --kernel-trace --stats -d $D/summ${C}_lds -o run --output-format csv \
+    -- python3 bench/kernel_bench.py "${A[@]}" > $D/summ${C}_lds.log 2>&1 || { echo "pmc lds $C failed"; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats -d $D/summ${C}_write -o run --output-format csv \
+    -- python3 bench/kernel_bench.py "${A[@]}" > $D/summ${C}_write.log 2>&1 || { echo "pmc write $C failed"; exit 1; }
+done
+timeout -k 10 180 python3 bench/kv_move_bench.py > $D/kv_move.json 2> $D/kv_move.err \
+  || { echo "kv_move failed"; tail -5 $D/kv_move.err; exit 1; }
+grep '^{' $D/kv_move.json | python3 -c "import json,sys;d=json.loads(sys.stdin.readline());print(d['kv_move']);print(d.get('beyond_cache'))"

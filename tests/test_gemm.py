@@ -265,11 +265,13 @@ def test_gemm_residual_matches_fp32(T, K, epi):
 @pytest.mark.gpu
 def test_8b_model_residual_gemm_matches_hipblaslt_path():
     """At a full-chip step (T = 4041 -> 256 tiles of o / down) the model's
-    o / down projections run on GM_EPI_RESID; hidden states equal the
-    hipBLASLt beta = 1 path to bf16 noise (2 layers, 8B dims)."""
+    o / down projections run on the residual GEMM epilogue (the default
+    since round 5); hidden states equal the hipBLASLt beta = 1 path to bf16
+    noise (2 layers, 8B dims)."""
     cfg = LlamaConfig(layers=2)
-    a = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=5, fused_resid=True)
-    b = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=5)
+    a = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=5)
+    b = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=5, fused_resid=False)
+    assert G.RESID_EPI == G.EPI_RESID_LDS
     T = 4041
     assert a.fused_resid and a._cus > 0 and not b.fused_resid
     if not G.residual_tiles_ok(T, cfg.dim, a._cus):

@@ -446,6 +446,53 @@ def test_summarise_project_and_salient():
         assert got == exp, (c, got, exp)
 
 
+@pytest.mark.parametrize("C,zero_every", [(16, 0), (70, 4)])
+def test_summarise_project_blocks_and_empty_segments(C, zero_every):
+    """Row blocks of 16 conversations x 4 column blocks, a partial last row
+    block, and conversations with no evicted message (mean 0)."""
+    from llm_message_queue_amd.ops.summarise import Summariser
+    torch.manual_seed(5)
+    counts = [0 if zero_every and c % zero_every == 1 else 1 + (c * 7) % 13 for c in range(C)]
+    M = sum(counts)
+    pooled = torch.randn(max(M, 1), 1024, device=DEV)
+    seg = torch.tensor([0] + list(np.cumsum(counts)), dtype=torch.int32, device=DEV)
+    sm = Summariser(dim=256, hidden=1024, alpha=0.6, device=DEV)
+    state = torch.randn(C, 256, device=DEV)
+    first = (torch.arange(C, device=DEV) % 3 == 0).to(torch.int32)
+    ref_state = state.clone()
+    sm.project(pooled, seg, state, first)
+    Pt = sm.Pt.float()
+    for c in range(C):
+        a, b = int(seg[c]), int(seg[c + 1])
+        mean = pooled[a:b].mean(0).to(torch.bfloat16).float() if b > a else torch.zeros(1024, device=DEV)
+        proj = Pt @ mean
+        exp = proj if first[c] else 0.6 * ref_state[c] + 0.4 * proj
+        assert torch.allclose(state[c], exp, atol=3e-2, rtol=3e-2), c
+
+
+def test_salient_topk_k64_many_distinct_tokens():
+    """K = 64 (the maximum) over ~1000 distinct tokens per conversation: the
+    per-wave top-K lists and wave 0's merge must give the oracle order."""
+    from llm_message_queue_amd.ops.summarise import Summariser
+    sm = Summariser(dim=256, hidden=1024, device=DEV)
+    g = torch.Generator().manual_seed(11)
+    C, per, L = 3, 20, 64
+    M = C * per
+    # skewed counts so the top 64 has many distinct count levels and ties
+    hashes = (torch.randint(1, 40, (M, L), generator=g) * torch.randint(1, 60, (M, L), generator=g)).to(torch.int32)
+    ntok = torch.randint(L // 2, L + 1, (M,), generator=g, dtype=torch.int32)
+    seg = torch.arange(0, M + 1, per, dtype=torch.int32)
+    no_stop = torch.zeros(1, dtype=torch.int32, device=DEV)      # hash 0 never occurs
+    hs, cs, ovf = sm.salient(hashes.to(DEV), ntok.to(DEV), seg.to(DEV), k=64, stop=no_stop)
+    assert not ovf.any()
+    hh, nn = hashes.numpy(), ntok.numpy()
+    for c in range(C):
+        toks = [int(x) for m in range(c * per, (c + 1) * per) for x in hh[m, :nn[m]]]
+        exp = oracle_salient(toks, 64)
+        got = [(int(h), int(n)) for h, n in zip(hs[c], cs[c]) if n > 0]
+        assert got == exp, c
+
+
 def oracle_salient(toks, k):
     cnt, first = {}, {}
     for i, t in enumerate(toks):

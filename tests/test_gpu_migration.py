@@ -24,16 +24,19 @@ def _port():
     return p
 
 
-def test_kv_move_pack_unpack_bit_exact():
+@pytest.mark.parametrize("max_ctx,cases", [(96, ((0, 1), (4, 37), (5, 96))),
+                                            # runs of 2-3 chunks of 2048 vectors (partial last chunk)
+                                            (320, ((1, 128), (2, 129), (5, 300), (0, 320)))])
+def test_kv_move_pack_unpack_bit_exact(max_ctx, cases):
     from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
     from llm_message_queue_amd.parallel.comm import SoloComm
     from llm_message_queue_amd.parallel.migration import KVMigrator
     cfg = LlamaConfig.tiny()
-    m = LlamaStub(cfg, slots=6, max_ctx=96, device=DEV, impl="hip", seed=3)
+    m = LlamaStub(cfg, slots=6, max_ctx=max_ctx, device=DEV, impl="hip", seed=3)
     for t in m.kcache + m.vcache:
         t.normal_()
     mig = KVMigrator(m, SoloComm())
-    for slot, n in ((0, 1), (4, 37), (5, 96)):
+    for slot, n in cases:
         buf = mig.pack(slot, n)
         torch.cuda.synchronize()
         ref = torch.stack([torch.stack([m.kcache[L][slot, :, :n], m.vcache[L][slot, :, :n]])
