@@ -146,6 +146,19 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   if (tile0 >= total) return;  // uniform across the block
   const int rows = min(EP_TM, total - tile0);
 
+  const int fr = lane & 15;   // fragment row / col within a 16x16 tile
+  const int fq = lane >> 4;   // k-quarter (A/B), row-quad (C)
+  const int wc0 = chunk0 + wv * 64;  // this wave's 64 output columns
+  // all 8 k-steps' B fragments issued at once (128 VGPRs), before the row
+  // search and the gather: their L2 round trip overlaps that dependent chain
+  // (hash load -> embedding row load) instead of following it
+  bf16x8 bfall[EP_D / 32][4];
+#pragma unroll
+  for (int ks = 0; ks < EP_D / 32; ++ks)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bfall[ks][j] = *reinterpret_cast<const bf16x8*>(W1t + (int64_t)(wc0 + j * 16 + fr) * EP_D + ks * 32 + fq * 8);
+
   if (!ntok_src) {
     // global row_off (large batches): wave 0 finds the tile's first message
     // mlo (largest m with row_off[m] <= tile0) by a 64-ary search -- ceil(log64
@@ -228,26 +241,13 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   }
   __syncthreads();
 
-  const int fr = lane & 15;   // fragment row / col within a 16x16 tile
-  const int fq = lane >> 4;   // k-quarter (A/B), row-quad (C)
-
   {
-    const int n0 = chunk0;
-    const int wc0 = n0 + wv * 64;  // this wave's 64 output columns
     f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // all 8 k-steps' B fragments issued at once (128 VGPRs): one L2 round
-    // trip per block instead of one per k-step
-    bf16x8 bfall[EP_D / 32][4];
-#pragma unroll
-    for (int ks = 0; ks < EP_D / 32; ++ks)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bfall[ks][j] = *reinterpret_cast<const bf16x8*>(W1t + (int64_t)(wc0 + j * 16 + fr) * EP_D + ks * 32 + fq * 8);
 #pragma unroll
     for (int ks = 0; ks < EP_D / 32; ++ks) {
       const bf16x8* bfrag = bfall[ks];
