@@ -60,15 +60,18 @@ def main():
         mig = KVMigrator(model, comm)
         out = {"kv_shape": "32 layers x 2 x 8 kv heads x n x 128 bf16 (128 KiB / token)", "kv_move": [],
                "rccl_self_p2p": []}
-        for n in (32, 300, 512):
-            nbytes = L * 2 * H * n * D * 2
-            buf = mig.pack(3, n)
-            ms_p = _time(lambda: mig._kv_move(buf, 3, True, torch.cuda.current_stream()), 50)
-            ms_u = _time(lambda: mig._kv_move(buf, 7, False, torch.cuda.current_stream()), 50)
-            out["kv_move"].append({"tokens": n, "bytes": nbytes, "pack_us": round(ms_p * 1e3, 2),
-                                   "unpack_us": round(ms_u * 1e3, 2),
-                                   "pack_GBps": round(2 * nbytes / (ms_p * 1e-3) / 1e9, 1),
-                                   "unpack_GBps": round(2 * nbytes / (ms_u * 1e-3) / 1e9, 1)})
+        variants = [int(v) for v in os.environ.get("KV_VARIANTS", "0").split(",")]
+        for var in variants:
+            mig.KV_VARIANT = var
+            for n in (32, 300, 512):
+                nbytes = L * 2 * H * n * D * 2
+                buf = mig.pack(3, n)
+                ms_p = _time(lambda: mig._kv_move(buf, 3, True, torch.cuda.current_stream()), 50)
+                ms_u = _time(lambda: mig._kv_move(buf, 7, False, torch.cuda.current_stream()), 50)
+                out["kv_move"].append({"variant": var, "tokens": n, "bytes": nbytes,
+                                       "pack_us": round(ms_p * 1e3, 2), "unpack_us": round(ms_u * 1e3, 2),
+                                       "pack_GBps": round(2 * nbytes / (ms_p * 1e-3) / 1e9, 1),
+                                       "unpack_GBps": round(2 * nbytes / (ms_u * 1e-3) / 1e9, 1)})
         # Beyond the 256 MiB Infinity Cache: pack 16
         # different 512-token conversations (64 MiB each) into 16 different
         # buffers in rotation -- 1 GiB read + 1 GiB written per round, so no
@@ -78,13 +81,6 @@ def main():
         nbytes = L * 2 * H * n * D * 2
         bufs = [mig.pack(s_, n) for s_ in range(nrot)]
         torch.cuda.synchronize()
-        rot = {"k": 0}
-
-        def pack_rot():
-            k = rot["k"]
-            mig._kv_move(bufs[k], k, True, torch.cuda.current_stream())
-            rot["k"] = (k + 1) % nrot
-        ms_r = _time(pack_rot, 4 * nrot)
         src = [torch.empty(nbytes, dtype=torch.uint8, device=DEV) for _ in range(nrot)]
         dst = [torch.empty_like(x) for x in src]
         rc = {"k": 0}
@@ -95,9 +91,20 @@ def main():
             rc["k"] = (k + 1) % nrot
         ms_rc = _time(copy_rot, 4 * nrot)
         out["beyond_cache"] = {"working_set_GiB": round(2 * nrot * nbytes / 2**30, 2), "bytes_per_launch": nbytes,
-                               "kv_move_pack_GBps": round(2 * nbytes / (ms_r * 1e-3) / 1e9, 1),
-                               "torch_copy_GBps": round(2 * nbytes / (ms_rc * 1e-3) / 1e9, 1),
-                               "kv_move_over_copy": round(ms_rc / ms_r, 3)}
+                               "torch_copy_GBps": round(2 * nbytes / (ms_rc * 1e-3) / 1e9, 1)}
+        for var in variants:
+            mig.KV_VARIANT = var
+            rot = {"k": 0}
+
+            def pack_rot():
+                k = rot["k"]
+                mig._kv_move(bufs[k], k, True, torch.cuda.current_stream())
+                rot["k"] = (k + 1) % nrot
+            ms_r = _time(pack_rot, 4 * nrot)
+            tag = "" if var == 0 else f"_v{var}"
+            out["beyond_cache"][f"kv_move_pack_GBps{tag}"] = round(2 * nbytes / (ms_r * 1e-3) / 1e9, 1)
+            out["beyond_cache"][f"kv_move_over_copy{tag}"] = round(ms_rc / ms_r, 3)
+        mig.KV_VARIANT = 0
         del bufs, src, dst
         # same bytes as one torch copy (reference point for the HBM roofline)
         a = torch.empty(512 * 128 * 1024, dtype=torch.uint8, device=DEV)

@@ -429,19 +429,21 @@ static void slot_census(uintptr_t slot_state, int S_, int tokens, uint32_t step,
 // ---------------------------------------------------------------------- KV migration
 // pack=true: cache rows -> buf; false: buf -> cache rows (see kv_migrate_kernels.h)
 static void kv_move(uintptr_t table, int layers, int slots, int slot, int n, int max_ctx, int hkv, int head_dim,
-                    uintptr_t buf, bool pack, uintptr_t stream) {
+                    uintptr_t buf, bool pack, uintptr_t stream, int variant = KV_LOOP) {
   require(head_dim == 128, "kv_move: head_dim must be 128");
   require(layers > 0 && hkv > 0 && slots > 0, "kv_move: bad cache shape");
   require(slot >= 0 && slot < slots, "kv_move: slot out of range");
   require(n > 0 && n <= max_ctx, "kv_move: token count out of range");
   require(table != 0 && buf != 0 && buf % 16 == 0, "kv_move: null or misaligned buffer");
-  const dim3 grid(layers * 2 * hkv, (n * 16 + KV_CHUNK - 1) / KV_CHUNK);   // (run, chunk of the run)
-  if (pack)
-    hipLaunchKernelGGL(kv_move_kernel<true>, grid, dim3(256), 0, S(stream), P<const uint64_t>(table), layers, slot,
-                       n, max_ctx, hkv, P<uint4>(buf));
-  else
-    hipLaunchKernelGGL(kv_move_kernel<false>, grid, dim3(256), 0, S(stream), P<const uint64_t>(table), layers,
-                       slot, n, max_ctx, hkv, P<uint4>(buf));
+  require(variant >= KV_LOOP && variant <= KV_CHUNK_NT, "kv_move: unknown variant");
+  const int runs = layers * 2 * hkv;
+  const dim3 grid(runs, variant == KV_LOOP ? 1 : (n * 16 + KV_CHUNK_VECS - 1) / KV_CHUNK_VECS);
+  auto k = pack ? (variant == KV_LOOP ? kv_move_kernel<true, KV_LOOP>
+                   : variant == KV_CHUNK ? kv_move_kernel<true, KV_CHUNK> : kv_move_kernel<true, KV_CHUNK_NT>)
+                : (variant == KV_LOOP ? kv_move_kernel<false, KV_LOOP>
+                   : variant == KV_CHUNK ? kv_move_kernel<false, KV_CHUNK> : kv_move_kernel<false, KV_CHUNK_NT>);
+  hipLaunchKernelGGL(k, grid, dim3(256), 0, S(stream), P<const uint64_t>(table), layers, slot, n, max_ctx, hkv,
+                     P<uint4>(buf));
   check_launch();
 }
 
@@ -513,5 +515,6 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("slot_census", &slot_census);
   m.def("device_info", &device_info);
   m.def("kv_move", &kv_move, py::arg("table"), py::arg("layers"), py::arg("slots"), py::arg("slot"), py::arg("n"),
-        py::arg("max_ctx"), py::arg("hkv"), py::arg("head_dim"), py::arg("buf"), py::arg("pack"), py::arg("stream"));
+        py::arg("max_ctx"), py::arg("hkv"), py::arg("head_dim"), py::arg("buf"), py::arg("pack"), py::arg("stream"),
+        py::arg("variant") = (int)KV_LOOP);
 }

@@ -8,14 +8,12 @@
 // n x 256 bytes.  Buffer layout: [layer][k|v][kv_head][n][128] -- the wire
 // format RCCL sends between GPUs (llm_message_queue_amd/parallel/migration.py).
 //
-// Grid: (layer, k|v, kv head) run x 32 KiB chunks of the run: each 256-thread
-// workgroup moves KV_UNROLL x 16 B per thread with all KV_UNROLL loads in
-// flight before the first store, non-temporal both ways (touched once).  The
-// round-4 form (one workgroup per run, a load -> store chain of one 16-byte
-// vector per thread per iteration: ~2 MiB in flight chip-wide) moved 4.37
-// TB/s beyond the 256 MiB Infinity Cache against a plain copy's 5.04 TB/s
-// (profiles/r5_preprocess_kernels_pmc.md); at 512 tokens this grid is 2048
-// workgroups with 32 MiB in flight.
+// Grid, KV_LOOP (default): one 256-thread workgroup per (layer, k|v, kv head)
+// run -- 32 x 2 x 8 = 512 workgroups for Llama-3-8B -- looping over the run
+// with 16-byte vectors.  KV_CHUNK / KV_CHUNK_NT (A/B, round 5): the run split
+// into 32 KiB chunks, one per workgroup, all 8 loads of a thread in flight
+// before its first store (plain / non-temporal).  Measured in
+// profiles/r5_preprocess_kernels_pmc.md ("kv_move" section).
 // The per-layer base pointers come from a device table [2 L] (k0..kL-1,
 // v0..vL-1) built once by the migrator.
 #pragma once
@@ -25,10 +23,11 @@
 namespace llmq {
 
 constexpr int KV_UNROLL = 8;
-constexpr int KV_CHUNK = 256 * KV_UNROLL;   // 16-byte vectors per workgroup
+constexpr int KV_CHUNK_VECS = 256 * KV_UNROLL;   // 16-byte vectors per chunk workgroup
+enum { KV_LOOP = 0, KV_CHUNK = 1, KV_CHUNK_NT = 2 };
 typedef unsigned int kv_u32x4 __attribute__((ext_vector_type(4)));
 
-template <bool PACK>
+template <bool PACK, int MODE>
 __global__ __launch_bounds__(256) void kv_move_kernel(const uint64_t* __restrict__ table, int layers, int slot,
                                                       int n, int max_ctx, int hkv, uint4* __restrict__ buf) {
   const int seg = blockIdx.x;                // ((layer * 2 + kv) * hkv + h)
@@ -42,17 +41,25 @@ __global__ __launch_bounds__(256) void kv_move_kernel(const uint64_t* __restrict
   const kv_u32x4* src = PACK ? c : b;
   kv_u32x4* dst = PACK ? b : c;
   const int nv = n * 16;
-  const int i0 = blockIdx.y * KV_CHUNK + threadIdx.x;
-  kv_u32x4 v[KV_UNROLL];
-#pragma unroll
-  for (int u = 0; u < KV_UNROLL; ++u) {
-    const int i = i0 + u * 256;
-    if (i < nv) v[u] = __builtin_nontemporal_load(src + i);
+  if (MODE == KV_LOOP) {
+    for (int i = threadIdx.x; i < nv; i += 256) dst[i] = src[i];
+    return;
   }
+  const int i0 = blockIdx.y * KV_CHUNK_VECS + threadIdx.x;
+  if (i0 + (KV_UNROLL - 1) * 256 < nv) {
+    // the whole chunk is inside the run: 8 loads, no per-vector predicate
+    // (a predicated unrolled form compiled to a load -> vmcnt(0) chain)
+    kv_u32x4 v[KV_UNROLL];
 #pragma unroll
-  for (int u = 0; u < KV_UNROLL; ++u) {
-    const int i = i0 + u * 256;
-    if (i < nv) __builtin_nontemporal_store(v[u], dst + i);
+    for (int u = 0; u < KV_UNROLL; ++u)
+      v[u] = MODE == KV_CHUNK_NT ? __builtin_nontemporal_load(src + i0 + u * 256) : src[i0 + u * 256];
+#pragma unroll
+    for (int u = 0; u < KV_UNROLL; ++u) {
+      if (MODE == KV_CHUNK_NT) __builtin_nontemporal_store(v[u], dst + i0 + u * 256);
+      else dst[i0 + u * 256] = v[u];
+    }
+  } else {
+    for (int i = i0; i < nv; i += 256) dst[i] = src[i];   // the run's last, partial chunk
   }
 }
 

@@ -22,8 +22,8 @@
 //   * all 32 B fragments of a wave's 8 k-steps x 4 column tiles are issued at
 //     kernel entry (Pt is 512 KiB, L2-resident), overlapping the mean pass;
 //   * the mean pass walks the 16 conversations' messages -- one contiguous
-//     run of pooled rows -- as ONE flat loop, 8 messages per round with the 8
-//     float4 loads in flight together; conversation boundaries are uniform
+//     run of pooled rows -- as ONE flat loop, 16 messages per round with the
+//     16 float4 loads in flight together; conversation boundaries are uniform
 //     (every lane handles the same message), and a finished row's mean goes
 //     to LDS as 4 packed bf16 (8-byte stores, chunk-swizzled), so the
 //     summation order per element is the old one (m ascending) and the means
@@ -55,6 +55,7 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
 constexpr int SM_NB = 64;                 // output columns per block
 constexpr int SM_KQ = SM_H / 4;           // K per wave
 constexpr int SM_RED = SM_NB + 4;         // reduction row stride (floats)
+constexpr int SM_MEAN_UNROLL = 16;       // message rows in flight per lane in the mean pass
 
 __global__ void __launch_bounds__(256)
 summarise_project_kernel(const float* __restrict__ pooled, const int32_t* __restrict__ seg_off, int C,
@@ -97,14 +98,14 @@ summarise_project_kernel(const float* __restrict__ pooled, const int32_t* __rest
     acc = make_float4(0.f, 0.f, 0.f, 0.f);
   };
   const int M0 = bnd[0], M1 = bnd[SM_ROWS];
-  for (int m = M0; m < M1; m += 8) {
-    float4 x[8];
+  for (int m = M0; m < M1; m += SM_MEAN_UNROLL) {
+    float4 x[SM_MEAN_UNROLL];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < SM_MEAN_UNROLL; ++u)
       x[u] = (m + u < M1) ? *reinterpret_cast<const float4*>(pooled + (int64_t)(m + u) * SM_H + kq + col4)
                           : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < SM_MEAN_UNROLL; ++u) {
       if (m + u >= M1) break;                        // uniform
       while (m + u >= bnd[r + 1]) flush(r++);        // uniform: rows ending before message m + u
       acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
@@ -186,6 +187,7 @@ __device__ __forceinline__ void sal_wave_pick(uint64_t (&v)[NV], F index_of, int
 // Top-k salient token hashes per conversation (one workgroup each).
 // tokens of message m: hashes[m*L .. m*L + ntok[m*stride]).
 constexpr int SAL_TABLE = 2048;
+constexpr int SAL_MAX_STOP = 128;
 __global__ void __launch_bounds__(256)
 salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __restrict__ ntok,
                     int stride, const int32_t* __restrict__ seg_off, const uint32_t* __restrict__ stop,
@@ -201,30 +203,69 @@ salient_topk_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* _
   if (tid == 0) overflow = 0;
   __syncthreads();
   const int a = seg_off[c], b = seg_off[c + 1];
-  int ord = 0;  // running token order across the conversation's messages
-  for (int m = a; m < b; ++m) {
-    const int n = ntok[(int64_t)m * stride];
-    for (int t = tid; t < n; t += 256) {
-      uint32_t h = hashes[(int64_t)m * L + t];
-      bool is_stop = false;
-      for (int s = 0; s < nstop; ++s) is_stop |= (stop[s] == h);
-      if (is_stop) continue;
-      if (h == 0u) h = 1u;  // 0 marks an empty slot
-      uint32_t slot = (h * 2654435761u) & (SAL_TABLE - 1);
-      bool placed = false;
-      for (int probe = 0; probe < SAL_TABLE; ++probe) {
-        const uint32_t prev = atomicCAS(&key[slot], 0u, h);
-        if (prev == 0u || prev == h) {
-          atomicAdd(&cnt[slot], 1);
-          atomicMin(&first[slot], ord + t);
-          placed = true;
-          break;
-        }
-        slot = (slot + 1) & (SAL_TABLE - 1);
+  // stop-word hashes in LDS (the list is ~30 words; a longer one stays global)
+  __shared__ uint32_t sstop[SAL_MAX_STOP];
+  const bool stop_lds = nstop <= SAL_MAX_STOP;
+  if (stop_lds && tid < nstop) sstop[tid] = stop[tid];
+  const uint32_t* stp = stop_lds ? sstop : stop;
+  auto insert = [&](uint32_t h, int ord) {
+    bool is_stop = false;
+    for (int s = 0; s < nstop; ++s) is_stop |= (stp[s] == h);
+    if (is_stop) return;
+    if (h == 0u) h = 1u;  // 0 marks an empty slot
+    uint32_t slot = (h * 2654435761u) & (SAL_TABLE - 1);
+    for (int probe = 0; probe < SAL_TABLE; ++probe) {
+      const uint32_t prev = atomicCAS(&key[slot], 0u, h);
+      if (prev == 0u || prev == h) {
+        atomicAdd(&cnt[slot], 1);
+        atomicMin(&first[slot], ord);
+        return;
       }
-      if (!placed) overflow = 1;  // benign race: every writer stores 1
+      slot = (slot + 1) & (SAL_TABLE - 1);
     }
-    ord += n;
+    overflow = 1;  // no table slot left: benign race, every writer stores 1
+  };
+  const int nm = b - a;
+  if (nm <= 256) {
+    // every token of the conversation at once: an exclusive scan of the
+    // messages' token counts, then thread j takes flat tokens j, j + 256, ...
+    // (its message by binary search; the flat index IS the token's order).
+    // Round 4 walked the messages one after another -- a dependent
+    // ntok -> hash -> insert chain per message, a flat ~26 us.
+    __shared__ int32_t moff[257];
+    __shared__ int32_t wsum[4];
+    const int lane = tid & 63, wv = tid >> 6;
+    const int v = tid < nm ? ntok[(int64_t)(a + tid) * stride] : 0;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();  // (also publishes sstop)
+    int pre = 0;
+    for (int k = 0; k < wv; ++k) pre += wsum[k];
+    moff[tid] = pre + x - v;
+    if (tid == 255) moff[256] = pre + x;
+    __syncthreads();
+    const int total = moff[256];
+    for (int j = tid; j < total; j += 256) {
+      int lo = 0, hi = nm - 1;  // largest k with moff[k] <= j
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (moff[mid] <= j) lo = mid; else hi = mid - 1;
+      }
+      insert(hashes[(int64_t)(a + lo) * L + (j - moff[lo])], j);
+    }
+  } else {
+    __syncthreads();  // sstop
+    int ord = 0;  // running token order across the conversation's messages
+    for (int m = a; m < b; ++m) {
+      const int n = ntok[(int64_t)m * stride];
+      for (int t = tid; t < n; t += 256) insert(hashes[(int64_t)m * L + t], ord + t);
+      ord += n;
+    }
   }
   __syncthreads();
   // ---- selection by (count desc, first occurrence asc); scores are unique

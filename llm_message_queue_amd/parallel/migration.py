@@ -103,10 +103,16 @@ class KVMigrator:
         m = self.model
         return torch.empty(self._shape(n), dtype=m.kcache[0].dtype, device=device or self.device)
 
+    # kv_move kernel form (csrc/kernels/kv_migrate_kernels.h): 0 one workgroup
+    # per (layer, k|v, head) run, 1 / 2 the run in 32 KiB chunks (plain /
+    # non-temporal) -- A/B in bench/kv_move_bench.py
+    KV_VARIANT = 0
+
     def _kv_move(self, buf: torch.Tensor, slot: int, pack: bool, stream) -> None:
         m, c = self.model, self.model.cfg
         self._ops.kv_move(self._table.data_ptr(), c.layers, m.slots, int(slot), int(buf.shape[3]), m.max_ctx,
-                          c.kv_heads, c.head_dim, buf.data_ptr(), bool(pack), stream.cuda_stream)
+                          c.kv_heads, c.head_dim, buf.data_ptr(), bool(pack), stream.cuda_stream,
+                          int(self.KV_VARIANT))
 
     def pack(self, slot: int, n: int) -> torch.Tensor:
         """The conversation's K/V rows of every layer, [L, 2, Hkv, n, 128]:

@@ -22,6 +22,6 @@ for C in ${CONVS:-16 64 256}; do
   timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats -d $D/summ${C}_write -o run --output-format csv \
     -- python3 bench/kernel_bench.py "${A[@]}" > $D/summ${C}_write.log 2>&1 || { echo "pmc write $C failed"; exit 1; }
 done
-timeout -k 10 180 python3 bench/kv_move_bench.py > $D/kv_move.json 2> $D/kv_move.err \
+KV_VARIANTS=${KV_VARIANTS:-0,1,2} timeout -k 10 240 python3 bench/kv_move_bench.py > $D/kv_move.json 2> $D/kv_move.err \
   || { echo "kv_move failed"; tail -5 $D/kv_move.err; exit 1; }
 grep '^{' $D/kv_move.json | python3 -c "import json,sys;d=json.loads(sys.stdin.readline());print(d['kv_move']);print(d.get('beyond_cache'))"

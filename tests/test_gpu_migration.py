@@ -27,7 +27,8 @@ def _port():
 @pytest.mark.parametrize("max_ctx,cases", [(96, ((0, 1), (4, 37), (5, 96))),
                                             # runs of 2-3 chunks of 2048 vectors (partial last chunk)
                                             (320, ((1, 128), (2, 129), (5, 300), (0, 320)))])
-def test_kv_move_pack_unpack_bit_exact(max_ctx, cases):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_kv_move_pack_unpack_bit_exact(max_ctx, cases, variant):
     from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
     from llm_message_queue_amd.parallel.comm import SoloComm
     from llm_message_queue_amd.parallel.migration import KVMigrator
@@ -36,6 +37,7 @@ def test_kv_move_pack_unpack_bit_exact(max_ctx, cases):
     for t in m.kcache + m.vcache:
         t.normal_()
     mig = KVMigrator(m, SoloComm())
+    mig.KV_VARIANT = variant
     for slot, n in cases:
         buf = mig.pack(slot, n)
         torch.cuda.synchronize()
