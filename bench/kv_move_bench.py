@@ -60,7 +60,8 @@ def main():
         mig = KVMigrator(model, comm)
         out = {"kv_shape": "32 layers x 2 x 8 kv heads x n x 128 bf16 (128 KiB / token)", "kv_move": [],
                "rccl_self_p2p": []}
-        variants = [int(v) for v in os.environ.get("KV_VARIANTS", "0").split(",")]
+        default_variant = mig.KV_VARIANT
+        variants = [int(v) for v in os.environ.get("KV_VARIANTS", str(default_variant)).split(",")]
         for var in variants:
             mig.KV_VARIANT = var
             for n in (32, 300, 512):
@@ -104,7 +105,7 @@ def main():
             tag = "" if var == 0 else f"_v{var}"
             out["beyond_cache"][f"kv_move_pack_GBps{tag}"] = round(2 * nbytes / (ms_r * 1e-3) / 1e9, 1)
             out["beyond_cache"][f"kv_move_over_copy{tag}"] = round(ms_rc / ms_r, 3)
-        mig.KV_VARIANT = 0
+        mig.KV_VARIANT = default_variant
         del bufs, src, dst
         # same bytes as one torch copy (reference point for the HBM roofline)
         a = torch.empty(512 * 128 * 1024, dtype=torch.uint8, device=DEV)

@@ -48,6 +48,7 @@ constexpr int EP_TM = 64;      // rows per tile
 constexpr int EP_D = 256;      // embedding dim (K)
 constexpr int EP_NCHUNK = 256; // columns per sweep step
 constexpr int EP_CHUNKS_PER_ROW = EP_D / 8;  // 16-byte chunks per A row
+constexpr uint32_t EP_NO_ROW = 0xFFFFFFFFu;
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
   return __uint_as_float(((uint32_t)b) << 16);
@@ -99,6 +100,7 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
   int32_t* rmsg = reinterpret_cast<int32_t*>(smem + EP_TM * EP_D * 2);
   int32_t* rinfo = rmsg + EP_TM;  // [0]=rows in tile, [1]=segments, [2..]=segment starts (+ end)
   int32_t* seg = rinfo + 2;
+  __shared__ uint32_t rbucket[EP_TM];   // row -> embedding bucket (EP_NO_ROW: past the tile's rows)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -223,21 +225,34 @@ embed_pool_kernel(const uint32_t* __restrict__ hashes, int L, const int32_t* __r
       rinfo[1] = __popcll(mask);
       seg[__popcll(mask)] = rows;
     }
+    // the row's embedding bucket: its ONE hash load, done once per row here
+    // (the gather below used to reload it per 16-byte chunk, inside a loop
+    // the compiler ran as 8 serial window -> hash -> row load chains: the
+    // ~20 us floor at serving batch sizes, profiles/r5_preprocess_kernels_pmc.md)
+    const int m = rmsg[tid];
+    rbucket[tid] = m >= 0 ? (hashes[(int64_t)m * L + (tile0 + tid - rofs(m))] & vmask) : EP_NO_ROW;
   }
+  __syncthreads();
 
-  // ---- gather the A tile: 64 rows x 32 chunks of 16 B, swizzled chunk ^ (row & 15)
-  for (int c = tid; c < EP_TM * EP_CHUNKS_PER_ROW; c += 256) {
-    const int r = c / EP_CHUNKS_PER_ROW;
-    const int ch = c % EP_CHUNKS_PER_ROW;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    const int m = rmsg[r];
-    if (m >= 0) {
-      const int tok = tile0 + r - rofs(m);
-      const uint32_t bucket = hashes[(int64_t)m * L + tok] & vmask;
-      v = *reinterpret_cast<const uint4*>(E + (int64_t)bucket * EP_D + ch * 8);
+  // ---- gather the A tile: 64 rows x 32 chunks of 16 B, swizzled chunk ^ (row & 15);
+  // all 8 loads of a thread in flight (unconditional: a missing row reads row 0)
+  {
+    constexpr int PER = EP_TM * EP_CHUNKS_PER_ROW / 256;
+    uint4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + u * 256;
+      const uint32_t bk = rbucket[c / EP_CHUNKS_PER_ROW];
+      v[u] = *reinterpret_cast<const uint4*>(E + (int64_t)(bk == EP_NO_ROW ? 0u : bk) * EP_D +
+                                             (c % EP_CHUNKS_PER_ROW) * 8);
     }
-    const int pch = ch ^ (r & 15);
-    *reinterpret_cast<uint4*>(At + r * EP_D + pch * 8) = v;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = tid + u * 256;
+      const int r = c / EP_CHUNKS_PER_ROW, ch = c % EP_CHUNKS_PER_ROW;
+      const uint4 x = rbucket[r] == EP_NO_ROW ? make_uint4(0u, 0u, 0u, 0u) : v[u];
+      *reinterpret_cast<uint4*>(At + r * EP_D + ((ch ^ (r & 15)) * 8)) = x;
+    }
   }
   __syncthreads();
 
@@ -330,6 +345,8 @@ struct ClassifyReadback {
 // CH_MSGS = 1 below ~1k messages: a serving micro-batch has few waves, and
 // the latency of one wave's chain, not L2 traffic, sets the time there
 // (profiles/r3_embed_pool_ab.md: 64 messages 9.5 us at 1 vs 14.4 us at 4).
+constexpr int CH_UNROLL = 4;   // hidden units per lane per load round (H % (64 * CH_UNROLL) == 0)
+
 template <int CH_MSGS>
 __global__ void __launch_bounds__(256)
 classify_head_kernel(const float* __restrict__ pooled, int B, int H, const float* __restrict__ W2,
@@ -352,15 +369,32 @@ classify_head_kernel(const float* __restrict__ pooled, int B, int H, const float
   for (int m = 0; m < CH_MSGS; ++m)
 #pragma unroll
     for (int o = 0; o < 8; ++o) part[m][o] = 0.f;
-  for (int h = lane; h < H; h += 64) {
-    const float4 wa = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8);
-    const float4 wb = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8 + 4);
+  // CH_UNROLL hidden units per lane per round, every load of the round in
+  // flight together and unconditional (rows past nm re-read row nm - 1; their
+  // partials are never written): the round-4 loop waited on each round's
+  // loads, 16 dependent round trips per wave at H = 1024
+  // (profiles/r5_preprocess_kernels_pmc.md).  Per message the summation
+  // order over h is unchanged.
+  for (int h0 = lane; h0 < H; h0 += 64 * CH_UNROLL) {
+    float4 wa[CH_UNROLL], wb[CH_UNROLL];
+    float x[CH_UNROLL][CH_MSGS];
 #pragma unroll
-    for (int m = 0; m < CH_MSGS; ++m) {
-      const float x = m < nm ? pooled[(int64_t)(b0 + m) * H + h] : 0.f;
-      part[m][0] += x * wa.x; part[m][1] += x * wa.y; part[m][2] += x * wa.z; part[m][3] += x * wa.w;
-      part[m][4] += x * wb.x; part[m][5] += x * wb.y; part[m][6] += x * wb.z; part[m][7] += x * wb.w;
+    for (int u = 0; u < CH_UNROLL; ++u) {
+      const int h = h0 + u * 64;
+      wa[u] = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8);
+      wb[u] = *reinterpret_cast<const float4*>(W2 + (int64_t)h * 8 + 4);
+#pragma unroll
+      for (int m = 0; m < CH_MSGS; ++m) x[u][m] = pooled[(int64_t)(b0 + min(m, nm - 1)) * H + h];
     }
+#pragma unroll
+    for (int u = 0; u < CH_UNROLL; ++u)
+#pragma unroll
+      for (int m = 0; m < CH_MSGS; ++m) {
+        const float xv = x[u][m];
+        part[m][0] += xv * wa[u].x; part[m][1] += xv * wa[u].y; part[m][2] += xv * wa[u].z;
+        part[m][3] += xv * wa[u].w; part[m][4] += xv * wb[u].x; part[m][5] += xv * wb[u].y;
+        part[m][6] += xv * wb[u].z; part[m][7] += xv * wb[u].w;
+      }
   }
 #pragma unroll
   for (int m = 0; m < CH_MSGS; ++m)

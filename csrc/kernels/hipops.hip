@@ -73,7 +73,7 @@ static void scan_rows(uintptr_t ntok, int stride, int B, uintptr_t row_off, uint
 
 static bool g_embed_attr = false;
 static constexpr size_t EP_SMEM_BASE = EP_TM * EP_D * 2 + 3 * EP_TM * 4 + 16;
-static constexpr size_t EP_SMEM_MAX = 160 * 1024 - 256;   // static __shared__ of the kernel counts too
+static constexpr size_t EP_SMEM_MAX = 160 * 1024 - 512;   // static __shared__ of the kernel (~280 B) counts too
 // largest batch whose row offsets fit in LDS next to the tile (in-block scan)
 static constexpr int EP_MAX_LDS_SCAN = (int)((EP_SMEM_MAX - EP_SMEM_BASE) / 4) - 1;
 // every block reads all B token counts, so the redundant scan costs
@@ -108,6 +108,7 @@ static void embed_pool(uintptr_t hashes, int L, uintptr_t row_off, int B, int ro
 
 static void classify_head(uintptr_t pooled, int B, int H, uintptr_t W2, uintptr_t b2, uintptr_t logits,
                           uintptr_t pred, uintptr_t stream, const ClassifyReadback& rb = ClassifyReadback{}) {
+  require(H % (64 * CH_UNROLL) == 0, "classify_head: hidden dim must be a multiple of 256");
   if (B == 0) return;
   // large batches: 4 messages per wave share each W2 load (L2-bound 88 -> 47 us at 4096);
   // small ones: a message per wave (latency-bound; more waves, shorter chains)

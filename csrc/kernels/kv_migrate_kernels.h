@@ -8,12 +8,14 @@
 // n x 256 bytes.  Buffer layout: [layer][k|v][kv_head][n][128] -- the wire
 // format RCCL sends between GPUs (llm_message_queue_amd/parallel/migration.py).
 //
-// Grid, KV_LOOP (default): one 256-thread workgroup per (layer, k|v, kv head)
-// run -- 32 x 2 x 8 = 512 workgroups for Llama-3-8B -- looping over the run
-// with 16-byte vectors.  KV_CHUNK / KV_CHUNK_NT (A/B, round 5): the run split
-// into 32 KiB chunks, one per workgroup, all 8 loads of a thread in flight
-// before its first store (plain / non-temporal).  Measured in
-// profiles/r5_preprocess_kernels_pmc.md ("kv_move" section).
+// Grid, KV_CHUNK_NT (the migrator's default, round 5): the (layer, k|v, kv
+// head) run split into 32 KiB chunks, one per 256-thread workgroup, all 8
+// loads of a thread in flight before its first store, non-temporal both ways
+// (the bytes are touched once): 5.50 TB/s beyond the 256 MiB Infinity Cache,
+// 1.09x a torch copy of the same bytes.  KV_LOOP (round 4): one workgroup per
+// run looping over it -- 4.47 TB/s there, though 6.5 TB/s on cache-resident
+// buffers.  KV_CHUNK: the chunked form with plain loads / stores.
+// Measured in profiles/r5_preprocess_kernels_pmc.md ("kv_move" section).
 // The per-layer base pointers come from a device table [2 L] (k0..kL-1,
 // v0..vL-1) built once by the migrator.
 #pragma once
@@ -46,20 +48,21 @@ __global__ __launch_bounds__(256) void kv_move_kernel(const uint64_t* __restrict
     return;
   }
   const int i0 = blockIdx.y * KV_CHUNK_VECS + threadIdx.x;
-  if (i0 + (KV_UNROLL - 1) * 256 < nv) {
-    // the whole chunk is inside the run: 8 loads, no per-vector predicate
-    // (a predicated unrolled form compiled to a load -> vmcnt(0) chain)
-    kv_u32x4 v[KV_UNROLL];
+  // loads unconditional (clamped into the run), stores predicated: a
+  // predicated load form compiled to a load -> vmcnt(0) chain
+  kv_u32x4 v[KV_UNROLL];
 #pragma unroll
-    for (int u = 0; u < KV_UNROLL; ++u)
-      v[u] = MODE == KV_CHUNK_NT ? __builtin_nontemporal_load(src + i0 + u * 256) : src[i0 + u * 256];
+  for (int u = 0; u < KV_UNROLL; ++u) {
+    const int i = min(i0 + u * 256, nv - 1);
+    v[u] = MODE == KV_CHUNK_NT ? __builtin_nontemporal_load(src + i) : src[i];
+  }
 #pragma unroll
-    for (int u = 0; u < KV_UNROLL; ++u) {
-      if (MODE == KV_CHUNK_NT) __builtin_nontemporal_store(v[u], dst + i0 + u * 256);
-      else dst[i0 + u * 256] = v[u];
+  for (int u = 0; u < KV_UNROLL; ++u) {
+    const int i = i0 + u * 256;
+    if (i < nv) {
+      if (MODE == KV_CHUNK_NT) __builtin_nontemporal_store(v[u], dst + i);
+      else dst[i] = v[u];
     }
-  } else {
-    for (int i = i0; i < nv; i += 256) dst[i] = src[i];   // the run's last, partial chunk
   }
 }
 

@@ -100,10 +100,11 @@ summarise_project_kernel(const float* __restrict__ pooled, const int32_t* __rest
   const int M0 = bnd[0], M1 = bnd[SM_ROWS];
   for (int m = M0; m < M1; m += SM_MEAN_UNROLL) {
     float4 x[SM_MEAN_UNROLL];
+    // unconditional loads (rows past M1 re-read row M1 - 1 and are not
+    // used): a predicated form compiled to a load -> vmcnt(0) chain
 #pragma unroll
     for (int u = 0; u < SM_MEAN_UNROLL; ++u)
-      x[u] = (m + u < M1) ? *reinterpret_cast<const float4*>(pooled + (int64_t)(m + u) * SM_H + kq + col4)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[u] = *reinterpret_cast<const float4*>(pooled + (int64_t)min(m + u, M1 - 1) * SM_H + kq + col4);
 #pragma unroll
     for (int u = 0; u < SM_MEAN_UNROLL; ++u) {
       if (m + u >= M1) break;                        // uniform

@@ -165,15 +165,29 @@ text_analyze_kernel(const uint8_t* __restrict__ bytes, const int64_t* __restrict
 #pragma unroll
   for (int s = 0; s < TA_SLOTS; ++s) score[s] = 0;
 
+  // Software-pipelined byte staging: the bytes of chunk base + 64 are loaded
+  // (clamped addresses, no predicate) while chunk base is processed, so a
+  // message costs one load round trip instead of one per 64-byte chunk (the
+  // flat ~27 us at serving batch sizes, profiles/r5_preprocess_kernels_pmc.md)
+  auto ldb = [&](int i) -> uint32_t { return src[min(max(i, 0), len - 1)]; };
+  uint32_t b0 = 0u, b1 = 0u;
+  if (len > 0) {
+    b0 = ldb(lane - 4);
+    b1 = ldb(lane + 60);
+  }
   for (int base = 0; base < len; base += 64) {
     // ---- stage bytes [base-4, base+100) into this wave's LDS window
     {
       const int i0 = base - 4 + lane;
-      win8[lane] = (i0 >= 0 && i0 < len) ? src[i0] : (uint8_t)0;
+      win8[lane] = (i0 >= 0 && i0 < len) ? (uint8_t)b0 : (uint8_t)0;
       if (lane < TA_WIN - 64) {
         const int i1 = base + 60 + lane;
-        win8[64 + lane] = (i1 < len) ? src[i1] : (uint8_t)0;
+        win8[64 + lane] = (i1 < len) ? (uint8_t)b1 : (uint8_t)0;
       }
+    }
+    if (base + 64 < len) {          // wave-uniform: the next chunk's bytes, in flight during this one
+      b0 = ldb(base + 60 + lane);
+      b1 = ldb(base + 124 + lane);
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): staged bytes visible to all lanes
     __builtin_amdgcn_wave_barrier();

@@ -105,8 +105,10 @@ class KVMigrator:
 
     # kv_move kernel form (csrc/kernels/kv_migrate_kernels.h): 0 one workgroup
     # per (layer, k|v, head) run, 1 / 2 the run in 32 KiB chunks (plain /
-    # non-temporal) -- A/B in bench/kv_move_bench.py
-    KV_VARIANT = 0
+    # non-temporal).  2 by default: 5.50 TB/s beyond the Infinity Cache, 1.09x
+    # a torch copy of the same bytes, against 4.47 for 0
+    # (profiles/r5_kernel_rework/kv_move_variants.json, bench/kv_move_bench.py)
+    KV_VARIANT = 2
 
     def _kv_move(self, buf: torch.Tensor, slot: int, pack: bool, stream) -> None:
         m, c = self.model, self.model.cfg

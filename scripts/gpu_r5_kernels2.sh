@@ -9,9 +9,19 @@ export TMPDIR=/tmp
 D=gpurun_out/r5_k2
 mkdir -p $D
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  tests/test_gpu_kernels.py tests/test_gpu_migration.py -k "summar or salient or kv_move or summary" \
+  tests/test_gpu_kernels.py tests/test_gpu_migration.py \
   > $D/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $D/pytest.log; exit 1; }
 tail -2 $D/pytest.log
+for N in ${SIZES:-64 256 4096}; do
+  A=(--only text --text-batches $N --reps 20)
+  timeout -k 5 120 python3 bench/kernel_bench.py "${A[@]}" > $D/time_text_$N.log 2>&1 || exit 1
+  grep '^{"kernel' $D/time_text_$N.log
+  timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats -d $D/text${N}_write -o run --output-format csv \
+    -- python3 bench/kernel_bench.py "${A[@]}" > $D/text${N}_write.log 2>&1 || { echo "pmc write text $N failed"; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE \
+    --kernel-trace --stats -d $D/text${N}_mfma -o run --output-format csv \
+    -- python3 bench/kernel_bench.py "${A[@]}" > $D/text${N}_mfma.log 2>&1 || { echo "pmc mfma text $N failed"; exit 1; }
+done
 for C in ${CONVS:-16 64 256}; do
   A=(--only summarise --summ-convs $C --reps 20)
   timeout -k 5 120 python3 bench/kernel_bench.py "${A[@]}" > $D/time_summ_$C.log 2>&1 || exit 1
