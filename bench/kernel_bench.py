@@ -34,11 +34,15 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
+    ap.add_argument("--lib-dir", default="", help="A/B: load the native modules from this directory instead of _lib")
     ap.add_argument("--text-batches", default="4096", help="preprocess batch sizes (messages), comma-separated")
     ap.add_argument("--summ-convs", default="64", help="summarise: conversations per batch (8 evicted turns each)")
     a = ap.parse_args()
     import numpy as np
     import torch
+    if a.lib_dir:
+        from llm_message_queue_amd import _native
+        _native._LIB = os.path.abspath(a.lib_dir)
 
     from llm_message_queue_amd.gateway.workload import Workload
     from llm_message_queue_amd.ops.llama_ops import HipOps, make_tiles, rope_tables
