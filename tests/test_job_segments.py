@@ -54,10 +54,11 @@ class Server:
     """A ``cli serve`` process (optionally under torchrun) whose stdout JSON
     events are collected by a reader thread."""
 
-    def __init__(self, args, env_extra=None, torchrun=0, mport=0, restarts=0, standalone=False):
+    def __init__(self, args, env_extra=None, torchrun=0, mport=0, restarts=0, standalone=False, gpu=False):
         self.port = _port()
         env = dict(os.environ, LLMQ_LOGGING__LEVEL="warning", OMP_NUM_THREADS="1", **(env_extra or {}))
-        cmd = [sys.executable, "-m", "llm_message_queue_amd.cli", "serve", "--cpu-ranks", "--port", str(self.port),
+        mode = ["--model", "tiny"] if gpu else ["--cpu-ranks"]     # gpu: every rank on the visible GPU(s)
+        cmd = [sys.executable, "-m", "llm_message_queue_amd.cli", "serve"] + mode + ["--port", str(self.port),
                "--host", "127.0.0.1"] + list(args)
         if torchrun:
             # static rendezvous (run id "none", as the round-4 HTTP runs), or
@@ -258,16 +259,10 @@ def test_sigkilled_job_leaves_nothing_and_next_job_completes_every_request():
     assert not [n for n in _shm_names() - before if rb[0]["job"] in n]
 
 
-@pytest.mark.parametrize("standalone", [True, False])
-def test_restart_after_peer_lost_gets_a_fresh_incarnation(standalone):
-    """``torchrun --max-restarts 1``: rank 0's backend stalls (injected), so
-    rank 1 loses its peer at the control-plane collective (``PeerLost``) and
-    exits non-zero; torchrun restarts the group.  The new incarnation has its
-    own token (restart count 1, new nonce) -- it does not see the old rings --
-    and serves every request."""
+def _restart_after_peer_lost(standalone, gpu=False):
     env = {"LLMQ_SERVER__FAULT_INJECTION": "true", "LLMQ_COLLECTIVE_TIMEOUT_S": "4",
            "LLMQ_SERVER__STALL_FATAL_AFTER": "0", "LLMQ_FATAL_EXIT_GRACE_S": "5"}
-    s = Server([], env_extra=env, torchrun=2, restarts=1, standalone=standalone)
+    s = Server([], env_extra=env, torchrun=2, restarts=1, standalone=standalone, gpu=gpu)
     try:
         r0 = s.ranks(2, restart=0)
         s.wait_for(lambda e: e.get("event") == "listening")
@@ -293,6 +288,27 @@ def test_restart_after_peer_lost_gets_a_fresh_incarnation(standalone):
         assert s.wait_completed(ids) == len(ids)
     finally:
         s.stop()
+
+
+@pytest.mark.parametrize("standalone", [True, False])
+def test_restart_after_peer_lost_gets_a_fresh_incarnation(standalone):
+    """``torchrun --max-restarts 1``: rank 0's backend stalls (injected), so
+    rank 1 loses its peer at the control-plane collective (``PeerLost``) and
+    exits non-zero; torchrun restarts the group.  The new incarnation has its
+    own token (restart count 1, new nonce) -- it does not see the old rings --
+    and serves every request."""
+    _restart_after_peer_lost(standalone)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_restart_after_peer_lost_on_gpu():
+    """The same restart with GPU backends: two ranks of ``cli serve --model
+    tiny`` on the box's GPU (time-sharing it; the data plane falls back to
+    gloo when ranks share a device), the stalled HIP engine, PeerLost, a
+    torchrun restart, and the new incarnation serving every request on the
+    GPU."""
+    _restart_after_peer_lost(True, gpu=True)
 
 
 def test_forced_stall_reports_503_then_exits_nonzero():
