@@ -137,8 +137,40 @@ def cmd_native_ingress(a) -> int:
     return 0
 
 
+def _start_tracemalloc(path: str, every_s: float = 60.0) -> None:
+    """``LLMQ_TRACEMALLOC=<file>``: a memory-growth probe for soaks.  Python
+    allocations are traced (8 frames), and every ``LLMQ_TRACEMALLOC_EVERY_S``
+    seconds (default 60) the 25 call sites that grew most since the first
+    snapshot are appended to ``<file>.<pid>``.  Costs ~2x interpreter time:
+    diagnosis only."""
+    import tracemalloc
+    tracemalloc.start(8)
+    out = f"{path}.{os.getpid()}"
+
+    def loop():
+        base = None
+        t0 = time.monotonic()
+        while True:
+            time.sleep(every_s)
+            snap = tracemalloc.take_snapshot().filter_traces(
+                (tracemalloc.Filter(False, tracemalloc.__file__), tracemalloc.Filter(False, "<frozen importlib._bootstrap>")))
+            if base is None:
+                base = snap
+                continue
+            cur, peak = tracemalloc.get_traced_memory()
+            with open(out, "a") as fh:
+                fh.write(f"=== t={time.monotonic() - t0:.0f}s traced={cur / 2**20:.1f} MiB peak={peak / 2**20:.1f} MiB\n")
+                for st in snap.compare_to(base, "traceback")[:25]:
+                    fh.write(f"{st.size_diff / 2**20:+.2f} MiB  {st.count_diff:+d} blocks\n")
+                    for line in st.traceback.format()[-8:]:
+                        fh.write(f"    {line}\n")
+    threading.Thread(target=loop, name="tracemalloc-probe", daemon=True).start()
+
+
 def cmd_serve(a, role: str = "serve") -> int:
     import torch
+    if os.environ.get("LLMQ_TRACEMALLOC"):
+        _start_tracemalloc(os.environ["LLMQ_TRACEMALLOC"], float(os.environ.get("LLMQ_TRACEMALLOC_EVERY_S", "60")))
     from ..balancer.load_balancer import Endpoint
     from ..gateway.app import GatewayApp
     from ..parallel.comm import init_from_env, local_device_index
