@@ -34,7 +34,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", default="3840,4041,4096,4226,4352")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib-dir", default="", help="A/B: load the native modules from this directory instead of _lib")
     a = ap.parse_args()
+    if a.lib_dir:
+        from llm_message_queue_amd import _native
+        _native._LIB = os.path.abspath(a.lib_dir)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     N = (HQ + 2 * HKV) * 128

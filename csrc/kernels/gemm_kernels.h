@@ -173,8 +173,15 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     const int xcd = bid & 7, loc = bid >> 3, q8 = full >> 3, r8 = full & 7;
     pid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
   } else {
-    pid = full + ((bid - full) >> 1);
-    khalf = (bid - full) & 1;
+    // split tiles: the same XCD-contiguous remap over the tail's blocks, so
+    // an XCD runs both K-halves of a contiguous run of tiles (their A / B
+    // panels share its L2) instead of one half of every 4th tile
+    const int t = bid - full, nt2 = nwg - full;
+    const int n2 = 2 * nt2;                        // blocks of the tail
+    const int xcd = t & 7, loc = t >> 3, q8 = n2 >> 3, r8 = n2 & 7;
+    const int j = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    pid = full + (j >> 1);
+    khalf = j & 1;
   }
   const int group = pid / (group_m * tiles_n);
   const int first_m = group * group_m;
