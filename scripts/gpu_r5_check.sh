@@ -13,6 +13,11 @@ if [ -z "${SKIP_TESTS:-}" ]; then
     > gpurun_out/r5_pytest_gpu.log 2>&1 || { echo "gpu tests failed rc=$?"; tail -30 gpurun_out/r5_pytest_gpu.log; exit 1; }
   tail -3 gpurun_out/r5_pytest_gpu.log
 fi
+if [ -z "${SKIP_SMOKE:-}" ]; then
+  timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/r5_smoke.log 2>&1 \
+    || { echo "smoke failed rc=$?"; tail -20 gpurun_out/r5_smoke.log; exit 1; }
+  echo "smoke ok"; tail -2 gpurun_out/r5_smoke.log
+fi
 if [ -z "${SKIP_BENCH:-}" ]; then
   timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/r5_bench.json 2> gpurun_out/r5_bench.err \
     || { echo "bench failed rc=$?"; tail -20 gpurun_out/r5_bench.err; exit 1; }
