@@ -1,7 +1,9 @@
 """Fixed-width int32 rows the ranks exchange in every tick's all_to_all
 (``parallel.comm``): request descriptors a router hands to another GPU,
 completion / failure / abort records owed back to the origin router, KV
-migration orders and cancels.  int64 fields travel as (lo, hi) int32 pairs."""
+migration orders and cancels.  int64 fields travel as (lo, hi) int32 pairs.
+The reference has no inter-service transport at all: its binaries do not
+share queues."""
 from __future__ import annotations
 
 import numpy as np

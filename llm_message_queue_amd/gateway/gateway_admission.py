@@ -2,7 +2,9 @@
 the realtime lane, admission into this rank's own free slots while a
 collective is in flight (only into the capacity held back from the published
 load), and the extra local forward a faster GPU takes while its peers are
-behind.  Serve-loop only."""
+behind.  Serve-loop only.  The reference dispatches from a ticker that
+batch-pops each queue every ``ProcessInterval``
+(`internal/priorityqueue/worker.go:110-130`)."""
 from __future__ import annotations
 
 import time

@@ -2,6 +2,9 @@
 dialog's KV lives (home GPU), the per-(home GPU, tier) pin counts every rank
 publishes to the planner, the handles of queued turns homed elsewhere, and
 the KV-migration orders and their execution (``parallel.migration``).
+The reference's only affinity is a session map keyed on a ``sessionID`` no
+caller passes (`internal/loadbalancer/load_balancer.go:233-240`); here the
+key is the conversation id and the target is the GPU holding its KV.
 
 Threads: the pin counts and the homed-away set are also changed from API /
 peer threads (``qm.on_remove`` when a queued turn is deleted), so ``_pin``

@@ -1,7 +1,9 @@
 """Latency histograms of the gateway data path: per-tier arrival -> dispatch
 and enqueue -> dispatch (``LatencyRecorder``), and where a request's arrival
 -> admission time goes, stage by stage (``StageRecorder``).  Log-binned
-int64 histograms, so every rank's can be summed over the control plane."""
+int64 histograms, so every rank's can be summed over the control plane.
+The reference declares a wait-time histogram it never observes
+(`internal/priorityqueue/queue_manager.go:116-122`)."""
 from __future__ import annotations
 
 import numpy as np
