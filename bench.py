@@ -102,6 +102,9 @@ def parse(argv=None):
                          "kept for the A/B scripts)")
     ap.add_argument("--no-fused-resid", action="store_true",
                     help="A/B: o / down projections on hipBLASLt beta = 1")
+    ap.add_argument("--no-fused-rms", action="store_true",
+                    help="A/B: the RMSNorm row scales by a separate row_rms pass instead of the residual GEMM's "
+                         "epilogue")
     ap.add_argument("--resid-epi", default="lds", choices=["regs", "lds", "pre"],
                     help="the fused residual tile through registers (GM_EPI_RESID), staged into LDS by DMA "
                          "(GM_EPI_RESID_LDS, default) or with its first quarter prefetched (GM_EPI_RESID_PRE)")
@@ -322,6 +325,7 @@ def main(argv=None) -> int:
                                fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
                                fused_head=False if a.no_fused_head else None,
                                fused_resid=False if a.no_fused_resid else None,
+                               fused_rms=False if a.no_fused_rms else None,
                                prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
@@ -670,6 +674,7 @@ def main(argv=None) -> int:
                    "row_scale_norm": bool(engine.model.row_scale_norm),
                    "fused_head": bool(engine.model.fused_head),
                    "fused_resid": bool(engine.model.fused_resid), "resid_epi": a.resid_epi,
+                   "fused_rms": bool(getattr(engine.model, "fused_rms", False)),
                    "prune_last": bool(getattr(engine.model, "prune_last", False))},
         # realtime tier, arrival -> LAST generated token (the 8B backend's 4
         # forwards included); the headline's clock is arrival -> dispatch

@@ -67,7 +67,7 @@ static void launch(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int
   const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
   hipLaunchKernelGGL((gemm_bf16_kernel<GM_EPI_SWIGLU, true, SCHED>), dim3(tiles), dim3(GM_THREADS), GM_LDS_BYTES, 0,
                      a, w, c, M, N, K, GM_GROUP_M, nullptr, GmRope{}, GmSplit{0, nullptr, nullptr},
-                     GmArgmax{reinterpret_cast<float*>(dbg), nullptr});
+                     GmSide{reinterpret_cast<float*>(dbg), nullptr});
 }
 
 int main(int argc, char** argv) {

@@ -73,9 +73,22 @@ constexpr int gm_lds_bytes() { return EPI == GM_EPI_RESID_PRE ? GM_LDS_BYTES + G
 // gemm_argmax_reduce_kernel picks the first maximum over the tiles (ties go
 // to the lower column, as torch.argmax does).  Values are the fp32
 // accumulators (not bf16-rounded logits).
-struct GmArgmax {
+// Epilogue side outputs.  GM_EPI_ARGMAX: per-(row, column tile) max value /
+// index partials (pv, pi).  GM_EPI_RESID_LDS with rpart != nullptr: the
+// RMSNorm row scale of the updated residual rows, fused into the epilogue --
+// each block's per-row sums of squares of the bf16 values it stores (rpart
+// [tiles_m][tiles_n][256], written through to memory), and the last of a
+// row tile's tiles_n blocks (rticket[tiles_m], zero at launch, re-zeroed)
+// adds them in column-tile order and writes 1 / sqrt(sum / N + reps) to
+// rscale[tm * 256 + row]: what row_rms_kernel computes, in a fixed order,
+// without the 33 MB re-read of the rows by a separate launch.
+struct GmSide {
   float* pv;
   int32_t* pi;
+  float* rpart;
+  int* rticket;
+  float* rscale;
+  float reps;
 };
 
 // GM_EPI_ROPE: the fused qkv projection's epilogue = the rope_kv kernel
@@ -157,7 +170,7 @@ template <int EPI, bool STAGGER = true, int SCHED = 2>
 __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
     int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp,
-    const GmArgmax am) {
+    const GmSide am) {
   extern __shared__ __align__(16) uint8_t smem[];
   static_assert(EPI != GM_EPI_RESID_PRE || SCHED >= 1, "the residual prefetch is issued by the SCHED >= 1 prologue");
 
@@ -707,6 +720,8 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
             }
     GM_LGKM(0);
     __builtin_amdgcn_wave_barrier();
+    const bool rms = am.rpart != nullptr;
+    float ssq[16];
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int qd = it * 64 + lane;               // row qd/8, chunk qd%8
@@ -714,6 +729,65 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
       const int grow = row0 + r;
       const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(rowp(r) + cb * 16);
       if (grow < M) *reinterpret_cast<gm_u32x4*>(C + (int64_t)grow * N + col0 + cb * 8) = v;
+      if (rms) {                                   // squares of the 8 stored bf16 values
+        float q = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = __uint_as_float(v[e] << 16), hi = __uint_as_float(v[e] & 0xFFFF0000u);
+          q += lo * lo + hi * hi;
+        }
+        ssq[it] = q;
+      }
+    }
+    if (rms) {
+      // row r = it * 8 + lane / 8 of this wave's 128: its 8 chunk lanes meet
+      // by three xor-shuffles; the wave's 128 partials go to the start of its
+      // own (now unused) 16 KiB of LDS, the block's 4 column waves of a row
+      // half are added in wc order, written through to rpart, and the last
+      // block of the row tile (ticket) finishes the scale
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        float q = ssq[it];
+        q += __shfl_xor(q, 1, 64);
+        q += __shfl_xor(q, 2, 64);
+        q += __shfl_xor(q, 4, 64);
+        ssq[it] = q;
+      }
+      GM_LGKM(0);
+      __builtin_amdgcn_wave_barrier();
+      float* wp = reinterpret_cast<float*>(cw);
+      if ((lane & 7) == 0) {
+#pragma unroll
+        for (int it = 0; it < 16; ++it) wp[it * 8 + (lane >> 3)] = ssq[it];
+      }
+      __syncthreads();
+      const int tiles_n_ = N / GM_BN;
+      if (tid < 256) {                             // block row tid: wave row tid / 128, row tid % 128
+        const int hw = tid >> 7, rr = tid & 127;
+        float sum = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sum += reinterpret_cast<const float*>(smem + (hw * 4 + c) * 16384)[rr];
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            am.rpart + (size_t)(tm * tiles_n_ + tn) * 256, 0, 256 * 4, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sum), prs, tid * 4, 0, GM_CPOL_SC1);
+      }
+      GM_VMCNT(0);
+      __syncthreads();
+      if (tid == 0)
+        *reinterpret_cast<int*>(smem) = __hip_atomic_fetch_add(am.rticket + tm, 1, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int done = *reinterpret_cast<volatile int*>(smem);
+      if (done == tiles_n_ - 1 && tid < 256) {     // the row tile's last block: finish its 256 scales
+        float sum = 0.f;
+        for (int t2 = 0; t2 < tiles_n_; ++t2) {
+          const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+              am.rpart + (size_t)(tm * tiles_n_ + t2) * 256, 0, 256 * 4, 0x00020000);
+          sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, tid * 4, 0, GM_CPOL_SC1));
+        }
+        am.rscale[tm * 256 + tid] = rsqrtf(sum / (float)N + am.reps);
+        if (tid == 0) __hip_atomic_store(am.rticket + tm, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   } else if (EPI == GM_EPI_SWIGLU) {
     // wave w: 128 rows x 32 features bf16 = 8 KiB at w * 8 KiB

@@ -203,7 +203,7 @@ template <int EPI, bool STAGGER = true, int SCHED = 2>
 static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st,
                         int group_m, const float* rs = nullptr, const GmRope& rp = GmRope{},
                         const GmSplit& sp = GmSplit{0, nullptr, nullptr},
-                        const GmArgmax& am = GmArgmax{nullptr, nullptr}) {
+                        const GmSide& am = GmSide{}) {
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
@@ -215,6 +215,30 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
   hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(grid), dim3(GM_THREADS), gm_lds_bytes<EPI>(), st,
                      a, w, c,
                      M, N, K, group_m, rs, rp, sp, am);
+}
+
+// C += A·Wᵀ (GM_EPI_RESID_LDS) and the RMSNorm scale of the updated rows in
+// the same launch: part [tiles_m * tiles_n * 256] fp32, ticket [tiles_m] int
+// (zero; the kernel leaves it zero), scale [tiles_m * 256] fp32 (what
+// row_rms_kernel writes, rows < M meaningful).
+static void gemm_residual_rms(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, uintptr_t stream,
+                              int group_m, uintptr_t part, uintptr_t ticket, uintptr_t scale, float eps) {
+  require(group_m >= 1 && group_m <= 64, "gemm: group_m out of range");
+  require(M > 0 && N > 0 && K > 0, "gemm: empty operand");
+  require(N % GM_BN == 0, "gemm: N must be a multiple of 256");
+  require(K % (2 * GM_BK) == 0, "gemm: K must be a multiple of 128");
+  require((int64_t)M * K < (int64_t)1 << 30 && (int64_t)N * K < (int64_t)1 << 30 && (int64_t)M * N < (int64_t)1 << 30,
+          "gemm: operand too large (2 GiB buffer descriptors)");
+  require(a % 16 == 0 && w % 16 == 0 && c % 16 == 0, "gemm: pointers must be 16-byte aligned");
+  require(part != 0 && ticket != 0 && scale != 0, "gemm_residual_rms: null workspace");
+  GmSide side{};
+  side.rpart = P<float>(part);
+  side.rticket = P<int>(ticket);
+  side.rscale = P<float>(scale);
+  side.reps = eps;
+  launch_gemm<GM_EPI_RESID_LDS>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
+                                group_m, nullptr, GmRope{}, GmSplit{0, nullptr, nullptr}, side);
+  check_launch();
 }
 
 // epi: 0 / 2 / 5 = store / SwiGLU / residual add (C += A·Wᵀ); 16 / 32 = store with the round-1 phase
@@ -301,7 +325,7 @@ static void gemm_argmax(uintptr_t a, uintptr_t w, int M, int N, int K, uintptr_t
   require((int64_t)M * K < (1LL << 30) && (int64_t)N * K < (1LL << 30), "gemm_argmax: operand > 2 GiB");
   require(a % 16 == 0 && w % 16 == 0 && pv % 4 == 0 && pi % 4 == 0 && out % 4 == 0, "gemm_argmax: alignment");
   launch_gemm<GM_EPI_ARGMAX>(P<const uint16_t>(a), P<const uint16_t>(w), nullptr, M, N, K, S(stream), GM_GROUP_M,
-                             nullptr, GmRope{}, GmSplit{0, nullptr, nullptr}, GmArgmax{P<float>(pv), P<int32_t>(pi)});
+                             nullptr, GmRope{}, GmSplit{0, nullptr, nullptr}, GmSide{P<float>(pv), P<int32_t>(pi)});
   hipLaunchKernelGGL(gemm_argmax_reduce_kernel, dim3((M + 3) / 4), dim3(256), 0, S(stream), P<const float>(pv),
                      P<const int32_t>(pi), M, N / GM_BN, P<int32_t>(out));
   check_launch();
@@ -492,6 +516,9 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("rmsnorm", &rmsnorm);
   m.def("silu_mul", &silu_mul, py::arg("gu"), py::arg("out"), py::arg("T"), py::arg("F"), py::arg("stream"),
         py::arg("perm") = false);
+  m.def("gemm_residual_rms", &gemm_residual_rms, py::arg("a"), py::arg("w"), py::arg("c"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("stream"), py::arg("group_m"), py::arg("part"), py::arg("ticket"),
+        py::arg("scale"), py::arg("eps"));
   m.def("gemm_bf16", &gemm_bf16, py::arg("a"), py::arg("w"), py::arg("c"), py::arg("M"), py::arg("N"),
         py::arg("K"), py::arg("epi"), py::arg("stream"), py::arg("group_m") = (int)GM_GROUP_M, py::arg("rs") = 0);
   m.def("gemm_qkv_rope", &gemm_qkv_rope, py::arg("a"), py::arg("w"), py::arg("M"), py::arg("N"), py::arg("K"),

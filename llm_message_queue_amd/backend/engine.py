@@ -102,7 +102,7 @@ class BackendEngine:
                  page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True,
                  split_qkv: bool = False, fused_mlp=None, fused_qkv=None, row_scale_norm: bool = True,
                  fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
-                 realtime_step_tokens: int = 0):
+                 realtime_step_tokens: int = 0, fused_rms=None):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
         self.step_timeout_s = float(step_timeout_s)
@@ -124,7 +124,7 @@ class BackendEngine:
         self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
                                fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
-                               fused_resid=fused_resid, prune_last=prune_last)
+                               fused_resid=fused_resid, fused_rms=fused_rms, prune_last=prune_last)
         self.impl = impl
         self.weight_bytes = self.model.weight_bytes()
         self.active: Dict[int, Request] = {}            # slot -> request

@@ -72,6 +72,7 @@ class LlamaStub:
                  fused_mlp: Optional[bool] = None, min_fused_tokens: int = 512,
                  fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048, row_scale_norm: bool = True,
                  fused_head: Optional[bool] = None, fused_resid: Optional[bool] = None,
+                 fused_rms: Optional[bool] = None,
                  prune_last: bool = True):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
@@ -121,6 +122,10 @@ class LlamaStub:
         # profiles/r5_resid_ab_1gpu.jsonl) and >= it in the serving A/B
         # (profiles/r5_resid_serving_ab_1gpu.jsonl).
         self.fused_resid = (impl == "hip") if fused_resid is None else bool(fused_resid)
+        # with the residual GEMM (LDS epilogue): the RMSNorm row scales of the
+        # updated residual rows come out of its epilogue (ops.gemm.
+        # gemm_residual_rms) instead of a separate row_rms pass
+        self.fused_rms = self.fused_resid if fused_rms is None else bool(fused_rms)
         self._cus = G._cu_count(self.device) if (self.fused_resid and self.device.type == "cuda") else 0
         # fused paths take the raw residual rows + a per-row RMSNorm scale
         # (True) or an rmsnorm'd copy of the rows (False, A/B)
@@ -226,10 +231,12 @@ class LlamaStub:
         if rows is not None and rows.numel() == T:
             rows = None                                  # every row sampled: nothing to drop
 
+        scale = None                                     # row scales of res from the previous down GEMM
         for i, L in enumerate(self.layers):
             if rows_qkv and self.row_scale_norm:
-                q = ops.qkv_rope_rows(res, L["wqkv"], ops.row_rms(res, cfg.eps), pos, slot, self.cos, self.sin,
-                                      cfg.heads, cfg.kv_heads, self.kcache[i], self.vcache[i])
+                q = ops.qkv_rope_rows(res, L["wqkv"], scale if scale is not None else ops.row_rms(res, cfg.eps),
+                                      pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads, self.kcache[i],
+                                      self.vcache[i])
             elif rows_qkv:
                 q = G.qkv_rope(ops.rmsnorm(res, L["attn_norm"], cfg.eps), L["wqkv"], pos, slot, self.cos,
                                self.sin, cfg.heads, cfg.kv_heads, self.kcache[i], self.vcache[i])
@@ -240,7 +247,7 @@ class LlamaStub:
                 if rows.numel() == 0:                    # nothing sampled (a step of unfinished prefill
                     return res[:0]                       # chunks): K/V written, no row kernel gets 0 rows
                 res, a = res.index_select(0, rows), a.index_select(0, rows)
-            self._mlp_block(res, a, L)
+            scale = self._mlp_block(res, a, L, want_scale=rows_qkv and self.row_scale_norm and i < last)
         return ops.rmsnorm(res, self.final_norm, cfg.eps)
 
     @torch.no_grad()
@@ -261,29 +268,35 @@ class LlamaStub:
             n += 1
         return n
 
-    def _mlp_block(self, res: torch.Tensor, a: torch.Tensor, L: dict) -> None:
+    def _mlp_block(self, res: torch.Tensor, a: torch.Tensor, L: dict, want_scale: bool = False):
         """res += o(a); res += down(swiglu(norm(res))) -- in place, with the
-        fused-path choices made for this block's row count."""
+        fused-path choices made for this block's row count.  Returns the
+        RMSNorm row scales of the final ``res`` when ``want_scale`` and the
+        down GEMM produced them in its epilogue (``fused_rms``), else None."""
         cfg, ops = self.cfg, self.ops
         M = res.shape[0]
         rows_mlp = self.fused_mlp and M >= self.min_fused_tokens
         resid_o = self._cus > 0 and G.residual_tiles_ok(M, cfg.dim, self._cus)
+        rms = resid_o and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS
 
-        def into_res(x, wt):                             # res += x · wtᵀ
+        def into_res(x, wt, scale_out):                  # res += x · wtᵀ (+ its row scales)
+            if rms and scale_out:
+                return G.gemm_residual_rms(x, wt, res, cfg.eps)
             if resid_o:
                 G.gemm_residual(x, wt, res)
             else:
                 res.addmm_(x, wt.t())
+            return None
 
-        into_res(a, L["wo"])
+        scale = into_res(a, L["wo"], rows_mlp and self.row_scale_norm)
         if rows_mlp and self.row_scale_norm:
-            act = ops.swiglu_rows(res, L["w_gu"], ops.row_rms(res, cfg.eps))
+            act = ops.swiglu_rows(res, L["w_gu"], scale if scale is not None else ops.row_rms(res, cfg.eps))
         elif rows_mlp:
             act = G.gemm_swiglu(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"])
         else:
             act = ops.mlp_up(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"], self.fused_mlp,
                              self.min_fused_tokens)
-        into_res(act, L["w_down"])
+        return into_res(act, L["w_down"], want_scale)
 
     def _qkv(self, x, L, i, pos, slot):
         """qkv projection (hipBLASLt) + RoPE / KV-cache write of normalised rows."""

@@ -137,6 +137,48 @@ def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None,
     return _launch(x, w_perm, y, EPI_SWIGLU, row_scale=row_scale)
 
 
+_RMS_WS = {}
+
+
+def _rms_workspace(device, stream: int, tiles_m: int, tiles_n: int):
+    """Per-(device, stream) scratch of the fused row-scale epilogue: fp32
+    row partials [tiles_m * tiles_n * 256] and int tickets [tiles_m] (zero;
+    every launch leaves them zero), grown on demand."""
+    key = (device.type, device.index, stream)
+    ws = _RMS_WS.get(key)
+    if ws is None or ws[0].numel() < tiles_m * tiles_n * 256 or ws[1].numel() < tiles_m:
+        tm = max(tiles_m, ws[1].numel() if ws else 0)
+        ws = (torch.empty(tm * max(tiles_n, 16) * 256, dtype=torch.float32, device=device),
+              torch.zeros(tm, dtype=torch.int32, device=device))
+        _RMS_WS[key] = ws
+    return ws
+
+
+def gemm_residual_rms(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor, eps: float) -> torch.Tensor:
+    """``res += x · wᵀ`` (the LDS-DMA residual epilogue) and, in the same
+    launch, the RMSNorm row scale of the updated ``res``: returns fp32
+    [row_scale_len(M)] holding ``1 / sqrt(mean(res[r]^2) + eps)`` for rows
+    r < M -- ``HipOps.row_rms(res, eps)`` without its separate pass over the
+    rows (the next fused GEMM applies it per row).  Sums of squares are
+    added in a fixed order, so the result is deterministic; it matches
+    ``row_rms`` to fp32 rounding of a different summation order."""
+    _check(x, "x")
+    _check(w, "w")
+    _check(res, "res")
+    M, K = x.shape
+    N = w.shape[0]
+    if res.shape != (M, N):
+        raise ValueError("gemm_residual_rms: res shape mismatch")
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    tiles_m, tiles_n = (M + TILE_M - 1) // TILE_M, N // TILE_N
+    part, ticket = _rms_workspace(x.device, stream, tiles_m, tiles_n)
+    scale = torch.empty(row_scale_len(M), dtype=torch.float32, device=x.device)
+    _native.require_hipops().gemm_residual_rms(x.data_ptr(), w.data_ptr(), res.data_ptr(), M, N, K, stream,
+                                               8, part.data_ptr(), ticket.data_ptr(), scale.data_ptr(),
+                                               float(eps))
+    return scale
+
+
 def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
     """``res += x · wᵀ`` in place (bf16 ``res`` [M][N]; the fp32 sum is
     rounded once, as hipBLASLt's beta = 1 epilogue) -- the o / down

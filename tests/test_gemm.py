@@ -247,10 +247,7 @@ def test_gemm_residual_matches_fp32(T, K, epi):
     big[:T] = torch.randn(T, N, generator=g, device=DEV).to(torch.bfloat16)
     res0 = big[:T].float().clone()
     ref = res0 + x.float() @ w.float().t()
-    if epi == "regs":
-        G.gemm_residual(x, w, big[:T])
-    else:
-        G._launch(x, w, big[:T], G.EPI_RESID_LDS if epi == "lds" else G.EPI_RESID_PRE)
+    G._launch(x, w, big[:T], {"regs": G.EPI_RESID, "lds": G.EPI_RESID_LDS, "pre": G.EPI_RESID_PRE}[epi])
     err = (big[:T].float() - ref).abs().max().item()
     assert err <= 0.01 * ref.abs().max().item() + 1e-3, err
     assert (big[T:] == 3.0).all()
@@ -260,6 +257,64 @@ def test_gemm_residual_matches_fp32(T, K, epi):
         d = (big[:T].float() - r2.float()).abs()
         assert d.max().item() <= 0.01 * ref.abs().max().item() + 1e-3
         assert (d == 0).float().mean().item() > 0.9, "residual epilogue should round like beta = 1"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K", [(37, 4096), (300, 1024), (4041, 4096), (4096, 14336)])
+def test_gemm_residual_rms_matches_row_rms(T, K):
+    """The residual GEMM with the fused RMSNorm row scale: ``res`` exactly as
+    the plain LDS epilogue leaves it, and the scales equal ``row_rms`` of the
+    updated rows (fp32, a different summation order); twice in a row (the
+    tickets the last block re-zeroes), bit-identical."""
+    from llm_message_queue_amd.ops.llama_ops import HipOps
+    N = 4096
+    x, w = _rand(T, K, N, seed=700 + T)
+    g = torch.Generator(device=DEV).manual_seed(T + 1)
+    res0 = torch.randn(T, N, generator=g, device=DEV).to(torch.bfloat16)
+    r_plain = res0.clone()
+    G._launch(x, w, r_plain, G.EPI_RESID_LDS)
+    scales = []
+    for _ in range(2):
+        r_rms = res0.clone()
+        sc = G.gemm_residual_rms(x, w, r_rms, 1e-5)
+        torch.cuda.synchronize()
+        assert torch.equal(r_rms, r_plain)
+        scales.append(sc[:T].clone())
+    assert torch.equal(scales[0], scales[1])
+    ref = HipOps().row_rms(r_plain, 1e-5)[:T]
+    assert torch.allclose(scales[0], ref, rtol=1e-5, atol=0), (scales[0] - ref).abs().max().item()
+    exact = r_plain.float().pow(2).mean(-1).add(1e-5).rsqrt()
+    assert torch.allclose(scales[0], exact, rtol=1e-4, atol=0)
+
+
+@pytest.mark.gpu
+def test_8b_model_fused_rms_matches_row_rms_path():
+    """The model with the row scales from the residual GEMM's epilogue (the
+    default) against the separate row_rms pass: same hidden states to bf16
+    noise at a full-chip step, and row_rms runs only for layer 0's qkv."""
+    from llm_message_queue_amd.ops import llama_ops
+    cfg = LlamaConfig(layers=3)
+    a = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=6)
+    b = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=6, fused_rms=False)
+    assert a.fused_rms and not b.fused_rms
+    T = 4041
+    if not G.residual_tiles_ok(T, cfg.dim, a._cus):
+        pytest.skip(f"{a._cus} CUs: T = {T} is not a whole wave of tiles here")
+    calls = []
+    orig = llama_ops.HipOps.row_rms
+    llama_ops.HipOps.row_rms = lambda self, *x: (calls.append(1), orig(self, *x))[1]
+    try:
+        tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
+        pos = (torch.arange(T, device=DEV, dtype=torch.int32) % 64)
+        slot = (torch.arange(T, device=DEV, dtype=torch.int32) // 64)
+        ha = a.hidden(tok, pos, slot).float()
+        n_fused = len(calls)
+        hb = b.hidden(tok, pos, slot).float()
+    finally:
+        llama_ops.HipOps.row_rms = orig
+    assert n_fused == 1 and len(calls) - n_fused == 2 * cfg.layers
+    rel = ((ha - hb).norm() / hb.norm()).item()
+    assert rel < 1e-2, rel
 
 
 @pytest.mark.gpu
