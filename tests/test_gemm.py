@@ -332,8 +332,9 @@ def test_8b_model_residual_gemm_matches_hipblaslt_path():
     if not G.residual_tiles_ok(T, cfg.dim, a._cus):
         pytest.skip(f"{a._cus} CUs: T = {T} is not a whole wave of tiles here")
     called = []
-    orig = G.gemm_residual
+    orig, orig_rms = G.gemm_residual, G.gemm_residual_rms
     G.gemm_residual = lambda *x: (called.append(1), orig(*x))[1]
+    G.gemm_residual_rms = lambda *x: (called.append(1), orig_rms(*x))[1]      # (with the row scales)
     try:
         tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
         pos = (torch.arange(T, device=DEV, dtype=torch.int32) % 64)
@@ -341,7 +342,7 @@ def test_8b_model_residual_gemm_matches_hipblaslt_path():
         ha = a.hidden(tok, pos, slot).float()
         hb = b.hidden(tok, pos, slot).float()
     finally:
-        G.gemm_residual = orig
+        G.gemm_residual, G.gemm_residual_rms = orig, orig_rms
     assert len(called) == 2 * cfg.layers
     rel = ((ha - hb).norm() / hb.norm()).item()
     assert rel < 1e-2, rel
