@@ -102,9 +102,9 @@ def parse(argv=None):
                          "kept for the A/B scripts)")
     ap.add_argument("--no-fused-resid", action="store_true",
                     help="A/B: o / down projections on hipBLASLt beta = 1")
-    ap.add_argument("--no-fused-rms", action="store_true",
-                    help="A/B: the RMSNorm row scales by a separate row_rms pass instead of the residual GEMM's "
-                         "epilogue")
+    ap.add_argument("--fused-rms", action="store_true",
+                    help="A/B: the RMSNorm row scales from the residual GEMM's epilogue instead of a separate "
+                         "row_rms pass (default off: profiles/r5_resid_rms_bench.jsonl)")
     ap.add_argument("--resid-epi", default="lds", choices=["regs", "lds", "pre"],
                     help="the fused residual tile through registers (GM_EPI_RESID), staged into LDS by DMA "
                          "(GM_EPI_RESID_LDS, default) or with its first quarter prefetched (GM_EPI_RESID_PRE)")
@@ -325,7 +325,7 @@ def main(argv=None) -> int:
                                fused_qkv=False if a.no_fused_qkv else None, row_scale_norm=not a.no_row_scale,
                                fused_head=False if a.no_fused_head else None,
                                fused_resid=False if a.no_fused_resid else None,
-                               fused_rms=False if a.no_fused_rms else None,
+                               fused_rms=True if a.fused_rms else None,
                                prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer

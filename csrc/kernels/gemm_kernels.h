@@ -58,7 +58,7 @@ constexpr int GM_LDS_BYTES = 2 * GM_BUF_BYTES;     // 128 KiB
 constexpr int GM_GROUP_M = 8;                    // default M-tiles per block-order group
 
 enum { GM_EPI_STORE = 0, GM_EPI_SWIGLU = 2, GM_EPI_ROPE = 3, GM_EPI_ARGMAX = 4, GM_EPI_RESID = 5,
-       GM_EPI_RESID_LDS = 6, GM_EPI_RESID_PRE = 7 };
+       GM_EPI_RESID_LDS = 6, GM_EPI_RESID_PRE = 7, GM_EPI_RESID_RMS = 8 };
 // GM_EPI_RESID_PRE: GM_EPI_RESID_LDS whose first quarter of the residual tile
 // (rows 0-31 of every wave's 128 x 64 block) is fetched into the 32 KiB of
 // LDS gfx950 has beyond the operand buffers at kernel start, so it is in LDS
@@ -74,7 +74,7 @@ constexpr int gm_lds_bytes() { return EPI == GM_EPI_RESID_PRE ? GM_LDS_BYTES + G
 // to the lower column, as torch.argmax does).  Values are the fp32
 // accumulators (not bf16-rounded logits).
 // Epilogue side outputs.  GM_EPI_ARGMAX: per-(row, column tile) max value /
-// index partials (pv, pi).  GM_EPI_RESID_LDS with rpart != nullptr: the
+// index partials (pv, pi).  GM_EPI_RESID_RMS (GM_EPI_RESID_LDS plus): the
 // RMSNorm row scale of the updated residual rows, fused into the epilogue --
 // each block's per-row sums of squares of the bf16 values it stores (rpart
 // [tiles_m][tiles_n][256], written through to memory), and the last of a
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         GM_LGKM(0);
         __builtin_amdgcn_wave_barrier();
       }
-  } else if (EPI == GM_EPI_RESID_LDS || EPI == GM_EPI_RESID_PRE) {
+  } else if (EPI == GM_EPI_RESID_LDS || EPI == GM_EPI_RESID_PRE || EPI == GM_EPI_RESID_RMS) {
     // The residual tile staged by DMA instead of through registers: the
     // wave's 128 x 64 bf16 block of C lands in its 16 KiB of LDS (16
     // buffer_load ... lds of 16 B per lane, row-major, the plain epilogue's
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
             }
     GM_LGKM(0);
     __builtin_amdgcn_wave_barrier();
-    const bool rms = am.rpart != nullptr;
+    constexpr bool rms = EPI == GM_EPI_RESID_RMS;   // + the RMSNorm row scales (GmSide.r*)
     float ssq[16];
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
       const int grow = row0 + r;
       const gm_u32x4 v = *reinterpret_cast<const gm_u32x4*>(rowp(r) + cb * 16);
       if (grow < M) *reinterpret_cast<gm_u32x4*>(C + (int64_t)grow * N + col0 + cb * 8) = v;
-      if (rms) {                                   // squares of the 8 stored bf16 values
+      if constexpr (rms) {                         // squares of the 8 stored bf16 values
         float q = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -739,7 +739,7 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
         ssq[it] = q;
       }
     }
-    if (rms) {
+    if constexpr (rms) {
       // row r = it * 8 + lane / 8 of this wave's 128: its 8 chunk lanes meet
       // by three xor-shuffles; the wave's 128 partials go to the start of its
       // own (now unused) 16 KiB of LDS, the block's 4 column waves of a row

@@ -217,7 +217,7 @@ static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M
                      M, N, K, group_m, rs, rp, sp, am);
 }
 
-// C += A·Wᵀ (GM_EPI_RESID_LDS) and the RMSNorm scale of the updated rows in
+// C += A·Wᵀ (GM_EPI_RESID_RMS = the LDS epilogue) and the RMSNorm scale of the updated rows in
 // the same launch: part [tiles_m * tiles_n * 256] fp32, ticket [tiles_m] int
 // (zero; the kernel leaves it zero), scale [tiles_m * 256] fp32 (what
 // row_rms_kernel writes, rows < M meaningful).
@@ -236,7 +236,7 @@ static void gemm_residual_rms(uintptr_t a, uintptr_t w, uintptr_t c, int M, int 
   side.rticket = P<int>(ticket);
   side.rscale = P<float>(scale);
   side.reps = eps;
-  launch_gemm<GM_EPI_RESID_LDS>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
+  launch_gemm<GM_EPI_RESID_RMS>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
                                 group_m, nullptr, GmRope{}, GmSplit{0, nullptr, nullptr}, side);
   check_launch();
 }

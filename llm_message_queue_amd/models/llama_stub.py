@@ -122,10 +122,13 @@ class LlamaStub:
         # profiles/r5_resid_ab_1gpu.jsonl) and >= it in the serving A/B
         # (profiles/r5_resid_serving_ab_1gpu.jsonl).
         self.fused_resid = (impl == "hip") if fused_resid is None else bool(fused_resid)
-        # with the residual GEMM (LDS epilogue): the RMSNorm row scales of the
-        # updated residual rows come out of its epilogue (ops.gemm.
-        # gemm_residual_rms) instead of a separate row_rms pass
-        self.fused_rms = self.fused_resid if fused_rms is None else bool(fused_rms)
+        # with the residual GEMM: the RMSNorm row scales of the updated
+        # residual rows out of its epilogue (ops.gemm.gemm_residual_rms)
+        # instead of a separate row_rms pass.  Off by default: the epilogue's
+        # cross-block reduction adds 0.5-7 us to the tail of a single-wave
+        # GEMM, more than the 12.8 us row_rms launch it removes saves
+        # (profiles/r5_resid_rms_bench.jsonl, profiles/r5_fused_rms_serving_ab_1gpu.jsonl)
+        self.fused_rms = False if fused_rms is None else bool(fused_rms)
         self._cus = G._cu_count(self.device) if (self.fused_resid and self.device.type == "cuda") else 0
         # fused paths take the raw residual rows + a per-row RMSNorm scale
         # (True) or an rmsnorm'd copy of the rows (False, A/B)

@@ -11,5 +11,5 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   > $D/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $D/pytest.log; exit 1; }
 tail -1 $D/pytest.log
 BENCH_T=300 bash scripts/gpu_bench_ab.sh "--steps 100 --warmup 5 --gateway-only-s 0 --slo-climb 0.5" \
-  - "--no-fused-rms" - "--no-fused-rms" || exit $?
+  "--fused-rms" - "--fused-rms" - || exit $?
 cp gpurun_out/bench_ab.jsonl $D/serving_ab.jsonl

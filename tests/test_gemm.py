@@ -289,13 +289,14 @@ def test_gemm_residual_rms_matches_row_rms(T, K):
 
 @pytest.mark.gpu
 def test_8b_model_fused_rms_matches_row_rms_path():
-    """The model with the row scales from the residual GEMM's epilogue (the
-    default) against the separate row_rms pass: same hidden states to bf16
-    noise at a full-chip step, and row_rms runs only for layer 0's qkv."""
+    """The model with the row scales from the residual GEMM's epilogue
+    (``fused_rms``, an A/B option) against the separate row_rms pass (the
+    default): same hidden states to bf16 noise at a full-chip step, and
+    row_rms runs only for layer 0's qkv."""
     from llm_message_queue_amd.ops import llama_ops
     cfg = LlamaConfig(layers=3)
-    a = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=6)
-    b = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=6, fused_rms=False)
+    a = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=6, fused_rms=True)
+    b = LlamaStub(cfg, slots=64, max_ctx=128, device=DEV, impl="hip", seed=6)
     assert a.fused_rms and not b.fused_rms
     T = 4041
     if not G.residual_tiles_ok(T, cfg.dim, a._cus):
