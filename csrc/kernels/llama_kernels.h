@@ -373,30 +373,55 @@ __device__ __forceinline__ void attention_seg_block(int bid, uint16_t* __restric
 
   for (int k0 = 0; k0 < ctx; k0 += SA_KEYS) {
     __syncthreads();
-    // K: KEYS keys x 16 chunks, row-coalesced, chunk-swizzled
+    // K: KEYS keys x 16 chunks of 16 B staged by DMA (buffer_load ... lds:
+    // no VGPRs, issued before the V loads so both share one round trip).
+    // Wave wv's j-th instruction fills LDS chunks [(wv NKI + j) 64, +64) of
+    // Ks, lane l chunk P: key P / 16 at swizzled slot P % 16 = ch ^ (key &
+    // 15), i.e. source chunk ch = (P % 16) ^ (key & 15).  Keys >= ctx read 0
+    // off the buffer descriptor (num_records ends at key ctx).  The round-4
+    // form loaded into registers under a per-key predicate, which compiled
+    // to a load -> vmcnt(0) -> store chain (profiles/r5_attn_ab.jsonl).
+    {
+      constexpr int NKI = KEYS * 16 / 256;
+      const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(kc + kvbase + (int64_t)k0 * 128), 0, (uint32_t)(ctx - k0) * 256u, 0x00020000);
 #pragma unroll
-    for (int r = 0; r < KEYS / 16; ++r) {
-      const int c = tid + r * 256;
-      const int key = c >> 4, ch = c & 15;
-      uint4 kv = make_uint4(0u, 0u, 0u, 0u);
-      if (k0 + key < ctx) kv = *reinterpret_cast<const uint4*>(kc + kvbase + (int64_t)(k0 + key) * 128 + ch * 8);
-      *reinterpret_cast<uint4*>(Ks + key * 128 + ((ch ^ (key & 15)) * 8)) = kv;
+      for (int j = 0; j < NKI; ++j) {
+        const int P = (wv * NKI + j) * 64 + lane;
+        const int key = P >> 4, ch = (P & 15) ^ (key & 15);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            krs, (__attribute__((address_space(3))) void*)(Ks + (wv * NKI + j) * 64 * 8), 16,
+            (uint32_t)(key * 256 + ch * 16), 0, 0, 0);
+      }
     }
-    // V^T: item = (key pair kp, chunk ch); two keys per dword store
+    // V^T: item = (key pair kp, chunk ch); two keys per dword store.  The
+    // rows come through a buffer descriptor ending at key ctx: unconditional
+    // loads (keys >= ctx read 0), all in flight together with the K DMA
+    {
+      const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(vc + kvbase + (int64_t)k0 * 128), 0, (uint32_t)(ctx - k0) * 256u, 0x00020000);
+      typedef unsigned int vu32x4 __attribute__((ext_vector_type(4)));
+      vu32x4 va[KEYS / 32], vb[KEYS / 32];
 #pragma unroll
-    for (int r = 0; r < KEYS / 32; ++r) {
-      const int c = tid + r * 256;
-      const int kp = c % (KEYS / 2), ch = c / (KEYS / 2);
-      const int ka = k0 + 2 * kp;
-      uint4 va = make_uint4(0u, 0u, 0u, 0u), vb = make_uint4(0u, 0u, 0u, 0u);
-      if (ka < ctx) va = *reinterpret_cast<const uint4*>(vc + kvbase + (int64_t)ka * 128 + ch * 8);
-      if (ka + 1 < ctx) vb = *reinterpret_cast<const uint4*>(vc + kvbase + (int64_t)(ka + 1) * 128 + ch * 8);
-      const uint16_t* ea = reinterpret_cast<const uint16_t*>(&va);
-      const uint16_t* eb = reinterpret_cast<const uint16_t*>(&vb);
+      for (int r = 0; r < KEYS / 32; ++r) {
+        const int c = tid + r * 256;
+        const int kp = c % (KEYS / 2), ch = c / (KEYS / 2);
+        va[r] = __builtin_bit_cast(vu32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, (2 * kp) * 256 + ch * 16, 0, 0));
+        vb[r] = __builtin_bit_cast(vu32x4, __builtin_amdgcn_raw_buffer_load_b128(vrs, (2 * kp + 1) * 256 + ch * 16, 0, 0));
+      }
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        *reinterpret_cast<uint32_t*>(Vt + (ch * 8 + i) * SA_VROW + 2 * kp) = (uint32_t)ea[i] | ((uint32_t)eb[i] << 16);
+      for (int r = 0; r < KEYS / 32; ++r) {
+        const int c = tid + r * 256;
+        const int kp = c % (KEYS / 2), ch = c / (KEYS / 2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t a = va[r][i], b = vb[r][i];
+          *reinterpret_cast<uint32_t*>(Vt + (ch * 8 + 2 * i) * SA_VROW + 2 * kp) = (a & 0xFFFFu) | (b << 16);
+          *reinterpret_cast<uint32_t*>(Vt + (ch * 8 + 2 * i + 1) * SA_VROW + 2 * kp) = (a >> 16) | (b & 0xFFFF0000u);
+        }
+      }
     }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's K DMA has landed
     __syncthreads();
 
     // ---- S = Q K^T (C layout: sc[j][k] = S[row 4fq+k][key k0 + 16j + fr])
