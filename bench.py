@@ -61,6 +61,15 @@ def parse(argv=None):
     ap.add_argument("--realtime-step-tokens", type=int, default=0,
                     help="cap a step at this many tokens while a realtime request is in the batch (A/B of "
                          "backend.realtime_step_tokens; 0 = off)")
+    ap.add_argument("--realtime-mode", default="", choices=["", "off", "cap", "micro"],
+                    help="how realtime requests are served (backend.realtime_mode): off = in the serving steps, "
+                         "cap = --realtime-step-tokens, micro = realtime micro-forwards over their own slot pool on "
+                         "their own stream; '' = cap if --realtime-step-tokens > 0 else off")
+    ap.add_argument("--micro-slots", type=int, default=64, help="micro mode: KV slots of the realtime pool")
+    ap.add_argument("--micro-inflight", type=int, default=4, help="micro mode: micro-forwards queued ahead")
+    ap.add_argument("--micro-budget", type=int, default=512, help="micro mode: tokens per micro-forward")
+    ap.add_argument("--micro-stream", default="high", choices=["high", "same"],
+                    help="micro mode: a high-priority HIP stream of their own, or the serving stream")
     ap.add_argument("--gen-tokens", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=2, help="forward steps queued ahead on the GPU")
     ap.add_argument("--aging-ms", default="50,100,150,200",
@@ -326,7 +335,10 @@ def main(argv=None) -> int:
                                fused_head=False if a.no_fused_head else None,
                                fused_resid=False if a.no_fused_resid else None,
                                fused_rms=True if a.fused_rms else None,
-                               prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens)
+                               prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens,
+                               realtime_mode=a.realtime_mode, micro_slots=a.micro_slots,
+                               micro_inflight=a.micro_inflight, micro_budget=a.micro_budget,
+                               micro_stream=a.micro_stream)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -502,6 +514,8 @@ def main(argv=None) -> int:
         r0 = gw.counters["remote_sent"]
         x0 = gw.counters["extra_steps"]
         tok0 = engine.total_tokens
+        fl0, ct0, cn0 = engine.matmul_flops, engine.completed_tokens, engine.completed_total
+        ms0, mg0, mt0 = engine.micro_steps, engine.micro_gpu_ms, engine.micro_timed
         gw.lockstep_stats(reset=True)
         engine.gpu_step_ms, engine.gpu_steps, engine.gpu_step_max_ms = 0.0, 0, 0.0
         engine.time_steps = True
@@ -523,6 +537,8 @@ def main(argv=None) -> int:
         # dispatches the requests still queued at t1; those must not count)
         dispatched_local = gw.counters["dispatched"] - d0
         tokens_local = engine.total_tokens - tok0
+        work_local = [engine.matmul_flops - fl0, engine.completed_tokens - ct0, engine.completed_total - cn0,
+                      engine.micro_steps - ms0, int((engine.micro_gpu_ms - mg0) * 1000), engine.micro_timed - mt0]
         remote_local = gw.counters["remote_sent"] - r0
         extra_local = gw.counters["extra_steps"] - x0
         if tracer is not None:
@@ -541,6 +557,7 @@ def main(argv=None) -> int:
         agg = comm.all_gather_i64(np.array([int(elapsed_local * 1e9), dispatched_local, tokens_local,
                                             arrived_local], dtype=np.int64))
         elapsed = agg[:, 0].max() / 1e9
+        work = comm.all_gather_i64(np.array(work_local, dtype=np.int64)).sum(axis=0)
         lockstep = lockstep_report(gw, engine, comm, elapsed)
         lockstep["ingested_by_rank"] = [int(v) for v in agg[:, 3].tolist()]   # requests each rank preprocessed
         # ... over the whole attempt (steady phase + timed window + drain): the
@@ -583,7 +600,7 @@ def main(argv=None) -> int:
         if a.test_miss_above_util > 0 and util > a.test_miss_above_util:
             met = False                   # test hook: pretend this operating point missed the SLO
         return {"util": util, "rate": rate, "value": value, "elapsed": elapsed, "lat": lat, "lat_done": lat_done,
-                "met": met, "dispatched": dispatched, "tokens": tokens, "arrived": arrived,
+                "met": met, "dispatched": dispatched, "tokens": tokens, "arrived": arrived, "work": work,
                 "remote_in_window": remote_in_window, "lockstep": lockstep, "acct": acct,
                 "host_timed": host_timed, "eng_host": eng_host1 - eng_host0, "breakdown": breakdown}
 
@@ -645,6 +662,12 @@ def main(argv=None) -> int:
         slo["reason"] = (f"no utilisation in {slo['util_tried']} held p99 <= {P99_TARGET_MS} ms (all tiers) and "
                          f"realtime p99 <= {REALTIME_P99_TARGET_MS} ms; value is 0 by construction")
     eh = res["eng_host"]
+    work = res["work"]
+    # what one request is: the tokens a completed request
+    # ran through the backend (prompt + replayed history + generated - 1), and
+    # the window's GEMM FLOP rate against the MI355X dense bf16 peak
+    tok_per_req = float(work[1]) / max(1, int(work[2]))
+    flops_per_s = float(work[0]) / elapsed if elapsed > 0 else 0.0
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -661,6 +684,14 @@ def main(argv=None) -> int:
                 "synthetic (Poisson arrivals, 10/30/40/20 tier mix, random-init weights)",
         "config": {"model": f"{a.model}-stub (32L, random bf16)" if a.model == "llama3-8b" else a.model,
                    "global_batch": a.slots * world, "seq_len": a.max_ctx,
+                   # seq_len above is the KV window per slot (max_ctx), not the
+                   # served request: prompts are <= prompt_cap tokens, see
+                   # "request_shape" at the top level
+                   "seq_len_is": "max_ctx", "max_ctx": a.max_ctx,
+                   "realtime_mode": engine.realtime_mode,
+                   "micro": ({"slots": engine.micro_slots, "inflight": engine.micro_inflight,
+                              "budget": engine.micro_budget, "stream": engine.micro_stream}
+                             if engine.micro else None),
                    "parallelism": f"dp{world}", "ingress": a.ingress, "door_share": a.door_share, "placement": a.lb,
                    "token_budget_by_rank": a.token_budget_by_rank or None,
                    "sim_gpu": a.sim_gpu or None, "extra_steps": not a.no_extra_steps,
@@ -679,6 +710,16 @@ def main(argv=None) -> int:
         # realtime tier, arrival -> LAST generated token (the 8B backend's 4
         # forwards included); the headline's clock is arrival -> dispatch
         "realtime_p99_e2e_ms": round(lat_done["p99_by_tier_ms"][0], 3),
+        "realtime_mode": engine.realtime_mode,
+        "request_shape": {"mean_prompt_tokens": round(tok_per_req - (a.gen_tokens - 1), 2),
+                          "gen_tokens": a.gen_tokens, "tokens_per_request": round(tok_per_req, 2),
+                          "prompt_cap": a.prompt_cap, "max_ctx": a.max_ctx},
+        "backend_matmul_tflops": round(flops_per_s / 1e12, 1),
+        # GEMM FLOP/s over the MI355X dense bf16 peak (2.5 PFLOP/s, no sparsity)
+        "mfma_peak_fraction": round(flops_per_s / 2.5e15, 4),
+        "micro_forwards": ({"count": int(work[3]), "per_s": round(int(work[3]) / elapsed, 1) if elapsed > 0 else 0.0,
+                            "mean_gpu_ms": round(work[4] / 1000.0 / max(1, int(work[5])), 3)}
+                           if engine.micro else None),
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),
         "p99_enqueue_to_dispatch_ms": round(lat["p99_enq_ms"], 3),

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "classify_kernels.h"
 #include "gemm_kernels.h"
@@ -472,6 +473,46 @@ static void kv_move(uintptr_t table, int layers, int slots, int slot, int n, int
   check_launch();
 }
 
+// ---------------------------------------------------------------------- CU partitions
+// Which hardware unit a workgroup ran on: HW_ID (cu / sh / se ids, gfx9
+// layout) and XCC_ID, read from the wave's hardware registers by lane 0.
+// The spin keeps each workgroup resident for a while so a launch of many
+// workgroups spreads over every CU the stream may use.
+__global__ void hw_probe_kernel(uint32_t* out, int spin) {
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = __builtin_amdgcn_s_getreg((4) | (31 << 11));      // HW_REG_HW_ID
+    out[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((20) | (31 << 11));  // HW_REG_XCC_ID
+  }
+  float x = (float)threadIdx.x;
+  for (int i = 0; i < spin; ++i) x = x * 1.0000001f + 1e-7f;
+  if (x == -1.0f) out[0] = 0;                      // (keeps the loop)
+}
+
+static std::vector<uint32_t> hw_probe(int blocks, int spin, uintptr_t stream) {
+  require(blocks > 0 && blocks <= (1 << 20), "hw_probe: bad block count");
+  uint32_t* d = nullptr;
+  HIP_CHECK(hipMalloc(&d, sizeof(uint32_t) * 2 * blocks));
+  hipLaunchKernelGGL(hw_probe_kernel, dim3(blocks), dim3(64), 0, S(stream), d, spin);
+  check_launch();
+  HIP_CHECK(hipStreamSynchronize(S(stream)));
+  std::vector<uint32_t> h(2 * (size_t)blocks);
+  HIP_CHECK(hipMemcpy(h.data(), d, sizeof(uint32_t) * 2 * blocks, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipFree(d));
+  return h;
+}
+
+// A stream whose kernels may only use the CUs set in ``mask`` (32 CUs a
+// word, the runtime's CU numbering): the serving steps and the realtime
+// micro-forwards each get a partition of the chip.
+static uintptr_t stream_with_cu_mask(std::vector<uint32_t> mask) {
+  require(!mask.empty(), "stream_with_cu_mask: empty mask");
+  hipStream_t s = nullptr;
+  HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  return (uintptr_t)s;
+}
+
+static void stream_destroy(uintptr_t s) { HIP_CHECK(hipStreamDestroy(S(s))); }
+
 static py::dict device_info(int dev) {
   hipDeviceProp_t p;
   HIP_CHECK(hipGetDeviceProperties(&p, dev));
@@ -542,6 +583,9 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("unregister_host_page", &unregister_host_page);
   m.def("slot_census", &slot_census);
   m.def("device_info", &device_info);
+  m.def("hw_probe", &hw_probe, py::arg("blocks"), py::arg("spin"), py::arg("stream"));
+  m.def("stream_with_cu_mask", &stream_with_cu_mask);
+  m.def("stream_destroy", &stream_destroy);
   m.def("kv_move", &kv_move, py::arg("table"), py::arg("layers"), py::arg("slots"), py::arg("slot"), py::arg("n"),
         py::arg("max_ctx"), py::arg("hkv"), py::arg("head_dim"), py::arg("buf"), py::arg("pack"), py::arg("stream"),
         py::arg("variant") = (int)KV_LOOP);

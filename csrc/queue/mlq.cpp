@@ -97,6 +97,7 @@ PYBIND11_MODULE(_mlq, m) {
   py::class_<DelayedQueue>(m, "DelayedQueue")
       .def(py::init<>())
       .def("schedule", &DelayedQueue::schedule)
+      .def("remove", &DelayedQueue::remove)
       .def("wait_ready", &DelayedQueue::wait_ready, py::call_guard<py::gil_scoped_release>())
       .def("size", &DelayedQueue::size)
       .def("ready_size", &DelayedQueue::ready_size)

@@ -542,12 +542,31 @@ class DelayedQueue {
     if (th_.joinable()) th_.join();
   }
 
+  // (Re)schedules ``handle``: a handle already waiting is moved to the new
+  // time (its old heap entry turns stale and is skipped when it surfaces).
   void schedule(int64_t handle, int64_t ready_at_ns) {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      heap_.push(Entry{ready_at_ns, seq_++, handle});
+      uint64_t s = seq_++;
+      live_[handle] = s;
+      heap_.push(Entry{ready_at_ns, s, handle});
     }
     cv_.notify_all();
+  }
+
+  // Takes ``handle`` out of the queue, whether still waiting (lazy delete:
+  // its heap entry is dropped when it reaches the top) or already due and
+  // not yet drained.  False if it is not here (never scheduled, delivered).
+  bool remove(int64_t handle) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (live_.erase(handle)) return true;
+    for (auto it = ready_.begin(); it != ready_.end(); ++it) {
+      if (*it == handle) {
+        ready_.erase(it);
+        return true;
+      }
+    }
+    return false;
   }
 
   // blocks up to timeout_s for ready items; returns up to max_n handles
@@ -567,7 +586,7 @@ class DelayedQueue {
 
   int64_t size() {
     std::lock_guard<std::mutex> lk(mu_);
-    return (int64_t)heap_.size();
+    return (int64_t)live_.size();
   }
   int64_t ready_size() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -577,6 +596,7 @@ class DelayedQueue {
   // (ok, handle, ready_at_ns)
   std::tuple<bool, int64_t, int64_t> peek() {
     std::lock_guard<std::mutex> lk(mu_);
+    drop_stale();
     if (heap_.empty()) return {false, 0, 0};
     return {true, heap_.top().handle, heap_.top().ready_at};
   }
@@ -585,9 +605,12 @@ class DelayedQueue {
     std::lock_guard<std::mutex> lk(mu_);
     std::vector<int64_t> out;
     while (!heap_.empty()) {
-      out.push_back(heap_.top().handle);
+      const Entry& e = heap_.top();
+      auto it = live_.find(e.handle);
+      if (it != live_.end() && it->second == e.seq) out.push_back(e.handle);
       heap_.pop();
     }
+    live_.clear();
     return out;
   }
 
@@ -611,10 +634,17 @@ class DelayedQueue {
       int64_t now = mono_ns();
       const int64_t tol = 1000000;  // 1 ms early-fire tolerance
       bool moved = false;
+      drop_stale();
       while (!heap_.empty() && heap_.top().ready_at < now + tol) {
-        ready_.push_back(heap_.top().handle);
+        const Entry e = heap_.top();
         heap_.pop();
-        moved = true;
+        auto it = live_.find(e.handle);
+        if (it != live_.end() && it->second == e.seq) {   // (else removed / rescheduled: stale)
+          live_.erase(it);
+          ready_.push_back(e.handle);
+          moved = true;
+        }
+        drop_stale();
       }
       if (moved) ready_cv_.notify_all();
       if (heap_.empty()) continue;
@@ -623,9 +653,20 @@ class DelayedQueue {
     }
   }
 
+  // pops heap tops that no longer name a waiting item (caller holds mu_)
+  void drop_stale() {
+    while (!heap_.empty()) {
+      const Entry& e = heap_.top();
+      auto it = live_.find(e.handle);
+      if (it != live_.end() && it->second == e.seq) return;
+      heap_.pop();
+    }
+  }
+
   std::mutex mu_;
   std::condition_variable cv_, ready_cv_;
   std::priority_queue<Entry, std::vector<Entry>, std::greater<Entry>> heap_;
+  std::unordered_map<int64_t, uint64_t> live_;   // waiting handle -> its current heap entry's seq
   std::deque<int64_t> ready_;
   uint64_t seq_ = 0;
   bool stop_;

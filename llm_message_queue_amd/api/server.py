@@ -310,10 +310,15 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None,
                 return {"status": "deleted", "message_id": mid, "dequeued": bool(res.get("dequeued")),
                         "cancelled": bool(res.get("cancelled"))}
             return _err(404, "Message not found")
+        # everywhere else in its lifecycle (inbox, preprocess, retry backoff,
+        # held for its KV, a GPU slot here or on another rank): cancelled
+        # through the gateway's request table -- after this 200 it is never
+        # dispatched or completed again
         removed = m.queue_name and G.standard.has_queue(m.queue_name) and G.standard.remove_message(m.queue_name, m)
-        cancelled = "" if removed else (G.cancel_inflight(m) if hasattr(G, "cancel_inflight") else "")
+        res = "" if removed else (G.cancel_inflight(m) if hasattr(G, "cancel_inflight") else "")
         G.messages.remove(mid)
-        return {"status": "deleted", "message_id": mid, "dequeued": bool(removed), "cancelled": bool(cancelled)}
+        return {"status": "deleted", "message_id": mid, "dequeued": bool(removed) or res == "dequeued",
+                "cancelled": res in ("cancelled", "forwarded", "pending")}
 
     # ------------------------------------------------------------------ conversations
     @app.post("/api/v1/conversations")
@@ -595,8 +600,6 @@ def create_app(gw_app, allowed_origins: Optional[List[str]] = None,
             if G.dead_letters("remove", mid) is not True:
                 return _err(404, "Message not found")
             return {"status": "removed", "message_id": mid}
-        if queue_type == "delayed":
-            return _err(404, "Message not found")
         if not G.dequeue(queue_type, mid):
             return _err(404, "Message not found")
         return {"status": "removed", "message_id": mid}

@@ -58,8 +58,16 @@ class Request:
     conv: int = -1                # conversation key: its KV stays resident in the slot between turns
     reused: int = 0               # context tokens served from the resident KV (not re-prefilled)
     history: Optional[np.ndarray] = None   # earlier dialog tokens, prefilled only if not resident
+    # compressed context of an evicted window (N5 salient tokens), prepended
+    # to a non-resident replay ahead of ``history``; never part of a resident KV
+    prefix: Optional[np.ndarray] = None
     timeout_ns: int = 0           # processing timeout of this attempt (0: none); the deadline starts at admission
     deadline_ns: int = 0          # admitted_ns + timeout_ns (monotonic), set by ``admit``
+    micro: bool = False           # served by the realtime micro-forwards (``realtime_mode="micro"``)
+    aborted: bool = False         # this attempt was aborted (timeout / cancel / evacuation)
+    # the greedy token ids this attempt generated, read back from the device
+    # with the step that sampled them (set when the request completes)
+    out_tokens: Optional[np.ndarray] = None
 
 
 @dataclass
@@ -70,6 +78,14 @@ class StepResult:
     completed: List[Request]
     first_tokens: List[Request]
     elapsed_ms: float
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 class BackendHung(Exception):
@@ -94,6 +110,10 @@ class _Inflight:
     out: object                   # device tensor of sampled tokens (kept alive for the next gather)
     t0_ns: int = 0                # monotonic launch time (tracing)
     ev_start: object = None       # timing event before the forward (``time_steps``)
+    micro: bool = False           # a realtime micro-forward (``_qm``), not a serving step
+    samp_slots: object = None     # int64 [S]: the slot each sampled row belongs to
+    gidx: object = None           # int64 [S]: which generated token of its request each row is
+    host_out: object = None       # pinned int32 [>= S]: the sampled ids, copied back behind the forward
 
 
 class BackendEngine:
@@ -102,7 +122,9 @@ class BackendEngine:
                  page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True,
                  split_qkv: bool = False, fused_mlp=None, fused_qkv=None, row_scale_norm: bool = True,
                  fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
-                 realtime_step_tokens: int = 0, fused_rms=None):
+                 realtime_step_tokens: int = 0, fused_rms=None, realtime_mode: str = "",
+                 micro_slots: int = 64, micro_budget: int = 512, micro_inflight: int = 4,
+                 micro_stream: str = "high"):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
         self.step_timeout_s = float(step_timeout_s)
@@ -111,17 +133,46 @@ class BackendEngine:
         # every generating slot gets its decode token each step (the on-device
         # token gather reads the previous step's output only)
         self.token_budget = max(token_budget, slots)
-        # realtime step cap (``backend.realtime_step_tokens``, 0 = off): while
-        # a realtime-lane request (tier < fast_tiers) is in the batch, a step
-        # carries at most this many tokens (never fewer than its decode rows),
-        # so the 4 forwards a realtime request needs finish sooner -- at the
-        # price of the smaller steps' GEMM efficiency for everyone in them
-        # (measured: profiles/r5_step_budget_sweep_1gpu.jsonl)
+        # How realtime requests (tier < fast_tiers) are served
+        # (``backend.realtime_mode``; docs/performance.md "Realtime modes"):
+        #   "off"   -- in the serving steps like everyone else (prefilled first);
+        #   "cap"   -- the step cap (``backend.realtime_step_tokens``): while a
+        #              realtime request is in the batch a step carries at most
+        #              that many tokens (never fewer than its decode rows), so
+        #              its 4 forwards finish sooner -- at the price of the
+        #              smaller steps' GEMM efficiency for everyone in them
+        #              (profiles/r5_step_budget_sweep_1gpu.jsonl);
+        #   "micro" -- realtime micro-forwards: realtime requests take slots of
+        #              a separate pool (``micro_slots``) that only small
+        #              forwards over those slots touch, launched back to back
+        #              on their own stream (``micro_stream``: "high" = a
+        #              high-priority HIP stream next to the serving stream,
+        #              "same" = the serving stream) while the big steps run.
+        # An empty mode follows ``realtime_step_tokens`` (> 0: "cap").
         self.rt_step_tokens = int(realtime_step_tokens)
+        mode = realtime_mode or ("cap" if self.rt_step_tokens > 0 else "off")
+        if mode not in ("off", "cap", "micro"):
+            raise ValueError(f"realtime_mode must be off / cap / micro, not {mode!r}")
+        if mode != "cap":
+            self.rt_step_tokens = 0
+        self.realtime_mode = mode
+        self.micro = mode == "micro"
+        self.micro_slots = int(micro_slots) if self.micro else 0
+        if self.micro and self.micro_slots < 1:
+            raise ValueError("realtime_mode micro needs micro_slots >= 1")
+        self.micro_budget = max(int(micro_budget), self.micro_slots + 1)
+        self.micro_inflight = max(1, int(micro_inflight))
+        self.n_all = slots + self.micro_slots             # KV slots: serving pool, then the micro pool
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.async_device = self.cuda          # forwards run asynchronously (a GPU stream)
-        self.model = LlamaStub(model_cfg, slots, max_ctx, device=self.device, impl=impl, seed=seed,
+        self.rt_stream = None
+        if self.micro and self.cuda and micro_stream == "high":
+            self.rt_stream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
+        elif self.micro and micro_stream not in ("high", "same"):
+            raise ValueError(f"micro_stream must be high / same, not {micro_stream!r}")
+        self.micro_stream = micro_stream if self.micro else ""
+        self.model = LlamaStub(model_cfg, self.n_all, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
                                fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
                                fused_resid=fused_resid, fused_rms=fused_rms, prune_last=prune_last)
@@ -129,6 +180,11 @@ class BackendEngine:
         self.weight_bytes = self.model.weight_bytes()
         self.active: Dict[int, Request] = {}            # slot -> request
         self.free: List[int] = list(range(slots - 1, -1, -1))
+        # the realtime micro pool: slots [slots, n_all), never in ``free`` /
+        # ``conv_lru``, so no serving step ever reads or writes their KV rows
+        # (the two streams never share a slot)
+        self.free_micro: List[int] = list(range(self.n_all - 1, slots - 1, -1))
+        n_all = self.n_all
         # Conversation KV residency (BASELINE config 4): when a request of a
         # conversation completes, its slot keeps the KV of the dialog so far
         # (prompt + generated tokens except the last) and parks in an LRU;
@@ -136,29 +192,36 @@ class BackendEngine:
         # prefills its new tokens.  Parked slots count as free: they are
         # evicted (LRU) when no truly free slot is left.
         self.conv_lru: "collections.OrderedDict[int, int]" = collections.OrderedDict()
-        self.s_conv = np.full(slots, -1, dtype=np.int64)
-        self.s_cached = np.zeros(slots, dtype=np.int64)
+        self.s_conv = np.full(n_all, -1, dtype=np.int64)
+        self.s_cached = np.zeros(n_all, dtype=np.int64)
         self.kv_reused_tokens = 0
         self.kv_evictions = 0
         self.kv_imported = 0
         self.kv_stale = 0                                   # parked copies found outdated at admission
         self._importing: Dict[int, int] = {}                # slot -> conv: KV arriving (migration in flight)
         # per-slot host state (the batch builder is vectorised over these)
-        self.s_prompt = np.zeros((slots, max_ctx), dtype=np.int32)
-        self.s_plen = np.zeros(slots, dtype=np.int64)
-        self.s_pref = np.zeros(slots, dtype=np.int64)       # prompt tokens prefilled
-        self.s_gen = np.zeros(slots, dtype=np.int64)        # tokens generated
-        self.s_gmax = np.zeros(slots, dtype=np.int64)       # tokens to generate
-        self.s_seq = np.zeros(slots, dtype=np.int64)        # admission order
-        self.s_out_idx = np.zeros(slots, dtype=np.int64)    # row of my last token in the step output
-        self.s_out_step = np.full(slots, -2, dtype=np.int64)
-        self.s_active = np.zeros(slots, dtype=bool)
-        self.s_tier = np.zeros(slots, dtype=np.int64)
+        self.s_prompt = np.zeros((n_all, max_ctx), dtype=np.int32)
+        self.s_plen = np.zeros(n_all, dtype=np.int64)
+        self.s_pref = np.zeros(n_all, dtype=np.int64)       # prompt tokens prefilled
+        self.s_gen = np.zeros(n_all, dtype=np.int64)        # tokens generated
+        self.s_gmax = np.zeros(n_all, dtype=np.int64)       # tokens to generate
+        self.s_seq = np.zeros(n_all, dtype=np.int64)        # admission order
+        self.s_out_idx = np.zeros(n_all, dtype=np.int64)    # row of my last token in the step output
+        self.s_out_step = np.full(n_all, -2, dtype=np.int64)
+        self.s_active = np.zeros(n_all, dtype=bool)
+        self.s_tier = np.zeros(n_all, dtype=np.int64)
+        self.s_micro = np.zeros(n_all, dtype=bool)
+        self.s_micro[slots:] = True
+        # host copy of every generated token id, per slot (written when the
+        # step that sampled it is reaped; steps of one pool are reaped in
+        # launch order, so a slot's next request never overwrites a row
+        # before the previous one's completion copied it out)
+        self.h_tokens = np.zeros((n_all, max_ctx), dtype=np.int32)
         # processing deadline per slot (monotonic ns, 0 = none): a request
         # still running past it is aborted by ``expire`` (the reference runs
         # every message under context.WithTimeout(msg.Timeout),
         # `internal/priorityqueue/worker.go:162-188`)
-        self.s_deadline = np.zeros(slots, dtype=np.int64)
+        self.s_deadline = np.zeros(n_all, dtype=np.int64)
         self.expired_total = 0
         self.cancelled_total = 0
         self._admit_seq = 0
@@ -176,14 +239,32 @@ class BackendEngine:
         self.total_tokens = 0
         self.completed_total = 0
         self.completed_tokens = 0
+        self.matmul_flops = 0                            # GEMM FLOPs of every launched forward (``_step_flops``)
         self._q: Deque[_Inflight] = collections.deque()
         self._reaped: List[_Inflight] = []               # reaped by launch(), not yet returned
         self._fence: List[object] = []                   # events of steps dropped by abort_all
         self.host_ns = np.zeros(3, dtype=np.int64)       # [batch build, wait for GPU, enqueue forward] host time
         self._prev_out = None                            # device int32 [n_samples] of the last launched step
-        # double-buffered pinned staging (a buffer is reused only after the
-        # step that read it has finished: <= 2 steps in flight)
-        self._pins = [self._alloc_pin(4 * (7 * self.token_budget + 2 * slots + 64)) for _ in range(2)]
+        # pinned staging rings (a buffer is reused only after the step that
+        # read it has finished: launch keeps <= max_inflight steps queued, so
+        # step k reuses step k - ring's buffer only once that one was reaped)
+        ring = max(2, self.max_inflight)
+        self._pins = [self._alloc_pin(4 * (7 * self.token_budget + 2 * slots + 64)) for _ in range(ring)]
+        # sampled token ids copied back behind each forward (read at reap)
+        self._out_pins = [self._alloc_pin(4 * self.n_all).view(torch.int32) for _ in range(ring)]
+        # realtime micro-forwards: their own queue, staging, token gather source
+        self._qm: Deque[_Inflight] = collections.deque()
+        self._reaped_m: List[_Inflight] = []
+        self._prev_out_m = None
+        self.micro_id = 0
+        self.micro_steps = 0
+        self.micro_gpu_ms = 0.0                          # device time of timed micro-forwards (``time_steps``)
+        self.micro_timed = 0
+        if self.micro:
+            mr = self.micro_inflight + 1
+            self._pins_m = [self._alloc_pin(4 * (7 * self.micro_budget + 2 * self.micro_slots + 64))
+                            for _ in range(mr)]
+            self._out_pins_m = [self._alloc_pin(4 * self.micro_slots).view(torch.int32) for _ in range(mr)]
         # segment-tiled MFMA attention on the HIP path (per-token otherwise)
         self.use_tiles = impl == "hip"
         self._state_pins = [self._alloc_pin(4 * slots) for _ in range(2)]
@@ -216,7 +297,11 @@ class BackendEngine:
         return len(self.free) + len(self.conv_lru)
 
     def inflight(self) -> int:
-        return self.slots - self.free_slots()
+        """Requests holding a slot (serving pool + realtime micro pool)."""
+        return self.slots - self.free_slots() + self.micro_slots - len(self.free_micro)
+
+    def _big_active(self) -> np.ndarray:
+        return self.s_active & ~self.s_micro if self.micro else self.s_active
 
     def _take_slot(self) -> int:
         if self.free:
@@ -241,7 +326,7 @@ class BackendEngine:
         free = len(self.free) + len(self.conv_lru)
         if free == 0:
             return 0
-        act = self.s_active
+        act = self._big_active()
         pending = int((self.s_plen[act] - self.s_pref[act]).sum())
         head = self.step_budget() - int(act.sum()) - pending
         if head <= 0:
@@ -329,7 +414,7 @@ class BackendEngine:
     def ready_tokens(self) -> int:
         """Tokens the next launch would run right now: one per decoding slot
         plus the pending prefill, capped at the token budget."""
-        act = self.s_active
+        act = self._big_active()
         if not act.any():
             return 0
         plen, pref = self.s_plen[act], self.s_pref[act]
@@ -350,16 +435,27 @@ class BackendEngine:
 
     def lane_capacity(self) -> int:
         """Slots a realtime request may take beyond ``admit_capacity``: every
-        free (or parked) slot.  Its prefill goes first in the next step, so
-        it starts computing there instead of waiting for headroom."""
-        return len(self.free) + len(self.conv_lru)
+        free (or parked) slot, plus the free micro-pool slots.  Its prefill
+        goes first in the next step (or into the next micro-forward), so it
+        starts computing there instead of waiting for headroom."""
+        return len(self.free) + len(self.conv_lru) + len(self.free_micro)
+
+    def _to_micro(self, r: Request) -> bool:
+        """Serve ``r`` on the micro pool: a realtime request, a free micro
+        slot, and no resident KV of its dialog in the serving pool (a
+        resident turn stays where its context is)."""
+        return (self.micro and 0 <= r.tier < self.fast_tiers and bool(self.free_micro)
+                and not (r.conv >= 0 and r.conv in self.conv_lru))
 
     def admit(self, reqs: Sequence[Request]) -> List[Request]:
         now = time.monotonic_ns()
         out = []
         cap = self.max_ctx - 1
         for r in reqs:
-            if not self.free and not self.conv_lru:
+            micro = self._to_micro(r)
+            if not micro and not self.free and not self.conv_lru:
+                if self.micro:
+                    continue                                  # (a later realtime request may still fit)
                 break
             if r.gen_tokens < 1:
                 r.gen_tokens = 1
@@ -367,9 +463,16 @@ class BackendEngine:
             r.prompt = np.asarray(r.prompt[:plen], dtype=np.int64) % self.cfg.vocab
             if len(r.prompt) == 0:
                 r.prompt = np.zeros(1, dtype=np.int64)
+            r.micro = micro
+            r.aborted = False
+            r.out_tokens = None
             base = 0
-            s = self.conv_lru.pop(r.conv, None) if r.conv >= 0 else None
-            if s is not None:
+            s = self.conv_lru.pop(r.conv, None) if (r.conv >= 0 and not micro) else None
+            if micro:
+                # a micro-pool slot keeps no dialog KV: the turn replays its
+                # history (``r.history``) and nothing is parked afterwards
+                s = self.free_micro.pop()
+            elif s is not None:
                 base = int(self.s_cached[s])
                 if r.history is not None and base < len(r.history):
                     # a stale copy: this GPU served an earlier turn, later turns
@@ -380,12 +483,17 @@ class BackendEngine:
                     base = 0                                  # context window full: restart the dialog KV
             else:
                 s = self._take_slot()
-            if base == 0 and r.history is not None and len(r.history):
-                # not resident here: replay the dialog (most recent tokens that fit)
+            if base == 0 and ((r.history is not None and len(r.history)) or (r.prefix is not None and len(r.prefix))):
+                # not resident here: replay the dialog -- its compressed
+                # context (if a window was evicted), then the most recent
+                # history tokens that fit
                 room = cap + 1 - r.gen_tokens - len(r.prompt)
                 if room > 0:
-                    h = np.asarray(r.history[-room:], dtype=np.int64) % self.cfg.vocab
-                    r.prompt = np.concatenate([h, r.prompt])
+                    pre = np.asarray(r.prefix if r.prefix is not None else (), dtype=np.int64)[:room // 4]
+                    hist = np.asarray(r.history if r.history is not None else (), dtype=np.int64)
+                    keep = room - len(pre)
+                    h = hist[len(hist) - keep:] if 0 < keep < len(hist) else (hist if keep > 0 else hist[:0])
+                    r.prompt = np.concatenate([pre % self.cfg.vocab, h % self.cfg.vocab, r.prompt])
             r.slot = s
             r.reused = base
             r.prefilled = 0
@@ -406,9 +514,10 @@ class BackendEngine:
             self._admit_seq += 1
             self.s_active[s] = True
             self.s_tier[s] = r.tier
-            self.s_conv[s] = r.conv
+            self.s_conv[s] = -1 if micro else r.conv
             self.kv_reused_tokens += base
-            self._mean_plen += 0.01 * (n - self._mean_plen)
+            if not micro:                                     # (the serving steps' headroom estimate)
+                self._mean_plen += 0.01 * (n - self._mean_plen)
             out.append(r)
         return out
 
@@ -430,7 +539,11 @@ class BackendEngine:
             self.s_deadline[s] = 0
             self.s_conv[s] = -1
             self.s_cached[s] = 0
-            self.free.append(s)                # reused first (``_take_slot`` pops from the end)
+            # reused first (``_take_slot`` pops from the end)
+            (self.free_micro if self.s_micro[s] else self.free).append(s)
+            # steps still queued on the GPU list it among their first tokens:
+            # their reap must not stamp an attempt that no longer exists
+            r.aborted = True
             out.append(r)
         return out
 
@@ -462,23 +575,29 @@ class BackendEngine:
         return out
 
     # ------------------------------------------------------------------ step
-    def _build(self):
-        """Vectorised batch construction over the per-slot state arrays:
-        decode rows first (one token per generating slot, ids gathered on the
-        device from the previous step's output), then chunked prefill in
-        admission order up to the token budget.  Returns int32 arrays."""
-        act = np.flatnonzero(self.s_active)
+    def _build(self, micro: bool = False):
+        """Vectorised batch construction over the per-slot state arrays of
+        one pool (the serving slots, or with ``micro`` the realtime micro
+        pool): decode rows first (one token per generating slot, ids gathered
+        on the device from the pool's previous step output), then chunked
+        prefill in admission order up to the step's token budget.  Returns
+        int32 arrays."""
+        if self.micro:
+            act = np.flatnonzero(self.s_active & (self.s_micro if micro else ~self.s_micro))
+        else:
+            act = np.flatnonzero(self.s_active)
         plen, pref = self.s_plen[act], self.s_pref[act]
         is_dec = pref >= plen
         dec = act[is_dec]
         D = len(dec)
-        if D and (self.s_out_step[dec] != self.step_id - 1).any():
+        prev = (self.micro_id if micro else self.step_id) - 1
+        if D and (self.s_out_step[dec] != prev).any():
             raise RuntimeError("decode token source is not the previous step")
         pre = act[~is_dec]
         if len(pre):
             pre = pre[np.argsort(self.s_seq[pre], kind="stable")]
         rem = self.s_plen[pre] - self.s_pref[pre]
-        budget = self.step_budget() - D
+        budget = (self.micro_budget if micro else self.step_budget()) - D
         before = np.cumsum(rem) - rem
         take = np.clip(budget - before, 0, rem)
         keep = take > 0
@@ -539,7 +658,7 @@ class BackendEngine:
         free slots; nothing it writes is ever read by a request)."""
         if not self.cuda:
             return 0
-        if self.active or self.conv_lru or self._q:
+        if self.active or self.conv_lru or self._q or self._qm:
             raise RuntimeError("warm_shapes needs an idle engine")
         if sizes is None:
             ladder, t = [], 48
@@ -569,6 +688,23 @@ class BackendEngine:
                 t = max(t + 1, t * 9 // 8)
                 tail.append(min(t, self.token_budget))
             n += self.model.warm_tail(tail)
+        if self.rt_stream is not None:
+            # the micro-forwards' stream: its per-stream GEMM workspaces and
+            # first launches there, on the micro pool's own slots
+            torch.cuda.synchronize(dev)
+            with torch.cuda.stream(self.rt_stream):
+                T = 1
+                while T <= self.micro_budget:
+                    r = torch.arange(T, device=dev, dtype=torch.int32)
+                    slot = (self.slots + r % self.micro_slots).to(torch.int32)
+                    pos = (r // self.micro_slots).to(torch.int32)
+                    tiles = torch.stack([r, torch.ones_like(r), slot, pos], 1).contiguous() \
+                        if self.use_tiles else None
+                    samp = torch.arange(min(T, self.micro_slots), device=dev, dtype=torch.long)
+                    self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(),
+                                       slot.contiguous(), samp, tiles=tiles, n_dec=0)
+                    n += 1
+                    T *= 2
         torch.cuda.synchronize(dev)
         self.warmed_shapes = n
         return n
@@ -596,16 +732,22 @@ class BackendEngine:
         them.  Steps not yet reaped by ``finish`` count as unfinished (their
         completions were never reported): at-least-once.  Makes no GPU call,
         so it is safe after a device error; reap first if the GPU is fine."""
-        out = [r for f in list(self._q) + self._reaped for r in f.completed]
+        steps = list(self._q) + self._reaped + list(self._qm) + self._reaped_m
+        out = [r for f in steps for r in f.completed]
         out += list(self.active.values())
+        for r in out:
+            r.aborted = True
         # steps still queued on the GPU keep reading their pinned staging
         # buffers (the async H2D copy may not have run yet): the next launch
         # must not refill a buffer before they finish, so their events stay
         # as a fence (waited in launch; a dead device raises there instead)
-        self._fence.extend(f.event for f in self._q if f.event is not None)
+        self._fence.extend(f.event for f in list(self._q) + list(self._qm) if f.event is not None)
         self._q.clear()
         self._reaped = []
         self._prev_out = None
+        self._qm.clear()
+        self._reaped_m = []
+        self._prev_out_m = None
         self.active.clear()
         self.s_active[:] = False
         self.s_deadline[:] = 0
@@ -613,6 +755,7 @@ class BackendEngine:
         self._importing.clear()
         self.s_conv[:] = -1
         self.free = list(range(self.slots - 1, -1, -1))
+        self.free_micro = list(range(self.n_all - 1, self.slots - 1, -1))
         return out
 
     def launch(self, wait_cb=None) -> None:
@@ -643,17 +786,25 @@ class BackendEngine:
             if f is not None:
                 self._reaped.append(f)
                 continue
+            if self.micro:
+                self.pump_micro()                      # realtime micro-forwards keep flowing meanwhile
             if not wait_cb():
                 time.sleep(0.0002)
+        self.host_ns[1] += time.perf_counter_ns() - ts
+        self._launch_pool(False)
+
+    def _launch_pool(self, micro: bool) -> bool:
+        """Build one pool's next token batch and enqueue its forward: the
+        serving step, or (``micro``) a realtime micro-forward on the micro
+        stream.  False if the pool had no token to run."""
         t0 = time.perf_counter()
         tb = time.perf_counter_ns()
         t_mono = time.monotonic_ns()
-        self.host_ns[1] += tb - ts
-        toks, pos, slot, samp, samp_slots, dec_rows, dec_src, tiles, n_pre, n_dec = self._build()
+        toks, pos, slot, samp, samp_slots, dec_rows, dec_src, tiles, n_pre, n_dec = self._build(micro)
         self.host_ns[0] += time.perf_counter_ns() - tb
         T = len(toks)
         if T == 0:
-            return
+            return False
         dev = self.device
         S, D, NT = len(samp), len(dec_rows), len(tiles)
         o_dec = 3 * T + S
@@ -667,30 +818,43 @@ class BackendEngine:
         buf[o_dec + D:o_til] = dec_src
         buf[o_til:] = tiles.reshape(-1)
         nbytes = buf.nbytes
-        pin = self._pins[self.step_id % 2]
+        sid = self.micro_id if micro else self.step_id
+        pins, outs = (self._pins_m, self._out_pins_m) if micro else (self._pins, self._out_pins)
+        k = sid % len(pins)
+        pin = pins[k]
         if pin.numel() < nbytes:
-            pin = self._pins[self.step_id % 2] = self._alloc_pin(2 * nbytes)
+            pin = pins[k] = self._alloc_pin(2 * nbytes)
         pin.numpy()[:nbytes] = buf.view(np.uint8)
-        d = pin[:nbytes].to(dev, non_blocking=True).view(torch.int32)
-        tok_d = d[:T].long()
-        if D:
-            if self._prev_out is None:
-                raise RuntimeError("decode token without a previous step output")
-            rows = d[o_dec:o_dec + D].long()
-            src = d[o_dec + D:o_til].long()
-            tok_d.index_copy_(0, rows, self._prev_out.index_select(0, src).long())
-        til = d[o_til:].view(NT, 4) if self.use_tiles else None
-        ev0 = self._start_event()
-        te = time.perf_counter_ns()
-        out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til, n_dec=D)
-        self.host_ns[2] += time.perf_counter_ns() - te
-        self._census(T)
-        ev = self._end_event(T, ev0 is not None)
+        host_out = outs[k]
+        prev = self._prev_out_m if micro else self._prev_out
+        stream = self.rt_stream if micro else None
+        ctx = torch.cuda.stream(stream) if stream is not None else _NullCtx()
+        with ctx:
+            d = pin[:nbytes].to(dev, non_blocking=True).view(torch.int32)
+            tok_d = d[:T].long()
+            if D:
+                if prev is None:
+                    raise RuntimeError("decode token without a previous step output")
+                rows = d[o_dec:o_dec + D].long()
+                src = d[o_dec + D:o_til].long()
+                tok_d.index_copy_(0, rows, prev.index_select(0, src).long())
+            til = d[o_til:].view(NT, 4) if self.use_tiles else None
+            ev0 = self._start_event()
+            te = time.perf_counter_ns()
+            out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til,
+                                     n_dec=D)
+            self.host_ns[2] += time.perf_counter_ns() - te
+            if not micro:
+                self._census(T)
+            # the sampled ids come back behind the forward (read at reap)
+            host_out[:S].copy_(out, non_blocking=True)
+            ev = self._end_event(T, ev0 is not None)
         # deterministic bookkeeping: every sampled slot gets one token
         ss = samp_slots
+        gidx = self.s_gen[ss].copy()
         self.s_gen[ss] += 1
         self.s_out_idx[ss] = np.arange(len(ss))
-        self.s_out_step[ss] = self.step_id
+        self.s_out_step[ss] = sid
         g = self.s_gen[ss]
         firsts = [self.active[int(x)] for x in ss[g == 1]]
         done = ss[g >= self.s_gmax[ss]]
@@ -700,7 +864,10 @@ class BackendEngine:
             r.prefilled = int(self.s_plen[x]) - r.reused
             r.generated = int(self.s_gen[x])
             completed.append(r)
-            if r.conv >= 0:
+            if micro:
+                self.s_conv[x] = -1
+                self.free_micro.append(x)
+            elif r.conv >= 0:
                 # park the dialog KV: every position but the last sampled token
                 self.s_cached[x] = self.s_plen[x] + self.s_gen[x] - 1
                 old = self.conv_lru.pop(r.conv, None)
@@ -712,12 +879,71 @@ class BackendEngine:
                 self.s_conv[x] = -1
                 self.free.append(x)
         self.s_active[done] = False
-        self._prev_out = out
-        self._q.append(_Inflight(self.step_id, ev, T, n_pre, n_dec, completed, firsts, t0, out, t_mono, ev0))
-        self.step_id += 1
+        f = _Inflight(sid, ev, T, n_pre, n_dec, completed, firsts, t0, out, t_mono, ev0, micro=micro,
+                      samp_slots=ss, gidx=gidx, host_out=host_out)
+        if micro:
+            self._prev_out_m = out
+            self._qm.append(f)
+            self.micro_id += 1
+            self.micro_steps += 1
+        else:
+            self._prev_out = out
+            self._q.append(f)
+            self.step_id += 1
         self.total_tokens += T
+        self.matmul_flops += self._step_flops(T, S)
         self.completed_total += len(completed)
         self.completed_tokens += sum(len(r.prompt) + r.gen_tokens - 1 for r in completed)
+        return True
+
+    def _step_flops(self, T: int, S: int) -> int:
+        """Matrix-multiply FLOPs of one forward of ``T`` tokens sampling ``S``
+        rows: every layer's qkv / o / gate-up / down over every row (the last
+        layer's o + MLP over the sampled rows only, with ``prune_last``) and
+        the LM head over the sampled rows.  Attention (<= max_ctx keys per
+        row, ~0.2 % at the serving shape) is not counted."""
+        c = self.cfg
+        d, hd = c.dim, c.head_dim
+        qkv = d * (c.heads + 2 * c.kv_heads) * hd
+        rest = c.heads * hd * d + 3 * d * c.ffn                 # o + gate/up + down
+        last = S if getattr(self.model, "prune_last", False) else T
+        return 2 * (T * (c.layers * qkv + (c.layers - 1) * rest) + last * rest + S * c.vocab * d)
+
+    # ------------------------------------------------------------------ realtime micro-forwards
+    def micro_pending(self) -> bool:
+        """A micro-pool request still has tokens no launched micro-forward
+        computes (prefill left, or generation not yet launched to the end)."""
+        if not self.micro or len(self.free_micro) == self.micro_slots:
+            return False
+        act = self.s_active & self.s_micro
+        return bool(act.any())
+
+    def pump_micro(self) -> int:
+        """Reap finished micro-forwards (their results go to the next
+        ``finish`` / ``finish_micro``) and launch the next ones while the
+        micro pool has work and fewer than ``micro_inflight`` are queued.
+        Bookkeeping is deterministic (greedy decode always yields a token),
+        so a realtime request's whole prefill + decode chain can be queued
+        at once: each micro-forward gathers its decode ids on the device from
+        the previous one.  Returns the number launched."""
+        if not self.micro:
+            return 0
+        while self._qm:
+            f = self._reap(block=False, micro=True)
+            if f is None:
+                break
+            self._reaped_m.append(f)
+        n = 0
+        while len(self._qm) < self.micro_inflight and self.micro_pending():
+            if not self._launch_pool(True):
+                break
+            n += 1
+        return n
+
+    def finish_micro(self) -> StepResult:
+        """Results of the micro-forwards reaped so far (non-blocking)."""
+        done, self._reaped_m = self._reaped_m, []
+        return self._result(done)
 
     def _start_event(self):
         """Timing event before a forward (``time_steps``), or None."""
@@ -742,10 +968,11 @@ class BackendEngine:
             raise BackendHung(f"forward step {f.step} ({f.T} tokens) incomplete "
                               f"{(time.monotonic_ns() - f.t0_ns) / 1e9:.1f} s after launch")
 
-    def _reap(self, block: bool) -> Optional[_Inflight]:
-        if not self._q:
+    def _reap(self, block: bool, micro: bool = False) -> Optional[_Inflight]:
+        q = self._qm if micro else self._q
+        if not q:
             return None
-        f = self._q[0]
+        f = q[0]
         if f.event is not None:
             if block:
                 if self.step_timeout_s > 0:
@@ -757,39 +984,60 @@ class BackendEngine:
             elif not f.event.query():
                 self._check_hung(f)
                 return None
-        self._q.popleft()
+        q.popleft()
         now = time.monotonic_ns()
         if f.ev_start is not None:
             ms = f.ev_start.elapsed_time(f.event)
-            self.gpu_step_ms += ms
-            self.gpu_steps += 1
-            self.gpu_step_max_ms = max(self.gpu_step_max_ms, ms)
+            if micro:
+                self.micro_gpu_ms += ms
+                self.micro_timed += 1
+            else:
+                self.gpu_step_ms += ms
+                self.gpu_steps += 1
+                self.gpu_step_max_ms = max(self.gpu_step_max_ms, ms)
         if self.tracer is not None:
             self.tracer.step(f.step, f.t0_ns, now, f.T)
+        if f.host_out is not None and f.samp_slots is not None and len(f.samp_slots):
+            # the step's sampled ids (valid now: the copy ran before its event)
+            ss = f.samp_slots
+            ok = f.gidx < self.max_ctx
+            self.h_tokens[ss[ok], f.gidx[ok]] = f.host_out.numpy()[:len(ss)][ok]
         for r in f.firsts:
-            r.first_token_ns = now
+            if not r.aborted:
+                r.first_token_ns = now
         for r in f.completed:
             r.done_ns = now
-        if self.page is not None and not self.cuda and not self.fault.get("drop_heartbeat"):
+            r.out_tokens = self.h_tokens[r.slot, :min(r.generated, self.max_ctx)].copy()
+        if self.page is not None and not self.cuda and not self.fault.get("drop_heartbeat") and not micro:
             self.page.write_host(self.inflight(), self.free_slots(), f.T, f.step)
         return f
 
     def queued_steps(self) -> int:
-        """Forward steps launched and not yet reaped."""
-        return len(self._q)
+        """Forward steps launched and not yet reaped (serving steps and
+        realtime micro-forwards)."""
+        return len(self._q) + len(self._qm)
 
     def poll_one(self) -> bool:
         """Reap the oldest queued step if the GPU finished it (non-blocking);
         its results are returned by the next ``finish``."""
         f = self._reap(block=False)
         if f is None:
+            if self._qm:
+                return self.pump_micro() > 0 or bool(self._reaped_m)
             return False
         self._reaped.append(f)
         return True
 
+    @staticmethod
+    def _result(done: List[_Inflight]) -> StepResult:
+        comp = [r for f in done for r in f.completed]
+        firsts = [r for f in done for r in f.firsts]
+        return StepResult(sum(f.T for f in done), sum(f.n_pre for f in done), sum(f.n_dec for f in done),
+                          comp, firsts, (time.perf_counter() - done[0].t0) * 1e3 if done else 0.0)
+
     def finish(self, block: bool = False) -> StepResult:
-        """Reap finished steps.  Non-blocking unless ``block`` (then waits for
-        every queued step)."""
+        """Reap finished steps (and micro-forwards).  Non-blocking unless
+        ``block`` (then waits for every queued one)."""
         done: List[_Inflight] = self._reaped
         self._reaped = []
         while self._q:
@@ -797,10 +1045,17 @@ class BackendEngine:
             if f is None:
                 break
             done.append(f)
-        comp = [r for f in done for r in f.completed]
-        firsts = [r for f in done for r in f.firsts]
-        return StepResult(sum(f.T for f in done), sum(f.n_pre for f in done), sum(f.n_dec for f in done),
-                          comp, firsts, (time.perf_counter() - done[0].t0) * 1e3 if done else 0.0)
+        if self.micro:
+            while True:
+                self.pump_micro()
+                done.extend(self._reaped_m)
+                self._reaped_m = []
+                if not block or not (self._qm or self.micro_pending()):
+                    break
+                f = self._reap(block=True, micro=True)
+                if f is not None:
+                    done.append(f)
+        return self._result(done)
 
     def step(self) -> StepResult:
         """Synchronous step: launch + wait."""
@@ -818,7 +1073,8 @@ class BackendEngine:
         st = pin.numpy().view(np.int32)
         st[:] = 0
         if self.active:
-            st[np.fromiter(self.active.keys(), dtype=np.int64)] = 1
+            a = np.fromiter(self.active.keys(), dtype=np.int64)
+            st[a[a < self.slots]] = 1                      # (the serving pool's census)
         self._slot_state_d.copy_(pin.view(torch.int32), non_blocking=True)
         from .. import _native
         _native.require_hipops().slot_census(self._slot_state_d.data_ptr(), self.slots, int(tokens),

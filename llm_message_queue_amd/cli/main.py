@@ -53,7 +53,9 @@ def _build_engine(cfg, model: str, device, job: str = ""):
     return BackendEngine(mcfg, slots=slots, max_ctx=cfg.backend.max_ctx,
                          token_budget=cfg.backend.token_budget, device=device, impl="hip", page=page, gpu_index=rank,
                          step_timeout_s=cfg.backend.step_timeout / 1e9,
-                         realtime_step_tokens=cfg.backend.realtime_step_tokens), page
+                         realtime_step_tokens=cfg.backend.realtime_step_tokens,
+                         realtime_mode=cfg.backend.realtime_mode, micro_slots=cfg.backend.micro_slots,
+                         micro_inflight=cfg.backend.micro_inflight, micro_stream=cfg.backend.micro_stream), page
 
 
 def fit_slots(mcfg, slots: int, max_ctx: int, reserve_gb: float, total_bytes: int) -> int:

@@ -328,6 +328,14 @@ class StateManager:
             conv = self._convs.get(conversation_id)
             return -1 if conv is None else conv.home_gpu
 
+    def summary_tokens(self, conversation_id: str) -> List[int]:
+        """The N5 salient tokens of the conversation's evicted window (empty
+        while nothing was evicted): the gateway prepends them to a
+        non-resident replay as the dialog's compressed context."""
+        with self._lock:
+            conv = self._convs.get(conversation_id)
+            return [] if conv is None else list(conv.summary_tokens)
+
     # ------------------------------------------------------------------ user caps
     def _add_to_active_users(self, user_id: str, conversation_id: str) -> None:
         ids = self._users.setdefault(user_id, [])

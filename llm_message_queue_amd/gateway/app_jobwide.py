@@ -11,7 +11,11 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 from ..models.message import Message, MessageStatus
+from .request_table import NONE, RETRY
 from .router import StageRecorder
+
+# cancel answers that mean "this request will not complete"
+CANCEL_ACCEPTED = ("cancelled", "forwarded", "pending")
 
 
 class JobWideMixin:
@@ -38,7 +42,8 @@ class JobWideMixin:
                 return False
             removed = bool(m.queue_name and self.standard.has_queue(m.queue_name)
                            and self.standard.remove_message(m.queue_name, m))
-            return {"dequeued": removed, "cancelled": bool(not removed and self.cancel_inflight(m))}
+            res = "" if removed else self.cancel_inflight(m)
+            return {"dequeued": removed or res == "dequeued", "cancelled": res in CANCEL_ACCEPTED}
         if op == "stats":
             return self._rank_stats()
         if op == "reset_latency":
@@ -99,18 +104,35 @@ class JobWideMixin:
         return res
 
     def cancel_inflight(self, m: Message, timeout_s: float = 1.5) -> str:
-        """Abort ``m`` if it runs on a GPU (``DELETE /api/v1/messages/{id}``
-        on a dispatched request): "cancelled" (aborted on this rank's GPU,
-        its slot freed), "forwarded" (the GPU running it was told to abort it
-        at the next exchange) or "" (not in flight from here)."""
-        if self.engine is None or m.status != MessageStatus.PROCESSING:
+        """Cancel ``m`` wherever it is in this router's request lifecycle
+        (``DELETE /api/v1/messages/{id}``; ``gateway.request_table``): inbox,
+        preprocess batch, queue, retry backoff, held for its KV, running on
+        this rank's GPU or on another's.  Gated on the lifecycle state, not
+        on ``status`` (a request placed on another rank's GPU
+        keeps status pending).  Returns the serve loop's answer ("dequeued",
+        "cancelled", "forwarded"), "pending" when the serve loop did not
+        answer in time (the request is tombstoned all the same: it ends at
+        the next tick and never completes), or "" (it had already ended)."""
+        if m.lc == NONE:
             return ""
+        f = self.gateway.request_cancel(m)
         try:
-            return self.gateway.request_cancel(m).result(timeout=timeout_s)
-        except Exception:                      # noqa: BLE001 -- serve loop busy / stopping: not cancelled
-            return ""
+            return f.result(timeout=timeout_s)
+        except Exception:                      # noqa: BLE001 -- serve loop busy / stopping
+            return "pending" if m.handle in self.gateway.table.tomb else ""
 
     def _dequeue_local(self, queue_type: str, mid: str) -> bool:
+        if queue_type == "delayed":
+            # a request waiting out a retry backoff (the gateway's retry queue
+            # is the factory's DelayedQueue): ended through the lifecycle, so
+            # no later delivery can requeue it
+            dq = self.factory.delayed_queue
+            m = self.messages.get(mid) or dq.find(mid)
+            if m is None:
+                return False
+            if m.lc == RETRY:
+                return self.cancel_inflight(m) in ("cancelled", "pending")
+            return dq.remove(m)
         mgr = self.factory.get_queue_manager(queue_type)
         m = self.messages.get(mid)
         return bool(mgr is not None and m is not None and m.queue_name and mgr.has_queue(m.queue_name)

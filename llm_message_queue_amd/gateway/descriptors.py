@@ -18,6 +18,14 @@ K_TIMEOUT, K_CANCELLED = 5, 6
 # (the origin retries with backoff) / it never ran there (requeued as is)
 FAIL_UNTOUCHED, FAIL_FAILED = 0, 1
 K_CANCEL = 7        # [kind, handle lo/hi, origin]: origin -> the GPU running its request: abort it
+# origin -> the GPU it dispatched a dialog turn to, one tick after the
+# K_DISPATCH row: the dialog's real token history for a non-resident replay,
+# HIST_SPAN tokens a row in the payload columns: [kind, handle lo/hi, origin,
+# offset, ..., n (col 10), ..., history length (col 14), prefix length (col 15)];
+# the payload is the compressed-context prefix (N5 salient tokens) then the history
+K_HIST = 8
+# completion records (K_DONE) carry the turn's generated token ids in the
+# payload columns, their count in col 10 (dialog turns: the origin's history)
 DESC_HDR = 17       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
 #                    dialog history length, decision - enq (us), processing timeout (ms)];
 #                    flags = (home GPU + 1) | KV_MIGRATE

@@ -132,6 +132,9 @@ class OwnAdmissionMixin:
         if not msgs:
             return 0
         self._popped(msgs, tiers)
+        msgs, tiers = self._drop_cancelled(msgs, tiers)
+        if not len(msgs):
+            return 0
         eng = self.engine
         reqs = []
         for m, t in zip(msgs, tiers):
@@ -145,10 +148,13 @@ class OwnAdmissionMixin:
             m.dispatched_at = now
             m.status = MessageStatus.PROCESSING
             m.endpoint_id = f"gpu{self.rank}"
-            self.local[m.handle] = m
+            self.table.to_local(m)
             self.inflight_by_tier[r.tier] += 1
-        for r in reqs[len(admitted):]:             # cannot happen (room was counted); requeue defensively
-            self._requeue(r.meta)
+        if len(admitted) < len(reqs):              # cannot happen (room was counted); requeue defensively
+            got = {id(r) for r in admitted}
+            for r in reqs:
+                if id(r) not in got:
+                    self._requeue(r.meta)
         self._record([r.tier for r in admitted], [r.meta.arrival_ns for r in admitted],
                      [r.meta.enqueued_at for r in admitted], now, [r.meta.popped_ns for r in admitted], path)
         self.counters["dispatched"] += len(admitted)

@@ -23,19 +23,29 @@ from .descriptors import conv_key
 
 
 class AffinityMixin:
-    def _remember_dialog(self, m: Message, gpu: int) -> None:
+    def _remember_dialog(self, m: Message, gpu: int, tokens=None) -> None:
         """Completion of a conversation turn: its home GPU (KV residency) and
-        the dialog tokens a non-resident replay needs (prompt + generated;
-        generated ids stay on the device, placeholders stand in for them --
-        the cost, not the values, is what a replay pays)."""
+        the dialog tokens a non-resident replay needs -- exactly what the
+        home GPU's parked KV holds for the turn: its prompt (as the engine
+        took it) and every generated id but the last (never fed back).
+        ``tokens``: the turn's generated ids, read back with the step that
+        sampled them (``Request.out_tokens``; carried in the K_DONE record
+        when another GPU ran it).  Without them (a backend that keeps no ids)
+        placeholders keep the replay's cost right."""
         cid = m.conversation_id
         if not cid:
             return
         self.conv_home[cid] = gpu
         self.conv_home.move_to_end(cid)
-        p = np.asarray(m.prompt_ids if m.prompt_ids is not None else [], dtype=np.uint32).astype(np.int32)
+        p = np.asarray(m.prompt_ids if m.prompt_ids is not None else [], dtype=np.uint32)[:self.prompt_cap]
+        p = p.astype(np.int64).astype(np.int32)
+        if not len(p):
+            p = np.zeros(1, dtype=np.int32)                   # (the engine's stand-in for an empty prompt)
         h = self.conv_hist.get(cid)
-        add = np.concatenate([p, np.zeros(max(0, self.gen_tokens - 1), dtype=np.int32)])
+        g = max(0, self.gen_tokens - 1)
+        gen = np.asarray(tokens, dtype=np.int32)[:g] if tokens is not None and len(tokens) >= g \
+            else np.zeros(g, dtype=np.int32)
+        add = np.concatenate([p, gen])
         h = add if h is None else np.concatenate([h, add])[-self.history_cap:]
         self.conv_hist[cid] = h
         self.conv_hist.move_to_end(cid)
@@ -102,9 +112,24 @@ class AffinityMixin:
 
     def awaiting_kv(self) -> int:
         """Turns dispatched here that wait for their KV (next tick, or an
-        RCCL transfer still in flight)."""
+        RCCL transfer still in flight) or for their dialog history."""
         return (sum(len(v) for v in self._await_kv.values())
-                + sum(len(v) for v in self._await_import.values()))
+                + sum(len(v) for v in self._await_import.values()) + len(self._await_hist))
+
+    def _dialog_context(self, m: Message):
+        """(history, prefix) a replay of ``m``'s dialog prefills: the real
+        token history (``conv_hist``) and, when the conversation's window
+        was evicted, its N5 salient tokens as compressed context."""
+        cid = m.conversation_id
+        if not cid:
+            return None, None
+        hist = self.conv_hist.get(cid)
+        pre = None
+        if self.state_manager is not None and hasattr(self.state_manager, "summary_tokens"):
+            sal = self.state_manager.summary_tokens(cid)
+            if sal:
+                pre = np.asarray(sal, dtype=np.uint32).astype(np.int64).astype(np.int32)
+        return hist, pre
 
     def _plan_migrations(self, dest: Dict[int, List[Message]]) -> Dict[int, int]:
         """Turns placed on a GPU other than their (alive) home GPU move their

@@ -27,8 +27,11 @@ from ..backend.engine import Request
 from ..models.message import Message, MessageStatus
 from ..parallel import planner
 from .descriptors import (DESC_HDR, FAIL_UNTOUCHED, K_CANCEL, K_CANCELLED, K_DISPATCH, K_DONE, K_FAIL,
-                          K_MIGRATE, K_TIMEOUT, KV_MIGRATE, _get64, _put64, conv_key)
+                          K_HIST, K_MIGRATE, K_TIMEOUT, KV_MIGRATE, _get64, _put64, conv_key)
+
+HIST_LEN_BITS = 20      # descriptor col 14: dialog history length | (compressed-context length << 20)
 from .latency import P_PLAN_LOCAL, P_PLAN_REMOTE
+from .request_table import HELD
 
 
 class ExchangeMixin:
@@ -47,6 +50,9 @@ class ExchangeMixin:
             # cancels for requests running on other GPUs: announced now (row
             # counts in L_MIGC), sent in this tick's all_to_all
             self._cancel_pub, self._cancel_out = self._cancel_out, {}
+            # dialog histories of the turns dispatched last tick: announced
+            # now, sent as K_HIST rows in this tick's all_to_all
+            self._hist_pub, self._hist_out = self._hist_out, {}
             # EWMA (alpha 0.25) of own enqueues per tick -> this tick's reserve
             a = 0.25
             self._enq_ewma = [(1 - a) * e + a * n for e, n in zip(self._enq_ewma, self._enq_tick)]
@@ -81,7 +87,8 @@ class ExchangeMixin:
             exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
             weights=self._weights(),
             migrate_rows=[sum(1 for _, h, _ in self._mig_out if h == j and j != self.rank)
-                          + (len(self._cancel_pub.get(j, ())) if j != self.rank else 0) for j in range(W)],
+                          + (len(self._cancel_pub.get(j, ())) + self._hist_rows(j) if j != self.rank else 0)
+                          for j in range(W)],
             migrate_busy=bool(self._mig_out) or bool(self._await_kv),
             kv_tokens=kv_tok, kv_capacity=kv_cap)
 
@@ -104,6 +111,7 @@ class ExchangeMixin:
         msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, int(per_tier.sum()), [0] * len(self.tiers),
                                                 [int(x) for x in per_tier], self.lifo_ns)
         self._popped(msgs, tier_idx)
+        msgs, tier_idx = self._drop_cancelled(msgs, tier_idx)
         self._pub_depth = None
         by_tier: Dict[int, List[Message]] = {t: [] for t in range(len(self.tiers))}
         for m, t in zip(msgs, tier_idx):
@@ -141,10 +149,13 @@ class ExchangeMixin:
             rows = dest[j] if j != me else []
             buf = np.zeros((len(rows) + done_for[j], width), dtype=np.int32)
             if rows:
-                self._fill_descs(buf[:len(rows)], rows, me, cap, migrate)
+                ctx = self._fill_descs(buf[:len(rows)], rows, me, cap, migrate)
+                for m, (hist, pre) in zip(rows, ctx):
+                    if (hist is not None and len(hist)) or (pre is not None and len(pre)):
+                        self._hist_out.setdefault(j, []).append((m.handle, pre, hist))
                 tname = f"gpu{j}"
                 for m in rows:
-                    self.remote_out[m.handle] = m
+                    self.table.to_remote(m)
                     self.inflight_by_tier[m.tier] += 1
                     m.endpoint_id = tname
                     m.dispatched_at = now_ns
@@ -152,7 +163,8 @@ class ExchangeMixin:
                 self.lb.note_dispatch(f"gpu{j}", len(rows))
             mig_rows = [(c, d) for c, h, d in orders_prev if h == j] if j != me else []
             can = self._cancel_pub.get(j, []) if j != me else []
-            if mig_rows or can:
+            hist_rows = self._hist_block(j, me, cap, width) if j != me else None
+            if mig_rows or can or hist_rows is not None:
                 extra = np.zeros((len(mig_rows) + len(can), width), dtype=np.int32)
                 nm = len(mig_rows)
                 if nm:
@@ -175,14 +187,27 @@ class ExchangeMixin:
                 d[:, 4] = a[:, 1]
                 _put64(d, 5, a[:, 2])
                 _put64(d, 7, a[:, 3])
+                toks = self._done_tok[j]
+                if toks:
+                    # a dialog turn's generated ids ride in its record's payload
+                    for k, h in enumerate(a[:, 0].tolist()):
+                        t = toks.pop(h, None)
+                        if t is not None:
+                            n = min(len(t), cap)
+                            d[k, 10] = n
+                            d[k, DESC_HDR:DESC_HDR + n] = np.asarray(t[:n], dtype=np.int32)
+                    toks.clear()
             self._done_owed[j] = []
-            send.append(np.concatenate([buf, extra]) if (mig_rows or can) else buf)
+            if hist_rows is not None:
+                extra = np.concatenate([extra, hist_rows])
+            send.append(np.concatenate([buf, extra]) if (mig_rows or can or hist_rows is not None) else buf)
             if j != me:
                 self.counters["remote_sent"] += len(rows)
         recv_counts = [int(quota[i, me].sum()) + int(loads[i, planner.L_DONE + me])
                        + int(loads[i, planner.L_MIGC + me]) if i != me else 0 for i in range(W)]
         send[me] = np.zeros((0, width), dtype=np.int32)
         self._cancel_pub = {}
+        self._hist_pub = {}
         tc0 = time.perf_counter_ns()
         pend = self.comm.all_to_all_rows_async(send, recv_counts, width)
         self._overlap(pend)
@@ -205,11 +230,22 @@ class ExchangeMixin:
             if not len(g):
                 continue
             kinds = g[:, 0]
+            hrows = g[kinds == K_HIST]
+            if len(hrows):                            # histories of turns dispatched here last tick
+                fresh.extend(self._take_histories(src, hrows))
             disp = g[kinds == K_DISPATCH]
             if len(disp):
                 for r, fl in zip(self._foreign_requests(disp, cap), disp[:, 11].tolist()):
+                    needs = (r.history is not None and len(r.history)) or (r.prefix is not None and len(r.prefix))
                     if fl & KV_MIGRATE:
                         newly_held.append((r, (fl & 0xFF) - 1))
+                        if needs:                     # (the replay if the KV never lands)
+                            self._hist_wait[(r.meta[0], r.meta[1])] = r
+                    elif needs and not self._resident_ok(r):
+                        # not resident here: it replays its dialog, whose real
+                        # tokens arrive from its router with the next exchange
+                        self._await_hist[(r.meta[0], r.meta[1])] = r
+                        self._hist_wait[(r.meta[0], r.meta[1])] = r
                     else:
                         fresh.append(r)
             done = g[kinds == K_DONE]
@@ -221,18 +257,25 @@ class ExchangeMixin:
                 self._remote_abort(row)
             can = g[kinds == K_CANCEL]
             if len(can):
-                self._cancel_foreign(src, _get64(can, 1))
+                self._cancel_foreign(src, _get64(can, 1), held_prev)
             mig = g[kinds == K_MIGRATE]
             if len(mig):
                 src_orders.extend((int(c), me, int(d)) for c, d in zip(_get64(mig, 1), mig[:, 3]))
         # execute last tick's orders (home side: send; dest side: receive),
         # then admit the turns that waited for them, ahead of new work
         ready = self._migrate(loads, src_orders, held_prev)
-        reqs: List[Request] = list(ready)
+        reqs: List[Request] = []
+        for r in ready:                               # held turns: one cancelled meanwhile ends here
+            if isinstance(r.meta, Message) and self.table.cancelled(r.meta):
+                self._finish_cancel(r.meta, dispatched=True)
+            else:
+                reqs.append(r)
         for r, h in newly_held:
             if h < 0:
                 reqs.append(r)
             else:
+                if isinstance(r.meta, Message):
+                    self.table.move(r.meta, HELD)
                 self._await_kv.setdefault(r.conv, []).append((r, h))
         reqs.extend(fresh)
         admitted = self.engine.admit(reqs) if (self.engine is not None and reqs and self.healthy) else []
@@ -243,7 +286,7 @@ class ExchangeMixin:
                 m = r.meta
                 m.dispatched_at = now
                 m.status = MessageStatus.PROCESSING
-                self.local[m.handle] = m
+                self.table.to_local(m)
                 self.inflight_by_tier[r.tier] += 1
                 tiers.append(r.tier); arr.append(m.arrival_ns); enqs.append(m.enqueued_at)
                 decs.append(m.popped_ns or now)
@@ -281,15 +324,17 @@ class ExchangeMixin:
         return len(admitted) + self._dispatch_own()
 
     def _fill_descs(self, buf: np.ndarray, msgs: Sequence[Message], origin: int, cap: int,
-                    migrate: Dict[int, int]) -> None:
+                    migrate: Dict[int, int]) -> list:
         """K_DISPATCH descriptors of ``msgs`` into ``buf`` [n][width], the
-        scalar fields as whole columns (one numpy op per field)."""
+        scalar fields as whole columns (one numpy op per field).  Returns
+        each message's dialog context (history, compressed-context prefix),
+        which follows as K_HIST rows with the next exchange."""
         n = len(msgs)
         v = np.empty((n, 4), dtype=np.int64)      # handle, arrival, enq, conversation key
         small = np.zeros((n, 6), dtype=np.int64)  # tier, plen, flags, hist len, decision - enq (us)
         kv = self.kv_residency
-        hist_of = self.conv_hist
         prompts = []
+        ctx = []
         for k, m in enumerate(msgs):
             cid = m.conversation_id
             v[k, 0], v[k, 1], v[k, 2] = m.handle, m.arrival_ns, m.enqueued_at
@@ -298,11 +343,13 @@ class ExchangeMixin:
             p = np.asarray(p if p is not None else (), dtype=np.uint32)[:cap]
             prompts.append(p)
             mf = migrate.get(id(m), -1)
-            hist = hist_of.get(cid) if cid else None
+            hist, pre = self._dialog_context(m) if cid else (None, None)
+            ctx.append((hist, pre))
             small[k, 0] = m.tier
             small[k, 1] = len(p)
             small[k, 2] = (mf + 1) | KV_MIGRATE if mf >= 0 else 0
-            small[k, 3] = 0 if hist is None else len(hist)
+            small[k, 3] = (0 if hist is None else min(len(hist), (1 << HIST_LEN_BITS) - 1)) \
+                | ((0 if pre is None else min(len(pre), 255)) << HIST_LEN_BITS)
             # decision time as microseconds after enqueue (the destination
             # records the decision -> admission hand-off stage)
             small[k, 4] = min(0x7FFFFFFF, max(0, (m.popped_ns - m.enqueued_at) // 1000)) \
@@ -324,6 +371,77 @@ class ExchangeMixin:
         for k, p in enumerate(prompts):
             if len(p):
                 buf[k, DESC_HDR:DESC_HDR + len(p)] = p.view(np.int32)
+        return ctx
+
+    # ------------------------------------------------------------------ dialog histories (K_HIST)
+    def _hist_rows(self, j: int) -> int:
+        """K_HIST rows this router owes GPU ``j`` this tick."""
+        cap = self.prompt_cap
+        return sum(-(-((0 if pre is None else len(pre)) + (0 if h is None else len(h))) // cap)
+                   for _hd, pre, h in self._hist_pub.get(j, ()))
+
+    def _hist_block(self, j: int, me: int, cap: int, width: int):
+        """The K_HIST rows of the histories owed to ``j`` (None: none):
+        ``cap`` tokens a row, prefix then history."""
+        items = self._hist_pub.get(j)
+        if not items:
+            return None
+        out = np.zeros((self._hist_rows(j), width), dtype=np.int32)
+        k = 0
+        for h, pre, hist in items:
+            pre = np.zeros(0, np.int32) if pre is None else np.asarray(pre, dtype=np.int32)
+            hist = np.zeros(0, np.int32) if hist is None else np.asarray(hist, dtype=np.int32)
+            allt = np.concatenate([pre, hist])
+            for off in range(0, len(allt), cap):
+                n = min(cap, len(allt) - off)
+                row = out[k]
+                row[0] = K_HIST
+                row[3] = me
+                row[4] = off
+                row[10] = n
+                row[14] = len(hist)
+                row[15] = len(pre)
+                row[DESC_HDR:DESC_HDR + n] = allt[off:off + n]
+                k += 1
+        _put64(out, 1, [h for h, pre, hist in items
+                        for _ in range(-(-((0 if pre is None else len(pre)) + (0 if hist is None else len(hist)))
+                                         // cap))])
+        return out
+
+    def _take_histories(self, src: int, rows: np.ndarray) -> List[Request]:
+        """K_HIST rows from ``src``: fill the dialog history (and compressed
+        context) of its turns held here; returns the ones that only waited
+        for it (admitted this tick)."""
+        parts: Dict[int, np.ndarray] = {}
+        for h, off, n, hl, pl, row in zip(_get64(rows, 1).tolist(), rows[:, 4].tolist(), rows[:, 10].tolist(),
+                                          rows[:, 14].tolist(), rows[:, 15].tolist(), rows):
+            buf = parts.get(h)
+            if buf is None:
+                buf = parts[h] = np.zeros(pl + hl, dtype=np.int32)
+            buf[off:off + n] = row[DESC_HDR:DESC_HDR + n]
+            parts[h] = buf
+            self._hist_len[(src, h)] = (hl, pl)
+        ready = []
+        for h, buf in parts.items():
+            hl, pl = self._hist_len.pop((src, h))
+            r = self._hist_wait.pop((src, h), None)
+            if r is None:
+                continue                              # (admitted resident, cancelled or handed back)
+            r.prefix = buf[:pl] if pl else None
+            r.history = buf[pl:] if hl else None
+            if self._await_hist.pop((src, h), None) is not None:
+                ready.append(r)
+        return ready
+
+    def _resident_ok(self, r: Request) -> bool:
+        """A foreign dialog turn can start now without its history: its
+        conversation's KV here is current and the turn fits the window."""
+        eng = self.engine
+        if eng is None or r.conv < 0 or not hasattr(eng, "resident_context"):
+            return False
+        have = eng.resident_context(r.conv)
+        need = 0 if r.history is None else len(r.history)
+        return have > 0 and have >= need and have + len(r.prompt) + r.gen_tokens <= eng.max_ctx
 
     def _foreign_requests(self, rows: np.ndarray, cap: int) -> List[Request]:
         """Requests for K_DISPATCH descriptor rows (another router's
@@ -331,27 +449,35 @@ class ExchangeMixin:
         handle, arrival, enq, ck = _get64(rows, 1), _get64(rows, 5), _get64(rows, 7), _get64(rows, 12)
         dec = enq + rows[:, 15].astype(np.int64) * 1000
         out = []
-        for k, (h, a, e, c, d, origin, tier, gen, plen, hl, to_ms) in enumerate(zip(
+        mask = (1 << HIST_LEN_BITS) - 1
+        for k, (h, a, e, c, d, origin, tier, gen, plen, hv, to_ms) in enumerate(zip(
                 handle.tolist(), arrival.tolist(), enq.tolist(), ck.tolist(), dec.tolist(), rows[:, 3].tolist(),
                 rows[:, 4].tolist(), rows[:, 9].tolist(), rows[:, 10].tolist(), rows[:, 14].tolist(),
                 rows[:, 16].tolist())):
             self._next_req += 1
-            # a non-resident turn replays its dialog: the origin router holds
-            # the history, the descriptor carries its length (the replay's
-            # prefill cost; generated tokens are placeholders there as well)
+            hl, pl = hv & mask, hv >> HIST_LEN_BITS
+            # the dialog context's LENGTH travels here (a resident turn only
+            # needs it to check its KV is current); a turn that must replay
+            # waits for the real tokens (K_HIST, next exchange), which replace
+            # these stand-ins
             out.append(Request(req_id=self._next_req, prompt=rows[k, DESC_HDR:DESC_HDR + max(1, plen)].copy(),
                                gen_tokens=gen, tier=tier, meta=(origin, h, tier, a, e, d), conv=c,
                                history=np.zeros(hl, dtype=np.int32) if hl > 0 else None,
+                               prefix=np.zeros(pl, dtype=np.int32) if pl > 0 else None,
                                timeout_ns=int(to_ms) * 1_000_000))
         return out
 
     def _remote_done_rows(self, rows: np.ndarray) -> None:
         """K_DONE rows: my requests another GPU finished."""
-        for h, gpu, adm, done in zip(_get64(rows, 1).tolist(), rows[:, 3].tolist(), _get64(rows, 5).tolist(),
-                                     _get64(rows, 7).tolist()):
+        for k, (h, gpu, adm, done, nt) in enumerate(zip(
+                _get64(rows, 1).tolist(), rows[:, 3].tolist(), _get64(rows, 5).tolist(), _get64(rows, 7).tolist(),
+                rows[:, 10].tolist())):
             m = self.remote_out.pop(h, None)
             if m is None:
                 continue
             self.inflight_by_tier[m.tier] -= 1
-            self._remember_dialog(m, int(gpu))
+            if self.table.cancelled(m):       # cancelled after that GPU launched its last token
+                self._finish_cancel(m, done - adm, dispatched=True)
+                continue
+            self._remember_dialog(m, int(gpu), rows[k, DESC_HDR:DESC_HDR + nt] if nt > 0 else None)
             self._complete(m, done - adm)     # (releases the balancer's gpu<j> endpoint with this RT)

@@ -21,6 +21,7 @@ from ..backend.engine import Request
 from ..models.message import Message, MessageStatus
 from ..queue.core import QueueError
 from .descriptors import FAIL_FAILED, FAIL_UNTOUCHED, K_CANCELLED, K_FAIL, K_TIMEOUT, _get64
+from .request_table import HELD, INBOX, LOCAL, NONE, PREPROCESS, QUEUED, REMOTE, RETRY
 
 
 class FailureMixin:
@@ -61,6 +62,7 @@ class FailureMixin:
         """Popped, expired requests -> status timeout + dead-letter queue."""
         for m in out:
             m.status = MessageStatus.TIMEOUT
+            self.table.end(m)
             self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
         if out:
             self.counters["expired"] += len(out)
@@ -91,6 +93,7 @@ class FailureMixin:
         self.inflight_by_tier[m.tier] -= 1
         if self.lb is not None and m.endpoint_id:
             self.lb.release_endpoint(m.endpoint_id, 0, failed)   # (note_dispatch counted it)
+        m.endpoint_id = ""
         if failed:
             self._retry(m, "backend failed while running the request")
         else:
@@ -149,19 +152,44 @@ class FailureMixin:
                 self.metrics.requests_rejected.labels("processing_timeout").inc()
             self._retry(m, f"processing timeout ({m.timeout / 1e9:.3g} s)")
             return
+        m.endpoint_id = ""                               # (released above)
+        self._finish_cancel(m, dispatched=True)
+
+    def _finish_cancel(self, m: Message, ran_ns: int = 0, dispatched: bool = False) -> None:
+        """End ``m`` as cancelled (wherever it was: the caller took it out of
+        its container).  ``dispatched``: it was popped for a GPU, so its
+        tier's processing count is closed as failed (as a backend failure
+        would be) and its balancer endpoint released."""
+        self.table.end(m)
+        self.table.ended_cancelled += 1
         self.counters["cancelled"] += 1
         m.status = MessageStatus.CANCELLED
         m.updated_at = time.time_ns()
-        self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
+        if dispatched:
+            if self.lb is not None and m.endpoint_id:
+                self.lb.release_endpoint(m.endpoint_id, ran_ns, False)
+                m.endpoint_id = ""
+            self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
+        if isinstance(m.metadata, dict):
+            m.metadata["last_error"] = "cancelled"
 
     def request_cancel(self, m: Message):
-        """Any thread: cancel ``m`` if it runs on a GPU.  Returns a Future the
-        serve loop resolves with "cancelled" (aborted on this rank's GPU),
-        "forwarded" (K_CANCEL sent to the GPU running it, which reports the
-        abort back) or "" (not in flight from this router)."""
+        """Any thread: cancel ``m`` wherever it is in this router's lifecycle
+        (``gateway.request_table``).  Returns a Future the serve loop
+        resolves with "dequeued" (taken out of its tier queue), "cancelled"
+        (ended here: inbox, preprocess batch, retry backoff, held for its
+        KV, or aborted on this rank's GPU), "forwarded" (K_CANCEL sent to the
+        GPU running it, which reports the abort back) or "" (not live here:
+        it had already ended).  From the moment this returns, the request
+        can no longer complete or re-enter service: its handle is
+        tombstoned and every re-entry point checks the tombstone."""
         from concurrent.futures import Future
         f: Future = Future()
         with self._cancel_lock:
+            if m.lc == NONE:
+                f.set_result("")
+                return f
+            self.table.tomb[m.handle] = m
             self._cancel_req.append((m, f))
         return f
 
@@ -172,29 +200,93 @@ class FailureMixin:
             reqs, self._cancel_req = self._cancel_req, []
         now = time.monotonic_ns()
         for m, f in reqs:
-            res = ""
-            if m.handle in self.local and self.engine is not None:
-                got = self.engine.cancel([m.handle])
-                for r in got:
-                    self._aborted(r, K_CANCELLED, now)
-                res = "cancelled" if got else ""
-            elif m.handle in self.remote_out and str(m.endpoint_id).startswith("gpu"):
-                j = int(m.endpoint_id[3:])
-                if 0 <= j < self.world and j != self.rank:
-                    self._cancel_out.setdefault(j, []).append(m.handle)
-                    res = "forwarded"
+            res = self._cancel_one(m, now)
             if not f.done():
                 f.set_result(res)
 
-    def _cancel_foreign(self, origin: int, handles) -> None:
+    def _cancel_one(self, m: Message, now: int) -> str:
+        st = m.lc
+        if st == NONE:                                   # ended before the serve loop got here:
+            self.table.tomb.pop(m.handle, None)          # by a re-entry check of the tombstone, or otherwise
+            return "cancelled" if m.status == MessageStatus.CANCELLED else ""
+        if st == INBOX:
+            with self._inbox_lock:
+                k = next((i for i, x in enumerate(self._inbox) if x is m), -1)
+                if k >= 0:
+                    del self._inbox[k]
+            if k >= 0:
+                self._finish_cancel(m)
+            return "cancelled"                           # (else taken meanwhile: the enqueue ends it)
+        if st == PREPROCESS:
+            return "cancelled"                           # ended by _enqueue when its batch lands
+        if st == QUEUED:
+            if m.queue_name and self.qm.has_queue(m.queue_name) and self.qm.remove_message(m.queue_name, m):
+                self._finish_cancel(m)                   # (on_remove released its pin)
+                return "dequeued"
+            return "cancelled"                           # popped this tick: the dispatch drops it
+        if st == RETRY:
+            q = self.retry_queue
+            took = q is not None and q.remove(m)
+            if not took:
+                with self._retry_lock:
+                    k = next((i for i, x in enumerate(self._retry_due) if x is m), -1)
+                    if k >= 0:
+                        del self._retry_due[k]
+                        took = True
+            if took:
+                self._finish_cancel(m, dispatched=True)      # (popped once: its processing count is open)
+            return "cancelled"                           # (else delivered meanwhile: the requeue ends it)
+        if st == HELD:
+            for d in (self._await_kv, self._await_import):
+                for ck, rs in list(d.items()):
+                    keep = [(r, h) for r, h in rs if r.meta is not m]
+                    if len(keep) != len(rs):
+                        if keep:
+                            d[ck] = keep
+                        else:
+                            del d[ck]
+            self._finish_cancel(m, dispatched=True)
+            return "cancelled"
+        if st == LOCAL:
+            got = self.engine.cancel([m.handle]) if self.engine is not None else []
+            for r in got:
+                self._aborted(r, K_CANCELLED, now)
+            return "cancelled"                           # (else its last token is launched: ends at completion)
+        if st == REMOTE:
+            if str(m.endpoint_id).startswith("gpu"):
+                j = int(m.endpoint_id[3:])
+                if 0 <= j < self.world and j != self.rank:
+                    self._cancel_out.setdefault(j, []).append(m.handle)
+            return "forwarded"                           # ends when that GPU reports back
+        return ""
+
+    def _cancel_foreign(self, origin: int, handles, held_prev=None) -> None:
         """K_CANCEL rows from ``origin``: abort those of its requests my GPU
-        is running (one that already completed is reported done as usual)."""
+        is running or holds for their KV (one that already completed is
+        reported done as usual; the origin's tombstone ends it there)."""
         hs = {int(h) for h in handles}
         ids = [rid for rid, (o, h, _t) in self.foreign.items() if o == origin and h in hs]
+        now = time.monotonic_ns()
         if ids and self.engine is not None:
-            now = time.monotonic_ns()
             for r in self.engine.cancel(ids):
                 self._aborted(r, K_CANCELLED, now)
+        for key in [k for k in self._await_hist if k[0] == origin and k[1] in hs]:   # waiting for its history
+            r = self._await_hist.pop(key)
+            self._hist_wait.pop(key, None)
+            self._done_owed[origin].append((r.meta[1], r.meta[2], now, now, K_CANCELLED))
+        for d in (self._await_kv, self._await_import, held_prev or {}):
+            for ck, rs in list(d.items()):
+                keep = []
+                for r, h in rs:
+                    if not isinstance(r.meta, Message) and r.meta[0] == origin and r.meta[1] in hs:
+                        self._done_owed[origin].append((r.meta[1], r.meta[2], now, now, K_CANCELLED))
+                    else:
+                        keep.append((r, h))
+                if len(keep) != len(rs):
+                    if keep:
+                        d[ck] = keep
+                    else:
+                        del d[ck]
 
     def attach_retry_queue(self, delayed, backoff=None) -> None:
         """Route backend-failure retries through ``delayed`` (a
@@ -209,6 +301,9 @@ class FailureMixin:
     def _retry(self, m: Message, reason: str) -> None:
         """A request a backend failure handed back: retry after a backoff, or
         dead-letter it once its retries are spent."""
+        if self.table.cancelled(m):
+            self._finish_cancel(m, dispatched=True)
+            return
         if self.retry_queue is None:
             self._requeue(m)
             return
@@ -218,6 +313,7 @@ class FailureMixin:
         if m.retry_count >= self.retry_backoff.max_retries():
             m.status = MessageStatus.FAILED
             m.endpoint_id = ""
+            self.table.end(m)
             self.counters["retry_exhausted"] += 1
             self.qm.fail_message(m.queue_name, m.id, None, m.priority, quiet=True)
             if self.dead_letter is not None:
@@ -231,6 +327,7 @@ class FailureMixin:
         m.endpoint_id = ""
         m.dispatched_at = 0
         self.counters["retried"] += 1
+        self.table.move(m, RETRY)
         self.retry_queue.schedule_after(m, self.retry_backoff.next_backoff(m.retry_count), target=self._retry_ready)
 
     def retrying(self) -> int:
@@ -258,9 +355,15 @@ class FailureMixin:
             self._requeue(m)
 
     def _requeue(self, m: Message) -> None:
+        if self.table.cancelled(m):
+            self._finish_cancel(m, dispatched=True)          # (every requeue follows a pop)
+            return
         m.status = MessageStatus.PENDING
         m.endpoint_id = ""
         m.dispatched_at = 0
+        self.table.local.pop(m.handle, None)
+        self.table.remote_out.pop(m.handle, None)
+        self.table.move(m, QUEUED)
         self.qm.requeue_after_failure(m.queue_name, m)
         if self.world > 1:
             self._pin(m, +1)
@@ -287,8 +390,11 @@ class FailureMixin:
         self._err_ewma = 0.9 * self._err_ewma + 0.1
         n = 0
         held = [r for d in (self._await_kv, self._await_import) for rs in d.values() for r, _h in rs]
+        held += list(self._await_hist.values())           # foreign turns waiting for their history
         self._await_kv = {}
         self._await_import = {}
+        self._await_hist = {}
+        self._hist_wait = {}
         for r in held:                                  # turns waiting for a KV that will not be used here
             n += 1
             if isinstance(r.meta, Message):

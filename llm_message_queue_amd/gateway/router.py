@@ -50,6 +50,7 @@ from .gateway_affinity import AffinityMixin
 from .gateway_exchange import ExchangeMixin
 from .gateway_failure import FailureMixin
 from .gateway_resources import ResourceMixin
+from .request_table import INBOX, NONE, PREPROCESS, QUEUED, RequestTable
 
 
 class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmissionMixin):
@@ -107,9 +108,13 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
                                         bool(getattr(q, "priority_monotone_caps", True)))
         for n in self.tiers:                          # D1: the level queues exist
             self.qm.create_queue(n)
+        # every request's lifecycle state and the in-flight maps (one owner:
+        # gateway.request_table)
+        self.table = RequestTable()
         # a queued message removed other than by dispatch (admin delete,
         # peer dequeue, retention cleanup) releases its (home GPU, tier) pin
-        self.qm.on_remove.append(lambda m: self._pin(m, -1))
+        # and leaves the lifecycle
+        self.qm.on_remove.append(self._queue_removed)
         self.metrics = metrics
         self._inbox: List[Message] = []
         self._inbox_lock = threading.Lock()
@@ -155,10 +160,21 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
             from ..parallel.migration import KVMigrator
             self.migrator = KVMigrator(engine.model, self.comm)
             self.comm.warm_data_plane()
-        self.local: Dict[int, Message] = {}          # handle -> msg dispatched to my engine (my origin)
-        self.remote_out: Dict[int, Message] = {}      # handle -> msg I sent to another rank
+        self.local: Dict[int, Message] = self.table.local        # handle -> msg dispatched to my engine
+        self.remote_out: Dict[int, Message] = self.table.remote_out  # handle -> msg sent to another rank
         self.foreign: Dict[int, Tuple[int, int, int]] = {}  # my engine req id -> (origin, handle, tier)
         self._done_owed: Dict[int, List[Tuple[int, int, int, int]]] = {r: [] for r in range(self.world)}
+        # generated ids of the dialog turns in _done_owed (origin -> handle -> ids)
+        self._done_tok: Dict[int, Dict[int, np.ndarray]] = {r: {} for r in range(self.world)}
+        # dialog histories owed to the GPUs this router dispatched turns to
+        # (sent one tick later as K_HIST rows, counted in that tick's load vector)
+        self._hist_out: Dict[int, List[Tuple[int, np.ndarray, np.ndarray]]] = {}
+        self._hist_pub: Dict[int, List[Tuple[int, np.ndarray, np.ndarray]]] = {}
+        # foreign turns that must replay their dialog, waiting for its history: (origin, handle) -> Request
+        self._await_hist: Dict[Tuple[int, int], Request] = {}
+        # every foreign turn a K_HIST is still expected for (also KV-held ones) and the lengths seen
+        self._hist_wait: Dict[Tuple[int, int], Request] = {}
+        self._hist_len: Dict[Tuple[int, int], Tuple[int, int]] = {}
         self.rec = LatencyRecorder(len(self.tiers))
         self.rec_stage = StageRecorder(len(self.tiers))
         self.counters = {"submitted": 0, "rejected": 0, "dispatched": 0, "completed": 0, "ticks": 0,
@@ -267,6 +283,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         now = time.monotonic_ns()
         for m in msgs:
             m.recv_ns = now
+            m.lc = INBOX                    # (not visible to any other thread before the inbox)
             if not m.arrival_ns:
                 m.arrival_ns = now
         with self._inbox_lock:
@@ -338,6 +355,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         now = time.monotonic_ns()
         for m in batch:
             m.ingest_ns = now
+        self.table.move_many(batch, PREPROCESS)
         return batch
 
     def preprocessing(self) -> int:
@@ -359,9 +377,13 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
 
     def _enqueue(self, batch) -> List[Tuple[Message, Optional[QueueError]]]:
         t1 = time.perf_counter_ns()
+        batch, dead, _ = self.table.split_cancelled(batch)
+        for m in dead:                      # cancelled while being preprocessed: never queued
+            self._finish_cancel(m)
         for m in batch:
             if not m.queue_name:
                 m.queue_name = priority_name(m.priority)
+        self.table.move_many(batch, QUEUED)
         errs = self.qm.push_routed(batch)
         self.ingest_ns[1] += time.perf_counter_ns() - t1
         self.ingest_ns[2] += len(batch)
@@ -377,6 +399,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
                 self._pin(m, +1)
             if e is not None:
                 m.status = MessageStatus.FAILED
+                self.table.move(m, NONE)
                 self.counters["rejected"] += 1
                 if self.metrics:
                     self.metrics.requests_rejected.labels(e.code).inc()
@@ -421,9 +444,9 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         p = np.asarray(prompt, dtype=np.uint32).astype(np.int64).astype(np.int32) \
             if len(prompt) else np.zeros(1, dtype=np.int32)
         ck = conv_key(m.conversation_id) if self.kv_residency else -1
-        hist = self.conv_hist.get(m.conversation_id) if m.conversation_id else None
+        hist, pre = self._dialog_context(m)
         return Request(req_id=m.handle, prompt=p, gen_tokens=self.gen_tokens, tier=tier, meta=m, conv=ck,
-                       history=hist, timeout_ns=self._timeout_ns(m))
+                       history=hist, prefix=pre, timeout_ns=self._timeout_ns(m))
 
     def _timeout_ns(self, m: Message) -> int:
         return int(m.timeout) if (self.inflight_timeout and m.timeout and m.timeout > 0) else 0
@@ -479,6 +502,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
             msgs, tier_idx, enq = self.qm.pop_tiers(self.tiers, free, self.aging_ns, self._budgets(),
                                                     self.lifo_ns)
             self._popped(msgs, tier_idx)
+            msgs, tier_idx = self._drop_cancelled(msgs, tier_idx)
         n_head = len(msgs)
         lane = self._lane_budget(len(msgs), int((np.asarray(tier_idx) == 0).sum()))
         if lane > 0:
@@ -490,6 +514,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
             m2, t2, _ = self.qm.pop_tiers(self.tiers, lane, [0] * len(self.tiers), b, None)
             if m2:
                 self._popped(m2, t2)
+                m2, t2 = self._drop_cancelled(m2, t2)
                 msgs = list(msgs) + list(m2)
                 tier_idx = np.concatenate([np.asarray(tier_idx, dtype=np.int64), np.asarray(t2, dtype=np.int64)])
         lane_ids = {id(m) for m in msgs[n_head:]}
@@ -518,7 +543,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
             m = r.meta
             m.dispatched_at = now
             m.status = MessageStatus.PROCESSING
-            self.local[m.handle] = m
+            self.table.to_local(m)
             self.inflight_by_tier[r.tier] += 1
         if self.lb is not None and admitted:
             for r in admitted:
@@ -530,19 +555,24 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         self._record([r.tier for r in admitted], [r.meta.arrival_ns for r in admitted],
                      [r.meta.enqueued_at for r in admitted], now, [r.meta.popped_ns for r in admitted])
         if len(admitted) < len(reqs):    # cannot happen (free slots were counted); requeue defensively
-            for r in reqs[len(admitted):]:
-                self.qm.requeue_after_failure(r.meta.queue_name, r.meta)
+            got = {id(r) for r in admitted}
+            for r in reqs:
+                if id(r) not in got:
+                    self._requeue(r.meta)
         self.counters["dispatched"] += len(admitted)
         return len(admitted)
 
     # ------------------------------------------------------------------ backend step
     def _complete(self, m: Message, process_ns: int) -> None:
+        self.table.end(m)
         m.status = MessageStatus.COMPLETED
         m.completed_at = time.time_ns()
         if self.tracer is not None:
             self.tracer.request(m)
         if m.arrival_ns:
-            self._done_buf.append((m.tier, m.arrival_ns, m.enqueued_at or m.arrival_ns))
+            # stamped now (the response exists on this router from here), not
+            # at the tick's flush: realtime micro-forwards complete mid-tick
+            self._done_buf.append((m.tier, m.arrival_ns, m.enqueued_at or m.arrival_ns, time.monotonic_ns()))
         self.qm.complete_message(m.queue_name, m.id, process_ns, m.priority)
         if self.lb is not None and m.endpoint_id:
             self.lb.release_endpoint(m.endpoint_id, process_ns, False)
@@ -563,6 +593,23 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         if self.engine is None:
             return None
         res = self.engine.finish(block=block)
+        self._on_results(res)
+        return res
+
+    def _finish_micro(self) -> bool:
+        """Realtime micro-forwards (``backend.realtime_mode = micro``): launch
+        the next ones and complete the requests the finished ones served at
+        once -- they finish every few ms, well inside a serving step, so
+        their completion is not held back to the tick's reap."""
+        eng = self.engine
+        if eng is None or not getattr(eng, "micro", False):
+            return False
+        n = eng.pump_micro()
+        res = eng.finish_micro()
+        self._on_results(res)
+        return bool(n or res.completed or res.first_tokens)
+
+    def _on_results(self, res) -> None:
         if res.completed:
             # this GPU's service-time EWMA (alpha 0.1 per completion, as the
             # reference's ReleaseEndpoint): published in the load vector for
@@ -578,12 +625,16 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
                 self.local.pop(m.handle, None)
                 if 0 <= r.tier < len(self.inflight_by_tier):
                     self.inflight_by_tier[r.tier] -= 1
-                self._remember_dialog(m, self.rank)
+                if self.table.cancelled(m):     # cancelled after its last token was launched
+                    self._finish_cancel(m, r.done_ns - r.admitted_ns, dispatched=True)
+                    continue
+                self._remember_dialog(m, self.rank, r.out_tokens)
                 self._complete(m, r.done_ns - r.admitted_ns)
             else:
                 origin, handle, tier = self.foreign.pop(r.req_id)
                 self._done_owed[origin].append((handle, tier, r.admitted_ns, r.done_ns, K_DONE))
-        return res
+                if r.conv >= 0 and r.out_tokens is not None:       # a dialog turn: its ids go home
+                    self._done_tok[origin][handle] = r.out_tokens
 
     def tick(self, pump=None):
         """One serving tick, pipelined so host work overlaps the forward:
@@ -615,6 +666,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         admission between collectives, ``_dispatch_own``)."""
         if pump is not None:
             pump()
+        micro = self._finish_micro()
         now = time.monotonic_ns()
         if self._pre_pending is not None and self.pre.batch_ready(self._pre_pending):
             # a finished preprocess batch is enqueued (and dispatched) at once
@@ -623,10 +675,10 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
                 self._admit_between()
             return True
         if not self._inbox:
-            return False
+            return micro
         if self.use_gpu_pre and len(self._inbox) < self.WAIT_INGEST_MSGS \
                 and now - self._last_ingest_ns < self.WAIT_INGEST_NS:
-            return False
+            return micro
         self._last_ingest_ns = now
         did = self.ingest_async()
         if admit:
@@ -651,8 +703,8 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
 
     def _tick(self, pump=None):
         self._pump = pump
-        self._drain_retries()
         self._process_cancels()
+        self._drain_retries()
         self._expire_inflight()
         res = None
         pc = time.perf_counter_ns
@@ -681,6 +733,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
             self.ingest()
         t4 = pc()
         n = self.dispatch()
+        self._finish_micro()                 # realtime requests just admitted start at once
         ht[3] += pc() - t4
         ht[4] += t4 - t0 if res is None else 0
         self.counters["ticks"] += 1
@@ -700,11 +753,10 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
     def flush_latency(self) -> None:
         """Move buffered completion timestamps into the e2e histogram."""
         if self._done_buf:
-            now = time.monotonic_ns()
             a = np.asarray(self._done_buf, dtype=np.int64)
             self._done_buf = []
             tiers = np.clip(a[:, 0], 0, len(self.tiers) - 1)
-            self.rec_done.record(tiers, now - a[:, 1], now - a[:, 2])
+            self.rec_done.record(tiers, a[:, 3] - a[:, 1], a[:, 3] - a[:, 2])
 
     def host_profile(self, reset: bool = False) -> Dict[str, float]:
         """Mean host milliseconds per tick in each phase (launch includes any
@@ -753,8 +805,32 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         n = 0
         for t in self.tiers:
             n += self.qm.size(t)
+            for m in self.qm.mlq.messages(t):
+                self._pin(m, -1)
+                self.table.end(m)
             self.qm.mlq.clear(t)
         with self._inbox_lock:
             n += len(self._inbox)
+            for m in self._inbox:
+                self.table.end(m)
             self._inbox = []
         return n
+
+    # ------------------------------------------------------------------ lifecycle helpers
+    def _queue_removed(self, m: Message) -> None:
+        """``qm.on_remove`` (API / peer threads): a queued message taken out
+        other than by dispatch leaves the lifecycle (its pin is released)."""
+        self._pin(m, -1)
+        if m.lc == QUEUED:
+            m.lc = NONE
+
+    def _drop_cancelled(self, msgs, tier_idx):
+        """Popped messages with a cancel pending end here instead of being
+        dispatched; returns the rest (and their tier indices)."""
+        if not self.table.tomb or not len(msgs):
+            return msgs, tier_idx
+        live, dead, t = self.table.split_cancelled(msgs, list(np.asarray(tier_idx).tolist()))
+        for m in dead:
+            self._pin(m, -1)
+            self._finish_cancel(m, dispatched=True)        # (popped: its processing count is open)
+        return live, np.asarray(t, dtype=np.int64)

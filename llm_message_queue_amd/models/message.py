@@ -196,7 +196,7 @@ class Message:
         "queue_name", "retry_count", "max_retries", "timeout", "created_at",
         "updated_at", "scheduled_at", "completed_at", "metadata", "handle",
         "enqueued_at", "dispatched_at", "arrival_ns", "prompt_ids", "endpoint_id", "tier", "pin_key",
-        "ingest_ns", "popped_ns", "recv_ns",
+        "ingest_ns", "popped_ns", "recv_ns", "lc",
     )
 
     def __init__(self, id: str = "", conversation_id: str = "", user_id: str = "",
@@ -232,6 +232,7 @@ class Message:
         self.ingest_ns = 0        # ns, taken from the gateway inbox into a preprocess batch
         self.popped_ns = 0        # ns, popped from its queue by a dispatch decision
         self.recv_ns = 0          # ns, handed to this process's gateway (Gateway.submit)
+        self.lc = 0               # lifecycle state at the origin router (gateway.request_table)
 
     # -- JSON ------------------------------------------------------------------
     def to_dict(self) -> Dict[str, Any]:

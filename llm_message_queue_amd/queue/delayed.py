@@ -37,6 +37,12 @@ class DelayedQueue:
         self._stop.clear()
         self._thread = threading.Thread(target=self._drain, name="delayed-queue", daemon=True)
         self._thread.start()
+        # a queue nobody closed: stop its drain thread before interpreter
+        # teardown destroys the native object it is blocked in
+        import atexit
+        import weakref
+        ref = weakref.ref(self)
+        atexit.register(lambda: (lambda q: q.stop() if q is not None else None)(ref()))
 
     def stop(self) -> None:
         self._stop.set()
@@ -62,6 +68,30 @@ class DelayedQueue:
 
     def schedule_after(self, message: Message, delay_ns: int, target=None) -> None:
         self.schedule(message, time.time_ns() + int(delay_ns), target)
+
+    def remove(self, message) -> bool:
+        """Take a scheduled message out before it is delivered (``DELETE
+        /api/v1/messages/{id}`` or ``DELETE /api/v1/admin/queues/delayed/{id}``
+        on a request waiting out a retry backoff).  ``message``: a Message or
+        its handle.  True if it was waiting (it will never be delivered);
+        False if it is not here, including one the drain thread already took
+        (the item map is the authority: delivery and removal both pop it
+        under the same lock, so exactly one of them wins)."""
+        h = message if isinstance(message, int) else message.handle
+        with self._lock:
+            item = self._items.pop(h, None)
+        if item is None:
+            return False
+        self._native.remove(h)
+        return True
+
+    def find(self, message_id: str) -> Optional[Message]:
+        """The scheduled message with this id (None: not waiting here)."""
+        with self._lock:
+            for msg, _ready, _t in self._items.values():
+                if msg.id == message_id:
+                    return msg
+        return None
 
     # -------------------------------------------------------------- delivery
     def _drain(self) -> None:

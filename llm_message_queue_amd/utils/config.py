@@ -312,10 +312,21 @@ class BackendConfig:
     # arrival -> last token p99 from ~270 ms to ~100 ms for ~29 % fewer
     # requests/s (profiles/r5_step_budget_sweep_1gpu.jsonl), so it is off
     realtime_step_tokens: int = 0
+    # how realtime requests are served (BackendEngine.realtime_mode): "off"
+    # (in the serving steps), "cap" (the step cap above), "micro" (realtime
+    # micro-forwards over their own slot pool, on their own stream); "" =
+    # "cap" if realtime_step_tokens > 0 else "off".  docs/performance.md
+    # "Realtime modes" has the measured trade-off.
+    realtime_mode: str = ""
+    micro_slots: int = 64              # micro mode: KV slots of the realtime pool
+    micro_inflight: int = 4            # micro mode: micro-forwards queued ahead on their stream
+    micro_stream: str = "high"         # micro mode: "high" (own high-priority stream) or "same"
     # a forward still incomplete this long after launch = a hung GPU: the
     # serve loop stops with a failure status (BackendHung) so the launcher
-    # restarts the job; 0 waits forever
-    step_timeout: int = 60 * S
+    # restarts the job; 0 waits forever.  Below server.stall_fatal_after, so
+    # a hung forward surfaces as BackendHung (which step, how many tokens)
+    # before the stall watchdog ends the process
+    step_timeout: int = 40 * S
 
 
 @dataclass
@@ -532,6 +543,16 @@ def validate(cfg: Config) -> Config:
         seen.add(lv.priority)
     if cfg.gpu.slots_per_gpu <= 0:
         raise ConfigError("gpu.slots_per_gpu must be > 0")
+    b = cfg.backend
+    if b.realtime_mode not in ("", "off", "cap", "micro"):
+        raise ConfigError("backend.realtime_mode must be off, cap or micro")
+    if b.micro_stream not in ("high", "same") or b.micro_slots < 1 or b.micro_inflight < 1:
+        raise ConfigError("backend.micro_stream must be high or same, micro_slots and micro_inflight >= 1")
+    fatal = cfg.server.stall_fatal_after
+    if fatal > 0 and b.step_timeout > 0 and fatal <= b.step_timeout:
+        # a hung forward stops the ticks: the stall watchdog would end the
+        # process before BackendHung could name the step
+        raise ConfigError("server.stall_fatal_after must exceed backend.step_timeout (both nonzero)")
     if cfg.server.front_door not in ("native", "python"):
         raise ConfigError("server.front_door must be native or python")
     auth = cfg.security.authentication

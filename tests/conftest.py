@@ -4,6 +4,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# every gateway built by a test checks its request-lifecycle transitions
+# (gateway/request_table.py: a transition from a state it may not come from raises)
+os.environ.setdefault("LLMQ_LIFECYCLE_DEBUG", "1")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
