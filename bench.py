@@ -68,8 +68,10 @@ def parse(argv=None):
     ap.add_argument("--micro-slots", type=int, default=64, help="micro mode: KV slots of the realtime pool")
     ap.add_argument("--micro-inflight", type=int, default=4, help="micro mode: micro-forwards queued ahead")
     ap.add_argument("--micro-budget", type=int, default=512, help="micro mode: tokens per micro-forward")
-    ap.add_argument("--micro-stream", default="high", choices=["high", "same"],
-                    help="micro mode: a high-priority HIP stream of their own, or the serving stream")
+    ap.add_argument("--micro-stream", default="high", choices=["high", "same", "partition"],
+                    help="micro mode: a high-priority HIP stream of their own, the serving stream, or a CU "
+                         "partition of the chip of their own (--micro-cus; the serving steps get the rest)")
+    ap.add_argument("--micro-cus", type=int, default=32, help="micro partition: CUs of the realtime partition")
     ap.add_argument("--gen-tokens", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=2, help="forward steps queued ahead on the GPU")
     ap.add_argument("--aging-ms", default="50,100,150,200",
@@ -162,6 +164,9 @@ def parse(argv=None):
                     help="multi-GPU placement strategy (loadbalancer.algorithm)")
     ap.add_argument("--control-plane", default="shm", choices=["shm", "gloo", "nccl"],
                     help="per-tick load/descriptor exchange: host gloo group or RCCL on a side stream")
+    ap.add_argument("--data-backend", default="", choices=["", "nccl", "gloo"],
+                    help="data plane (KV migration): nccl = RCCL after a preflight (gloo fallback, flagged in "
+                         "comm.data_backend), gloo; '' = nccl on GPUs, gloo in --cpu-dry-run")
     ap.add_argument("--gateway-only-s", type=float, default=3.0,
                     help="seconds of the secondary null-backend gateway measurement (0 = skip)")
     ap.add_argument("--gateway-only-rate", type=float, default=50000.0)
@@ -274,7 +279,8 @@ def main(argv=None) -> int:
         # CPU rehearsal of the exact control flow (collectives, tick counts,
         # reductions) with a tiny model and gloo -- never a measurement
         dev = torch.device("cpu")
-        comm = init_from_env(backend="gloo", control="gloo" if a.control_plane == "nccl" else a.control_plane)
+        comm = init_from_env(backend=a.data_backend or "gloo",
+                             control="gloo" if a.control_plane == "nccl" else a.control_plane)
         if not a.sim_gpu:
             a.model, a.slots, a.max_ctx, a.token_budget, a.prompt_cap = "tiny", 16, 64, 128, 16
     else:
@@ -289,7 +295,7 @@ def main(argv=None) -> int:
         from llm_message_queue_amd.parallel.placement import bind_rank
         binding = bind_rank("gpu" if a.pin_cpu else a.cpu_bind,
                             extra_pids=[door.proc.pid] if door is not None and door.proc is not None else ())
-        comm = init_from_env(control=a.control_plane)
+        comm = init_from_env(backend=a.data_backend or None, control=a.control_plane)
     comm_kind = "solo" if world == 1 else str(getattr(comm, "backend", a.control_plane))
     evidence = comm_evidence(comm, dev, world, dry, binding=None if dry else binding)
 
@@ -338,7 +344,7 @@ def main(argv=None) -> int:
                                prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens,
                                realtime_mode=a.realtime_mode, micro_slots=a.micro_slots,
                                micro_inflight=a.micro_inflight, micro_budget=a.micro_budget,
-                               micro_stream=a.micro_stream)
+                               micro_stream=a.micro_stream, micro_cus=a.micro_cus)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -657,6 +663,10 @@ def main(argv=None) -> int:
     value = res["value"] if res["met"] else 0.0
     slo = {"util_tried": [t["util"] for t in tried], "attempts": tried,
            "value_util": round(res["util"], 4) if res["met"] else None,
+           # the first window (at --util) next to the headline, so a climbed
+           # value can be compared with single-window rounds
+           "first_window": {"util": tried[0]["util"], "value": tried[0]["value"] if tried[0]["met"] else 0.0,
+                            "met": tried[0]["met"]},
            "search_s": round(time.monotonic() - t_search, 1), "directions": "climb + backoff"}
     if not res["met"]:
         slo["reason"] = (f"no utilisation in {slo['util_tried']} held p99 <= {P99_TARGET_MS} ms (all tiers) and "
@@ -690,7 +700,8 @@ def main(argv=None) -> int:
                    "seq_len_is": "max_ctx", "max_ctx": a.max_ctx,
                    "realtime_mode": engine.realtime_mode,
                    "micro": ({"slots": engine.micro_slots, "inflight": engine.micro_inflight,
-                              "budget": engine.micro_budget, "stream": engine.micro_stream}
+                              "budget": engine.micro_budget, "stream": engine.micro_stream,
+                              "cus": engine.micro_cus or None}
                              if engine.micro else None),
                    "parallelism": f"dp{world}", "ingress": a.ingress, "door_share": a.door_share, "placement": a.lb,
                    "token_budget_by_rank": a.token_budget_by_rank or None,
@@ -742,6 +753,9 @@ def main(argv=None) -> int:
         "remote_dispatched": int(comm.all_gather_i64(np.array([gw.counters["remote_sent"]], dtype=np.int64)).sum()),
         "remote_dispatched_in_window": res["remote_in_window"],
         "comm": evidence,
+        # the data plane the job ran on: "nccl" (RCCL passed its preflight on
+        # every rank), "gloo-fallback" (it did not: flagged), "gloo", "none"
+        "data_plane": evidence.get("data_backend", "none"),
         "lockstep": res["lockstep"],
         "latency_breakdown": res["breakdown"],
         "steady_ticks": steady,
@@ -800,6 +814,13 @@ def main(argv=None) -> int:
     page.close(unlink=True)
     if world > 1:
         import torch.distributed as dist
+        if getattr(comm, "data_backend", "") == "gloo-fallback":
+            # an RCCL group that failed its preflight may still hold a helper
+            # thread inside the communicator: tearing it down could block, so
+            # this rank ends here (its result line is already out)
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
         dist.destroy_process_group()
     return 0
 

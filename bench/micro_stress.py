@@ -25,7 +25,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--stream", default="high", choices=["high", "same"])
+    ap.add_argument("--stream", default="high", choices=["high", "same", "partition"])
+    ap.add_argument("--micro-cus", type=int, default=32)
+    ap.add_argument("--budget", type=int, default=4096)
+    ap.add_argument("--slots", type=int, default=1536)
     ap.add_argument("--blas", default="", choices=["", "lt", "rocblas"],
                     help="library GEMM backend for F.linear / addmm (torch preferred_blas_library)")
     ap.add_argument("--mode", default="micro", choices=["micro", "off"])
@@ -43,8 +46,8 @@ def main() -> int:
     if a.blas:
         torch.backends.cuda.preferred_blas_library("cublaslt" if a.blas == "lt" else "cublas")
     dev = torch.device("cuda", 0)
-    eng = BackendEngine(LlamaConfig.llama3_8b(), slots=1536, max_ctx=512, token_budget=4096, device=dev,
-                        impl="hip", realtime_mode=a.mode, micro_stream=a.stream,
+    eng = BackendEngine(LlamaConfig.llama3_8b(), slots=a.slots, max_ctx=512, token_budget=a.budget, device=dev,
+                        impl="hip", realtime_mode=a.mode, micro_stream=a.stream, micro_cus=a.micro_cus,
                         micro_inflight=a.micro_inflight, step_timeout_s=a.step_timeout)
     eng.warm_shapes()
     eng.time_steps = True
@@ -58,26 +61,37 @@ def main() -> int:
 
     t0 = time.monotonic()
     t_rep = t0
-    rt_next = t0
+    rt_next = [t0]
     lat = []
-    n_rt = 0
+
+    def rt_poll() -> bool:
+        """Realtime arrivals due now are admitted (micro pool) and the
+        micro-forwards pumped / reaped while the serving step runs."""
+        now = time.monotonic()
+        rts = []
+        while rt_next[0] <= now:
+            rts.append(req(0))
+            rt_next[0] += rng.exponential(1.0 / a.rt_rate)
+        for r in rts:
+            r.meta = time.monotonic_ns()
+        if rts:
+            eng.admit(rts)
+        n = eng.pump_micro()
+        res = eng.finish_micro()
+        t = time.monotonic_ns()
+        for r in res.completed:
+            if r.tier == 0 and isinstance(r.meta, int):
+                lat.append((t - r.meta) / 1e6)
+        return bool(rts or n or res.completed)
+
     try:
         while time.monotonic() - t0 < a.seconds:
-            now = time.monotonic()
-            rts = []
-            while rt_next <= now:
-                rts.append(req(0))
-                rt_next += rng.exponential(1.0 / a.rt_rate)
-            if rts:
-                for r in rts:
-                    r.meta = time.monotonic_ns()
-                eng.admit(rts)
-                n_rt += len(rts)
+            rt_poll()
             cap = eng.admit_capacity()
             if cap:
                 eng.admit([req(2) for _ in range(cap)])
-            eng.launch(wait_cb=lambda: eng.pump_micro() > 0)
-            eng.pump_micro()
+            eng.launch(wait_cb=rt_poll)
+            rt_poll()
             res = eng.finish()
             t_done = time.monotonic_ns()
             for r in res.completed:

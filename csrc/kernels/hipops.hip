@@ -246,8 +246,12 @@ static void gemm_residual_rms(uintptr_t a, uintptr_t w, uintptr_t c, int M, int 
 // schedule / without the wave-row stagger; 50 / 66 / 82 = SwiGLU with
 // s_setprio around every MFMA cluster / the static priority on wave row 0 /
 // no priority (A/B only; the default is a static priority on wave row 1).
+// split_ws != 0: tiles [split_full, tiles) run split-K over two blocks each
+// (GmSplit; epilogues store / SwiGLU / residual-LDS): a step too small to
+// fill its CUs with whole tiles -- the realtime micro-forwards on their CU
+// partition, where o / down are 16 tiles for 32 CUs.
 static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t stream,
-                      int group_m, uintptr_t rs) {
+                      int group_m, uintptr_t rs, int split_full, uintptr_t split_ws, uintptr_t split_cnt) {
   require(group_m >= 1 && group_m <= 64, "gemm: group_m out of range");
   require(M > 0 && N > 0 && K > 0, "gemm: empty operand");
   require(N % GM_BN == 0, "gemm: N must be a multiple of 256");
@@ -255,17 +259,26 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
   require((int64_t)M * K < (int64_t)1 << 30 && (int64_t)N * K < (int64_t)1 << 30, "gemm: operand too large (2 GiB buffer descriptors)");
   require(a % 16 == 0 && w % 16 == 0 && c % 16 == 0, "gemm: pointers must be 16-byte aligned");
   const float* rsp = rs ? P<const float>(rs) : nullptr;
+  GmSplit sp{0, nullptr, nullptr};
+  if (split_ws) {
+    const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+    require(split_full >= 0 && split_full < tiles, "gemm: bad split");
+    require((K / GM_BK) % 4 == 0 && K / GM_BK >= 8, "gemm: split-K needs K % 256 == 0 and K >= 512");
+    require(split_cnt != 0 && split_ws % 16 == 0, "gemm: split workspace");
+    require(epi == GM_EPI_STORE || epi == GM_EPI_SWIGLU || epi == GM_EPI_RESID_LDS, "gemm: split-K epilogue");
+    sp = GmSplit{split_full, P<float>(split_ws), P<int>(split_cnt)};
+  }
   if (epi == GM_EPI_STORE)
     launch_gemm<GM_EPI_STORE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m,
-                              rsp);
+                              rsp, GmRope{}, sp);
   else if (epi == GM_EPI_SWIGLU)
     launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m,
-                               rsp);
+                               rsp, GmRope{}, sp);
   else if (epi == GM_EPI_RESID)                    // C += A·Wᵀ in place (no row scales)
     launch_gemm<GM_EPI_RESID>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_RESID_LDS)                // the same, residual tile staged by DMA (A/B)
     launch_gemm<GM_EPI_RESID_LDS>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
-                                  group_m);
+                                  group_m, nullptr, GmRope{}, sp);
   else if (epi == GM_EPI_RESID_PRE)                // ... with its first quarter prefetched at start (A/B)
     launch_gemm<GM_EPI_RESID_PRE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
                                   group_m);
@@ -561,7 +574,8 @@ PYBIND11_MODULE(_hipops, m) {
         py::arg("N"), py::arg("K"), py::arg("stream"), py::arg("group_m"), py::arg("part"), py::arg("ticket"),
         py::arg("scale"), py::arg("eps"));
   m.def("gemm_bf16", &gemm_bf16, py::arg("a"), py::arg("w"), py::arg("c"), py::arg("M"), py::arg("N"),
-        py::arg("K"), py::arg("epi"), py::arg("stream"), py::arg("group_m") = (int)GM_GROUP_M, py::arg("rs") = 0);
+        py::arg("K"), py::arg("epi"), py::arg("stream"), py::arg("group_m") = (int)GM_GROUP_M, py::arg("rs") = 0,
+        py::arg("split_full") = 0, py::arg("split_ws") = 0, py::arg("split_cnt") = 0);
   m.def("gemm_qkv_rope", &gemm_qkv_rope, py::arg("a"), py::arg("w"), py::arg("M"), py::arg("N"), py::arg("K"),
         py::arg("pos"), py::arg("slot"), py::arg("cos_t"), py::arg("sin_t"), py::arg("Hq"), py::arg("Hkv"),
         py::arg("max_ctx"), py::arg("n_slots"), py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("stream"),

@@ -124,7 +124,7 @@ class BackendEngine:
                  fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
                  realtime_step_tokens: int = 0, fused_rms=None, realtime_mode: str = "",
                  micro_slots: int = 64, micro_budget: int = 512, micro_inflight: int = 4,
-                 micro_stream: str = "high"):
+                 micro_stream: str = "high", micro_cus: int = 16):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
         self.step_timeout_s = float(step_timeout_s)
@@ -167,10 +167,22 @@ class BackendEngine:
         self.cuda = self.device.type == "cuda"
         self.async_device = self.cuda          # forwards run asynchronously (a GPU stream)
         self.rt_stream = None
+        self.main_stream = None          # (partition: the serving steps' CU-masked stream)
+        self.micro_cus = 0
+        if self.micro and micro_stream not in ("high", "same", "partition"):
+            raise ValueError(f"micro_stream must be high / same / partition, not {micro_stream!r}")
         if self.micro and self.cuda and micro_stream == "high":
             self.rt_stream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
-        elif self.micro and micro_stream not in ("high", "same"):
-            raise ValueError(f"micro_stream must be high / same, not {micro_stream!r}")
+        elif self.micro and self.cuda and micro_stream == "partition":
+            # the chip split in two CU partitions: the micro-forwards own
+            # ``micro_cus`` CUs, the serving steps the rest (their GEMM tile
+            # plans size waves for that count), so neither waits for the
+            # other's kernels to drain (docs/performance.md "Realtime modes")
+            from .cu_partition import partition_streams
+            self.micro_cus = int(micro_cus)
+            self.main_stream, self.rt_stream, big_cus = partition_streams(self.device, self.micro_cus)
+            from ..ops import gemm as _G
+            _G.EFFECTIVE_CUS[self.device.index if self.device.index is not None else 0] = big_cus
         self.micro_stream = micro_stream if self.micro else ""
         self.model = LlamaStub(model_cfg, self.n_all, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
@@ -668,26 +680,27 @@ class BackendEngine:
             sizes = list(range(1, 33)) + ladder + [self.token_budget]
         dev = self.device
         n = 0
-        for T in sizes:
-            T = int(min(max(1, T), self.token_budget))
-            r = torch.arange(T, device=dev, dtype=torch.int32)
-            seg = min(16, self.max_ctx)
-            slot = (r // seg) % self.slots
-            pos = r % seg
-            t0 = torch.arange(0, T, seg, device=dev, dtype=torch.int32)
-            tiles = torch.stack([t0, torch.clamp(T - t0, max=seg), (t0 // seg) % self.slots,
-                                 torch.zeros_like(t0)], 1).contiguous() if self.use_tiles else None
-            samp = torch.arange(min(T, self.slots), device=dev, dtype=torch.long)
-            self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(), slot.contiguous(),
-                               samp, tiles=tiles, n_dec=0)
-            n += 1
-        if getattr(self.model, "prune_last", False) and hasattr(self.model, "warm_tail"):
-            # the pruned last layer runs at the sampled-row count: a finer ladder
-            tail, t = list(range(1, 33)), 32
-            while t < self.token_budget:
-                t = max(t + 1, t * 9 // 8)
-                tail.append(min(t, self.token_budget))
-            n += self.model.warm_tail(tail)
+        with self.stream_ctx():
+            for T in sizes:
+                T = int(min(max(1, T), self.token_budget))
+                r = torch.arange(T, device=dev, dtype=torch.int32)
+                seg = min(16, self.max_ctx)
+                slot = (r // seg) % self.slots
+                pos = r % seg
+                t0 = torch.arange(0, T, seg, device=dev, dtype=torch.int32)
+                tiles = torch.stack([t0, torch.clamp(T - t0, max=seg), (t0 // seg) % self.slots,
+                                     torch.zeros_like(t0)], 1).contiguous() if self.use_tiles else None
+                samp = torch.arange(min(T, self.slots), device=dev, dtype=torch.long)
+                self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(),
+                                   slot.contiguous(), samp, tiles=tiles, n_dec=0)
+                n += 1
+            if getattr(self.model, "prune_last", False) and hasattr(self.model, "warm_tail"):
+                # the pruned last layer runs at the sampled-row count: a finer ladder
+                tail, t = list(range(1, 33)), 32
+                while t < self.token_budget:
+                    t = max(t + 1, t * 9 // 8)
+                    tail.append(min(t, self.token_budget))
+                n += self.model.warm_tail(tail)
         if self.rt_stream is not None:
             # the micro-forwards' stream: its per-stream GEMM workspaces and
             # first launches there, on the micro pool's own slots
@@ -702,7 +715,8 @@ class BackendEngine:
                         if self.use_tiles else None
                     samp = torch.arange(min(T, self.micro_slots), device=dev, dtype=torch.long)
                     self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(),
-                                       slot.contiguous(), samp, tiles=tiles, n_dec=0)
+                                       slot.contiguous(), samp, tiles=tiles, n_dec=0,
+                                       **({"small_cus": self.micro_cus} if self.micro_cus else {}))
                     n += 1
                     T *= 2
         torch.cuda.synchronize(dev)
@@ -793,6 +807,12 @@ class BackendEngine:
         self.host_ns[1] += time.perf_counter_ns() - ts
         self._launch_pool(False)
 
+    def stream_ctx(self):
+        """Context that makes the serving steps' stream current (a no-op
+        unless the chip is CU-partitioned): anything else ordered with the
+        serving steps -- KV imports, the slot census -- runs inside it."""
+        return torch.cuda.stream(self.main_stream) if self.main_stream is not None else _NullCtx()
+
     def _launch_pool(self, micro: bool) -> bool:
         """Build one pool's next token batch and enqueue its forward: the
         serving step, or (``micro``) a realtime micro-forward on the micro
@@ -827,7 +847,7 @@ class BackendEngine:
         pin.numpy()[:nbytes] = buf.view(np.uint8)
         host_out = outs[k]
         prev = self._prev_out_m if micro else self._prev_out
-        stream = self.rt_stream if micro else None
+        stream = self.rt_stream if micro else self.main_stream
         ctx = torch.cuda.stream(stream) if stream is not None else _NullCtx()
         with ctx:
             d = pin[:nbytes].to(dev, non_blocking=True).view(torch.int32)
@@ -842,7 +862,7 @@ class BackendEngine:
             ev0 = self._start_event()
             te = time.perf_counter_ns()
             out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til,
-                                     n_dec=D)
+                                     n_dec=D, **({"small_cus": self.micro_cus} if micro and self.micro_cus else {}))
             self.host_ns[2] += time.perf_counter_ns() - te
             if not micro:
                 self._census(T)

@@ -192,23 +192,29 @@ class LlamaStub:
 
     @torch.no_grad()
     def forward(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
-                sample_idx: torch.Tensor, tiles: Optional[torch.Tensor] = None, n_dec: int = 0) -> torch.Tensor:
+                sample_idx: torch.Tensor, tiles: Optional[torch.Tensor] = None, n_dec: int = 0,
+                small_cus: int = 0) -> torch.Tensor:
         """One step over T tokens; returns greedy next-token ids for the rows
         in ``sample_idx`` (the last token of each request's chunk).
         ``tiles`` (int32 [n, 4], see ``ops.llama_ops.make_tiles``) groups the
         tokens into per-slot segments for the MFMA attention kernel (its first
         ``n_dec`` rows are 1-token decode tiles); without it attention runs
-        per token."""
+        per token.  ``small_cus`` > 0: a small step confined to that many CUs
+        (a realtime micro-forward on its CU partition) -- every GEMM on the
+        hand-written kernels whatever the row count (no library kernel, none
+        of whose persistent / stream-K grids assume the whole chip), split-K
+        where the tiles cannot fill the partition."""
         if self.prune_last and self.residual_in_gemm:
-            sel = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec, rows=sample_idx)
+            sel = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec, rows=sample_idx, small_cus=small_cus)
         else:
-            sel = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec).index_select(0, sample_idx)
-        return self.ops.greedy_head(sel, self.lm_head, self.fused_head)
+            sel = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec,
+                              small_cus=small_cus).index_select(0, sample_idx)
+        return self.ops.greedy_head(sel, self.lm_head, self.fused_head, min_rows=1 if small_cus else 256)
 
     @torch.no_grad()
     def hidden(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
                tiles: Optional[torch.Tensor] = None, n_dec: int = 0,
-               rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+               rows: Optional[torch.Tensor] = None, small_cus: int = 0) -> torch.Tensor:
         """The 32-layer trunk: final-normed hidden states [T, d] (writes the
         step's K/V into the cache).
 
@@ -229,7 +235,13 @@ class LlamaStub:
             return self._hidden_residual_norm(tokens, pos, slot, tiles, n_dec)
         res = F.embedding(tokens, self.embed)            # [T, d], updated in place
         T = res.shape[0]
-        rows_qkv = self.fused_qkv and T >= self.min_fused_qkv_tokens
+        small = small_cus > 0 and self.impl == "hip"
+        rows_qkv = self.fused_qkv and (T >= self.min_fused_qkv_tokens or small)
+        qkv_split = {}
+        if small:
+            d = cfg.dim
+            f = G.split_all(T, (cfg.heads + 2 * cfg.kv_heads) * cfg.head_dim, d, small_cus)
+            qkv_split = {"split": f is not None, "split_full": f}
         last = len(self.layers) - 1
         if rows is not None and rows.numel() == T:
             rows = None                                  # every row sampled: nothing to drop
@@ -239,7 +251,7 @@ class LlamaStub:
             if rows_qkv and self.row_scale_norm:
                 q = ops.qkv_rope_rows(res, L["wqkv"], scale if scale is not None else ops.row_rms(res, cfg.eps),
                                       pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads, self.kcache[i],
-                                      self.vcache[i])
+                                      self.vcache[i], **qkv_split)
             elif rows_qkv:
                 q = G.qkv_rope(ops.rmsnorm(res, L["attn_norm"], cfg.eps), L["wqkv"], pos, slot, self.cos,
                                self.sin, cfg.heads, cfg.kv_heads, self.kcache[i], self.vcache[i])
@@ -250,7 +262,8 @@ class LlamaStub:
                 if rows.numel() == 0:                    # nothing sampled (a step of unfinished prefill
                     return res[:0]                       # chunks): K/V written, no row kernel gets 0 rows
                 res, a = res.index_select(0, rows), a.index_select(0, rows)
-            scale = self._mlp_block(res, a, L, want_scale=rows_qkv and self.row_scale_norm and i < last)
+            scale = self._mlp_block(res, a, L, want_scale=rows_qkv and self.row_scale_norm and i < last,
+                                    small_cus=small_cus if small else 0)
         return ops.rmsnorm(res, self.final_norm, cfg.eps)
 
     @torch.no_grad()
@@ -271,28 +284,34 @@ class LlamaStub:
             n += 1
         return n
 
-    def _mlp_block(self, res: torch.Tensor, a: torch.Tensor, L: dict, want_scale: bool = False):
+    def _mlp_block(self, res: torch.Tensor, a: torch.Tensor, L: dict, want_scale: bool = False,
+                   small_cus: int = 0):
         """res += o(a); res += down(swiglu(norm(res))) -- in place, with the
         fused-path choices made for this block's row count.  Returns the
         RMSNorm row scales of the final ``res`` when ``want_scale`` and the
-        down GEMM produced them in its epilogue (``fused_rms``), else None."""
+        down GEMM produced them in its epilogue (``fused_rms``), else None.
+        ``small_cus``: a micro-forward's small step on its CU partition --
+        the hand-written kernels at any row count, split-K (``forward``)."""
         cfg, ops = self.cfg, self.ops
         M = res.shape[0]
-        rows_mlp = self.fused_mlp and M >= self.min_fused_tokens
-        resid_o = self._cus > 0 and G.residual_tiles_ok(M, cfg.dim, self._cus)
-        rms = resid_o and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS
+        small = small_cus > 0
+        rows_mlp = self.fused_mlp and (M >= self.min_fused_tokens or small)
+        resid_o = small or (self._cus > 0 and G.residual_tiles_ok(M, cfg.dim, self._cus))
+        rms = resid_o and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS and not small
 
         def into_res(x, wt, scale_out):                  # res += x · wtᵀ (+ its row scales)
             if rms and scale_out:
                 return G.gemm_residual_rms(x, wt, res, cfg.eps)
             if resid_o:
-                G.gemm_residual(x, wt, res)
+                G.gemm_residual(x, wt, res, split_cus=small_cus)
             else:
                 res.addmm_(x, wt.t())
             return None
 
         scale = into_res(a, L["wo"], rows_mlp and self.row_scale_norm)
-        if rows_mlp and self.row_scale_norm:
+        if rows_mlp and self.row_scale_norm and small:
+            act = G.gemm_swiglu(res, L["w_gu"], row_scale=ops.row_rms(res, cfg.eps), split_cus=small_cus)
+        elif rows_mlp and self.row_scale_norm:
             act = ops.swiglu_rows(res, L["w_gu"], scale if scale is not None else ops.row_rms(res, cfg.eps))
         elif rows_mlp:
             act = G.gemm_swiglu(ops.rmsnorm(res, L["mlp_norm"], cfg.eps), L["w_gu"])

@@ -99,7 +99,18 @@ def _row_scale_ptr(rs, M: int) -> int:
     return rs.data_ptr()
 
 
-def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group_m: int = 8, row_scale=None):
+def split_all(M: int, N: int, K: int, cus: int):
+    """Split-K for a step too small to fill ``cus`` CUs with whole tiles:
+    every tile runs as two K-half blocks (returns 0 = the first whole
+    tile index) when twice the tiles still fit one wave, else None."""
+    tiles = (M + TILE_M - 1) // TILE_M * (N // TILE_N)
+    if cus <= 0 or 2 * tiles > cus or K % 256 or K < 512:
+        return None
+    return 0
+
+
+def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group_m: int = 8, row_scale=None,
+            split_cus: int = 0):
     k = _native.require_hipops()
     M, K = x.shape
     N = w.shape[0]
@@ -107,22 +118,33 @@ def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group
         raise ValueError("gemm: inner dimensions differ")
     if not supported(M, N, K):
         raise ValueError(f"gemm: unsupported shape M={M} N={N} K={K}")
-    k.gemm_bf16(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, epi,
-                torch.cuda.current_stream(x.device).cuda_stream, group_m, _row_scale_ptr(row_scale, M))
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    f = split_all(M, N, K, split_cus) if split_cus else None
+    ws = cnt = 0
+    if f is not None:
+        n_split = (M + TILE_M - 1) // TILE_M * (N // TILE_N) - f
+        w_t, c_t = _split_workspace(x.device, stream, n_split, max(split_cus, 2 * n_split))
+        ws, cnt = w_t.data_ptr(), c_t.data_ptr()
+    k.gemm_bf16(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, epi, stream, group_m,
+                _row_scale_ptr(row_scale, M), f or 0, ws, cnt)
     return out
 
 
-def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, row_scale=None) -> torch.Tensor:
+def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, row_scale=None,
+         split_cus: int = 0) -> torch.Tensor:
     """x [M][K] · w[N][K]ᵀ -> [M][N] bf16 on the hand-written kernel
-    (``row_scale`` [M] fp32: output row i is multiplied by row_scale[i])."""
+    (``row_scale`` [M] fp32: output row i is multiplied by row_scale[i];
+    ``split_cus``: run split-K when the tiles cannot fill that many CUs,
+    :func:`split_all`)."""
     _check(x, "x")
     _check(w, "w")
     y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
     _check(y, "out")
-    return _launch(x, w, y, EPI_STORE, row_scale=row_scale)
+    return _launch(x, w, y, EPI_STORE, row_scale=row_scale, split_cus=split_cus)
 
 
-def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None, row_scale=None) -> torch.Tensor:
+def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None, row_scale=None,
+                split_cus: int = 0) -> torch.Tensor:
     """silu(x·Wgᵀ) * (x·Wuᵀ) -> [M][F] bf16, ``w_perm`` from :func:`swiglu_permute`.
     ``row_scale`` [M] fp32 scales row i of both products first: with the
     RMSNorm weight folded into W and row_scale = ``row_rms(x)`` this is the
@@ -134,7 +156,7 @@ def gemm_swiglu(x: torch.Tensor, w_perm: torch.Tensor, out: torch.Tensor = None,
     _check(y, "out")
     if y.shape != (x.shape[0], F):
         raise ValueError("gemm_swiglu: out shape mismatch")
-    return _launch(x, w_perm, y, EPI_SWIGLU, row_scale=row_scale)
+    return _launch(x, w_perm, y, EPI_SWIGLU, row_scale=row_scale, split_cus=split_cus)
 
 
 _RMS_WS = {}
@@ -179,7 +201,7 @@ def gemm_residual_rms(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor, eps: 
     return scale
 
 
-def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor, split_cus: int = 0) -> torch.Tensor:
     """``res += x · wᵀ`` in place (bf16 ``res`` [M][N]; the fp32 sum is
     rounded once, as hipBLASLt's beta = 1 epilogue) -- the o / down
     projections accumulating into the residual stream.  Pulling the residual
@@ -192,7 +214,9 @@ def gemm_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor) -> torch.
     _check(res, "res")
     if res.shape != (x.shape[0], w.shape[0]):
         raise ValueError("gemm_residual: res shape mismatch")
-    return _launch(x, w, res, RESID_EPI)
+    if split_cus and RESID_EPI != EPI_RESID_LDS:
+        split_cus = 0                                  # (split-K is wired for the LDS epilogue only)
+    return _launch(x, w, res, RESID_EPI, split_cus=split_cus)
 
 
 def residual_tiles_ok(M: int, N: int, cus: int, min_fill: float = 0.97) -> bool:
@@ -232,13 +256,13 @@ def _split_workspace(device, stream: int, n_split: int, cus: int):
     is keyed by (device, stream) so concurrent streams never do."""
     key = (device.type, device.index, stream)
     ws = _SPLIT_WS.get(key)
-    if ws is None:
-        cap = cus // 2
+    if ws is None or n_split > ws[1].numel() // 2:
+        # (grown in stream order: a launch still using the old slabs is ahead
+        # on this same stream, and the caching allocator reuses them after it)
+        cap = max(cus // 2, n_split, ws[1].numel() // 2 if ws is not None else 0)
         ws = (torch.empty(cap * 512 * 128, dtype=torch.float32, device=device),
               torch.zeros(cap * 2, dtype=torch.int32, device=device))
         _SPLIT_WS[key] = ws
-    if n_split > ws[1].numel() // 2:
-        raise ValueError("split workspace too small")
     return ws
 
 
@@ -247,8 +271,15 @@ def _cu_count_idx(index: int) -> int:
     return torch.cuda.get_device_properties(index).multi_processor_count
 
 
+# device index -> CUs the serving steps' stream may use, when the chip is
+# split into CU partitions (backend.cu_partition): wave / split-K plans are
+# sized for the partition, not the whole chip
+EFFECTIVE_CUS = {}
+
+
 def _cu_count(device) -> int:
-    return _cu_count_idx(device.index if device.index is not None else torch.cuda.current_device())
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return EFFECTIVE_CUS.get(idx) or _cu_count_idx(idx)
 
 
 def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,

@@ -78,9 +78,10 @@ class HipOps:
         from . import gemm as G
         return G.gemm_swiglu(x, w_perm, row_scale=r)
 
-    def qkv_rope_rows(self, x, wqkv, r, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc):
+    def qkv_rope_rows(self, x, wqkv, r, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, split=True, split_full=None):
         from . import gemm as G
-        return G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, row_scale=r)
+        return G.qkv_rope(x, wqkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, row_scale=r, split=split,
+                          split_full=split_full)
 
     def greedy_head(self, x, w, fused: bool = True, min_rows: int = 256):
         """Greedy tokens of the LM head (int32 [M]): the hand-written GEMM
@@ -200,7 +201,7 @@ class RefOps:
         gu = (x.float() * r[:, None]) @ w.t()
         return (torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]).to(torch.bfloat16)
 
-    def qkv_rope_rows(self, x, wqkv, r, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc):
+    def qkv_rope_rows(self, x, wqkv, r, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc, split=True, split_full=None):
         qkv = ((x.float() * r[:, None]) @ wqkv.float().t()).to(torch.bfloat16)
         return self.rope_kv(qkv, pos, slot, cos_t, sin_t, Hq, Hkv, kc, vc)
 

@@ -660,15 +660,144 @@ def _restart_store(timeout):
     return dist.PrefixStore(f"llmq/attempt_{attempt}", base)
 
 
-def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_s: Optional[float] = None):
+PREFLIGHT_FAULT_ENV = "LLMQ_RCCL_PREFLIGHT_FAULT"    # "fail" / "hang": rehearse a broken RCCL data plane
+
+
+def rccl_preflight(group, device) -> dict:
+    """Before a job serves on an RCCL data group: a 1 KiB all_gather (the
+    communicator's lazy init happens here) and a 1 MiB send/recv around the
+    ring of ranks (every rank to its neighbour and back from the other),
+    each checked for content.  Raises on a failed or wrong collective;
+    returns the latencies.  Run by ``_rccl_data_group`` under a deadline in
+    a helper thread, so a hang costs the deadline, not the job."""
+    import os
+    import time
+    import torch
+    import torch.distributed as dist
+    fault = os.environ.get(PREFLIGHT_FAULT_ENV, "")
+    if fault == "hang":
+        while True:                                    # (a communicator that never comes up)
+            time.sleep(3600)
+    if fault == "fail":
+        raise RuntimeError("injected RCCL preflight failure")
+    if device is None or not torch.cuda.is_available():
+        raise RuntimeError("no GPU visible for the RCCL data plane")
+    torch.cuda.set_device(device)                      # (the device is per host thread)
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    out = {"rccl_world": world}
+    t0 = time.perf_counter()
+    x = torch.full((256,), rank, dtype=torch.int32, device=device)
+    got = torch.empty(world * 256, dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(got, x, group=group)
+    torch.cuda.synchronize(device)
+    want = torch.arange(world, dtype=torch.int32, device=device).repeat_interleave(256)
+    if not torch.equal(got, want):
+        raise RuntimeError("RCCL preflight: all_gather returned wrong data")
+    t1 = time.perf_counter()
+    n = (1 << 20) // 4
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+    snd = torch.full((n,), rank + 1, dtype=torch.int32, device=device)
+    rcv = torch.zeros(n, dtype=torch.int32, device=device)
+    peer = lambda r: dist.get_global_rank(group, r)     # noqa: E731 -- P2POp takes global ranks
+    for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, snd, peer(nxt), group),
+                                     dist.P2POp(dist.irecv, rcv, peer(prv), group)]):
+        w.wait()
+    torch.cuda.synchronize(device)
+    if int(rcv[0].item()) != prv + 1 or int(rcv[-1].item()) != prv + 1:
+        raise RuntimeError("RCCL preflight: send/recv returned wrong data")
+    t2 = time.perf_counter()
+    out.update(ok=True, all_gather_1k_ms=round((t1 - t0) * 1e3, 3), p2p_1m_ms=round((t2 - t1) * 1e3, 3))
+    return out
+
+
+def _rccl_data_group(timeout, preflight_s: float):
+    """The RCCL data group, or None when it did not pass ``rccl_preflight``
+    within ``preflight_s`` on EVERY rank (the verdict is agreed over the gloo
+    default group, so all ranks take the same data plane).  Returns (group |
+    None, report).  A rank whose preflight hangs leaves its helper thread
+    behind; the job then never touches that group again."""
+    import os
+    import threading
+    import torch
+    import torch.distributed as dist
+    rep: dict = {"deadline_s": preflight_s}
+    g = None
+    fault = os.environ.get(PREFLIGHT_FAULT_ENV, "")
+    try:
+        # (an injected fault rehearses the preflight itself, also on hosts without RCCL)
+        g = dist.new_group(backend="nccl", timeout=timeout) if not fault else "fault"
+    except Exception as e:                             # noqa: BLE001 -- no RCCL here: fall back
+        rep["error"] = f"new_group: {type(e).__name__}: {e}"
+    if g is not None:
+        box: dict = {}
+        dev = torch.device("cuda", local_device_index()) if torch.cuda.is_available() else None
+
+        def run():
+            try:
+                box.update(rccl_preflight(g, dev))
+            except BaseException as e:                 # noqa: BLE001
+                box["error"] = f"{type(e).__name__}: {e}"
+        t0 = __import__("time").perf_counter()
+        th = threading.Thread(target=run, name="rccl-preflight", daemon=True)
+        th.start()
+        th.join(preflight_s)
+        rep.update(box)
+        if th.is_alive():
+            rep["error"] = f"no answer within {preflight_s:g} s (hang)"
+        rep["wall_ms"] = round((__import__("time").perf_counter() - t0) * 1e3, 1)
+    ok = bool(rep.get("ok")) and "error" not in rep
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)        # (the gloo default group: every rank agrees)
+    rep["ok_all_ranks"] = bool(flag.item())
+    if not rep["ok_all_ranks"]:
+        import sys
+        print(f"comm: RCCL data plane failed its preflight on some rank ({rep.get('error', 'a peer failed')}); "
+              "the data plane falls back to gloo", file=sys.stderr, flush=True)
+        os.environ["LLMQ_DATA_PLANE"] = "gloo-fallback"
+        return None, rep
+    return g, rep
+
+
+def check_distinct_devices() -> list:
+    """Every rank's (PCI domain, bus, device) of its GPU, gathered over the
+    default group; raises if two ranks map one device (unless the job
+    deliberately oversubscribes the GPUs, a rehearsal layout)."""
+    import torch
+    import torch.distributed as dist
+    if not torch.cuda.is_available():
+        return []
+    p = torch.cuda.get_device_properties(local_device_index())
+    mine = torch.tensor([int(getattr(p, "pci_domain_id", 0)), int(getattr(p, "pci_bus_id", -1)),
+                         int(getattr(p, "pci_device_id", 0))], dtype=torch.int64)
+    world = dist.get_world_size()
+    rows = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(rows, mine)
+    ids = [tuple(int(v) for v in r.tolist()) for r in rows]
+    if not gpus_oversubscribed():
+        seen = {}
+        for r, k in enumerate(ids):
+            if k in seen:
+                raise RuntimeError(f"ranks {seen[k]} and {r} map the same GPU (PCI {k}); "
+                                   "one process per GPU is required (check HIP_VISIBLE_DEVICES / LOCAL_RANK)")
+            seen[k] = r
+    return ids
+
+
+def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_s: Optional[float] = None,
+                  preflight_s: Optional[float] = None):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/...).
 
-    The default process group is ``backend`` (nccl = RCCL when a GPU is
-    present): it carries the data plane (KV migration over xGMI).  The
-    control plane uses a ``control`` group: "shm" (one shared-memory segment
-    on the node, ``ShmComm``; falls back to gloo when the ranks span nodes),
-    "gloo" (host TCP) or "nccl" (RCCL on a high-priority stream, see
-    ``TorchComm``)."""
+    The default process group is always gloo (host TCP): the rendezvous,
+    the setup barriers, and the fallback data plane.  ``backend`` nccl (=
+    RCCL, the default when a GPU is present) adds an RCCL subgroup for the
+    data plane (KV migration over xGMI), admitted only after
+    ``rccl_preflight`` passed on every rank within ``preflight_s``
+    (the first 8-GPU run must fail soft); otherwise the
+    data plane stays on gloo and ``comm.data_backend`` says "gloo-fallback".
+    The control plane uses a ``control`` group: "shm" (one shared-memory
+    segment on the node, ``ShmComm``; falls back to gloo when the ranks span
+    nodes), "gloo" (host TCP) or "nccl" (RCCL on a high-priority stream, see
+    ``TorchComm``; gloo if the RCCL preflight failed)."""
     import datetime
     import os
     import torch
@@ -678,6 +807,8 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_
         return SoloComm()
     if timeout_s is None:
         timeout_s = float(os.environ.get("LLMQ_COLLECTIVE_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+    if preflight_s is None:
+        preflight_s = float(os.environ.get("LLMQ_RCCL_PREFLIGHT_S", "45"))
     shm = control == "shm"
     if shm:
         if single_node():
@@ -691,36 +822,38 @@ def init_from_env(backend: Optional[str] = None, control: str = "gloo", timeout_
     # (10-30 min); RCCL's watchdog aborts a timed-out communicator
     to = datetime.timedelta(seconds=timeout_s)
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl" and gpus_oversubscribed():
+        import sys
+        print("comm: more ranks than GPUs on this node -- RCCL needs one device per rank, "
+              "using gloo for every group (rehearsal layout, not a measurement of xGMI)", file=sys.stderr)
+        backend = control = "gloo"
     if not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl" and gpus_oversubscribed():
-            import sys
-            print("comm: more ranks than GPUs on this node -- RCCL needs one device per rank, "
-                  "using gloo for every group (rehearsal layout, not a measurement of xGMI)", file=sys.stderr)
-            backend = control = "gloo"
-        kw = {}
-        if backend == "nccl":
-            local = local_device_index()
-            torch.cuda.set_device(local)
-            kw["device_id"] = torch.device("cuda", local)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local_device_index())
         store = _restart_store(to)
         if store is not None:
-            dist.init_process_group(backend=backend, timeout=to, store=store, rank=int(os.environ["RANK"]),
-                                    world_size=world, **kw)
+            dist.init_process_group(backend="gloo", timeout=to, store=store, rank=int(os.environ["RANK"]),
+                                    world_size=world)
         else:
-            dist.init_process_group(backend=backend, timeout=to, **kw)
-    default_backend = dist.get_backend()
-    if control == default_backend or (control == "gloo" and default_backend == "gloo"):
-        comm = TorchComm()
+            dist.init_process_group(backend="gloo", timeout=to)
+    data_group, data_backend, preflight = None, "gloo", None
+    if backend == "nccl":
+        check_distinct_devices()
+        data_group, preflight = _rccl_data_group(to, preflight_s)
+        data_backend = "nccl" if data_group is not None else "gloo-fallback"
+    if control == "nccl" and data_group is not None:
+        comm = TorchComm(group=data_group, data_group=data_group)
     else:
-        ctrl = dist.new_group(backend=control, timeout=to)
-        comm = TorchComm(group=ctrl, data_group=dist.group.WORLD,
-                         device=torch.device("cpu") if control == "gloo" else None)
+        comm = TorchComm(data_group=data_group, device=torch.device("cpu"))
+    comm.data_backend, comm.preflight = data_backend, preflight
     if shm:
         job = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT", "0")
         try:
-            return ShmComm(comm, f"/llmq_ctrl_{job}_{os.environ.get('MASTER_PORT', '0')}", timeout_s=timeout_s)
+            sc = ShmComm(comm, f"/llmq_ctrl_{job}_{os.environ.get('MASTER_PORT', '0')}", timeout_s=timeout_s)
+            sc.data_backend, sc.preflight = data_backend, preflight
+            return sc
         except ShmUnavailable as e:                    # raised on every rank together
             import sys
             print(f"comm: shared-memory control plane unavailable ({e}); using the torch group", file=sys.stderr)

@@ -50,7 +50,12 @@ def comm_evidence(comm, dev, world: int, dry: bool, binding: dict = None) -> dic
     if world == 1:
         return ev
     import torch.distributed as dist
-    ev["data_backend"] = dist.get_backend()
+    inner = getattr(comm, "data", comm)
+    group = getattr(inner, "data_group", None)
+    ev["data_backend"] = getattr(comm, "data_backend", None) or dist.get_backend(group)
+    if getattr(comm, "preflight", None) is not None:
+        ev["preflight"] = comm.preflight
+        ev["rccl_world"] = int(comm.preflight.get("rccl_world", 0)) if ev["data_backend"] == "nccl" else 0
     ev["oversubscribed"] = bool(gpus_oversubscribed()) if not dry else False
     if dev.type == "cuda":
         ev["one_gpu_per_rank"] = ev["distinct_devices"] == world
@@ -61,14 +66,14 @@ def comm_evidence(comm, dev, world: int, dry: bool, binding: dict = None) -> dic
     try:
         x = torch.ones(nbytes // 4, dtype=torch.float32, device=tdev)
         for _ in range(2):
-            dist.all_reduce(x)
+            dist.all_reduce(x, group=group)
         iters = 5
         if tdev.type == "cuda":
             torch.cuda.synchronize(tdev)
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
-            dist.all_reduce(x)
+            dist.all_reduce(x, group=group)
         if tdev.type == "cuda":
             torch.cuda.synchronize(tdev)
         dt = (time.perf_counter() - t0) / iters

@@ -53,6 +53,55 @@ def test_bench_single_rank_dry_run():
     lb = d["latency_breakdown"]
     assert set(lb) >= {"ingress", "inbox", "preprocess", "queue", "handoff", "admitted_by_path"}
     assert sum(sum(v) for v in lb["admitted_by_path"].values()) > 0
+    # what one request is: its shape and the GEMM FLOP rate vs peak
+    rs = d["request_shape"]
+    assert rs["gen_tokens"] == 4 and 1 <= rs["mean_prompt_tokens"] <= rs["prompt_cap"]
+    assert abs(rs["tokens_per_request"] - (rs["mean_prompt_tokens"] + 3)) < 0.02
+    assert 0 <= d["mfma_peak_fraction"] < 1 and d["backend_matmul_tflops"] >= 0
+    assert d["config"]["seq_len_is"] == "max_ctx" and d["config"]["max_ctx"] == d["config"]["seq_len"]
+    assert d["realtime_mode"] == d["config"]["realtime_mode"] == "off"
+    assert d["data_plane"] == "none"
+
+
+def test_bench_realtime_micro_mode_dry_run():
+    d = _run([sys.executable, "bench.py", "--cpu-dry-run", "--steps", "4", "--warmup", "2", "--gateway-only-s", "0",
+              "--realtime-mode", "micro", "--micro-slots", "4"])
+    assert d["realtime_mode"] == "micro" and d["config"]["micro"]["slots"] == 4
+    assert d["micro_forwards"]["count"] >= 0 and d["requests_accounted"]["lost"] == 0
+
+
+def _preflight_run(fault):
+    env = dict(os.environ, OMP_NUM_THREADS="1", LLMQ_RCCL_PREFLIGHT_S="3")
+    if fault:
+        env["LLMQ_RCCL_PREFLIGHT_FAULT"] = fault
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                        "--cpu-dry-run", "--data-backend", "nccl", "--steps", "4", "--warmup", "2",
+                        "--gateway-only-s", "0", "--slo-climb", ""],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0]), r.stderr
+
+
+def test_rccl_preflight_hang_falls_back_to_gloo_data_plane():
+    """an RCCL data plane whose preflight hangs (or
+    fails) must not cost the run its headline -- every rank agrees on the
+    gloo fallback, the job serves, and the JSON says so."""
+    d, err = _preflight_run("hang")
+    assert d["data_plane"] == "gloo-fallback" and d["comm"]["data_backend"] == "gloo-fallback"
+    pf = d["comm"]["preflight"]
+    assert not pf["ok_all_ranks"] and "hang" in pf["error"] and pf["wall_ms"] >= 2900
+    assert d["comm"]["rccl_world"] == 0
+    assert d["requests_accounted"]["completed"] > 0 and "falls back to gloo" in err
+
+
+def test_rccl_preflight_failure_falls_back_to_gloo_data_plane():
+    d, _err = _preflight_run("fail")
+    assert d["data_plane"] == "gloo-fallback"
+    assert "injected" in d["comm"]["preflight"]["error"]
+    assert d["requests_accounted"]["completed"] > 0
 
 
 def test_bench_four_ranks_torchrun_dry_run():

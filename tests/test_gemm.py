@@ -475,3 +475,56 @@ def test_tiny_model_fused_head_matches_fp32_argmax():
         assert 0 <= gap <= 1e-3 * ref[i].abs().max().item(), (i, gap)
     # forward() (hidden + the fused head) gives the same tokens: the trunk is deterministic
     assert torch.equal(a.forward(tok, pos, slot, samp).long(), got)
+
+
+# ---------------------------------------------------------------------- split-K for small steps (micro partition)
+def test_split_all_plans_only_when_twice_the_tiles_fit():
+    assert G.split_all(37, 4096, 4096, 32) == 0              # 16 tiles -> 32 K-half blocks on 32 CUs
+    assert G.split_all(37, 6144, 4096, 32) is None           # 24 tiles: 48 blocks would not fit one wave
+    assert G.split_all(300, 4096, 14336, 64) == 0            # 32 tiles on 64 CUs
+    assert G.split_all(37, 4096, 384, 32) is None            # K too short to halve in whole 128-deep steps
+    assert G.split_all(37, 4096, 4096, 0) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K", [(1, 4096), (37, 4096), (64, 14336), (300, 4096)])
+def test_split_k_store_swiglu_residual_match_fp32(T, K):
+    """Every tile split over two K-half blocks (the micro partition's small
+    steps): store, SwiGLU (with row scales) and the residual epilogue equal
+    the fp32 reference of the whole product."""
+    x, w = _rand(T, K, 4096, seed=11 * T + K)
+    ref = x.float() @ w.float().t()
+    out = G.gemm(x, w, split_cus=256).float()
+    assert (out - ref).abs().max().item() <= 0.01 * ref.abs().max().item() + 1e-3
+    res = torch.randn(T, 4096, device=DEV).to(torch.bfloat16)
+    want = res.float() + ref
+    got = G.gemm_residual(x, w, res.clone(), split_cus=256).float()
+    assert (got - want).abs().max().item() <= 0.01 * want.abs().max().item() + 1e-2
+    xs, ws = _rand(T, K, 2 * 1024, seed=7 * T + K)
+    r = torch.rand(G.row_scale_len(T), device=DEV) + 0.5
+    sref = G.swiglu_reference((xs.float() * r[:T, None]).to(torch.bfloat16), ws).float()
+    sout = G.gemm_swiglu(xs, G.swiglu_permute(ws), row_scale=r, split_cus=256).float()
+    assert (sout - sref).abs().max().item() <= 0.02 * sref.abs().max().item() + 1e-3
+
+
+@pytest.mark.gpu
+def test_small_step_forward_matches_the_serving_path():
+    """The 8B-shaped stub's small-step mode (hand-written kernels at any row
+    count, split-K, argmax head) gives the same greedy ids as the serving
+    path (library GEMMs at these row counts) -- the micro-forwards' numerics."""
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
+    cfg = LlamaConfig(vocab=32000, dim=4096, layers=2, heads=32, kv_heads=8, ffn=14336)
+    m = LlamaStub(cfg, slots=8, max_ctx=64, device=DEV, impl="hip", seed=5)
+    T = 40
+    tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
+    pos = torch.arange(T, device=DEV, dtype=torch.int32) % 20
+    slot = (torch.arange(T, device=DEV, dtype=torch.int32) // 20)
+    samp = torch.tensor([19, 39], device=DEV, dtype=torch.long)
+    a = m.hidden(tok, pos, slot, rows=samp).float()
+    m2 = LlamaStub(cfg, slots=8, max_ctx=64, device=DEV, impl="hip", seed=5)
+    b = m2.hidden(tok, pos, slot, rows=samp, small_cus=32).float()
+    assert (a - b).abs().max().item() <= 0.03 * a.abs().max().item()
+    # the small step's head: the argmax epilogue at 2 rows = argmax of the fp32 logits
+    sel = b.to(torch.bfloat16)
+    ids = m2.ops.greedy_head(sel, m2.lm_head, True, min_rows=1)
+    assert ids.tolist() == torch.argmax(sel.float() @ m2.lm_head.float().t(), dim=-1).tolist()

@@ -87,13 +87,19 @@ def test_inflight_timeout_aborts_retries_then_dead_letters():
     gw.tick()
     assert next(r.slot for r in eng.active.values() if r.meta is fresh) in slots
     time.sleep(0.03)                                 # backoff over: the retries re-enter and are admitted
+    # (queue-deadline shedding is covered by tests/test_gateway_retry.py; here
+    # a slow host -- a 40-token CPU forward per tick -- must not shed a retry
+    # that waited out a tick behind the fresh request's steps)
+    gw.shed_expired = False
     for _ in range(40):                              # (the timer thread may run late on a loaded host)
         gw.tick()
         if all(m.status == MessageStatus.PROCESSING for m in msgs):
             break
         time.sleep(0.002)
-    assert all(m.status == MessageStatus.PROCESSING for m in msgs)
-    assert gw.counters["expired"] == 0               # a retry's queue deadline restarted at its requeue
+    gw.shed_expired = True
+    assert all(m.status == MessageStatus.PROCESSING for m in msgs), (
+        [(m.status, m.retry_count) for m in msgs], dict(gw.counters))
+    assert gw.counters["expired"] == 0
     time.sleep(0.2)
     gw.tick()                                        # the retry times out too: retries spent
     assert gw.counters["retry_exhausted"] == 3 and dlq.size() == 3
@@ -274,3 +280,19 @@ def test_gpu_cancelled_slot_reuse_matches_a_fresh_slot():
     s1, t1 = run(True)
     s2, t2 = run(False)
     assert t1 == t2 and len(t1) == 6
+
+
+def test_a_retry_gets_a_fresh_queue_deadline():
+    """A retried request is judged against its REQUEUE time, not its first
+    arrival (its first deadline has passed by definition)."""
+    from llm_message_queue_amd.gateway.gateway_failure import FailureMixin
+    now = time.monotonic_ns()
+    m = Workload(seed=12).make(1)[0]
+    m.timeout = 100_000_000
+    m.arrival_ns = now - 500_000_000
+    m.enqueued_at = now - 10_000_000
+    assert FailureMixin._expired(m, now)                 # first attempt: 500 ms since arrival
+    m.retry_count = 1
+    assert not FailureMixin._expired(m, now)             # retry: 10 ms since its requeue
+    m.enqueued_at = now - 200_000_000
+    assert FailureMixin._expired(m, now)
