@@ -812,6 +812,7 @@ def main(argv=None) -> int:
             with open(a.json_out, "w") as fh:
                 fh.write(line + "\n")
     page.close(unlink=True)
+    engine.close()
     if world > 1:
         import torch.distributed as dist
         if getattr(comm, "data_backend", "") == "gloo-fallback":

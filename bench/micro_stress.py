@@ -27,6 +27,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--stream", default="high", choices=["high", "same", "partition"])
     ap.add_argument("--micro-cus", type=int, default=32)
+    ap.add_argument("--micro-gemm", default="hip", choices=["hip", "rocblas"])
     ap.add_argument("--budget", type=int, default=4096)
     ap.add_argument("--slots", type=int, default=1536)
     ap.add_argument("--blas", default="", choices=["", "lt", "rocblas"],
@@ -47,7 +48,7 @@ def main() -> int:
         torch.backends.cuda.preferred_blas_library("cublaslt" if a.blas == "lt" else "cublas")
     dev = torch.device("cuda", 0)
     eng = BackendEngine(LlamaConfig.llama3_8b(), slots=a.slots, max_ctx=512, token_budget=a.budget, device=dev,
-                        impl="hip", realtime_mode=a.mode, micro_stream=a.stream, micro_cus=a.micro_cus,
+                        impl="hip", realtime_mode=a.mode, micro_stream=a.stream, micro_cus=a.micro_cus, micro_gemm=a.micro_gemm,
                         micro_inflight=a.micro_inflight, step_timeout_s=a.step_timeout)
     eng.warm_shapes()
     eng.time_steps = True
@@ -108,6 +109,7 @@ def main() -> int:
                                   "rt_p99_ms": round(float(np.percentile(la, 99)), 1),
                                   "tok_s": round(eng.total_tokens / (t_rep - t0), 0)}), flush=True)
         eng.finish(block=True)
+        eng.close()
     except BackendHung as e:
         print(json.dumps({"hung": str(e), "t_s": round(time.monotonic() - t0, 1), "micro": eng.micro_steps}),
               flush=True)

@@ -19,6 +19,7 @@
 #include "gemm_kernels.h"
 #include "kv_migrate_kernels.h"
 #include "llama_kernels.h"
+#include "skinny_kernels.h"
 #include "summarise_kernels.h"
 #include "text_kernels.h"
 
@@ -486,6 +487,43 @@ static void kv_move(uintptr_t table, int layers, int slots, int slot, int n, int
   check_launch();
 }
 
+// ---------------------------------------------------------------------- skinny GEMM (M <= 64)
+// C (+)= A . W^T for the small steps (skinny_kernels.h): split-K partials into
+// ws [S][M][N] fp32, then the finalize kernel (row scale, epilogue, bf16).
+static void skinny_gemm(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t rs,
+                        uintptr_t ws, int nsplit, uintptr_t stream) {
+  require(M >= 1 && M <= 64, "skinny_gemm: M must be in [1, 64]");
+  require(N % SK_NB == 0, "skinny_gemm: N must be a multiple of 128");
+  require(nsplit >= 1 && K % (SK_KS * nsplit) == 0, "skinny_gemm: K must be a multiple of 128 * S");
+  require(epi == SK_EPI_STORE || epi == SK_EPI_RESID || epi == SK_EPI_SWIGLU, "skinny_gemm: unknown epilogue");
+  require(epi != SK_EPI_SWIGLU || N % 256 == 0, "skinny_gemm: SwiGLU needs N % 256 == 0");
+  require(a % 16 == 0 && w % 16 == 0 && c % 16 == 0 && ws % 16 == 0 && ws != 0, "skinny_gemm: alignment");
+  require((int64_t)N * K < (int64_t)1 << 31, "skinny_gemm: weight too large");
+  const int mt = (M + 15) / 16;
+  const dim3 grid(N / SK_NB, nsplit);
+  const int kc = K / nsplit;
+  auto* A_ = P<const uint16_t>(a);
+  auto* W_ = P<const uint16_t>(w);
+  auto* ws_ = P<float>(ws);
+  if (mt == 1) hipLaunchKernelGGL(skinny_partial_kernel<1>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
+  else if (mt == 2) hipLaunchKernelGGL(skinny_partial_kernel<2>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
+  else if (mt == 3) hipLaunchKernelGGL(skinny_partial_kernel<3>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
+  else hipLaunchKernelGGL(skinny_partial_kernel<4>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
+  check_launch();
+  const int nout = epi == SK_EPI_SWIGLU ? N / 2 : N;
+  const int threads = M * (nout / 4);
+  const dim3 fgrid((threads + 255) / 256);
+  const float* rs_ = rs ? P<const float>(rs) : nullptr;
+  auto* C_ = P<uint16_t>(c);
+  if (epi == SK_EPI_STORE)
+    hipLaunchKernelGGL(skinny_finalize_kernel<SK_EPI_STORE>, fgrid, dim3(256), 0, S(stream), ws_, nsplit, M, N, rs_, C_);
+  else if (epi == SK_EPI_RESID)
+    hipLaunchKernelGGL(skinny_finalize_kernel<SK_EPI_RESID>, fgrid, dim3(256), 0, S(stream), ws_, nsplit, M, N, rs_, C_);
+  else
+    hipLaunchKernelGGL(skinny_finalize_kernel<SK_EPI_SWIGLU>, fgrid, dim3(256), 0, S(stream), ws_, nsplit, M, N, rs_, C_);
+  check_launch();
+}
+
 // ---------------------------------------------------------------------- CU partitions
 // Which hardware unit a workgroup ran on: HW_ID (cu / sh / se ids, gfx9
 // layout) and XCC_ID, read from the wave's hardware registers by lane 0.
@@ -598,6 +636,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("slot_census", &slot_census);
   m.def("device_info", &device_info);
   m.def("hw_probe", &hw_probe, py::arg("blocks"), py::arg("spin"), py::arg("stream"));
+  m.def("skinny_gemm", &skinny_gemm, py::arg("a"), py::arg("w"), py::arg("c"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("epi"), py::arg("rs"), py::arg("ws"), py::arg("S"), py::arg("stream"));
   m.def("stream_with_cu_mask", &stream_with_cu_mask);
   m.def("stream_destroy", &stream_destroy);
   m.def("kv_move", &kv_move, py::arg("table"), py::arg("layers"), py::arg("slots"), py::arg("slot"), py::arg("n"),

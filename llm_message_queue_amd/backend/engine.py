@@ -80,6 +80,23 @@ class StepResult:
     elapsed_ms: float
 
 
+class _blas:
+    """torch's library-GEMM backend for a block ("cublas" = rocBLAS on ROCm,
+    "cublaslt" = hipBLASLt), restored after it (the serve loop is one thread)."""
+
+    def __init__(self, lib: str):
+        self.lib = lib
+
+    def __enter__(self):
+        self.prev = torch.backends.cuda.preferred_blas_library()
+        torch.backends.cuda.preferred_blas_library(self.lib)
+        return self
+
+    def __exit__(self, *exc):
+        torch.backends.cuda.preferred_blas_library(self.prev)
+        return False
+
+
 class _NullCtx:
     def __enter__(self):
         return self
@@ -124,7 +141,7 @@ class BackendEngine:
                  fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
                  realtime_step_tokens: int = 0, fused_rms=None, realtime_mode: str = "",
                  micro_slots: int = 64, micro_budget: int = 512, micro_inflight: int = 4,
-                 micro_stream: str = "high", micro_cus: int = 16):
+                 micro_stream: str = "high", micro_cus: int = 16, micro_gemm: str = "hip"):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
         self.step_timeout_s = float(step_timeout_s)
@@ -184,6 +201,17 @@ class BackendEngine:
             from ..ops import gemm as _G
             _G.EFFECTIVE_CUS[self.device.index if self.device.index is not None else 0] = big_cus
         self.micro_stream = micro_stream if self.micro else ""
+        # the micro-forwards' GEMMs on a CU partition: "hip" = the hand-written
+        # kernels (split-K small steps), "rocblas" = the library through
+        # rocBLAS (classic, non-persistent kernels: safe on a CU mask, unlike
+        # hipBLASLt's stream-K grids sized for the whole chip)
+        if micro_gemm not in ("hip", "rocblas"):
+            raise ValueError(f"micro_gemm must be hip / rocblas, not {micro_gemm!r}")
+        self.micro_gemm = micro_gemm
+        if self.micro_cus and micro_gemm == "rocblas":
+            import os
+            # rocBLAS may hand some GEMMs to hipBLASLt on gfx950: keep them classic
+            os.environ.setdefault("ROCBLAS_USE_HIPBLASLT", "0")
         self.model = LlamaStub(model_cfg, self.n_all, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
                                fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
@@ -274,7 +302,11 @@ class BackendEngine:
         self.micro_timed = 0
         if self.micro:
             mr = self.micro_inflight + 1
-            self._pins_m = [self._alloc_pin(4 * (7 * self.micro_budget + 2 * self.micro_slots + 64))
+            # a micro step's staging: tokens, pos, slot (3T), samples + decode
+            # gather rows (<= 3T) and ~one 1-token tile per row (4T) -- sized
+            # so it never grows (a grown pinned buffer frees the old one
+            # behind the copies still queued from it)
+            self._pins_m = [self._alloc_pin(4 * (11 * self.micro_budget + 2 * self.micro_slots + 64))
                             for _ in range(mr)]
             self._out_pins_m = [self._alloc_pin(4 * self.micro_slots).view(torch.int32) for _ in range(mr)]
         # segment-tiled MFMA attention on the HIP path (per-token otherwise)
@@ -714,9 +746,14 @@ class BackendEngine:
                     tiles = torch.stack([r, torch.ones_like(r), slot, pos], 1).contiguous() \
                         if self.use_tiles else None
                     samp = torch.arange(min(T, self.micro_slots), device=dev, dtype=torch.long)
-                    self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(),
-                                       slot.contiguous(), samp, tiles=tiles, n_dec=0,
-                                       **({"small_cus": self.micro_cus} if self.micro_cus else {}))
+                    if self.micro_cus and self.micro_gemm == "rocblas":
+                        with _blas("cublas"):
+                            self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(),
+                                               slot.contiguous(), samp, tiles=tiles, n_dec=0)
+                    else:
+                        self.model.forward(torch.zeros(T, dtype=torch.long, device=dev), pos.contiguous(),
+                                           slot.contiguous(), samp, tiles=tiles, n_dec=0,
+                                           **({"small_cus": self.micro_cus} if self.micro_cus else {}))
                     n += 1
                     T *= 2
         torch.cuda.synchronize(dev)
@@ -807,6 +844,19 @@ class BackendEngine:
         self.host_ns[1] += time.perf_counter_ns() - ts
         self._launch_pool(False)
 
+    def close(self) -> None:
+        """Release the CU-partition streams (``micro_stream=partition``):
+        the GPU is drained first, then the runtime streams are destroyed, so
+        nothing references them at interpreter teardown."""
+        if self.micro_cus and self.main_stream is not None:
+            from .. import _native
+            torch.cuda.synchronize(self.device)
+            k = _native.require_hipops()
+            for st in (self.main_stream, self.rt_stream):
+                k.stream_destroy(st.cuda_stream)
+            self.main_stream = self.rt_stream = None
+            self.micro_cus = 0
+
     def stream_ctx(self):
         """Context that makes the serving steps' stream current (a no-op
         unless the chip is CU-partitioned): anything else ordered with the
@@ -861,8 +911,14 @@ class BackendEngine:
             til = d[o_til:].view(NT, 4) if self.use_tiles else None
             ev0 = self._start_event()
             te = time.perf_counter_ns()
-            out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til,
-                                     n_dec=D, **({"small_cus": self.micro_cus} if micro and self.micro_cus else {}))
+            if micro and self.micro_cus and self.micro_gemm == "rocblas":
+                with _blas("cublas"):
+                    out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til,
+                                             n_dec=D)
+            else:
+                out = self.model.forward(tok_d, d[T:2 * T], d[2 * T:3 * T], d[3 * T:o_dec].long(), tiles=til,
+                                         n_dec=D,
+                                         **({"small_cus": self.micro_cus} if micro and self.micro_cus else {}))
             self.host_ns[2] += time.perf_counter_ns() - te
             if not micro:
                 self._census(T)

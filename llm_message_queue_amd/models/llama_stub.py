@@ -236,6 +236,9 @@ class LlamaStub:
         res = F.embedding(tokens, self.embed)            # [T, d], updated in place
         T = res.shape[0]
         small = small_cus > 0 and self.impl == "hip"
+        # M <= 64: the skinny kernel (a stream over the weights) for every
+        # layer GEMM; larger small steps: the 256x256-tile kernel, split-K
+        skinny = small and T <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
         rows_qkv = self.fused_qkv and (T >= self.min_fused_qkv_tokens or small)
         qkv_split = {}
         if small:
@@ -248,7 +251,12 @@ class LlamaStub:
 
         scale = None                                     # row scales of res from the previous down GEMM
         for i, L in enumerate(self.layers):
-            if rows_qkv and self.row_scale_norm:
+            if skinny:
+                qkv = torch.empty((T, L["wqkv"].shape[0]), dtype=res.dtype, device=res.device)
+                G.skinny(res, L["wqkv"], qkv, G.SK_STORE, row_scale=ops.row_rms(res, cfg.eps), cus=small_cus)
+                q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads, self.kcache[i],
+                                self.vcache[i])
+            elif rows_qkv and self.row_scale_norm:
                 q = ops.qkv_rope_rows(res, L["wqkv"], scale if scale is not None else ops.row_rms(res, cfg.eps),
                                       pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads, self.kcache[i],
                                       self.vcache[i], **qkv_split)
@@ -299,17 +307,24 @@ class LlamaStub:
         resid_o = small or (self._cus > 0 and G.residual_tiles_ok(M, cfg.dim, self._cus))
         rms = resid_o and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS and not small
 
+        skinny = small and M <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
+
         def into_res(x, wt, scale_out):                  # res += x · wtᵀ (+ its row scales)
             if rms and scale_out:
                 return G.gemm_residual_rms(x, wt, res, cfg.eps)
-            if resid_o:
+            if skinny:
+                G.skinny(x, wt, res, G.SK_RESID, cus=small_cus)
+            elif resid_o:
                 G.gemm_residual(x, wt, res, split_cus=small_cus)
             else:
                 res.addmm_(x, wt.t())
             return None
 
         scale = into_res(a, L["wo"], rows_mlp and self.row_scale_norm)
-        if rows_mlp and self.row_scale_norm and small:
+        if skinny:
+            act = torch.empty((M, L["w_gu"].shape[0] // 2), dtype=res.dtype, device=res.device)
+            G.skinny(res, L["w_gu"], act, G.SK_SWIGLU, row_scale=ops.row_rms(res, cfg.eps), cus=small_cus)
+        elif rows_mlp and self.row_scale_norm and small:
             act = G.gemm_swiglu(res, L["w_gu"], row_scale=ops.row_rms(res, cfg.eps), split_cus=small_cus)
         elif rows_mlp and self.row_scale_norm:
             act = ops.swiglu_rows(res, L["w_gu"], scale if scale is not None else ops.row_rms(res, cfg.eps))

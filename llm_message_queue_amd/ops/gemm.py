@@ -326,6 +326,60 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
     return q
 
 
+# ---------------------------------------------------------------------- skinny (M <= 64) small steps
+SKINNY_MAX_M = 64
+SK_STORE, SK_RESID, SK_SWIGLU = 0, 1, 2
+_SKINNY_WS = {}
+
+
+def skinny_splits(N: int, K: int, cus: int) -> int:
+    """Split-K factor of a skinny GEMM: the fewest K-splits that give at
+    least two 128-column blocks per CU, each split a multiple of 128 deep
+    and at least 512."""
+    blocks = N // 128
+    best = 1
+    for s in (1, 2, 4, 7, 8, 14, 16):
+        if K % (128 * s) or K // s < 512:
+            continue
+        best = s
+        if blocks * s >= 2 * cus:
+            break
+    return best
+
+
+def skinny(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, row_scale=None, cus: int = 32):
+    """``out`` (+)= ``x`` [M <= 64][K] . ``w`` [N][K]^T on the skinny kernel
+    (``csrc/kernels/skinny_kernels.h``): SK_STORE (out [M][N]), SK_RESID
+    (out += ..., one rounding), SK_SWIGLU (``w`` swiglu-permuted, out [M][N/2]);
+    ``row_scale`` multiplies row i of the product first (the folded RMSNorm).
+    ``cus``: CUs the launch may use (the split-K factor is sized for them)."""
+    _check(x, "x")
+    _check(w, "w")
+    _check(out, "out")
+    M, K = x.shape
+    N = w.shape[0]
+    if w.shape[1] != K or not 1 <= M <= SKINNY_MAX_M or N % 128 or K % 128:
+        raise ValueError(f"skinny: unsupported shape M={M} N={N} K={K}")
+    want = (M, N // 2) if epi == SK_SWIGLU else (M, N)
+    if tuple(out.shape) != want:
+        raise ValueError(f"skinny: out shape {tuple(out.shape)} != {want}")
+    S = skinny_splits(N, K, cus)
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    key = (x.device.type, x.device.index, stream)
+    need = S * M * N
+    ws = _SKINNY_WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = _SKINNY_WS[key] = torch.empty(max(need, SKINNY_MAX_M * 32768), dtype=torch.float32, device=x.device)
+    rs = 0
+    if row_scale is not None:
+        if row_scale.dtype != torch.float32 or not row_scale.is_contiguous() or row_scale.numel() < M:
+            raise ValueError("skinny: row_scale must be contiguous float32 [>= M]")
+        rs = row_scale.data_ptr()
+    _native.require_hipops().skinny_gemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, epi, rs,
+                                         ws.data_ptr(), S, stream)
+    return out
+
+
 _ARGMAX_WS = {}
 
 

@@ -320,7 +320,9 @@ class BackendConfig:
     realtime_mode: str = ""
     micro_slots: int = 64              # micro mode: KV slots of the realtime pool
     micro_inflight: int = 4            # micro mode: micro-forwards queued ahead on their stream
-    micro_stream: str = "high"         # micro mode: "high" (own high-priority stream) or "same"
+    micro_stream: str = "high"         # micro mode: "high" (own stream), "same", "partition" (own CU partition)
+    micro_cus: int = 32                # micro partition: CUs of the realtime partition (a multiple of 8)
+    micro_gemm: str = "hip"            # micro partition: "hip" (hand-written) or "rocblas" GEMMs
     # a forward still incomplete this long after launch = a hung GPU: the
     # serve loop stops with a failure status (BackendHung) so the launcher
     # restarts the job; 0 waits forever.  Below server.stall_fatal_after, so
@@ -546,13 +548,21 @@ def validate(cfg: Config) -> Config:
     b = cfg.backend
     if b.realtime_mode not in ("", "off", "cap", "micro"):
         raise ConfigError("backend.realtime_mode must be off, cap or micro")
-    if b.micro_stream not in ("high", "same") or b.micro_slots < 1 or b.micro_inflight < 1:
-        raise ConfigError("backend.micro_stream must be high or same, micro_slots and micro_inflight >= 1")
+    if b.micro_stream not in ("high", "same", "partition") or b.micro_slots < 1 or b.micro_inflight < 1:
+        raise ConfigError("backend.micro_stream must be high, same or partition; micro_slots, micro_inflight >= 1")
+    if b.micro_cus % 8 or b.micro_cus < 8 or b.micro_gemm not in ("hip", "rocblas"):
+        raise ConfigError("backend.micro_cus must be a positive multiple of 8; micro_gemm hip or rocblas")
     fatal = cfg.server.stall_fatal_after
     if fatal > 0 and b.step_timeout > 0 and fatal <= b.step_timeout:
         # a hung forward stops the ticks: the stall watchdog would end the
-        # process before BackendHung could name the step
-        raise ConfigError("server.stall_fatal_after must exceed backend.step_timeout (both nonzero)")
+        # process before BackendHung could name the step -- the
+        # forward's own deadline is brought under the watchdog's
+        import warnings
+        new = max(S, fatal * 3 // 4)
+        warnings.warn(f"backend.step_timeout {b.step_timeout / S:g}s >= server.stall_fatal_after "
+                      f"{fatal / S:g}s: step_timeout lowered to {new / S:g}s so a hung forward is reported "
+                      "as BackendHung before the stall watchdog ends the process")
+        b.step_timeout = new
     if cfg.server.front_door not in ("native", "python"):
         raise ConfigError("server.front_door must be native or python")
     auth = cfg.security.authentication

@@ -528,3 +528,37 @@ def test_small_step_forward_matches_the_serving_path():
     sel = b.to(torch.bfloat16)
     ids = m2.ops.greedy_head(sel, m2.lm_head, True, min_rows=1)
     assert ids.tolist() == torch.argmax(sel.float() @ m2.lm_head.float().t(), dim=-1).tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 17, 40, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 14336), (6144, 512)])
+def test_skinny_gemm_matches_fp32(M, N, K):
+    """The skinny kernel (M <= 64, weights streamed once, split-K partials
+    summed in order): store and residual epilogues with a row scale, equal to
+    the fp32 reference."""
+    x, w = _rand(M, K, N, seed=3 * M + N + K)
+    r = torch.rand(M, device=DEV) + 0.5
+    ref = (x.float() * r[:, None]) @ w.float().t()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    G.skinny(x, w, out, G.SK_STORE, row_scale=r, cus=32)
+    assert (out.float() - ref).abs().max().item() <= 0.01 * ref.abs().max().item() + 1e-3
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    want = res.float() + x.float() @ w.float().t()
+    got = res.clone()
+    G.skinny(x, w, got, G.SK_RESID, cus=32)
+    assert (got.float() - want).abs().max().item() <= 0.01 * want.abs().max().item() + 1e-2
+    again = res.clone()
+    G.skinny(x, w, again, G.SK_RESID, cus=32)
+    assert torch.equal(got, again)                            # deterministic (partials summed in order)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [3, 64])
+def test_skinny_swiglu_matches_fp32(M):
+    x, w = _rand(M, 4096, 2 * 1536, seed=40 + M)
+    r = torch.rand(M, device=DEV) + 0.5
+    ref = G.swiglu_reference((x.float() * r[:, None]).to(torch.bfloat16), w).float()
+    out = torch.empty(M, 1536, dtype=torch.bfloat16, device=DEV)
+    G.skinny(x, G.swiglu_permute(w), out, G.SK_SWIGLU, row_scale=r, cus=32)
+    assert (out.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-3

@@ -99,8 +99,9 @@ def test_micro_mode_config_validation():
         validate(cfg)
     cfg = default_config()
     cfg.backend.step_timeout = cfg.server.stall_fatal_after
-    with pytest.raises(ConfigError):
+    with pytest.warns(UserWarning):
         validate(cfg)
+    assert 0 < cfg.backend.step_timeout < cfg.server.stall_fatal_after     # (the hung-GPU path is reachable)
     with pytest.raises(ValueError):
         _engine("turbo")
 
