@@ -123,6 +123,11 @@ def parse(argv=None):
                     help="qkv on hipBLASLt + rope_kv instead of the GEMM with the RoPE/KV epilogue (A/B)")
     ap.add_argument("--no-fused-mlp", action="store_true",
                     help="gate/up on hipBLASLt + silu_mul instead of the hand-written SwiGLU GEMM (A/B)")
+    ap.add_argument("--library-gemm", action="store_true",
+                    help="hipBLASLt for the sub-wave o / down projections and small LM heads (round-5 routing); "
+                         "default: every GEMM on the hand-written kernels (skinny below 65 rows, split-K where "
+                         "whole tiles leave CUs idle)")
+    ap.add_argument("--no-library-gemm", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-prune-last", action="store_true",
                     help="run the last layer's o projection and MLP on every row (A/B; default: sampled rows only)")
     ap.add_argument("--split-qkv", action="store_true",
@@ -344,7 +349,8 @@ def main(argv=None) -> int:
                                prune_last=not a.no_prune_last, realtime_step_tokens=a.realtime_step_tokens,
                                realtime_mode=a.realtime_mode, micro_slots=a.micro_slots,
                                micro_inflight=a.micro_inflight, micro_budget=a.micro_budget,
-                               micro_stream=a.micro_stream, micro_cus=a.micro_cus)
+                               micro_stream=a.micro_stream, micro_cus=a.micro_cus,
+                               library_gemm=a.library_gemm)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -717,7 +723,8 @@ def main(argv=None) -> int:
                    "fused_head": bool(engine.model.fused_head),
                    "fused_resid": bool(engine.model.fused_resid), "resid_epi": a.resid_epi,
                    "fused_rms": bool(getattr(engine.model, "fused_rms", False)),
-                   "prune_last": bool(getattr(engine.model, "prune_last", False))},
+                   "prune_last": bool(getattr(engine.model, "prune_last", False)),
+                   "library_gemm": bool(getattr(engine.model, "library_gemm", True))},
         # realtime tier, arrival -> LAST generated token (the 8B backend's 4
         # forwards included); the headline's clock is arrival -> dispatch
         "realtime_p99_e2e_ms": round(lat_done["p99_by_tier_ms"][0], 3),

@@ -141,7 +141,8 @@ class BackendEngine:
                  fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
                  realtime_step_tokens: int = 0, fused_rms=None, realtime_mode: str = "",
                  micro_slots: int = 64, micro_budget: int = 512, micro_inflight: int = 4,
-                 micro_stream: str = "high", micro_cus: int = 16, micro_gemm: str = "hip"):
+                 micro_stream: str = "high", micro_cus: int = 16, micro_gemm: str = "hip",
+                 library_gemm: bool = False):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
         self.step_timeout_s = float(step_timeout_s)
@@ -215,7 +216,8 @@ class BackendEngine:
         self.model = LlamaStub(model_cfg, self.n_all, max_ctx, device=self.device, impl=impl, seed=seed,
                                residual_in_gemm=residual_in_gemm, split_qkv=split_qkv, fused_mlp=fused_mlp,
                                fused_qkv=fused_qkv, row_scale_norm=row_scale_norm, fused_head=fused_head,
-                               fused_resid=fused_resid, fused_rms=fused_rms, prune_last=prune_last)
+                               fused_resid=fused_resid, fused_rms=fused_rms, prune_last=prune_last,
+                               library_gemm=library_gemm)
         self.impl = impl
         self.weight_bytes = self.model.weight_bytes()
         self.active: Dict[int, Request] = {}            # slot -> request

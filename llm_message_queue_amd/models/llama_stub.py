@@ -73,7 +73,7 @@ class LlamaStub:
                  fused_qkv: Optional[bool] = None, min_fused_qkv_tokens: int = 2048, row_scale_norm: bool = True,
                  fused_head: Optional[bool] = None, fused_resid: Optional[bool] = None,
                  fused_rms: Optional[bool] = None,
-                 prune_last: bool = True):
+                 prune_last: bool = True, library_gemm: bool = False):
         if cfg.head_dim != 128:
             raise ValueError("kernels assume head_dim = 128")
         self.cfg = cfg
@@ -129,6 +129,13 @@ class LlamaStub:
         # GEMM, more than the 12.8 us row_rms launch it removes saves
         # (profiles/r5_resid_rms_bench.jsonl, profiles/r5_fused_rms_serving_ab_1gpu.jsonl)
         self.fused_rms = False if fused_rms is None else bool(fused_rms)
+        # False (the default since round 6): no library GEMM at any row
+        # count -- skinny below 65 rows, 256x256 tiles (split-K where whole
+        # tiles leave CUs idle) above, the argmax head at any row count.
+        # True: hipBLASLt where it was faster (sub-wave o / down, the head
+        # under 256 rows); measured equal within 0.4 % on the bench
+        # (profiles/r6_realtime_modes.md).  fused_resid=False keeps the library.
+        self.library_gemm = bool(library_gemm) or impl != "hip" or not self.fused_resid
         self._cus = G._cu_count(self.device) if (self.fused_resid and self.device.type == "cuda") else 0
         # fused paths take the raw residual rows + a per-row RMSNorm scale
         # (True) or an rmsnorm'd copy of the rows (False, A/B)
@@ -209,7 +216,8 @@ class LlamaStub:
         else:
             sel = self.hidden(tokens, pos, slot, tiles=tiles, n_dec=n_dec,
                               small_cus=small_cus).index_select(0, sample_idx)
-        return self.ops.greedy_head(sel, self.lm_head, self.fused_head, min_rows=1 if small_cus else 256)
+        hand = small_cus or not self.library_gemm
+        return self.ops.greedy_head(sel, self.lm_head, self.fused_head, min_rows=1 if hand else 256)
 
     @torch.no_grad()
     def hidden(self, tokens: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor,
@@ -236,15 +244,19 @@ class LlamaStub:
         res = F.embedding(tokens, self.embed)            # [T, d], updated in place
         T = res.shape[0]
         small = small_cus > 0 and self.impl == "hip"
+        nolib = not self.library_gemm and self._cus > 0
         # M <= 64: the skinny kernel (a stream over the weights) for every
         # layer GEMM; larger small steps: the 256x256-tile kernel, split-K
-        skinny = small and T <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
-        rows_qkv = self.fused_qkv and (T >= self.min_fused_qkv_tokens or small)
+        skinny = (small or nolib) and T <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
+        sk_cus = small_cus if small else self._cus
+        rows_qkv = self.fused_qkv and (T >= self.min_fused_qkv_tokens or small or nolib)
         qkv_split = {}
-        if small:
+        if small or nolib:
             d = cfg.dim
-            f = G.split_all(T, (cfg.heads + 2 * cfg.kv_heads) * cfg.head_dim, d, small_cus)
-            qkv_split = {"split": f is not None, "split_full": f}
+            f = G.split_all(T, (cfg.heads + 2 * cfg.kv_heads) * cfg.head_dim, d, sk_cus)
+            # every tile split when twice the tiles fit one wave; else the
+            # default half-empty-last-wave plan (split_plan)
+            qkv_split = {"split": True, "split_full": f} if f is not None else {}
         last = len(self.layers) - 1
         if rows is not None and rows.numel() == T:
             rows = None                                  # every row sampled: nothing to drop
@@ -253,7 +265,7 @@ class LlamaStub:
         for i, L in enumerate(self.layers):
             if skinny:
                 qkv = torch.empty((T, L["wqkv"].shape[0]), dtype=res.dtype, device=res.device)
-                G.skinny(res, L["wqkv"], qkv, G.SK_STORE, row_scale=ops.row_rms(res, cfg.eps), cus=small_cus)
+                G.skinny(res, L["wqkv"], qkv, G.SK_STORE, row_scale=ops.row_rms(res, cfg.eps), cus=sk_cus)
                 q = ops.rope_kv(qkv, pos, slot, self.cos, self.sin, cfg.heads, cfg.kv_heads, self.kcache[i],
                                 self.vcache[i])
             elif rows_qkv and self.row_scale_norm:
@@ -303,19 +315,24 @@ class LlamaStub:
         cfg, ops = self.cfg, self.ops
         M = res.shape[0]
         small = small_cus > 0
-        rows_mlp = self.fused_mlp and (M >= self.min_fused_tokens or small)
-        resid_o = small or (self._cus > 0 and G.residual_tiles_ok(M, cfg.dim, self._cus))
-        rms = resid_o and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS and not small
+        # library-free (``library_gemm`` False): the hand-written kernels at
+        # every row count, split-K where whole tiles leave CUs idle
+        nolib = not small and not self.library_gemm and self._cus > 0
+        cus = small_cus if small else (self._cus if nolib else 0)
+        rows_mlp = self.fused_mlp and (M >= self.min_fused_tokens or small or nolib)
+        tiles_ok = self._cus > 0 and G.residual_tiles_ok(M, cfg.dim, self._cus)
+        resid_o = small or nolib or tiles_ok
+        rms = tiles_ok and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS and not small
 
-        skinny = small and M <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
+        skinny = (small or nolib) and M <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
 
         def into_res(x, wt, scale_out):                  # res += x · wtᵀ (+ its row scales)
             if rms and scale_out:
                 return G.gemm_residual_rms(x, wt, res, cfg.eps)
             if skinny:
-                G.skinny(x, wt, res, G.SK_RESID, cus=small_cus)
+                G.skinny(x, wt, res, G.SK_RESID, cus=cus)
             elif resid_o:
-                G.gemm_residual(x, wt, res, split_cus=small_cus)
+                G.gemm_residual(x, wt, res, split_cus=cus if (small or not tiles_ok) else 0)
             else:
                 res.addmm_(x, wt.t())
             return None
@@ -323,9 +340,10 @@ class LlamaStub:
         scale = into_res(a, L["wo"], rows_mlp and self.row_scale_norm)
         if skinny:
             act = torch.empty((M, L["w_gu"].shape[0] // 2), dtype=res.dtype, device=res.device)
-            G.skinny(res, L["w_gu"], act, G.SK_SWIGLU, row_scale=ops.row_rms(res, cfg.eps), cus=small_cus)
-        elif rows_mlp and self.row_scale_norm and small:
-            act = G.gemm_swiglu(res, L["w_gu"], row_scale=ops.row_rms(res, cfg.eps), split_cus=small_cus)
+            G.skinny(res, L["w_gu"], act, G.SK_SWIGLU, row_scale=ops.row_rms(res, cfg.eps), cus=cus)
+        elif rows_mlp and self.row_scale_norm and (small or nolib):
+            act = G.gemm_swiglu(res, L["w_gu"], row_scale=scale if scale is not None else ops.row_rms(res, cfg.eps),
+                                split_cus=cus)
         elif rows_mlp and self.row_scale_norm:
             act = ops.swiglu_rows(res, L["w_gu"], scale if scale is not None else ops.row_rms(res, cfg.eps))
         elif rows_mlp:

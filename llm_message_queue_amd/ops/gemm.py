@@ -119,7 +119,10 @@ def _launch(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, group
     if not supported(M, N, K):
         raise ValueError(f"gemm: unsupported shape M={M} N={N} K={K}")
     stream = torch.cuda.current_stream(x.device).cuda_stream
-    f = split_all(M, N, K, split_cus) if split_cus else None
+    f = None
+    if split_cus:                                      # every tile split, else only a half-empty last wave
+        f = split_all(M, N, K, split_cus)
+        f = split_plan(M, N, K, split_cus) if f is None else f
     ws = cnt = 0
     if f is not None:
         n_split = (M + TILE_M - 1) // TILE_M * (N // TILE_N) - f
@@ -135,7 +138,7 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, row_scale=N
     """x [M][K] · w[N][K]ᵀ -> [M][N] bf16 on the hand-written kernel
     (``row_scale`` [M] fp32: output row i is multiplied by row_scale[i];
     ``split_cus``: run split-K when the tiles cannot fill that many CUs,
-    :func:`split_all`)."""
+    :func:`split_all`, or on a half-empty last wave, :func:`split_plan`)."""
     _check(x, "x")
     _check(w, "w")
     y = out if out is not None else torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)

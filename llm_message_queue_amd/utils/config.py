@@ -323,6 +323,7 @@ class BackendConfig:
     micro_stream: str = "high"         # micro mode: "high" (own stream), "same", "partition" (own CU partition)
     micro_cus: int = 32                # micro partition: CUs of the realtime partition (a multiple of 8)
     micro_gemm: str = "hip"            # micro partition: "hip" (hand-written) or "rocblas" GEMMs
+    library_gemm: bool = False         # True: hipBLASLt for the sub-wave o / down and small heads
     # a forward still incomplete this long after launch = a hung GPU: the
     # serve loop stops with a failure status (BackendHung) so the launcher
     # restarts the job; 0 waits forever.  Below server.stall_fatal_after, so

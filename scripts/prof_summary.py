@@ -16,6 +16,8 @@ from collections import defaultdict
 
 CATEGORIES = [
     ("gemm+swiglu (HIP)", re.compile(r"gemm_bf16_kernel")),
+    ("skinny gemm (HIP)", re.compile(r"skinny_(partial|finalize)_kernel")),
+    ("lm-head argmax (HIP)", re.compile(r"gemm_argmax_reduce_kernel")),
     ("gemm (hipBLASLt)", re.compile(r"^(Custom_)?Cijk_|gemm|Gemm")),
     ("attention (HIP)", re.compile(r"attention|attn")),
     ("rmsnorm (HIP)", re.compile(r"rmsnorm")),

@@ -334,7 +334,7 @@ def test_8b_model_residual_gemm_matches_hipblaslt_path():
         pytest.skip(f"{a._cus} CUs: T = {T} is not a whole wave of tiles here")
     called = []
     orig, orig_rms = G.gemm_residual, G.gemm_residual_rms
-    G.gemm_residual = lambda *x: (called.append(1), orig(*x))[1]
+    G.gemm_residual = lambda *x, **kw: (called.append(1), orig(*x, **kw))[1]
     G.gemm_residual_rms = lambda *x: (called.append(1), orig_rms(*x))[1]      # (with the row scales)
     try:
         tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
@@ -514,7 +514,7 @@ def test_small_step_forward_matches_the_serving_path():
     path (library GEMMs at these row counts) -- the micro-forwards' numerics."""
     from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
     cfg = LlamaConfig(vocab=32000, dim=4096, layers=2, heads=32, kv_heads=8, ffn=14336)
-    m = LlamaStub(cfg, slots=8, max_ctx=64, device=DEV, impl="hip", seed=5)
+    m = LlamaStub(cfg, slots=8, max_ctx=64, device=DEV, impl="hip", seed=5, library_gemm=True)
     T = 40
     tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
     pos = torch.arange(T, device=DEV, dtype=torch.int32) % 20
@@ -562,3 +562,66 @@ def test_skinny_swiglu_matches_fp32(M):
     out = torch.empty(M, 1536, dtype=torch.bfloat16, device=DEV)
     G.skinny(x, G.swiglu_permute(w), out, G.SK_SWIGLU, row_scale=r, cus=32)
     assert (out.float() - ref).abs().max().item() <= 0.02 * ref.abs().max().item() + 1e-3
+
+
+def test_split_cus_falls_back_to_the_tail_plan():
+    """``split_cus`` splits every tile when twice the tiles fit one wave, else
+    only a half-empty last wave (what the library-free path relies on)."""
+    assert G.split_all(300, 4096, 4096, 224) == 0            # 32 tiles -> 64 blocks
+    assert G.split_all(3000, 4096, 4096, 224) is None        # 192 tiles: whole
+    assert G.split_plan(3000, 4096, 4096, 224) is None       # one 86 % wave
+    assert G.split_plan(4041, 4096, 14336, 224) == 224       # 256 tiles: 224 whole + 32 split
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 37, 300, 900, 3000, 4041])
+@pytest.mark.parametrize("K", [4096, 14336])
+def test_library_free_residual_matches_fp32(T, K):
+    """o / down into the residual on the hand-written kernels at every row
+    count the serving steps produce: the skinny kernel
+    for T <= 64, 256x256 tiles with split-K otherwise -- each equal to the
+    fp32 ``res + x·wᵀ`` and to hipBLASLt's beta = 1 ``addmm_`` within one
+    bf16 rounding of the output."""
+    cus = G._cu_count(DEV)
+    x, w = _rand(T, K, 4096, seed=T + K)
+    res = torch.randn(T, 4096, device=DEV).to(torch.bfloat16)
+    want = res.float() + x.float() @ w.float().t()
+    got = res.clone()
+    if T <= G.SKINNY_MAX_M:
+        G.skinny(x, w, got, G.SK_RESID, cus=cus)
+    else:
+        G.gemm_residual(x, w, got, split_cus=cus)
+    tol = 0.01 * want.abs().max().item() + 1e-2
+    assert (got.float() - want).abs().max().item() <= tol
+    lib = res.clone().addmm_(x, w.t())
+    assert (got.float() - lib.float()).abs().max().item() <= tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 40, 300, 900])
+def test_library_free_model_matches_the_default_routing(T):
+    """``library_gemm=False`` (no hipBLASLt call in the forward) gives the
+    same hidden rows as the default routing to bf16 tolerance and the same
+    greedy ids."""
+    from llm_message_queue_amd.models.llama_stub import LlamaConfig, LlamaStub
+    cfg = LlamaConfig(vocab=32000, dim=4096, layers=2, heads=32, kv_heads=8, ffn=14336)
+    tok = torch.randint(0, cfg.vocab, (T,), device=DEV)
+    pos = torch.arange(T, device=DEV, dtype=torch.int32) % 64
+    slot = (torch.arange(T, device=DEV, dtype=torch.int32) // 64)
+    samp = torch.arange(min(T, 63), T, 64, device=DEV, dtype=torch.long)
+    if samp.numel() == 0:
+        samp = torch.tensor([T - 1], device=DEV, dtype=torch.long)
+    out = []
+    for lib in (True, False):
+        m = LlamaStub(cfg, slots=16, max_ctx=64, device=DEV, impl="hip", seed=5, library_gemm=lib)
+        out.append((m.hidden(tok, pos, slot, rows=samp).float(),
+                    m.forward(tok, pos, slot, sample_idx=samp).tolist()))
+    a, b = out[0][0], out[1][0]
+    assert (a - b).abs().max().item() <= 0.03 * a.abs().max().item()
+    # greedy ids agree wherever the top-2 logit gap exceeds the routing's difference
+    W = m.lm_head.float()
+    la, lb = a.to(torch.bfloat16).float() @ W.t(), b.to(torch.bfloat16).float() @ W.t()
+    top = torch.topk(la, 2, dim=-1).values
+    clear = ((top[:, 0] - top[:, 1]) > 2 * (la - lb).abs().max(dim=-1).values).tolist()
+    for i, (x, y) in enumerate(zip(out[0][1], out[1][1])):
+        assert x == y or not clear[i]
