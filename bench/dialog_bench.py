@@ -186,9 +186,11 @@ def main(argv=None) -> int:
             if batch:
                 gw.submit(batch)
 
-        keys = ("kv_migrated", "kv_migrate_replays", "remote_sent", "remote_recv", "dispatched")
+        keys = ("kv_migrated", "kv_migrate_replays", "remote_sent", "remote_recv", "dispatched",
+                "dialog_ids_real", "dialog_ids_placeholder", "hist_tokens_sent", "hist_tokens_recv")
         c0 = {k: gw.counters[k] for k in keys}
         tok0, reuse0, imp0 = engine.total_tokens, engine.kv_reused_tokens, engine.kv_imported
+        rp0 = (getattr(engine, "replay_tokens", 0), getattr(engine, "replay_nonzero", 0))
         bytes0 = gw.migrator.bytes_sent if gw.migrator is not None else 0
         dsync()
         comm.barrier()
@@ -210,7 +212,9 @@ def main(argv=None) -> int:
         row = [finished[0], engine.total_tokens - tok0, engine.kv_reused_tokens - reuse0,
                engine.kv_imported - imp0,
                (gw.migrator.bytes_sent - bytes0) if gw.migrator is not None else 0] \
-            + [gw.counters[k] - c0[k] for k in keys] + [target, int(el * 1e6)]
+            + [gw.counters[k] - c0[k] for k in keys] \
+            + [getattr(engine, "replay_tokens", 0) - rp0[0], getattr(engine, "replay_nonzero", 0) - rp0[1]] \
+            + [target, int(el * 1e6)]
         rows = comm.all_gather_i64(np.array(row, dtype=np.int64))
         done = comm.all_gather_i64(gw.rec_done.arr.reshape(-1)).sum(axis=0).reshape(gw.rec_done.arr.shape)
         lat = LatencyRecorder(len(gw.tiers)).summary(done, done)
@@ -221,6 +225,10 @@ def main(argv=None) -> int:
                 "forward_tokens_per_turn": round(int(tot[1]) / max(1, int(tot[0])), 1),
                 "kv_reused_tokens": int(tot[2]), "kv_imported": int(tot[3]), "kv_bytes_moved": int(tot[4]),
                 **{k: int(tot[5 + i]) for i, k in enumerate(keys)},
+                # real dialog context: replayed history tokens and how many are
+                # not 0 (the round-5 placeholders were all 0)
+                "replay_history_tokens": int(tot[5 + len(keys)]),
+                "replay_history_nonzero": int(tot[6 + len(keys)]),
                 "p50_turn_ms": round(lat["p50_ms"], 2), "p99_turn_ms": round(lat["p99_ms"], 2),
                 "by_rank": {"turns_completed": rows[:, 0].tolist(), "forward_tokens": rows[:, 1].tolist(),
                             "kv_reused_tokens": rows[:, 2].tolist(),

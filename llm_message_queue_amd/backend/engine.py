@@ -68,6 +68,10 @@ class Request:
     # the greedy token ids this attempt generated, read back from the device
     # with the step that sampled them (set when the request completes)
     out_tokens: Optional[np.ndarray] = None
+    # a conversation turn dispatched by another router: its ``out_tokens``
+    # go back with the completion record even when ``conv`` is -1 (no KV
+    # residency), so the origin's dialog history holds the real ids
+    dialog: bool = False
 
 
 @dataclass
@@ -240,6 +244,8 @@ class BackendEngine:
         self.kv_evictions = 0
         self.kv_imported = 0
         self.kv_stale = 0                                   # parked copies found outdated at admission
+        self.replay_tokens = 0                              # dialog tokens prefilled by non-resident replays
+        self.replay_nonzero = 0                             # ... of which not the id 0 (placeholders were 0)
         self._importing: Dict[int, int] = {}                # slot -> conv: KV arriving (migration in flight)
         # per-slot host state (the batch builder is vectorised over these)
         self.s_prompt = np.zeros((n_all, max_ctx), dtype=np.int32)
@@ -540,6 +546,8 @@ class BackendEngine:
                     keep = room - len(pre)
                     h = hist[len(hist) - keep:] if 0 < keep < len(hist) else (hist if keep > 0 else hist[:0])
                     r.prompt = np.concatenate([pre % self.cfg.vocab, h % self.cfg.vocab, r.prompt])
+                    self.replay_tokens += len(pre) + len(h)
+                    self.replay_nonzero += int(np.count_nonzero(pre)) + int(np.count_nonzero(h))
             r.slot = s
             r.reused = base
             r.prefilled = 0

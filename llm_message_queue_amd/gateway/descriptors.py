@@ -28,8 +28,9 @@ K_HIST = 8
 # payload columns, their count in col 10 (dialog turns: the origin's history)
 DESC_HDR = 17       # [kind, handle lo/hi, origin, tier, arrival lo/hi, enq lo/hi, gen, plen, flags, conv lo/hi,
 #                    dialog history length, decision - enq (us), processing timeout (ms)];
-#                    flags = (home GPU + 1) | KV_MIGRATE
+#                    flags = (home GPU + 1) | KV_MIGRATE | DIALOG_TURN
 KV_MIGRATE = 1 << 8     # descriptor flag: hold the turn until its KV arrives from the home GPU
+DIALOG_TURN = 1 << 9    # descriptor flag: a conversation turn -- its generated ids go back with K_DONE
 
 
 def conv_key(conversation_id: str) -> int:

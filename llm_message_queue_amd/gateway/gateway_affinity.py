@@ -43,8 +43,9 @@ class AffinityMixin:
             p = np.zeros(1, dtype=np.int32)                   # (the engine's stand-in for an empty prompt)
         h = self.conv_hist.get(cid)
         g = max(0, self.gen_tokens - 1)
-        gen = np.asarray(tokens, dtype=np.int32)[:g] if tokens is not None and len(tokens) >= g \
-            else np.zeros(g, dtype=np.int32)
+        real = tokens is not None and len(tokens) >= g
+        gen = np.asarray(tokens, dtype=np.int32)[:g] if real else np.zeros(g, dtype=np.int32)
+        self.counters["dialog_ids_real" if real else "dialog_ids_placeholder"] += 1
         add = np.concatenate([p, gen])
         h = add if h is None else np.concatenate([h, add])[-self.history_cap:]
         self.conv_hist[cid] = h

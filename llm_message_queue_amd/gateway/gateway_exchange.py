@@ -26,7 +26,7 @@ import numpy as np
 from ..backend.engine import Request
 from ..models.message import Message, MessageStatus
 from ..parallel import planner
-from .descriptors import (DESC_HDR, FAIL_UNTOUCHED, K_CANCEL, K_CANCELLED, K_DISPATCH, K_DONE, K_FAIL,
+from .descriptors import (DESC_HDR, DIALOG_TURN, FAIL_UNTOUCHED, K_CANCEL, K_CANCELLED, K_DISPATCH, K_DONE, K_FAIL,
                           K_HIST, K_MIGRATE, K_TIMEOUT, KV_MIGRATE, _get64, _put64, conv_key)
 
 HIST_LEN_BITS = 20      # descriptor col 14: dialog history length | (compressed-context length << 20)
@@ -347,7 +347,7 @@ class ExchangeMixin:
             ctx.append((hist, pre))
             small[k, 0] = m.tier
             small[k, 1] = len(p)
-            small[k, 2] = (mf + 1) | KV_MIGRATE if mf >= 0 else 0
+            small[k, 2] = ((mf + 1) | KV_MIGRATE if mf >= 0 else 0) | (DIALOG_TURN if cid else 0)
             small[k, 3] = (0 if hist is None else min(len(hist), (1 << HIST_LEN_BITS) - 1)) \
                 | ((0 if pre is None else min(len(pre), 255)) << HIST_LEN_BITS)
             # decision time as microseconds after enqueue (the destination
@@ -392,6 +392,7 @@ class ExchangeMixin:
             pre = np.zeros(0, np.int32) if pre is None else np.asarray(pre, dtype=np.int32)
             hist = np.zeros(0, np.int32) if hist is None else np.asarray(hist, dtype=np.int32)
             allt = np.concatenate([pre, hist])
+            self.counters["hist_tokens_sent"] += len(allt)
             for off in range(0, len(allt), cap):
                 n = min(cap, len(allt) - off)
                 row = out[k]
@@ -424,6 +425,7 @@ class ExchangeMixin:
         ready = []
         for h, buf in parts.items():
             hl, pl = self._hist_len.pop((src, h))
+            self.counters["hist_tokens_recv"] += len(buf)
             r = self._hist_wait.pop((src, h), None)
             if r is None:
                 continue                              # (admitted resident, cancelled or handed back)
@@ -450,10 +452,10 @@ class ExchangeMixin:
         dec = enq + rows[:, 15].astype(np.int64) * 1000
         out = []
         mask = (1 << HIST_LEN_BITS) - 1
-        for k, (h, a, e, c, d, origin, tier, gen, plen, hv, to_ms) in enumerate(zip(
+        for k, (h, a, e, c, d, origin, tier, gen, plen, hv, to_ms, fl) in enumerate(zip(
                 handle.tolist(), arrival.tolist(), enq.tolist(), ck.tolist(), dec.tolist(), rows[:, 3].tolist(),
                 rows[:, 4].tolist(), rows[:, 9].tolist(), rows[:, 10].tolist(), rows[:, 14].tolist(),
-                rows[:, 16].tolist())):
+                rows[:, 16].tolist(), rows[:, 11].tolist())):
             self._next_req += 1
             hl, pl = hv & mask, hv >> HIST_LEN_BITS
             # the dialog context's LENGTH travels here (a resident turn only
@@ -464,7 +466,7 @@ class ExchangeMixin:
                                gen_tokens=gen, tier=tier, meta=(origin, h, tier, a, e, d), conv=c,
                                history=np.zeros(hl, dtype=np.int32) if hl > 0 else None,
                                prefix=np.zeros(pl, dtype=np.int32) if pl > 0 else None,
-                               timeout_ns=int(to_ms) * 1_000_000))
+                               timeout_ns=int(to_ms) * 1_000_000, dialog=bool(fl & DIALOG_TURN)))
         return out
 
     def _remote_done_rows(self, rows: np.ndarray) -> None:

@@ -181,7 +181,8 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
                          "remote_sent": 0, "remote_recv": 0, "evacuated": 0, "handed_back": 0, "expired": 0,
                          "overcommit": 0, "kv_migrated": 0, "kv_migrate_replays": 0, "realtime_local": 0,
                          "extra_steps": 0, "extra_admitted": 0, "retried": 0, "retry_exhausted": 0,
-                         "inflight_timeout": 0, "cancelled": 0}
+                         "inflight_timeout": 0, "cancelled": 0, "dialog_ids_real": 0, "dialog_ids_placeholder": 0,
+                         "hist_tokens_sent": 0, "hist_tokens_recv": 0}
         # In-flight processing timeout: the reference runs every message under
         # context.WithTimeout(msg.Timeout) and retries / dead-letters it on
         # expiry (`internal/priorityqueue/worker.go:162-188, 202-239`).  Here a
@@ -633,7 +634,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
             else:
                 origin, handle, tier = self.foreign.pop(r.req_id)
                 self._done_owed[origin].append((handle, tier, r.admitted_ns, r.done_ns, K_DONE))
-                if r.conv >= 0 and r.out_tokens is not None:       # a dialog turn: its ids go home
+                if (r.conv >= 0 or r.dialog) and r.out_tokens is not None:   # a dialog turn: its ids go home
                     self._done_tok[origin][handle] = r.out_tokens
 
     def tick(self, pump=None):

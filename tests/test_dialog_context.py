@@ -159,13 +159,18 @@ def test_remote_replay_carries_the_real_history():
     assert np.array_equal(h2[len(hist) + len(p2):] % MICRO.vocab, np.asarray(ids2[:-1]))
 
 
-def test_k_done_records_carry_generated_ids_home():
+@pytest.mark.parametrize("residency", [True, False])
+def test_k_done_records_carry_generated_ids_home(residency):
     """A dialog turn run on another rank: its generated ids travel back in
-    the completion record and extend the origin's history."""
+    the completion record and extend the origin's history -- also with KV
+    residency off (the descriptor's conversation key is then -1; the
+    DIALOG_TURN flag still marks it a dialog turn)."""
     W = 2
     comms = FakeComm.make(W, timeout_s=20)
     gws = [Gateway(_cfg("round_robin"), engine=_eng(seed=7), comm=comms[r], use_gpu_preprocess=False,
                    prompt_cap=12, gen_tokens=3) for r in range(W)]
+    for g in gws:
+        g.kv_residency = residency
     outs = [[], []]
     for g, o in zip(gws, outs):
         _record_outputs(g.engine, o)
@@ -181,6 +186,8 @@ def test_k_done_records_carry_generated_ids_home():
         ids = next(x[1] for x in outs[1] if isinstance(x[0], tuple) and x[0][1] == t.handle)
         h = gws[0].conv_hist[t.conversation_id]
         assert h[-2:].tolist() == ids[:-1]
+    assert gws[0].counters["dialog_ids_placeholder"] == 0
+    assert gws[0].counters["dialog_ids_real"] == len(turns)
 
 
 def test_evicted_window_prefix_is_prepended_to_a_replay():
