@@ -166,12 +166,14 @@ __device__ __forceinline__ void gm_stage(__amdgpu_buffer_rsrc_t rs, uint32_t v0,
     GM_FENCE();                       \
   } while (0)
 
-template <int EPI, bool STAGGER = true, int SCHED = 2>
-__global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
-    const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
-    int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp,
-    const GmSide am) {
-  extern __shared__ __align__(16) uint8_t smem[];
+// One output tile (or one K-half of a split tile): block ``bid`` of the
+// launch's block order.  gemm_bf16_kernel runs one per block, or -- PERSIST --
+// a grid of at most one block per CU walks bid, bid + gridDim.x, ...
+template <int EPI, bool STAGGER, int SCHED>
+__device__ __forceinline__ void gemm_tile(
+    uint8_t* __restrict__ smem, const uint16_t* __restrict__ A, const uint16_t* __restrict__ W,
+    uint16_t* __restrict__ C, int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope& rp,
+    const GmSplit& sp, const GmSide& am, const int bid) {
   static_assert(EPI != GM_EPI_RESID_PRE || SCHED >= 1, "the residual prefetch is issued by the SCHED >= 1 prologue");
 
   const int tiles_m = (M + GM_BM - 1) / GM_BM;
@@ -180,7 +182,6 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   const int full = sp.ws ? sp.full : nwg;
   // XCD-contiguous remap (bijective for any count) of the whole tiles, then
   // 8-M-tile grouping; split tiles take two consecutive blocks
-  const int bid = blockIdx.x;
   int pid, khalf = -1;
   if (bid < full) {
     const int xcd = bid & 7, loc = bid >> 3, q8 = full >> 3, r8 = full & 7;
@@ -930,12 +931,37 @@ __global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
   if constexpr (SCHED == 8 || SCHED == 9) {
     const uint64_t st_t1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
     if (tid == 0 && am.pv != nullptr) {
-      uint64_t* dbg = reinterpret_cast<uint64_t*>(am.pv) + (size_t)blockIdx.x * 4;
+      uint64_t* dbg = reinterpret_cast<uint64_t*>(am.pv) + (size_t)bid * 4;
       dbg[0] = st_t0;
       dbg[1] = st_t1;
       dbg[2] = st_r0;
       dbg[3] = st_r1;
     }
+  }
+}
+
+// PERSIST: the grid (host: at most one block per CU the stream can use, so
+// every block is resident -- a split tile's second half may wait for its
+// first) walks the block order with stride gridDim.x.  Block b keeps XCD
+// b % 8 (gridDim.x % 8 == 0), so the XCD-contiguous tile runs are unchanged;
+// what changes is that a tile's epilogue stores drain while the same block
+// issues the next tile's prologue DMA, instead of the CU idling between a
+// block's exit and the next block's first loads.
+template <int EPI, bool STAGGER = true, int SCHED = 2, bool PERSIST = false>
+__global__ __launch_bounds__(GM_THREADS) void gemm_bf16_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, uint16_t* __restrict__ C,
+    int M, int N, int K, int group_m, const float* __restrict__ rs, const GmRope rp, const GmSplit sp,
+    const GmSide am) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  if constexpr (PERSIST) {
+    const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+    const int nb = sp.ws ? sp.full + 2 * (tiles - sp.full) : tiles;
+    for (int vb = blockIdx.x; vb < nb; vb += gridDim.x) {
+      gemm_tile<EPI, STAGGER, SCHED>(smem, A, W, C, M, N, K, group_m, rs, rp, sp, am, vb);
+      __syncthreads();                             // the tile's LDS reads retire before the next DMA
+    }
+  } else {
+    gemm_tile<EPI, STAGGER, SCHED>(smem, A, W, C, M, N, K, group_m, rs, rp, sp, am, (int)blockIdx.x);
   }
 }
 

@@ -201,20 +201,33 @@ static void rmsnorm(uintptr_t x, uintptr_t res, uintptr_t w, uintptr_t y, int T,
 
 // C = A · Wᵀ (epi 0, C [M][N]) or H = silu(A·Wgᵀ) * (A·Wuᵀ) over a
 // swiglu-permuted W (epi 2, C [M][N/2]); A [M][K], W [N][K], bf16.
+// persist_cus > 0: the persistent form (gemm_bf16_kernel PERSIST) on a grid of
+// min(blocks, persist_cus) -- persist_cus must not exceed the CUs the stream
+// can run on (every block resident; a multiple of 8 keeps blocks on their XCD)
 template <int EPI, bool STAGGER = true, int SCHED = 2>
 static void launch_gemm(const uint16_t* a, const uint16_t* w, uint16_t* c, int M, int N, int K, hipStream_t st,
                         int group_m, const float* rs = nullptr, const GmRope& rp = GmRope{},
                         const GmSplit& sp = GmSplit{0, nullptr, nullptr},
-                        const GmSide& am = GmSide{}) {
-  static bool attr = false;
+                        const GmSide& am = GmSide{}, int persist_cus = 0) {
+  static bool attr = false, attr_p = false;
+  const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  const int nb = sp.ws ? sp.full + 2 * (tiles - sp.full) : tiles;
+  if (persist_cus > 0 && nb > persist_cus) {
+    if (!attr_p) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, gm_lds_bytes<EPI>()));
+      attr_p = true;
+    }
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED, true>), dim3(persist_cus), dim3(GM_THREADS),
+                       gm_lds_bytes<EPI>(), st, a, w, c, M, N, K, group_m, rs, rp, sp, am);
+    return;
+  }
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, STAGGER, SCHED>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, gm_lds_bytes<EPI>()));
     attr = true;
   }
-  const int tiles = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
-  const int grid = sp.ws ? sp.full + 2 * (tiles - sp.full) : tiles;
-  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(grid), dim3(GM_THREADS), gm_lds_bytes<EPI>(), st,
+  hipLaunchKernelGGL((gemm_bf16_kernel<EPI, STAGGER, SCHED>), dim3(nb), dim3(GM_THREADS), gm_lds_bytes<EPI>(), st,
                      a, w, c,
                      M, N, K, group_m, rs, rp, sp, am);
 }
@@ -251,8 +264,21 @@ static void gemm_residual_rms(uintptr_t a, uintptr_t w, uintptr_t c, int M, int 
 // (GmSplit; epilogues store / SwiGLU / residual-LDS): a step too small to
 // fill its CUs with whole tiles -- the realtime micro-forwards on their CU
 // partition, where o / down are 16 tiles for 32 CUs.
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return 0;
+  if (!cus[dev]) HIP_CHECK(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  return cus[dev];
+}
+
+constexpr int GM_PERSIST_FLAG = 256;   // epi | flag: the persistent grid (one block per CU of the device)
+
 static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t stream,
                       int group_m, uintptr_t rs, int split_full, uintptr_t split_ws, uintptr_t split_cnt) {
+  const int pc = (epi & GM_PERSIST_FLAG) ? device_cus() & ~7 : 0;
+  epi &= ~GM_PERSIST_FLAG;
   require(group_m >= 1 && group_m <= 64, "gemm: group_m out of range");
   require(M > 0 && N > 0 && K > 0, "gemm: empty operand");
   require(N % GM_BN == 0, "gemm: N must be a multiple of 256");
@@ -271,15 +297,15 @@ static void gemm_bf16(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K
   }
   if (epi == GM_EPI_STORE)
     launch_gemm<GM_EPI_STORE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m,
-                              rsp, GmRope{}, sp);
+                              rsp, GmRope{}, sp, GmSide{}, pc);
   else if (epi == GM_EPI_SWIGLU)
     launch_gemm<GM_EPI_SWIGLU>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m,
-                               rsp, GmRope{}, sp);
+                               rsp, GmRope{}, sp, GmSide{}, pc);
   else if (epi == GM_EPI_RESID)                    // C += A·Wᵀ in place (no row scales)
     launch_gemm<GM_EPI_RESID>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream), group_m);
   else if (epi == GM_EPI_RESID_LDS)                // the same, residual tile staged by DMA (A/B)
     launch_gemm<GM_EPI_RESID_LDS>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
-                                  group_m, nullptr, GmRope{}, sp);
+                                  group_m, nullptr, GmRope{}, sp, GmSide{}, pc);
   else if (epi == GM_EPI_RESID_PRE)                // ... with its first quarter prefetched at start (A/B)
     launch_gemm<GM_EPI_RESID_PRE>(P<const uint16_t>(a), P<const uint16_t>(w), P<uint16_t>(c), M, N, K, S(stream),
                                   group_m);

@@ -4,8 +4,8 @@ unpacks into an engine request (``_foreign_requests``), and a completion
 record completes the origin's message (``_remote_done_rows``)."""
 import numpy as np
 
-from llm_message_queue_amd.gateway.descriptors import (DESC_HDR, K_DISPATCH, K_DONE, KV_MIGRATE, _get64, _put64,
-                                                       conv_key)
+from llm_message_queue_amd.gateway.descriptors import (DESC_HDR, DIALOG_TURN, K_DISPATCH, K_DONE, KV_MIGRATE, _get64,
+                                                       _put64, conv_key)
 from tests.test_tier_caps import _gateway
 
 
@@ -39,7 +39,8 @@ def test_descriptor_roundtrip():
     buf = np.zeros((len(msgs), DESC_HDR + cap), dtype=np.int32)
     gw._fill_descs(buf, msgs, 3, cap, {id(msgs[2]): 1})
     assert (buf[:, 0] == K_DISPATCH).all()
-    assert buf[2, 11] == (2 | KV_MIGRATE) and buf[0, 11] == 0       # home GPU 1 -> flags (1 + 1) | KV_MIGRATE
+    # home GPU 1 -> flags (1 + 1) | KV_MIGRATE; conversation turns flagged DIALOG_TURN
+    assert buf[2, 11] == (2 | KV_MIGRATE | DIALOG_TURN) and buf[0, 11] == DIALOG_TURN and buf[1, 11] == 0
     reqs = gw._foreign_requests(buf, cap)
     for m, r in zip(msgs, reqs):
         origin, h, tier, arr, enq, dec = r.meta
@@ -52,6 +53,7 @@ def test_descriptor_roundtrip():
         assert r.prompt.tolist() == want                                   # prompts are truncated to the cap
         assert r.conv == (conv_key(m.conversation_id) if m.conversation_id else -1)
         assert r.timeout_ns == m.timeout // 1_000_000 * 1_000_000
+        assert r.dialog == bool(m.conversation_id)
     assert reqs[2].history is not None and len(reqs[2].history) == 5     # replay length of a non-resident dialog
     assert reqs[0].history is None
 
