@@ -68,7 +68,7 @@ def parse(argv=None):
     ap.add_argument("--micro-slots", type=int, default=64, help="micro mode: KV slots of the realtime pool")
     ap.add_argument("--micro-inflight", type=int, default=4, help="micro mode: micro-forwards queued ahead")
     ap.add_argument("--micro-budget", type=int, default=512, help="micro mode: tokens per micro-forward")
-    ap.add_argument("--micro-stream", default="high", choices=["high", "same", "partition"],
+    ap.add_argument("--micro-stream", default="partition", choices=["high", "same", "partition"],
                     help="micro mode: a high-priority HIP stream of their own, the serving stream, or a CU "
                          "partition of the chip of their own (--micro-cus; the serving steps get the rest)")
     ap.add_argument("--micro-cus", type=int, default=32, help="micro partition: CUs of the realtime partition")

@@ -110,6 +110,10 @@ def main() -> int:
                                   "tok_s": round(eng.total_tokens / (t_rep - t0), 0)}), flush=True)
         eng.finish(block=True)
         eng.close()
+        if a.stream == "partition":
+            from llm_message_queue_amd.backend.cu_partition import release_streams
+            del eng, res
+            release_streams()
     except BackendHung as e:
         print(json.dumps({"hung": str(e), "t_s": round(time.monotonic() - t0, 1), "micro": eng.micro_steps}),
               flush=True)

@@ -24,12 +24,26 @@ def mask_words(bits, ncu: int):
     return words
 
 
+_STREAMS = {}
+
+
 def partition_streams(device, micro_cus: int) -> Tuple[object, object, int]:
-    """(serving stream, micro stream, serving CU count) on ``device``."""
+    """(serving stream, micro stream, serving CU count) on ``device``.
+
+    The streams live for the process, one pair per (device, micro_cus),
+    shared by every engine that asks: blocks of PyTorch's caching allocator
+    stay associated with the stream that allocated them, so a tensor freed
+    after its stream was destroyed would record an event on a dead stream
+    (a segfault in the deallocation).  PyTorch never destroys its own pool
+    streams for the same reason."""
     import torch
     from .. import _native
     k = _native.require_hipops()
     idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, int(micro_cus))
+    got = _STREAMS.get(key)
+    if got is not None:
+        return got
     ncu = int(k.device_info(idx)["cus"])
     if micro_cus % 8 or not 8 <= micro_cus <= ncu // 2:
         raise ValueError(f"micro_cus must be a multiple of 8 (one per XCD) in [8, {ncu // 2}], not {micro_cus}")
@@ -37,4 +51,28 @@ def partition_streams(device, micro_cus: int) -> Tuple[object, object, int]:
     with torch.cuda.device(idx):
         hs = k.stream_with_cu_mask(mask_words(range(big), ncu))
         hm = k.stream_with_cu_mask(mask_words(range(big, ncu), ncu))
-    return (torch.cuda.ExternalStream(hs, device=device), torch.cuda.ExternalStream(hm, device=device), big)
+    dev = torch.device("cuda", idx)
+    got = _STREAMS[key] = (torch.cuda.ExternalStream(hs, device=dev), torch.cuda.ExternalStream(hm, device=dev), big)
+    return got
+
+
+def release_streams() -> None:
+    """Destroy the process's partition streams -- only when no tensor
+    allocated on them can be freed later: the caller dropped every engine
+    and tensor first.  The GPU is drained and the allocator's cached blocks
+    released before the streams go (a profiler's exit-time teardown then
+    finds no live external stream)."""
+    if not _STREAMS:
+        return
+    import gc
+
+    import torch
+    from .. import _native
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    k = _native.require_hipops()
+    for big, micro, _n in list(_STREAMS.values()):
+        for st in (big, micro):
+            k.stream_destroy(st.cuda_stream)
+    _STREAMS.clear()

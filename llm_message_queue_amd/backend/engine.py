@@ -145,7 +145,7 @@ class BackendEngine:
                  fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
                  realtime_step_tokens: int = 0, fused_rms=None, realtime_mode: str = "",
                  micro_slots: int = 64, micro_budget: int = 512, micro_inflight: int = 4,
-                 micro_stream: str = "high", micro_cus: int = 16, micro_gemm: str = "hip",
+                 micro_stream: str = "partition", micro_cus: int = 32, micro_gemm: str = "hip",
                  library_gemm: bool = False):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
@@ -855,17 +855,13 @@ class BackendEngine:
         self._launch_pool(False)
 
     def close(self) -> None:
-        """Release the CU-partition streams (``micro_stream=partition``):
-        the GPU is drained first, then the runtime streams are destroyed, so
-        nothing references them at interpreter teardown."""
-        if self.micro_cus and self.main_stream is not None:
-            from .. import _native
+        """Drain the GPU work of this engine.  The CU-partition streams
+        (``micro_stream=partition``) are process-wide and stay alive
+        (``cu_partition.partition_streams``): tensors this engine allocated
+        on them may outlive it, and freeing one returns its block to the
+        stream it was allocated on."""
+        if self.cuda:
             torch.cuda.synchronize(self.device)
-            k = _native.require_hipops()
-            for st in (self.main_stream, self.rt_stream):
-                k.stream_destroy(st.cuda_stream)
-            self.main_stream = self.rt_stream = None
-            self.micro_cus = 0
 
     def stream_ctx(self):
         """Context that makes the serving steps' stream current (a no-op

@@ -320,7 +320,7 @@ class BackendConfig:
     realtime_mode: str = ""
     micro_slots: int = 64              # micro mode: KV slots of the realtime pool
     micro_inflight: int = 4            # micro mode: micro-forwards queued ahead on their stream
-    micro_stream: str = "high"         # micro mode: "high" (own stream), "same", "partition" (own CU partition)
+    micro_stream: str = "partition"    # micro mode: "partition" (own CU partition; the best measured), "high", "same"
     micro_cus: int = 32                # micro partition: CUs of the realtime partition (a multiple of 8)
     micro_gemm: str = "hip"            # micro partition: "hip" (hand-written) or "rocblas" GEMMs
     library_gemm: bool = False         # True: hipBLASLt for the sub-wave o / down and small heads

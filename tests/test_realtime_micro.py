@@ -132,13 +132,15 @@ def test_gateway_serves_realtime_on_micro_pool_cpu():
 
 
 @pytest.mark.gpu
-def test_micro_stream_same_tokens_gpu():
-    """The HIP path: micro-forwards on a high-priority stream running
-    concurrently with the serving steps produce the same greedy ids as the
-    serving steps do for the same requests."""
+@pytest.mark.parametrize("stream", ["partition", "high"])
+def test_micro_stream_same_tokens_gpu(stream):
+    """The HIP path: micro-forwards on a CU partition of their own (the
+    default) or a high-priority stream, running concurrently with the
+    serving steps, produce the same greedy ids as the serving steps do for
+    the same requests."""
     dev = torch.device("cuda", 0)
     a = _serve(_engine("off", device=dev, impl="hip", slots=16, budget=64), _requests(24, seed=5))
-    eng = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream="high")
+    eng = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream=stream)
     assert eng.rt_stream is not None
     b = _serve(eng, _requests(24, seed=5))
     assert sorted(a) == sorted(b) == list(range(24))
@@ -146,3 +148,4 @@ def test_micro_stream_same_tokens_gpu():
     assert same == 24, {k: (a[k][0], b[k][0]) for k in a if a[k][0] != b[k][0]}
     # 8 realtime requests, 4 micro slots: the pool fills, the rest ride the serving steps
     assert 4 <= sum(v[1] for v in b.values()) <= 8 and eng.micro_steps >= 4
+    eng.close()
