@@ -147,6 +147,10 @@ def main() -> None:
                     help="every this many seconds of the measured run: add + remove a keyword rule (copied to "
                          "every rank), scrape /metrics, list dead letters, read /queues/status; reports their "
                          "latencies and errors")
+    ap.add_argument("--cancel-churn", type=float, default=0.0,
+                    help="per second during the measured run: POST a message through the front door, wait 0-60 ms "
+                         "(it may be in the ring, a rank's inbox, its tier queue or on a GPU by then) and DELETE it; "
+                         "reports the DELETE outcomes and the job's request accounting after the drain")
     ap.add_argument("--bench-config", action="store_true",
                     help="spawned GPU dispatcher runs bench.py's serving config (1536 slots, 4096-token steps, "
                          "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
@@ -269,6 +273,47 @@ def main() -> None:
                         churn["ms"].append((time.perf_counter() - t0) * 1e3)
             if a.admin_churn > 0 and api_url:
                 threading.Thread(target=_churn, daemon=True).start()
+            cancels = {"posted": 0, "post_errors": 0, "deleted": 0, "dequeued": 0, "cancelled": 0,
+                       "already_done": 0, "not_found": 0, "errors": 0}
+
+            def _cancel_churn():
+                import random
+                rnd = random.Random(11)
+                period = 1.0 / a.cancel_churn
+                nxt = time.monotonic()
+                k = 0
+                while not churn_stop.is_set():
+                    nxt += period
+                    k += 1
+                    try:
+                        req = urllib.request.Request(urls[0] + "/api/v1/messages", method="POST",
+                                                     data=json.dumps({"content": f"cancel me {k}", "user_id": "cc",
+                                                                      "priority": 1 + k % 4}).encode(),
+                                                     headers={"Content-Type": "application/json"})
+                        mid = json.loads(urllib.request.urlopen(req, timeout=10).read())["message_id"]
+                        cancels["posted"] += 1
+                    except Exception:                      # noqa: BLE001 -- counted
+                        cancels["post_errors"] += 1
+                        continue
+                    time.sleep(rnd.uniform(0.0, 0.06))
+                    try:
+                        req = urllib.request.Request(urls[0] + f"/api/v1/messages/{mid}", method="DELETE")
+                        d = json.loads(urllib.request.urlopen(req, timeout=10).read())
+                        cancels["deleted"] += 1
+                        if d.get("dequeued"):
+                            cancels["dequeued"] += 1
+                        elif d.get("cancelled"):
+                            cancels["cancelled"] += 1
+                        else:
+                            cancels["already_done"] += 1
+                    except urllib.error.HTTPError as e:
+                        cancels["not_found" if e.code == 404 else "errors"] += 1
+                    except Exception:                      # noqa: BLE001 -- counted
+                        cancels["errors"] += 1
+                    time.sleep(max(0.0, nxt - time.monotonic()))
+            if a.cancel_churn > 0:
+                import urllib.error
+                threading.Thread(target=_cancel_churn, daemon=True).start()
             # server memory over the measured run (every spawned process and
             # its children): a leak shows up as a growing series; a progress
             # line on stderr every sample keeps long soaks visibly alive
@@ -307,6 +352,16 @@ def main() -> None:
                 time.sleep(2.0)
                 with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
                     st = json.loads(rr.read())
+                t_drain = time.monotonic()
+                while a.cancel_churn > 0 and time.monotonic() - t_drain < 60:
+                    dd = (st.get("job") or st).get("dispatch") or {}
+                    ended = sum(int(dd.get(k, 0)) for k in ("completed", "cancelled", "expired", "retry_exhausted",
+                                                            "rejected"))
+                    if int(dd.get("submitted", 0)) - ended - cancels["dequeued"] <= 0:
+                        break                    # drained: every accepted request has ended
+                    time.sleep(1.0)
+                    with urllib.request.urlopen(api_url + "/api/v1/queues/stats", timeout=10) as rr:
+                        st = json.loads(rr.read())
                 if "job" in st:                  # multi-rank: every rank's counters and histograms
                     st, st_end = st["job"], st_end["job"]
                     out["ranks"] = st.get("ranks")
@@ -322,6 +377,19 @@ def main() -> None:
             if rss:
                 out["server_rss_mib"] = {"every_s": a.rss_every, "first": rss[0][1], "last": rss[-1][1],
                                          "max": max(v for _t, v in rss), "series": rss}
+            if a.cancel_churn > 0:
+                out["cancel_churn"] = dict(cancels, per_s=a.cancel_churn)
+                dsp = (out.get("dispatcher") or {}).get("dispatch") or {}
+                if dsp:
+                    # every accepted request ends exactly once: completed, cancelled
+                    # (in flight / in backoff / held), shed at its deadline, dead-lettered,
+                    # or taken out of its tier queue by a DELETE (client-side "dequeued")
+                    ended = sum(int(dsp.get(k, 0)) for k in ("completed", "cancelled", "expired",
+                                                             "retry_exhausted", "rejected"))
+                    out["cancel_churn"]["accounting"] = {
+                        "submitted": int(dsp.get("submitted", 0)), "ended": ended,
+                        "dequeued_by_delete": cancels["dequeued"],
+                        "unaccounted": int(dsp.get("submitted", 0)) - ended - cancels["dequeued"]}
             if a.admin_churn > 0 and churn["ms"]:
                 ms = sorted(churn["ms"])
                 out["admin_churn"] = {"every_s": a.admin_churn, "calls": churn["calls"], "errors": churn["errors"],

@@ -79,9 +79,13 @@ class ExchangeMixin:
         else:
             used, total = self._hbm_mib() if eng is not None else (0, 0)
         self._pub_depth = list(depth) if W > 1 else None
+        # completion records announced now are exactly the ones this tick's
+        # all_to_all carries (more may be reaped while the collective is in
+        # flight -- realtime micro-forwards -- and wait for the next tick)
+        self._done_pub = [len(self._done_owed[r]) for r in range(W)]
         return planner.make_load(
             free, inflight, depth, age, hbm_used_mib=used, hbm_total_mib=total, healthy=up, epoch=self.epoch,
-            done_for=[len(self._done_owed[r]) for r in range(W)],
+            done_for=list(self._done_pub),
             pinned=self.pinned if self.affinity else None, stopping=self.stopping,
             slots_free=slots_free, slots_total=eng.slots if eng is not None else 0,
             exclude_mask=self._exclude_mask(), rt_us=int(self._rt_ewma_us), err_ppm=int(self._err_ewma * 1e6),
@@ -142,12 +146,17 @@ class ExchangeMixin:
                     dest[j].extend(rest[k:k + n])
                     k += n
         migrate = self._plan_migrations(dest)         # id(msg) -> home GPU sending its KV
-        done_for = [len(self._done_owed[r]) for r in range(W)]
+        done_for = self._done_pub
         send = []
         now_ns = time.monotonic_ns()
         for j in range(W):
             rows = dest[j] if j != me else []
-            buf = np.zeros((len(rows) + done_for[j], width), dtype=np.int32)
+            # GPU j expects exactly its grant from me: a grant the pop could
+            # not fill -- a queued request removed between the published depth
+            # and the pop (DELETE, peer remove, admin dequeue) or a popped one
+            # found cancelled -- leaves empty rows (kind 0, ignored there)
+            grant = int(mine[j].sum()) if j != me else 0
+            buf = np.zeros((grant + done_for[j], width), dtype=np.int32)
             if rows:
                 ctx = self._fill_descs(buf[:len(rows)], rows, me, cap, migrate)
                 for m, (hist, pre) in zip(rows, ctx):
@@ -176,11 +185,11 @@ class ExchangeMixin:
                     ec[:, 0] = K_CANCEL
                     _put64(ec, 1, can)
                     ec[:, 3] = me
-            recs = self._done_owed[j]
+            recs = self._done_owed[j][:done_for[j]]
             if recs:
                 # completion records: (handle, tier, admitted ns, done ns, kind)
                 a = np.asarray(recs, dtype=np.int64).reshape(-1, 5)
-                d = buf[len(rows):]
+                d = buf[grant:]
                 d[:, 0] = a[:, 4]
                 _put64(d, 1, a[:, 0])
                 d[:, 3] = me
@@ -196,8 +205,7 @@ class ExchangeMixin:
                             n = min(len(t), cap)
                             d[k, 10] = n
                             d[k, DESC_HDR:DESC_HDR + n] = np.asarray(t[:n], dtype=np.int32)
-                    toks.clear()
-            self._done_owed[j] = []
+            self._done_owed[j] = self._done_owed[j][done_for[j]:]
             if hist_rows is not None:
                 extra = np.concatenate([extra, hist_rows])
             send.append(np.concatenate([buf, extra]) if (mig_rows or can or hist_rows is not None) else buf)

@@ -164,6 +164,7 @@ class Gateway(ExchangeMixin, FailureMixin, AffinityMixin, ResourceMixin, OwnAdmi
         self.remote_out: Dict[int, Message] = self.table.remote_out  # handle -> msg sent to another rank
         self.foreign: Dict[int, Tuple[int, int, int]] = {}  # my engine req id -> (origin, handle, tier)
         self._done_owed: Dict[int, List[Tuple[int, int, int, int]]] = {r: [] for r in range(self.world)}
+        self._done_pub: List[int] = [0] * self.world      # records of _done_owed announced this tick
         # generated ids of the dialog turns in _done_owed (origin -> handle -> ids)
         self._done_tok: Dict[int, Dict[int, np.ndarray]] = {r: {} for r in range(self.world)}
         # dialog histories owed to the GPUs this router dispatched turns to

@@ -144,6 +144,47 @@ def test_fakecomm_multirank_dispatch(world):
     assert not gws[0].remote_out and all(not g.foreign for g in gws)
 
 
+def test_grant_shortfall_from_concurrent_removal_keeps_the_exchange():
+    """A queued request removed between the published load and the pop (a
+    DELETE on the API thread, a peer 'remove', an admin dequeue) -- or popped
+    and found cancelled -- leaves the router short of the plan's grant.  The
+    receiving GPU expects exactly the grant's row count: the sender pads the
+    shortfall with empty rows instead of breaking the all_to_all (found by
+    the round-6 HTTP soak with DELETE churn: 'expected 4 rows from 0, got 3')."""
+    world = 2
+    comms = FakeComm.make(world)
+    gws = [Gateway(cfg(), engine=engine(slots=8, seed=r), comm=comms[r], use_gpu_preprocess=False, prompt_cap=8,
+                   gen_tokens=2) for r in range(world)]
+    # few requests, room for all: the plan grants the whole published depth,
+    # part of it to GPU 1
+    msgs = Workload(seed=7).make(6)
+    for m in msgs:
+        m.priority = 3
+    gws[0].submit(msgs)
+    gws[0].ingest()
+    gw0 = gws[0]
+    removed, short = [], []
+    orig_pop = gw0.qm.pop_tiers
+
+    def racing_pop(tiers, n, *args, **kw):
+        # the API thread dequeues one queued message right before the pop
+        if not removed and n > 0:
+            for m in msgs:
+                if m.queue_name and gw0.qm.remove_message(m.queue_name, m):
+                    removed.append(m)
+                    break
+        out = orig_pop(tiers, n, *args, **kw)
+        short.append(n - len(out[0]))
+        return out
+    gw0.qm.pop_tiers = racing_pop
+    assert run_until_done(gws, 5, max_ticks=100)
+    assert len(removed) == 1 and max(short) == 1                      # the grant was not filled
+    assert gw0.counters["completed"] == 5 and all(g.pending() == 0 for g in gws)
+    assert gw0.counters["remote_sent"] > 0
+    assert not gw0.remote_out and all(not g.foreign for g in gws)
+    assert removed[0].dispatched_at == 0
+
+
 # ---------------------------------------------------------------- multi-process gloo
 def _free_port():
     s = socket.socket()
