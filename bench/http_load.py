@@ -151,6 +151,10 @@ def main() -> None:
                     help="per second during the measured run: POST a message through the front door, wait 0-60 ms "
                          "(it may be in the ring, a rank's inbox, its tier queue or on a GPU by then) and DELETE it; "
                          "reports the DELETE outcomes and the job's request accounting after the drain")
+    ap.add_argument("--dialog-frac", type=float, default=0.0,
+                    help="--workload: this fraction of the bodies are turns of --dialog-convs conversations "
+                         "(conversation_id set: KV residency, affinity, history replay / migration across ranks)")
+    ap.add_argument("--dialog-convs", type=int, default=2000)
     ap.add_argument("--bench-config", action="store_true",
                     help="spawned GPU dispatcher runs bench.py's serving config (1536 slots, 4096-token steps, "
                          "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
@@ -231,11 +235,17 @@ def main() -> None:
             if a.workload:
                 from llm_message_queue_amd.gateway.workload import Workload
                 bpath = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"llmq_bodies_{os.getpid()}.jsonl")
+                import random
+                rnd = random.Random(3)
                 with open(bpath, "w") as fh:
                     for m in Workload(seed=7).make(int(a.rate * (a.duration + a.warmup)) + 1000):
                         b = {"content": m.content, "user_id": m.user_id}
                         if m.priority:
                             b["priority"] = m.priority
+                        if a.dialog_frac > 0 and rnd.random() < a.dialog_frac:
+                            c = rnd.randrange(a.dialog_convs)
+                            b["conversation_id"] = f"conv-{c}"
+                            b["user_id"] = f"du{c}"
                         fh.write(json.dumps(b) + "\n")
                 extra = [bpath]
             if a.warmup > 0:
