@@ -131,6 +131,43 @@ def test_gateway_serves_realtime_on_micro_pool_cpu():
     assert len(eng.free_micro) == eng.micro_slots
 
 
+def test_two_ranks_realtime_on_micro_pools_fakecomm():
+    """Two ranks in micro mode: realtime requests placed on the other rank
+    run on its micro pool and complete while the ranks wait at the tick's
+    collectives (``_while_waiting`` reaps micro-forwards).  Completion
+    records reaped after a rank announced its row counts wait for the next
+    tick, so the all_to_all always carries exactly what was announced."""
+    import threading
+
+    from llm_message_queue_amd.gateway.router import Gateway
+    from llm_message_queue_amd.models.message import Message
+    from llm_message_queue_amd.parallel.comm import FakeComm
+    from llm_message_queue_amd.utils.config import default_config
+    cfg = default_config()
+    cfg.queue.enable_metrics = False
+    comms = FakeComm.make(2)
+    engs = [_engine("micro", slots=8, budget=64, micro_slots=4) for _ in range(2)]
+    gws = [Gateway(cfg, engine=engs[r], comm=comms[r], use_gpu_preprocess=False, prompt_cap=16, gen_tokens=3)
+           for r in range(2)]
+    done = []
+    gws[0].on_complete = done.append
+    msgs = [Message(id=f"m{i}", content=("server down, need help" if i % 2 == 0 else "please summarise this"),
+                    priority=1 if i % 2 == 0 else 3, user_id="u") for i in range(48)]
+    gws[0].submit(msgs)
+    for _ in range(300):
+        ths = [threading.Thread(target=g.tick) for g in gws]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if len(done) == len(msgs):
+            break
+    assert len(done) == len(msgs)
+    assert engs[1].micro_steps > 0 and gws[0].counters["remote_sent"] > 0
+    assert not gws[0].remote_out and all(not g.foreign for g in gws)
+    assert all(len(e.free_micro) == e.micro_slots for e in engs)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("stream", ["partition", "high"])
 def test_micro_stream_same_tokens_gpu(stream):
