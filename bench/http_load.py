@@ -155,6 +155,11 @@ def main() -> None:
                     help="--workload: this fraction of the bodies are turns of --dialog-convs conversations "
                          "(conversation_id set: KV residency, affinity, history replay / migration across ranks)")
     ap.add_argument("--dialog-convs", type=int, default=2000)
+    ap.add_argument("--timeout-frac", type=float, default=0.0,
+                    help="--workload: this fraction of the bodies carry a short processing timeout "
+                         "(--timeout-val, Go duration) and max_retries 2: in-flight timeouts, retry backoff "
+                         "in the DelayedQueue, dead-lettering")
+    ap.add_argument("--timeout-val", default="150ms")
     ap.add_argument("--bench-config", action="store_true",
                     help="spawned GPU dispatcher runs bench.py's serving config (1536 slots, 4096-token steps, "
                          "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
@@ -246,6 +251,9 @@ def main() -> None:
                             c = rnd.randrange(a.dialog_convs)
                             b["conversation_id"] = f"conv-{c}"
                             b["user_id"] = f"du{c}"
+                        if a.timeout_frac > 0 and rnd.random() < a.timeout_frac:
+                            b["timeout"] = a.timeout_val
+                            b["max_retries"] = 2
                         fh.write(json.dumps(b) + "\n")
                 extra = [bpath]
             if a.warmup > 0:
