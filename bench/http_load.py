@@ -160,6 +160,10 @@ def main() -> None:
                          "(--timeout-val, Go duration) and max_retries 2: in-flight timeouts, retry backoff "
                          "in the DelayedQueue, dead-lettering")
     ap.add_argument("--timeout-val", default="150ms")
+    ap.add_argument("--fault-cycle", type=float, default=0.0,
+                    help="every this many seconds of the measured run: inject a failed launch into rank 0's GPU "
+                         "backend (it evacuates; its requests re-route to the other ranks), then half a cycle "
+                         "later set its endpoint healthy again (the spawned server runs with fault injection on)")
     ap.add_argument("--bench-config", action="store_true",
                     help="spawned GPU dispatcher runs bench.py's serving config (1536 slots, 4096-token steps, "
                          "32-token prompts, 4 generated tokens, tier caps = slots, aging 50/100/150/200 ms)")
@@ -170,6 +174,8 @@ def main() -> None:
     env = dict(os.environ, PYTHONUNBUFFERED="1", LLMQ_LOGGING__LEVEL="warning", LLMQ_SERVER__MODE="release",
                LLMQ_QUEUE__WORKER__MAX_CONCURRENT="512", LLMQ_QUEUE__WORKER__MAX_BATCH_SIZE="256",
                LLMQ_QUEUE__WORKER__PROCESS_INTERVAL="5ms")
+    if a.fault_cycle > 0:
+        env["LLMQ_SERVER__FAULT_INJECTION"] = "true"
     gpu = [] if a.gpu else ["--no-gpu"]
     cfg_args = []
     if a.bench_config:
@@ -332,6 +338,28 @@ def main() -> None:
             if a.cancel_churn > 0:
                 import urllib.error
                 threading.Thread(target=_cancel_churn, daemon=True).start()
+            faults = {"injected": 0, "restored": 0, "errors": 0}
+
+            def _fault_cycle():
+                def call(method, path, body):
+                    req = urllib.request.Request(api_url + path, method=method, data=json.dumps(body).encode(),
+                                                 headers={"Content-Type": "application/json"})
+                    urllib.request.urlopen(req, timeout=10).read()
+                while not churn_stop.wait(a.fault_cycle / 2):
+                    try:
+                        call("POST", "/api/v1/admin/faults", {"fail_launch": 1})
+                        faults["injected"] += 1
+                    except Exception:                      # noqa: BLE001 -- counted
+                        faults["errors"] += 1
+                    if churn_stop.wait(a.fault_cycle / 2):
+                        break
+                    try:
+                        call("PUT", "/api/v1/endpoints/gpu0/status", {"status": "healthy"})
+                        faults["restored"] += 1
+                    except Exception:                      # noqa: BLE001 -- counted
+                        faults["errors"] += 1
+            if a.fault_cycle > 0 and api_url:
+                threading.Thread(target=_fault_cycle, daemon=True).start()
             # server memory over the measured run (every spawned process and
             # its children): a leak shows up as a growing series; a progress
             # line on stderr every sample keeps long soaks visibly alive
@@ -395,6 +423,8 @@ def main() -> None:
             if rss:
                 out["server_rss_mib"] = {"every_s": a.rss_every, "first": rss[0][1], "last": rss[-1][1],
                                          "max": max(v for _t, v in rss), "series": rss}
+            if a.fault_cycle > 0:
+                out["fault_cycle"] = dict(faults, every_s=a.fault_cycle)
             if a.cancel_churn > 0:
                 out["cancel_churn"] = dict(cancels, per_s=a.cancel_churn)
                 dsp = (out.get("dispatcher") or {}).get("dispatch") or {}
