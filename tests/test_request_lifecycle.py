@@ -22,7 +22,7 @@ import pytest
 
 from llm_message_queue_amd.backend.engine import BackendEngine
 from llm_message_queue_amd.balancer.load_balancer import Endpoint, LoadBalancer
-from llm_message_queue_amd.gateway.request_table import NONE, RequestTable
+from llm_message_queue_amd.gateway.request_table import NONE, QUEUED, RequestTable
 from llm_message_queue_amd.gateway.router import Gateway
 from llm_message_queue_amd.gateway.workload import Workload
 from llm_message_queue_amd.models.llama_stub import LlamaConfig
@@ -60,11 +60,20 @@ def _tick_all(gws, n=1, sleep=0.0):
         if len(gws) == 1:
             gws[0].tick()
         else:
-            ths = [threading.Thread(target=g.tick) for g in gws]
+            errs = []
+
+            def run(g):
+                try:
+                    g.tick()
+                except BaseException as e:     # noqa: BLE001 -- re-raised on the test thread
+                    errs.append(e)
+            ths = [threading.Thread(target=run, args=(g,)) for g in gws]
             for t in ths:
                 t.start()
             for t in ths:
                 t.join()
+            if errs:
+                raise errs[0]
         if sleep:
             time.sleep(sleep)
 
@@ -401,21 +410,39 @@ st = hyp.strategies
 
 @hyp.settings(max_examples=int(__import__("os").environ.get("LIFECYCLE_EXAMPLES", "20")), deadline=None, suppress_health_check=list(hyp.HealthCheck))
 @hyp.given(ops=st.lists(st.tuples(st.sampled_from(["submit", "tick", "cancel", "short_timeout", "evacuate",
-                                                   "sleep"]), st.integers(0, 10**6)), min_size=5, max_size=40),
+                                                   "sleep", "api_dequeue"]), st.integers(0, 10**6)),
+                        min_size=5, max_size=40),
            two=st.booleans())
 def test_random_lifecycles_end_balanced(ops, two):
     """Random submit / tick / cancel / in-flight timeout / evacuate sequences
-    on one or two ranks: every request ends exactly once (completed,
-    cancelled, dead-lettered), a cancelled one never completes, and every
+    on one or two ranks, plus API-thread dequeues that land between a
+    rank's published load and its pop (the race the round-6 HTTP soak
+    found): every request ends exactly once (completed, cancelled,
+    dead-lettered, dequeued), a cancelled one never completes, and every
     counter, map and slot returns to zero."""
     if two:
-        (g0, e0, d0), (g1, e1, _d1) = _two(slots0=3, slots1=3, backoff_ms=5, max_retries=1, gen_tokens=6)
+        # (rank 0's GPU is the smaller one: most of its grants go to rank 1)
+        (g0, e0, d0), (g1, e1, _d1) = _two(slots0=1, slots1=4, backoff_ms=5, max_retries=1, gen_tokens=6)
         gws = [g0, g1]
     else:
         g0, e0, d0 = _gw(slots=3, backoff_ms=5, max_retries=1, gen_tokens=6)
         gws = [g0]
     wl = Workload(seed=11)
     msgs, cancelled = [], []
+    armed, dequeued = [0], set()
+    pop0 = g0.qm.pop_tiers
+
+    def racing_pop(*args, **kw):
+        # an armed DELETE takes a queued message out on "the API thread" after
+        # the load was published, right before the pop
+        while armed[0] > 0:
+            armed[0] -= 1
+            for m in msgs:
+                if m.lc == QUEUED and id(m) not in dequeued and g0.qm.remove_message(m.queue_name, m):
+                    dequeued.add(id(m))
+                    break
+        return pop0(*args, **kw)
+    g0.qm.pop_tiers = racing_pop
     for op, x in ops:
         if op == "submit":
             new = wl.make(1 + x % 3)
@@ -435,6 +462,9 @@ def test_random_lifecycles_end_balanced(ops, two):
             g.set_healthy(True)
         elif op == "sleep":
             time.sleep(0.003)
+        elif op == "api_dequeue":
+            armed[0] += 1
+    armed[0] = 0
     for _ in range(600):
         _tick_all(gws)
         if all(m.lc == NONE for m in msgs) and all(g.engine.inflight() == 0 for g in gws):
@@ -442,7 +472,8 @@ def test_random_lifecycles_end_balanced(ops, two):
         time.sleep(0.001)
     assert all(m.lc == NONE for m in msgs), RequestTable.census(msgs)
     ends = {MessageStatus.COMPLETED, MessageStatus.CANCELLED, MessageStatus.FAILED, MessageStatus.TIMEOUT}
-    assert all(m.status in ends for m in msgs), [m.status for m in msgs]
+    assert all(m.status in ends for m in msgs if id(m) not in dequeued), [m.status for m in msgs]
+    assert not any(m.status == MessageStatus.COMPLETED for m in msgs if id(m) in dequeued)
     c = g0.counters
     n_completed = sum(m.status == MessageStatus.COMPLETED for m in msgs)
     assert c["completed"] == n_completed
@@ -452,5 +483,5 @@ def test_random_lifecycles_end_balanced(ops, two):
         if f.done() and f.result() != "":
             assert m.status == MessageStatus.CANCELLED, (m.id, f.result(), m.status)
     assert c["submitted"] == len(msgs) == (c["completed"] + c["cancelled"] + c["retry_exhausted"] + c["expired"]
-                                           + c["rejected"])
+                                           + c["rejected"] + len(dequeued))
     _assert_clean(gws)
