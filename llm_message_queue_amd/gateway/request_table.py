@@ -20,8 +20,10 @@ in-flight states live here, so ``Gateway.local`` / ``remote_out`` are this
 table's.  Threads: INBOX is entered by ingest threads under the inbox lock
 before the message is visible to anyone else; a queued message removed by
 an API / peer thread (``qm.on_remove``) leaves QUEUED there -- the native
-queue's removal is atomic, so it and a dispatch pop never both win.  All
-other transitions run on the serve loop.
+queue's removal is atomic, so it and a dispatch pop never both win (the
+pop may then fill less than the tick plan granted; the exchange sends empty
+rows for the difference, ``ExchangeMixin._dispatch_global``).  All other
+transitions run on the serve loop.
 
 Cancellation is a tombstone: ``tomb`` holds the requests a cancel was asked
 for (any thread, under the gateway's cancel lock) and not yet ended.  The
