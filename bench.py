@@ -72,6 +72,8 @@ def parse(argv=None):
                     help="micro mode: a high-priority HIP stream of their own, the serving stream, or a CU "
                          "partition of the chip of their own (--micro-cus; the serving steps get the rest)")
     ap.add_argument("--micro-cus", type=int, default=32, help="micro partition: CUs of the realtime partition")
+    ap.add_argument("--no-micro-graph", action="store_true",
+                    help="micro mode: launch decode micro-forwards kernel by kernel instead of replaying HIP graphs")
     ap.add_argument("--gen-tokens", type=int, default=4)
     ap.add_argument("--inflight", type=int, default=2, help="forward steps queued ahead on the GPU")
     ap.add_argument("--aging-ms", default="50,100,150,200",
@@ -350,7 +352,7 @@ def main(argv=None) -> int:
                                realtime_mode=a.realtime_mode, micro_slots=a.micro_slots,
                                micro_inflight=a.micro_inflight, micro_budget=a.micro_budget,
                                micro_stream=a.micro_stream, micro_cus=a.micro_cus,
-                               library_gemm=a.library_gemm)
+                               library_gemm=a.library_gemm, micro_graph=not a.no_micro_graph)
     pre = Preprocessor(cfg.preprocessor, use_gpu=not dry, device=str(dev))
     lbcfg = cfg.loadbalancer
     lbcfg.algorithm = a.lb
@@ -736,7 +738,9 @@ def main(argv=None) -> int:
         # GEMM FLOP/s over the MI355X dense bf16 peak (2.5 PFLOP/s, no sparsity)
         "mfma_peak_fraction": round(flops_per_s / 2.5e15, 4),
         "micro_forwards": ({"count": int(work[3]), "per_s": round(int(work[3]) / elapsed, 1) if elapsed > 0 else 0.0,
-                            "mean_gpu_ms": round(work[4] / 1000.0 / max(1, int(work[5])), 3)}
+                            "mean_gpu_ms": round(work[4] / 1000.0 / max(1, int(work[5])), 3),
+                            "graph_replays": int(getattr(engine, "micro_graph_steps", 0)),
+                            "micro_graph": bool(getattr(engine, "micro_graph", False))}
                            if engine.micro else None),
         "p99_ms": round(lat["p99_ms"], 3),                       # arrival -> dispatch
         "p50_ms": round(lat["p50_ms"], 3),

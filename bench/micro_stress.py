@@ -38,6 +38,7 @@ def main() -> int:
     ap.add_argument("--micro-inflight", type=int, default=4)
     ap.add_argument("--step-timeout", type=float, default=15.0)
     ap.add_argument("--report-s", type=float, default=5.0)
+    ap.add_argument("--no-graph", action="store_true", help="decode micro-forwards launched eagerly (no HIP graphs)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -49,7 +50,7 @@ def main() -> int:
     dev = torch.device("cuda", 0)
     eng = BackendEngine(LlamaConfig.llama3_8b(), slots=a.slots, max_ctx=512, token_budget=a.budget, device=dev,
                         impl="hip", realtime_mode=a.mode, micro_stream=a.stream, micro_cus=a.micro_cus, micro_gemm=a.micro_gemm,
-                        micro_inflight=a.micro_inflight, step_timeout_s=a.step_timeout)
+                        micro_inflight=a.micro_inflight, step_timeout_s=a.step_timeout, micro_graph=not a.no_graph)
     eng.warm_shapes()
     eng.time_steps = True
     rng = np.random.default_rng(0)
@@ -107,7 +108,8 @@ def main() -> int:
                                   "micro_ms": round(eng.micro_gpu_ms / max(1, eng.micro_timed), 2),
                                   "rt_done": len(lat), "rt_p50_ms": round(float(np.percentile(la, 50)), 1),
                                   "rt_p99_ms": round(float(np.percentile(la, 99)), 1),
-                                  "tok_s": round(eng.total_tokens / (t_rep - t0), 0)}), flush=True)
+                                  "tok_s": round(eng.total_tokens / (t_rep - t0), 0),
+                                  "graph_steps": eng.micro_graph_steps}), flush=True)
         eng.finish(block=True)
         eng.close()
         if a.stream == "partition":

@@ -138,6 +138,8 @@ class _Inflight:
 
 
 class BackendEngine:
+    MICRO_GRAPH_BUCKETS = (8, 16, 32, 64)
+
     def __init__(self, model_cfg: LlamaConfig, slots: int = 256, max_ctx: int = 512,
                  token_budget: int = 2048, device="cuda", impl: str = "hip", seed: int = 0,
                  page=None, gpu_index: int = 0, max_inflight: int = 2, residual_in_gemm: bool = True,
@@ -146,7 +148,7 @@ class BackendEngine:
                  realtime_step_tokens: int = 0, fused_rms=None, realtime_mode: str = "",
                  micro_slots: int = 64, micro_budget: int = 512, micro_inflight: int = 4,
                  micro_stream: str = "partition", micro_cus: int = 32, micro_gemm: str = "hip",
-                 library_gemm: bool = False):
+                 library_gemm: bool = False, micro_graph: bool = True):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
         self.step_timeout_s = float(step_timeout_s)
@@ -184,9 +186,18 @@ class BackendEngine:
             raise ValueError("realtime_mode micro needs micro_slots >= 1")
         self.micro_budget = max(int(micro_budget), self.micro_slots + 1)
         self.micro_inflight = max(1, int(micro_inflight))
-        self.n_all = slots + self.micro_slots             # KV slots: serving pool, then the micro pool
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
+        # decode-only micro-forwards (<= 64 rows) replay HIP graphs captured
+        # at warm-up, one per row bucket (``MICRO_GRAPH_BUCKETS``): a
+        # micro-forward is ~350 kernel launches the serve loop's host thread
+        # would otherwise issue one by one between pumping arrivals.  The
+        # padding rows of a bucket run on a scratch slot past the micro pool.
+        self.micro_graph = bool(micro_graph) and self.micro and self.cuda and impl == "hip" \
+            and micro_stream in ("high", "partition")
+        self.scratch_slot = slots + self.micro_slots if self.micro_graph else -1
+        # KV slots: serving pool, then the micro pool (+ the graphs' scratch slot)
+        self.n_all = slots + self.micro_slots + (1 if self.micro_graph else 0)
         self.async_device = self.cuda          # forwards run asynchronously (a GPU stream)
         self.rt_stream = None
         self.main_stream = None          # (partition: the serving steps' CU-masked stream)
@@ -229,7 +240,7 @@ class BackendEngine:
         # the realtime micro pool: slots [slots, n_all), never in ``free`` /
         # ``conv_lru``, so no serving step ever reads or writes their KV rows
         # (the two streams never share a slot)
-        self.free_micro: List[int] = list(range(self.n_all - 1, slots - 1, -1))
+        self.free_micro: List[int] = list(range(slots + self.micro_slots - 1, slots - 1, -1))
         n_all = self.n_all
         # Conversation KV residency (BASELINE config 4): when a request of a
         # conversation completes, its slot keeps the KV of the dialog so far
@@ -308,6 +319,8 @@ class BackendEngine:
         self.micro_steps = 0
         self.micro_gpu_ms = 0.0                          # device time of timed micro-forwards (``time_steps``)
         self.micro_timed = 0
+        self._mg: Dict[int, tuple] = {}                  # bucket -> (graph, static inputs, token ids, output)
+        self.micro_graph_steps = 0
         if self.micro:
             mr = self.micro_inflight + 1
             # a micro step's staging: tokens, pos, slot (3T), samples + decode
@@ -766,8 +779,116 @@ class BackendEngine:
                                            **({"small_cus": self.micro_cus} if self.micro_cus else {}))
                     n += 1
                     T *= 2
+        if self.micro_graph:
+            n += self._capture_micro_graphs()
         torch.cuda.synchronize(dev)
         self.warmed_shapes = n
+        return n
+
+    def _launch_micro_graph(self, Tb: int, t0: float, t_mono: int, pos, slot, samp_slots, dec_src) -> bool:
+        """A decode-only micro-forward of D <= Tb rows as a replay of bucket
+        Tb's graph: one staging copy, the decode-id gather from the previous
+        micro-forward's output, the replay, the id copy back.  Rows D.. Tb
+        stay on the scratch slot."""
+        graph, g_in, g_tok, out = self._mg[Tb]
+        D = len(pos)
+        buf = np.empty(7 * Tb, dtype=np.int32)
+        buf[:Tb] = 0
+        buf[:D] = pos
+        buf[Tb:2 * Tb] = self.scratch_slot
+        buf[Tb:Tb + D] = slot
+        til = buf[2 * Tb:6 * Tb].reshape(Tb, 4)
+        til[:, 0] = np.arange(Tb)
+        til[:, 1] = 1
+        til[:, 2] = buf[Tb:2 * Tb]
+        til[:, 3] = buf[:Tb]
+        buf[6 * Tb:6 * Tb + D] = dec_src
+        buf[6 * Tb + D:] = 0
+        sid = self.micro_id
+        k = sid % len(self._pins_m)
+        pin = self._pins_m[k]
+        pin.numpy()[:buf.nbytes] = buf.view(np.uint8)
+        host_out = self._out_pins_m[k]
+        prev = self._prev_out_m
+        with torch.cuda.stream(self.rt_stream):
+            g_in.copy_(pin[:buf.nbytes].view(torch.int32), non_blocking=True)
+            g_tok[:D] = prev.index_select(0, g_in[6 * Tb:6 * Tb + D].long()).long()
+            if D < Tb:
+                g_tok[D:] = 0
+            ev0 = self._start_event()
+            te = time.perf_counter_ns()
+            graph.replay()
+            self.host_ns[2] += time.perf_counter_ns() - te
+            host_out[:D].copy_(out[:D], non_blocking=True)
+            ev = self._end_event(D, ev0 is not None)
+        # the same deterministic bookkeeping as an eager micro-forward
+        ss = samp_slots
+        gidx = self.s_gen[ss].copy()
+        self.s_gen[ss] += 1
+        self.s_out_idx[ss] = np.arange(len(ss))
+        self.s_out_step[ss] = sid
+        g = self.s_gen[ss]
+        firsts = [self.active[int(x)] for x in ss[g == 1]]
+        done = ss[g >= self.s_gmax[ss]]
+        completed = []
+        for x in done.tolist():
+            r = self.active.pop(x)
+            r.prefilled = int(self.s_plen[x]) - r.reused
+            r.generated = int(self.s_gen[x])
+            completed.append(r)
+            self.s_conv[x] = -1
+            self.free_micro.append(x)
+        self.s_active[done] = False
+        f = _Inflight(sid, ev, D, 0, D, completed, firsts, t0, out, t_mono, ev0, micro=True,
+                      samp_slots=ss, gidx=gidx, host_out=host_out)
+        self._prev_out_m = out
+        self._qm.append(f)
+        self.micro_id += 1
+        self.micro_steps += 1
+        self.micro_graph_steps += 1
+        self.total_tokens += D
+        self.matmul_flops += self._step_flops(D, D)
+        self.completed_total += len(completed)
+        self.completed_tokens += sum(len(r.prompt) + r.gen_tokens - 1 for r in completed)
+        return True
+
+    def _micro_forward_kw(self) -> dict:
+        return {"small_cus": self.micro_cus} if self.micro_cus else {}
+
+    def _capture_micro_graphs(self) -> int:
+        """Capture the decode-only micro-forward once per row bucket on the
+        micro stream (after ``warm_shapes`` ran it eagerly: workspaces and
+        first launches exist).  Static inputs per bucket: int32 [pos | slot |
+        tiles (4 per row) | gather rows] and the int64 token ids; every row
+        starts on the scratch slot at position 0, so a replay's padding rows
+        write and read only that slot."""
+        dev, rt = self.device, self.rt_stream
+        pool = torch.cuda.graph_pool_handle()
+        n = 0
+        for Tb in self.MICRO_GRAPH_BUCKETS:
+            if Tb > max(self.MICRO_GRAPH_BUCKETS[0], self.micro_slots):
+                break
+            g_in = torch.zeros(6 * Tb + Tb, dtype=torch.int32, device=dev)
+            g_tok = torch.zeros(Tb, dtype=torch.long, device=dev)
+            pos, slot = g_in[:Tb], g_in[Tb:2 * Tb]
+            til = g_in[2 * Tb:6 * Tb].view(Tb, 4)
+            slot.fill_(self.scratch_slot)
+            til[:, 0] = torch.arange(Tb, device=dev, dtype=torch.int32)
+            til[:, 1] = 1
+            til[:, 2] = self.scratch_slot
+            samp = torch.arange(Tb, device=dev, dtype=torch.long)
+            kw = self._micro_forward_kw()
+            torch.cuda.synchronize(dev)
+            with torch.cuda.stream(rt):
+                for _ in range(2):
+                    self.model.forward(g_tok, pos, slot, samp, tiles=til, n_dec=Tb, **kw)
+            torch.cuda.synchronize(dev)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, pool=pool, stream=rt, capture_error_mode="thread_local"):
+                out = self.model.forward(g_tok, pos, slot, samp, tiles=til, n_dec=Tb, **kw)
+            torch.cuda.synchronize(dev)
+            self._mg[Tb] = (graph, g_in, g_tok, out)
+            n += 1
         return n
 
     def inject(self, **fault) -> None:
@@ -816,7 +937,7 @@ class BackendEngine:
         self._importing.clear()
         self.s_conv[:] = -1
         self.free = list(range(self.slots - 1, -1, -1))
-        self.free_micro = list(range(self.n_all - 1, self.slots - 1, -1))
+        self.free_micro = list(range(self.slots + self.micro_slots - 1, self.slots - 1, -1))
         return out
 
     def launch(self, wait_cb=None) -> None:
@@ -883,6 +1004,10 @@ class BackendEngine:
             return False
         dev = self.device
         S, D, NT = len(samp), len(dec_rows), len(tiles)
+        if micro and self._mg and n_pre == 0 and D == T and self._prev_out_m is not None:
+            Tb = next((b for b in self.MICRO_GRAPH_BUCKETS if b >= T and b in self._mg), 0)
+            if Tb:
+                return self._launch_micro_graph(Tb, t0, t_mono, pos, slot, samp_slots, dec_src)
         o_dec = 3 * T + S
         o_til = o_dec + 2 * D
         buf = np.empty(o_til + 4 * NT, dtype=np.int32)

@@ -57,7 +57,7 @@ def _build_engine(cfg, model: str, device, job: str = ""):
                          realtime_mode=cfg.backend.realtime_mode, micro_slots=cfg.backend.micro_slots,
                          micro_inflight=cfg.backend.micro_inflight, micro_stream=cfg.backend.micro_stream,
                          micro_cus=cfg.backend.micro_cus, micro_gemm=cfg.backend.micro_gemm,
-                         library_gemm=cfg.backend.library_gemm), page
+                         library_gemm=cfg.backend.library_gemm, micro_graph=cfg.backend.micro_graph), page
 
 
 def fit_slots(mcfg, slots: int, max_ctx: int, reserve_gb: float, total_bytes: int) -> int:

@@ -324,6 +324,7 @@ class BackendConfig:
     micro_cus: int = 32                # micro partition: CUs of the realtime partition (a multiple of 8)
     micro_gemm: str = "hip"            # micro partition: "hip" (hand-written) or "rocblas" GEMMs
     library_gemm: bool = False         # True: hipBLASLt for the sub-wave o / down and small heads
+    micro_graph: bool = True           # micro mode: decode micro-forwards replay HIP graphs
     # a forward still incomplete this long after launch = a hung GPU: the
     # serve loop stops with a failure status (BackendHung) so the launcher
     # restarts the job; 0 waits forever.  Below server.stall_fatal_after, so

@@ -169,6 +169,29 @@ def test_two_ranks_realtime_on_micro_pools_fakecomm():
 
 
 @pytest.mark.gpu
+def test_micro_decode_graph_replays_match_eager_gpu():
+    """Decode-only micro-forwards replayed from HIP graphs (row buckets,
+    padding rows on the scratch slot) produce the same greedy ids as the
+    same micro-forwards launched kernel by kernel, and the serving pool's
+    results are untouched."""
+    dev = torch.device("cuda", 0)
+    eager = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream="partition",
+                    micro_graph=False)
+    eager.warm_shapes([1, 8, 64])
+    a = _serve(eager, _requests(24, seed=9, gen=6))
+    eager.close()
+    graph = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream="partition")
+    graph.warm_shapes([1, 8, 64])
+    assert graph.micro_graph and graph._mg
+    b = _serve(graph, _requests(24, seed=9, gen=6))
+    assert graph.micro_graph_steps > 0
+    assert sorted(a) == sorted(b) == list(range(24))
+    assert {k: v[0] for k, v in a.items()} == {k: v[0] for k, v in b.items()}
+    assert graph.scratch_slot not in graph.free_micro and len(graph.free_micro) == graph.micro_slots
+    graph.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("stream", ["partition", "high"])
 def test_micro_stream_same_tokens_gpu(stream):
     """The HIP path: micro-forwards on a CU partition of their own (the
