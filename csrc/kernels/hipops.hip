@@ -513,28 +513,37 @@ static void kv_move(uintptr_t table, int layers, int slots, int slot, int n, int
   check_launch();
 }
 
-// ---------------------------------------------------------------------- skinny GEMM (M <= 64)
+// ---------------------------------------------------------------------- skinny GEMM (M <= 256)
 // C (+)= A . W^T for the small steps (skinny_kernels.h): split-K partials into
 // ws [S][M][N] fp32, then the finalize kernel (row scale, epilogue, bf16).
 static void skinny_gemm(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t rs,
                         uintptr_t ws, int nsplit, uintptr_t stream) {
-  require(M >= 1 && M <= 64, "skinny_gemm: M must be in [1, 64]");
+  require(M >= 1 && M <= SK_MAX_M, "skinny_gemm: M must be in [1, 256]");
   require(N % SK_NB == 0, "skinny_gemm: N must be a multiple of 128");
   require(nsplit >= 1 && K % (SK_KS * nsplit) == 0, "skinny_gemm: K must be a multiple of 128 * S");
   require(epi == SK_EPI_STORE || epi == SK_EPI_RESID || epi == SK_EPI_SWIGLU, "skinny_gemm: unknown epilogue");
   require(epi != SK_EPI_SWIGLU || N % 256 == 0, "skinny_gemm: SwiGLU needs N % 256 == 0");
   require(a % 16 == 0 && w % 16 == 0 && c % 16 == 0 && ws % 16 == 0 && ws != 0, "skinny_gemm: alignment");
   require((int64_t)N * K < (int64_t)1 << 31, "skinny_gemm: weight too large");
-  const int mt = (M + 15) / 16;
-  const dim3 grid(N / SK_NB, nsplit);
+  const int nm = (M + 127) / 128;                   // 128-row chunks of A (M > 128)
+  const int mt = nm > 1 ? 8 : (M + 15) / 16;
+  const dim3 grid(N / SK_NB * nm, nsplit);
   const int kc = K / nsplit;
   auto* A_ = P<const uint16_t>(a);
   auto* W_ = P<const uint16_t>(w);
   auto* ws_ = P<float>(ws);
-  if (mt == 1) hipLaunchKernelGGL(skinny_partial_kernel<1>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
-  else if (mt == 2) hipLaunchKernelGGL(skinny_partial_kernel<2>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
-  else if (mt == 3) hipLaunchKernelGGL(skinny_partial_kernel<3>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
-  else hipLaunchKernelGGL(skinny_partial_kernel<4>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc);
+#define SK_LAUNCH(T) hipLaunchKernelGGL(skinny_partial_kernel<T>, grid, dim3(256), 0, S(stream), A_, W_, ws_, M, N, K, kc, nm)
+  switch (mt) {
+    case 1: SK_LAUNCH(1); break;
+    case 2: SK_LAUNCH(2); break;
+    case 3: SK_LAUNCH(3); break;
+    case 4: SK_LAUNCH(4); break;
+    case 5: SK_LAUNCH(5); break;
+    case 6: SK_LAUNCH(6); break;
+    case 7: SK_LAUNCH(7); break;
+    default: SK_LAUNCH(8); break;
+  }
+#undef SK_LAUNCH
   check_launch();
   const int nout = epi == SK_EPI_SWIGLU ? N / 2 : N;
   const int threads = M * (nout / 4);

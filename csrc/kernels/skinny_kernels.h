@@ -1,4 +1,4 @@
-// Skinny GEMMs for small steps (M <= 64 rows): C = A[M][K] . W[N][K]^T with
+// Skinny GEMMs for small steps (M <= 64 rows, up to 256 in 64-row chunks): C = A[M][K] . W[N][K]^T with
 // the realtime micro-forwards' epilogues (store, residual add, SwiGLU over the
 // permuted gate/up weight, optional per-row RMSNorm scale).
 //
@@ -43,24 +43,52 @@ constexpr int SK_LDA = SK_KS + 8;   // LDS row stride of the A tile (elements)
 
 enum { SK_EPI_STORE = 0, SK_EPI_RESID = 1, SK_EPI_SWIGLU = 2 };
 
+// M > 64 (up to SK_MAX_M): blockIdx.x also selects one of nm 128-row chunks
+// of A (MT = 8; a chunk's A rows staged in two 64-row groups).  Every chunk re-reads its column block's weights, so the nm
+// chunks of a column block run on one XCD back to back (block b -> XCD b % 8:
+// chunk fastest within the XCD's share) and the repeats come from its L2.
+constexpr int SK_MAX_M = 256;
+
 template <int MT>
 __global__ void __launch_bounds__(256)
 skinny_partial_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ W, float* __restrict__ ws,
-                      int M, int N, int K, int kc) {
+                      int M, int N, int K, int kc, int nm) {
   __shared__ __align__(16) uint16_t As[2][MT * 16][SK_LDA];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int n0 = blockIdx.x * SK_NB + w * 32;
+  const int ncb = N / SK_NB;
+  int cb = blockIdx.x, mc = 0;
+  if (nm > 1) {
+    if ((ncb & 7) == 0) {
+      const int b = blockIdx.x, idx = b >> 3;
+      cb = (idx / nm) * 8 + (b & 7);
+      mc = idx % nm;
+    } else {
+      cb = blockIdx.x / nm;
+      mc = blockIdx.x % nm;
+    }
+  }
+  const int m0 = mc * (MT * 16);
+  const int Ml = min(M - m0, MT * 16);             // rows of this chunk
+  const int n0 = cb * SK_NB + w * 32;
   const int kb = blockIdx.y * kc;
   const int nsteps = kc / SK_KS;
   // weight rows of this lane's two fragments; K offset of its 64-byte run
   const uint16_t* wp0 = W + (size_t)(n0 + fr) * K + kb + fq * 32;
   const uint16_t* wp1 = wp0 + (size_t)16 * K;
-  // A staging: thread t -> row t / 4, chunks (t % 4) * 4 .. + 3 (16 B each)
+  // A staging: thread t -> row g * 64 + t / 4 of each 64-row group g,
+  // chunks (t % 4) * 4 .. + 3 (16 B each)
+  constexpr int RG = (MT * 16 + 63) / 64;
   const int arow = tid >> 2, acb = (tid & 3) * 4;
-  const bool a_on = arow < MT * 16;
-  const bool a_live = a_on && arow < M;
-  const uint16_t* ap = A + (size_t)(a_live ? arow : 0) * K + kb + acb * 8;
+  bool a_on[RG], a_live[RG];
+  const uint16_t* ap[RG];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int r = g * 64 + arow;
+    a_on[g] = r < MT * 16;
+    a_live[g] = a_on[g] && r < Ml;
+    ap[g] = A + (size_t)(m0 + (a_live[g] ? r : 0)) * K + kb + acb * 8;
+  }
 
   sk_f32x4 acc[MT][2];
 #pragma unroll
@@ -73,7 +101,7 @@ skinny_partial_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict
   // a fragment a step: enough bytes outstanding per CU to stream the weights
   // at the partition's bandwidth); the stage index is compile-time below
   sk_u32x4 wb[3][2][4];
-  sk_u32x4 ab[4];
+  sk_u32x4 ab[RG][4];
   auto load_w = [&](auto stc, int step) {
     constexpr int ST = decltype(stc)::value;
     const int ko = step * SK_KS;
@@ -86,13 +114,19 @@ skinny_partial_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict
   auto load_a = [&](int step) {
     const int ko = step * SK_KS;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      ab[i] = a_live ? *reinterpret_cast<const sk_u32x4*>(ap + ko + 8 * i) : sk_u32x4{0u, 0u, 0u, 0u};
+    for (int g = 0; g < RG; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        ab[g][i] = a_live[g] ? *reinterpret_cast<const sk_u32x4*>(ap[g] + ko + 8 * i) : sk_u32x4{0u, 0u, 0u, 0u};
   };
   auto store_a = [&](int buf) {
-    if (a_on) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) *reinterpret_cast<sk_u32x4*>(&As[buf][arow][(acb + i) * 8]) = ab[i];
+    for (int g = 0; g < RG; ++g) {
+      if (a_on[g]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<sk_u32x4*>(&As[buf][g * 64 + arow][(acb + i) * 8]) = ab[g][i];
+      }
     }
   };
   // one 128-deep step from register stage CUR (= step % 3) and A buffer
@@ -137,7 +171,7 @@ skinny_partial_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = m * 16 + fq * 4 + e;
-        if (row < M) out[(size_t)row * N + n0 + j * 16 + fr] = acc[m][j][e];
+        if (row < Ml) out[(size_t)(m0 + row) * N + n0 + j * 16 + fr] = acc[m][j][e];
       }
 }
 

@@ -130,7 +130,7 @@ class LlamaStub:
         # (profiles/r5_resid_rms_bench.jsonl, profiles/r5_fused_rms_serving_ab_1gpu.jsonl)
         self.fused_rms = False if fused_rms is None else bool(fused_rms)
         # False (the default since round 6): no library GEMM at any row
-        # count -- skinny below 65 rows, 256x256 tiles (split-K where whole
+        # count -- skinny for small steps, 256x256 tiles (split-K where whole
         # tiles leave CUs idle) above, the argmax head at any row count.
         # True: hipBLASLt where it was faster (sub-wave o / down, the head
         # under 256 rows); measured equal within 0.4 % on the bench
@@ -245,9 +245,10 @@ class LlamaStub:
         T = res.shape[0]
         small = small_cus > 0 and self.impl == "hip"
         nolib = not self.library_gemm and self._cus > 0
-        # M <= 64: the skinny kernel (a stream over the weights) for every
-        # layer GEMM; larger small steps: the 256x256-tile kernel, split-K
-        skinny = (small or nolib) and T <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
+        # the skinny kernel (a stream over the weights) for qkv up to
+        # SKINNY_PROJ_MAX_M rows; larger steps: the 256x256-tile kernel, split-K
+        # (profiles/r6_skinny_chunked.jsonl)
+        skinny = (small or nolib) and T <= G.SKINNY_PROJ_MAX_M and self.row_scale_norm and self.fused_mlp
         sk_cus = small_cus if small else self._cus
         rows_qkv = self.fused_qkv and (T >= self.min_fused_qkv_tokens or small or nolib)
         qkv_split = {}
@@ -324,7 +325,10 @@ class LlamaStub:
         resid_o = small or nolib or tiles_ok
         rms = tiles_ok and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS and not small
 
-        skinny = (small or nolib) and M <= G.SKINNY_MAX_M and self.row_scale_norm and self.fused_mlp
+        # skinny: o / down up to SKINNY_PROJ_MAX_M rows, gate/up (N = 28,672:
+        # enough tiles to fill the chip) only up to SKINNY_MAX_M
+        skinny = (small or nolib) and M <= G.SKINNY_PROJ_MAX_M and self.row_scale_norm and self.fused_mlp
+        skinny_gu = skinny and M <= G.SKINNY_MAX_M
 
         def into_res(x, wt, scale_out):                  # res += x · wtᵀ (+ its row scales)
             if rms and scale_out:
@@ -338,7 +342,7 @@ class LlamaStub:
             return None
 
         scale = into_res(a, L["wo"], rows_mlp and self.row_scale_norm)
-        if skinny:
+        if skinny_gu:
             act = torch.empty((M, L["w_gu"].shape[0] // 2), dtype=res.dtype, device=res.device)
             G.skinny(res, L["w_gu"], act, G.SK_SWIGLU, row_scale=ops.row_rms(res, cfg.eps), cus=cus)
         elif rows_mlp and self.row_scale_norm and (small or nolib):

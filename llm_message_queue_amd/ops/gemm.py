@@ -329,17 +329,19 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
     return q
 
 
-# ---------------------------------------------------------------------- skinny (M <= 64) small steps
-SKINNY_MAX_M = 64
+# ---------------------------------------------------------------------- skinny small steps
+SKINNY_MAX_M = 64              # the model's gate/up on the skinny kernel up to this many rows
+SKINNY_PROJ_MAX_M = 256        # ... and qkv / o / down up to this many (profiles/r6_skinny_chunked.jsonl)
+SKINNY_CHUNKED_MAX_M = 256     # the kernel itself: 128-row chunks of A up to this many rows
 SK_STORE, SK_RESID, SK_SWIGLU = 0, 1, 2
 _SKINNY_WS = {}
 
 
-def skinny_splits(N: int, K: int, cus: int) -> int:
+def skinny_splits(N: int, K: int, cus: int, M: int = 1) -> int:
     """Split-K factor of a skinny GEMM: the fewest K-splits that give at
-    least two 128-column blocks per CU, each split a multiple of 128 deep
-    and at least 512."""
-    blocks = N // 128
+    least two blocks (128 columns x one 128-row chunk of M) per CU, each
+    split a multiple of 128 deep and at least 512."""
+    blocks = N // 128 * max(1, -(-M // 128))
     best = 1
     for s in (1, 2, 4, 7, 8, 14, 16):
         if K % (128 * s) or K // s < 512:
@@ -351,7 +353,7 @@ def skinny_splits(N: int, K: int, cus: int) -> int:
 
 
 def skinny(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, row_scale=None, cus: int = 32):
-    """``out`` (+)= ``x`` [M <= 64][K] . ``w`` [N][K]^T on the skinny kernel
+    """``out`` (+)= ``x`` [M <= 256][K] . ``w`` [N][K]^T on the skinny kernel
     (``csrc/kernels/skinny_kernels.h``): SK_STORE (out [M][N]), SK_RESID
     (out += ..., one rounding), SK_SWIGLU (``w`` swiglu-permuted, out [M][N/2]);
     ``row_scale`` multiplies row i of the product first (the folded RMSNorm).
@@ -361,12 +363,12 @@ def skinny(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, row_sc
     _check(out, "out")
     M, K = x.shape
     N = w.shape[0]
-    if w.shape[1] != K or not 1 <= M <= SKINNY_MAX_M or N % 128 or K % 128:
+    if w.shape[1] != K or not 1 <= M <= SKINNY_CHUNKED_MAX_M or N % 128 or K % 128:
         raise ValueError(f"skinny: unsupported shape M={M} N={N} K={K}")
     want = (M, N // 2) if epi == SK_SWIGLU else (M, N)
     if tuple(out.shape) != want:
         raise ValueError(f"skinny: out shape {tuple(out.shape)} != {want}")
-    S = skinny_splits(N, K, cus)
+    S = skinny_splits(N, K, cus, M)
     stream = torch.cuda.current_stream(x.device).cuda_stream
     key = (x.device.type, x.device.index, stream)
     need = S * M * N

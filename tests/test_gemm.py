@@ -531,12 +531,12 @@ def test_small_step_forward_matches_the_serving_path():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M", [1, 17, 40, 64])
+@pytest.mark.parametrize("M", [1, 17, 40, 64, 65, 128, 129, 200, 256])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 14336), (6144, 512)])
 def test_skinny_gemm_matches_fp32(M, N, K):
-    """The skinny kernel (M <= 64, weights streamed once, split-K partials
-    summed in order): store and residual epilogues with a row scale, equal to
-    the fp32 reference."""
+    """The skinny kernel (M <= 64 in one block; up to 256 rows in 128-row
+    chunks of A; split-K partials summed in order): store and residual
+    epilogues with a row scale, equal to the fp32 reference."""
     x, w = _rand(M, K, N, seed=3 * M + N + K)
     r = torch.rand(M, device=DEV) + 0.5
     ref = (x.float() * r[:, None]) @ w.float().t()
@@ -554,7 +554,7 @@ def test_skinny_gemm_matches_fp32(M, N, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M", [3, 64])
+@pytest.mark.parametrize("M", [3, 64, 160])
 def test_skinny_swiglu_matches_fp32(M):
     x, w = _rand(M, 4096, 2 * 1536, seed=40 + M)
     r = torch.rand(M, device=DEV) + 0.5
@@ -598,7 +598,7 @@ def test_library_free_residual_matches_fp32(T, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T", [1, 40, 300, 900])
+@pytest.mark.parametrize("T", [1, 40, 165, 256, 300, 900])
 def test_library_free_model_matches_the_default_routing(T):
     """``library_gemm=False`` (no hipBLASLt call in the forward) gives the
     same hidden rows as the default routing to bf16 tolerance and the same
