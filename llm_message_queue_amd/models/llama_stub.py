@@ -248,7 +248,10 @@ class LlamaStub:
         # the skinny kernel (a stream over the weights) for qkv up to
         # SKINNY_PROJ_MAX_M rows; larger steps: the 256x256-tile kernel, split-K
         # (profiles/r6_skinny_chunked.jsonl)
-        skinny = (small or nolib) and T <= G.SKINNY_PROJ_MAX_M and self.row_scale_norm and self.fused_mlp
+        # (on a micro-forward's CU partition only up to SKINNY_MAX_M: there the
+        # split-K tiles were faster for larger steps)
+        skinny = (small or nolib) and T <= (G.SKINNY_MAX_M if small else G.SKINNY_PROJ_MAX_M) \
+            and self.row_scale_norm and self.fused_mlp
         sk_cus = small_cus if small else self._cus
         rows_qkv = self.fused_qkv and (T >= self.min_fused_qkv_tokens or small or nolib)
         qkv_split = {}
@@ -327,7 +330,8 @@ class LlamaStub:
 
         # skinny: o / down up to SKINNY_PROJ_MAX_M rows, gate/up (N = 28,672:
         # enough tiles to fill the chip) only up to SKINNY_MAX_M
-        skinny = (small or nolib) and M <= G.SKINNY_PROJ_MAX_M and self.row_scale_norm and self.fused_mlp
+        skinny = (small or nolib) and M <= (G.SKINNY_MAX_M if small else G.SKINNY_PROJ_MAX_M) \
+            and self.row_scale_norm and self.fused_mlp
         skinny_gu = skinny and M <= G.SKINNY_MAX_M
 
         def into_res(x, wt, scale_out):                  # res += x · wtᵀ (+ its row scales)
