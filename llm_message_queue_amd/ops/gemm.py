@@ -352,12 +352,14 @@ def skinny_splits(N: int, K: int, cus: int, M: int = 1) -> int:
     return best
 
 
-def skinny(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, row_scale=None, cus: int = 32):
+def skinny(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, row_scale=None, cus: int = 32,
+           splits: int = 0):
     """``out`` (+)= ``x`` [M <= 256][K] . ``w`` [N][K]^T on the skinny kernel
     (``csrc/kernels/skinny_kernels.h``): SK_STORE (out [M][N]), SK_RESID
     (out += ..., one rounding), SK_SWIGLU (``w`` swiglu-permuted, out [M][N/2]);
     ``row_scale`` multiplies row i of the product first (the folded RMSNorm).
-    ``cus``: CUs the launch may use (the split-K factor is sized for them)."""
+    ``cus``: CUs the launch may use (the split-K factor is sized for them);
+    ``splits`` > 0 forces the split-K factor (measurements)."""
     _check(x, "x")
     _check(w, "w")
     _check(out, "out")
@@ -368,7 +370,9 @@ def skinny(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, row_sc
     want = (M, N // 2) if epi == SK_SWIGLU else (M, N)
     if tuple(out.shape) != want:
         raise ValueError(f"skinny: out shape {tuple(out.shape)} != {want}")
-    S = skinny_splits(N, K, cus, M)
+    S = splits or skinny_splits(N, K, cus, M)
+    if K % (128 * S):
+        raise ValueError(f"skinny: K={K} does not split {S} ways in 128-deep steps")
     stream = torch.cuda.current_stream(x.device).cuda_stream
     key = (x.device.type, x.device.index, stream)
     need = S * M * N
