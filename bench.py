@@ -65,13 +65,13 @@ def parse(argv=None):
                     help="how realtime requests are served (backend.realtime_mode): off = in the serving steps, "
                          "cap = --realtime-step-tokens, micro = realtime micro-forwards over their own slot pool on "
                          "their own stream; '' = cap if --realtime-step-tokens > 0 else off")
-    ap.add_argument("--micro-slots", type=int, default=64, help="micro mode: KV slots of the realtime pool")
-    ap.add_argument("--micro-inflight", type=int, default=4, help="micro mode: micro-forwards queued ahead")
+    ap.add_argument("--micro-slots", type=int, default=96, help="micro mode: KV slots of the realtime pool")
+    ap.add_argument("--micro-inflight", type=int, default=1, help="micro mode: micro-forwards queued ahead")
     ap.add_argument("--micro-budget", type=int, default=512, help="micro mode: tokens per micro-forward")
     ap.add_argument("--micro-stream", default="partition", choices=["high", "same", "partition"],
                     help="micro mode: a high-priority HIP stream of their own, the serving stream, or a CU "
                          "partition of the chip of their own (--micro-cus; the serving steps get the rest)")
-    ap.add_argument("--micro-cus", type=int, default=32, help="micro partition: CUs of the realtime partition")
+    ap.add_argument("--micro-cus", type=int, default=64, help="micro partition: CUs of the realtime partition")
     ap.add_argument("--no-micro-graph", action="store_true",
                     help="micro mode: launch decode micro-forwards kernel by kernel instead of replaying HIP graphs")
     ap.add_argument("--gen-tokens", type=int, default=4)

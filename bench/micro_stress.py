@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--stream", default="high", choices=["high", "same", "partition"])
-    ap.add_argument("--micro-cus", type=int, default=32)
+    ap.add_argument("--micro-cus", type=int, default=64)
     ap.add_argument("--micro-gemm", default="hip", choices=["hip", "rocblas"])
     ap.add_argument("--budget", type=int, default=4096)
     ap.add_argument("--slots", type=int, default=1536)
@@ -35,7 +35,7 @@ def main() -> int:
     ap.add_argument("--mode", default="micro", choices=["micro", "off"])
     ap.add_argument("--seconds", type=float, default=40.0)
     ap.add_argument("--rt-rate", type=float, default=560.0)
-    ap.add_argument("--micro-inflight", type=int, default=4)
+    ap.add_argument("--micro-inflight", type=int, default=1)
     ap.add_argument("--step-timeout", type=float, default=15.0)
     ap.add_argument("--report-s", type=float, default=5.0)
     ap.add_argument("--no-graph", action="store_true", help="decode micro-forwards launched eagerly (no HIP graphs)")

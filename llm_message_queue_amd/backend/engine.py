@@ -146,8 +146,8 @@ class BackendEngine:
                  split_qkv: bool = False, fused_mlp=None, fused_qkv=None, row_scale_norm: bool = True,
                  fused_head=None, fused_resid=None, prune_last: bool = True, step_timeout_s: float = 60.0,
                  realtime_step_tokens: int = 0, fused_rms=None, realtime_mode: str = "",
-                 micro_slots: int = 64, micro_budget: int = 512, micro_inflight: int = 4,
-                 micro_stream: str = "partition", micro_cus: int = 32, micro_gemm: str = "hip",
+                 micro_slots: int = 96, micro_budget: int = 512, micro_inflight: int = 1,
+                 micro_stream: str = "partition", micro_cus: int = 64, micro_gemm: str = "hip",
                  library_gemm: bool = False, micro_graph: bool = True):
         self.cfg = model_cfg
         # a queued forward older than this raises BackendHung (0 = wait forever)
@@ -216,6 +216,10 @@ class BackendEngine:
             self.main_stream, self.rt_stream, big_cus = partition_streams(self.device, self.micro_cus)
             from ..ops import gemm as _G
             _G.EFFECTIVE_CUS[self.device.index if self.device.index is not None else 0] = big_cus
+            # serving steps of whole waves on the remaining CUs: 16 row tiles
+            # per 256 CUs (4,096 tokens on the chip, 3,072 on 192 CUs --
+            # profiles/r6_token_budget_sweep_1gpu.jsonl, r6_realtime_modes.md)
+            self.token_budget = max(min(self.token_budget, 16 * big_cus), slots)
         self.micro_stream = micro_stream if self.micro else ""
         # the micro-forwards' GEMMs on a CU partition: "hip" = the hand-written
         # kernels (split-K small steps), "rocblas" = the library through

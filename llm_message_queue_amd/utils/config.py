@@ -318,10 +318,10 @@ class BackendConfig:
     # "cap" if realtime_step_tokens > 0 else "off".  docs/performance.md
     # "Realtime modes" has the measured trade-off.
     realtime_mode: str = ""
-    micro_slots: int = 64              # micro mode: KV slots of the realtime pool
-    micro_inflight: int = 4            # micro mode: micro-forwards queued ahead on their stream
+    micro_slots: int = 96              # micro mode: KV slots of the realtime pool
+    micro_inflight: int = 1            # micro mode: micro-forwards queued ahead on their stream
     micro_stream: str = "partition"    # micro mode: "partition" (own CU partition; the best measured), "high", "same"
-    micro_cus: int = 32                # micro partition: CUs of the realtime partition (a multiple of 8)
+    micro_cus: int = 64                # micro partition: CUs of the realtime partition (a multiple of 8)
     micro_gemm: str = "hip"            # micro partition: "hip" (hand-written) or "rocblas" GEMMs
     library_gemm: bool = False         # True: hipBLASLt for the sub-wave o / down and small heads
     micro_graph: bool = True           # micro mode: decode micro-forwards replay HIP graphs
