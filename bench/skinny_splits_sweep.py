@@ -33,19 +33,29 @@ def main() -> int:
         torch.cuda.synchronize()
         return a.elapsed_time(b) / reps * 1e3
 
-    shapes = {"qkv": (6144, 4096, G.SK_STORE), "o": (4096, 4096, G.SK_RESID), "down": (4096, 14336, G.SK_RESID)}
+    only = os.environ.get("SWEEP_ONLY", "")
+    shapes = {"qkv": (6144, 4096, G.SK_STORE), "o": (4096, 4096, G.SK_RESID), "down": (4096, 14336, G.SK_RESID),
+              "gate_up": (28672, 4096, G.SK_SWIGLU)}
+    if only:
+        shapes = {k: v for k, v in shapes.items() if k in only.split(",")}
     for name, (N, K, epi) in shapes.items():
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
         for M in (96, 128, 165, 200, 256):
             x = torch.randn(M, K, device=dev).to(torch.bfloat16)
-            o = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
+            o = torch.zeros(M, N // 2 if epi == G.SK_SWIGLU else N, device=dev, dtype=torch.bfloat16)
             row = {"gemm": name, "M": M, "default_S": G.skinny_splits(N, K, cus, M)}
             for S in (1, 2, 4, 8, 16):
                 if K % (128 * S) or K // S < 256:
                     continue
                 row[f"S{S}_us"] = round(timed(lambda: G.skinny(x, w, o, epi, cus=cus, splits=S)), 1)
-            row["hipblaslt_us"] = round(timed(lambda: o.addmm_(x, w.t()) if epi == G.SK_RESID
-                                              else torch.mm(x, w.t(), out=o)), 1)
+            if epi == G.SK_SWIGLU:
+                wp = G.swiglu_permute(w)
+                row["tiles_split_us"] = round(timed(lambda: G.gemm_swiglu(x, wp, o, split_cus=cus)), 1)
+                big = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+                row["hipblaslt_us"] = round(timed(lambda: torch.mm(x, w.t(), out=big)), 1)
+            else:
+                row["hipblaslt_us"] = round(timed(lambda: o.addmm_(x, w.t()) if epi == G.SK_RESID
+                                                  else torch.mm(x, w.t(), out=o)), 1)
             print(json.dumps(row), flush=True)
     return 0
 
