@@ -169,18 +169,19 @@ def test_two_ranks_realtime_on_micro_pools_fakecomm():
 
 
 @pytest.mark.gpu
-def test_micro_decode_graph_replays_match_eager_gpu():
+@pytest.mark.parametrize("stream", ["partition", "high"])
+def test_micro_decode_graph_replays_match_eager_gpu(stream):
     """Decode-only micro-forwards replayed from HIP graphs (row buckets,
     padding rows on the scratch slot) produce the same greedy ids as the
     same micro-forwards launched kernel by kernel, and the serving pool's
     results are untouched."""
     dev = torch.device("cuda", 0)
-    eager = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream="partition",
+    eager = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream=stream,
                     micro_graph=False)
     eager.warm_shapes([1, 8, 64])
     a = _serve(eager, _requests(24, seed=9, gen=6))
     eager.close()
-    graph = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream="partition")
+    graph = _engine("micro", device=dev, impl="hip", slots=16, budget=64, micro_stream=stream)
     graph.warm_shapes([1, 8, 64])
     assert graph.micro_graph and graph._mg
     b = _serve(graph, _requests(24, seed=9, gen=6))
