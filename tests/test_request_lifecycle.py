@@ -14,6 +14,7 @@ removable queue type there, a 501 stub), ``DELETE /messages/:id``
 (`docs/api.md:240-261`), the retry path `internal/priorityqueue/worker.go:202-239`.
 CPU engines on the fp32 reference ops; multi-rank cases run FakeComm ranks in
 threads."""
+import random
 import threading
 import time
 
@@ -485,3 +486,79 @@ def test_random_lifecycles_end_balanced(ops, two):
     assert c["submitted"] == len(msgs) == (c["completed"] + c["cancelled"] + c["retry_exhausted"] + c["expired"]
                                            + c["rejected"] + len(dequeued))
     _assert_clean(gws)
+
+# ---------------------------------------------------------------------- four ranks, seeded
+@pytest.mark.parametrize("seed", [3, 15, 43])
+def test_four_ranks_random_lifecycles_end_balanced(seed):
+    """Four FakeComm ranks with engines of 1-4 slots, every rank submitting
+    (30 % of the turns in 6 conversations: affinity, history rows, KV
+    moves), cancels on the submitting rank, short timeouts, evacuations with
+    and without failure, and API-thread dequeues between a rank's published
+    load and its pop: every request ends exactly once on its origin, an
+    acknowledged cancel never completes, every map and counter drains.
+    (Seeds 0-59 were run while writing it; three stay in the suite.)"""
+    _four_rank_run(seed)
+
+
+def _four_rank_run(seed, W=4, steps=120):
+    rnd = random.Random(seed)
+    comms = FakeComm.make(W, timeout_s=20)
+    gs = [_gw(slots=rnd.choice([1, 2, 3, 4]), comm=comms[r], backoff_ms=5, max_retries=1, gen_tokens=5) for r in range(W)]
+    gws = [g for g, _e, _d in gs]
+    wl = Workload(seed=seed)
+    msgs = {r: [] for r in range(W)}
+    armed = {r: [0] for r in range(W)}
+    dequeued = set()
+    for r, g in enumerate(gws):
+        pop0 = g.qm.pop_tiers
+        def racing(*a, _g=g, _r=r, _pop=pop0, **kw):
+            while armed[_r][0] > 0:
+                armed[_r][0] -= 1
+                for m in msgs[_r]:
+                    if m.lc == QUEUED and id(m) not in dequeued and _g.qm.remove_message(m.queue_name, m):
+                        dequeued.add(id(m)); break
+            return _pop(*a, **kw)
+        g.qm.pop_tiers = racing
+    cancelled = []
+    for _ in range(steps):
+        op = rnd.random()
+        r = rnd.randrange(W)
+        g = gws[r]
+        if op < 0.35:
+            new = wl.make(rnd.randint(1, 4))
+            for m in new:
+                if rnd.random() < 0.3:
+                    m.conversation_id = f"c{rnd.randrange(6)}"
+            msgs[r].extend(new); g.submit(new)
+        elif op < 0.65:
+            _tick_all(gws, rnd.randint(1, 3))
+        elif op < 0.75 and msgs[r]:
+            m = rnd.choice(msgs[r])
+            if m.lc != NONE:
+                cancelled.append((m, g.request_cancel(m)))
+        elif op < 0.82 and msgs[r]:
+            rnd.choice(msgs[r]).timeout = 2_000_000
+        elif op < 0.88:
+            g.set_healthy(False, "stress", failure=rnd.random() < 0.5); g.set_healthy(True)
+        elif op < 0.95:
+            armed[r][0] += 1
+        else:
+            time.sleep(0.002)
+    for a in armed.values():
+        a[0] = 0
+    allm = [m for r in range(W) for m in msgs[r]]
+    for _ in range(1500):
+        _tick_all(gws)
+        if all(m.lc == NONE for m in allm) and all(g.engine.inflight() == 0 for g in gws):
+            break
+        time.sleep(0.001)
+    assert all(m.lc == NONE for m in allm), RequestTable.census(allm)
+    for m, f in cancelled:
+        if f.done() and f.result() != "":
+            assert m.status == MessageStatus.CANCELLED, (m.id, f.result(), m.status)
+    for r, g in enumerate(gws):
+        c = g.counters
+        ded = sum(1 for m in msgs[r] if id(m) in dequeued)
+        assert c["submitted"] == len(msgs[r]) == c["completed"] + c["cancelled"] + c["retry_exhausted"] + c["expired"] + c["rejected"] + ded, (r, dict(c), ded)
+    _assert_clean(gws)
+    return sum(len(v) for v in msgs.values()), len(dequeued), len(cancelled)
