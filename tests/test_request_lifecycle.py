@@ -516,7 +516,8 @@ def _four_rank_run(seed, W=4, steps=120):
                 armed[_r][0] -= 1
                 for m in msgs[_r]:
                     if m.lc == QUEUED and id(m) not in dequeued and _g.qm.remove_message(m.queue_name, m):
-                        dequeued.add(id(m)); break
+                        dequeued.add(id(m))
+                        break
             return _pop(*a, **kw)
         g.qm.pop_tiers = racing
     cancelled = []
@@ -529,7 +530,8 @@ def _four_rank_run(seed, W=4, steps=120):
             for m in new:
                 if rnd.random() < 0.3:
                     m.conversation_id = f"c{rnd.randrange(6)}"
-            msgs[r].extend(new); g.submit(new)
+            msgs[r].extend(new)
+            g.submit(new)
         elif op < 0.65:
             _tick_all(gws, rnd.randint(1, 3))
         elif op < 0.75 and msgs[r]:
@@ -539,7 +541,8 @@ def _four_rank_run(seed, W=4, steps=120):
         elif op < 0.82 and msgs[r]:
             rnd.choice(msgs[r]).timeout = 2_000_000
         elif op < 0.88:
-            g.set_healthy(False, "stress", failure=rnd.random() < 0.5); g.set_healthy(True)
+            g.set_healthy(False, "stress", failure=rnd.random() < 0.5)
+            g.set_healthy(True)
         elif op < 0.95:
             armed[r][0] += 1
         else:
@@ -559,6 +562,7 @@ def _four_rank_run(seed, W=4, steps=120):
     for r, g in enumerate(gws):
         c = g.counters
         ded = sum(1 for m in msgs[r] if id(m) in dequeued)
-        assert c["submitted"] == len(msgs[r]) == c["completed"] + c["cancelled"] + c["retry_exhausted"] + c["expired"] + c["rejected"] + ded, (r, dict(c), ded)
+        ended = c["completed"] + c["cancelled"] + c["retry_exhausted"] + c["expired"] + c["rejected"]
+        assert c["submitted"] == len(msgs[r]) == ended + ded, (r, dict(c), ded)
     _assert_clean(gws)
     return sum(len(v) for v in msgs.values()), len(dequeued), len(cancelled)
