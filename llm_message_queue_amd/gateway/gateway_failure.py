@@ -364,7 +364,19 @@ class FailureMixin:
         self.table.local.pop(m.handle, None)
         self.table.remote_out.pop(m.handle, None)
         self.table.move(m, QUEUED)
-        self.qm.requeue_after_failure(m.queue_name, m)
+        if not self.qm.requeue_after_failure(m.queue_name, m):
+            # its tier is full (overload): it cannot go back -- dead-letter it
+            # rather than raise into the serve loop (found by the round-6
+            # 4-rank overload soak, a fatal 'queue is full')
+            m.status = MessageStatus.FAILED
+            self.table.end(m)
+            self.counters["rejected"] += 1
+            if self.dead_letter is not None:
+                try:
+                    self.dead_letter.push(m, "tier full on requeue", m.queue_name)
+                except QueueError:
+                    self.log.warning("dead-letter queue full; failed request dropped", message_id=m.id)
+            return
         if self.world > 1:
             self._pin(m, +1)
 

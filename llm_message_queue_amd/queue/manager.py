@@ -24,7 +24,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 from ..models.message import Message, QueueStats, priority_name, now_ns
 from ..utils.logging import get_logger
 from ..utils.metrics import QueueMetrics, default_metrics
-from .core import MultiLevelQueue, QueueError, QueueNotFound
+from .core import MultiLevelQueue, QueueError, QueueFull, QueueNotFound
 
 
 @dataclass
@@ -250,14 +250,22 @@ class QueueManager:
             self.metrics.processing.labels(self.name, queue_name, p).dec()
             self.metrics.failed.labels(self.name, queue_name, p).inc()
 
-    def requeue_after_failure(self, queue_name: str, message: Message) -> None:
-        """A popped message goes back (retry): processing-- then push."""
+    def requeue_after_failure(self, queue_name: str, message: Message) -> bool:
+        """A popped message goes back (retry): push, then processing--.
+        False when its tier is full (an overloaded queue): the message is
+        counted failed instead, and the caller decides where it goes (the
+        gateway dead-letters it) -- a retry must not raise into a serve loop."""
+        try:
+            self.push_message(queue_name, message)
+        except QueueFull:
+            self.fail_message(queue_name, message.id, None, message.priority, quiet=True)
+            return False
         if queue_name in self._queues:
             self.mlq.unprocess(queue_name)
             if self.metrics:
                 self.metrics.processing.labels(self.name, queue_name,
                                                priority_name(message.priority)).dec()
-        self.push_message(queue_name, message)
+        return True
 
     # ------------------------------------------------------------- stats
     def get_queue_stats(self, queue_name: str) -> QueueStats:

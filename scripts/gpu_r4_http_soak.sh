@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 R=${RANKS:-2}; RATE=${RATE:-4500}; D=${DURATION:-120}
-timeout -k 10 $((D + 240)) python bench/http_load.py --spawn multirank --ranks $R --gpu --bench-config --client native \
+timeout -k 10 $((D + 240)) python bench/http_load.py --spawn multirank --ranks $R --gpu --bench-config --slots ${SLOTS:-1536} --client native \
   --workload --procs 2 --conns 16 --threads 2 --rate $RATE --duration $D --warmup 10 --admin-churn 5 \
   --cancel-churn ${CANCEL:-0} --dialog-frac ${DIALOG:-0} --dialog-convs ${CONVS:-5000} \
   --timeout-frac ${TOFRAC:-0} --timeout-val ${TOVAL:-150ms} --fault-cycle ${FAULTS:-0} \

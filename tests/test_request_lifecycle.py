@@ -487,6 +487,37 @@ def test_random_lifecycles_end_balanced(ops, two):
                                            + c["rejected"] + len(dequeued))
     _assert_clean(gws)
 
+def test_retry_into_a_full_tier_is_dead_lettered_not_raised():
+    """A backend failure sends a request to retry; by the time its backoff
+    ends its tier is full (overload).  The requeue is refused: the request is
+    dead-lettered and counted rejected instead of raising QueueFull into the
+    serve loop (a fatal exit in the round-6 4-rank overload soak)."""
+    c = _cfg()
+    c.queue.default_max_size = 3
+    eng = BackendEngine(MICRO, slots=1, max_ctx=64, token_budget=128, device="cpu", impl="ref", seed=7)
+    dlq = DeadLetterQueue()
+    gw = Gateway(c, engine=eng, use_gpu_preprocess=False, prompt_cap=8, gen_tokens=30, dead_letter=dlq)
+    gw.attach_retry_queue(DelayedQueue(), FixedBackoff(5_000_000, 3))
+    first = Message(id="first", content="please summarise this", priority=3, user_id="u")
+    gw.submit([first])
+    _tick_all([gw], 2)
+    assert first.lc == 6                                      # LOCAL: running in the one slot
+    gw.set_healthy(False, "test", failure=True)               # it goes to the retry backoff
+    rest = [Message(id=f"r{i}", content="please summarise this", priority=3, user_id="u") for i in range(3)]
+    gw.submit(rest)
+    gw.ingest()                                               # the tier (3) is now full
+    time.sleep(0.02)
+    _tick_all([gw], 3)                                        # backoff over: the requeue is refused
+    assert first.status == MessageStatus.FAILED and first.lc == NONE
+    assert dlq.size() == 1 and gw.counters["rejected"] == 1
+    gw.set_healthy(True)
+    _settle([gw], rest)
+    assert all(m.status == MessageStatus.COMPLETED for m in rest)
+    cc = gw.counters
+    assert cc["submitted"] == 4 == cc["completed"] + cc["rejected"]
+    _assert_clean([gw])
+
+
 # ---------------------------------------------------------------------- four ranks, seeded
 @pytest.mark.parametrize("seed", [3, 15, 43])
 def test_four_ranks_random_lifecycles_end_balanced(seed):
