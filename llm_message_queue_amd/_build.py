@@ -132,6 +132,15 @@ def build_one(name: str, t: dict, verbose: bool = False) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"native build of {name} failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    # a kernel whose host-side stub clang silently skipped (e.g. a target
+    # builtin inside a lambda of a kernel template) links fine and fails only
+    # at import on the GPU box: refuse it here
+    if shutil.which("nm"):
+        und = subprocess.run(["nm", "-D", "--undefined-only", tmp], capture_output=True, text=True).stdout
+        stubs = [ln.split()[-1] for ln in und.splitlines() if "__device_stub__" in ln]
+        if stubs:
+            os.unlink(tmp)
+            raise RuntimeError(f"native build of {name}: kernel stubs missing (host side dropped them): {stubs[:4]}")
     os.replace(tmp, out)
     return out
 
