@@ -200,14 +200,15 @@ def _timed_out_into_backoff(gw, msgs):
 
 
 def test_cancel_in_retry_backoff():
-    gw, eng, done = _gw(backoff_ms=300)
+    # a backoff long enough that a loaded CI host cannot outrun it before the cancel
+    gw, eng, done = _gw(backoff_ms=1500)
     msgs = Workload(seed=7).make(3)
     _timed_out_into_backoff(gw, msgs)
     assert gw.retry_queue.size() == 1
     f = gw.request_cancel(msgs[0])
     gw.tick()
     assert f.result(timeout=1) == "cancelled" and gw.retry_queue.size() == 0
-    time.sleep(0.35)                                 # the backoff would be over now
+    time.sleep(1.6)                                  # the backoff would be over now
     _settle([gw], msgs)
     assert msgs[0].status == MessageStatus.CANCELLED and gw.counters["retried"] == 1
     assert gw.counters["dispatched"] == 3, "re-dispatched after the cancel"
