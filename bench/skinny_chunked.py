@@ -37,9 +37,13 @@ def main() -> int:
         return a.elapsed_time(b) / reps * 1e3
 
     shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+    only = os.environ.get("SK_GEMMS", "")
+    if only:
+        shapes = {k: v for k, v in shapes.items() if k in only.split(",")}
+    ms = tuple(int(m) for m in os.environ.get("SK_MS", "48,65,128,165,200,256").split(","))
     for name, (N, K) in shapes.items():
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
-        for M in (48, 65, 128, 165, 200, 256):
+        for M in ms:
             x = torch.randn(M, K, device=dev).to(torch.bfloat16)
             row = {"gemm": name, "M": M, "N": N, "K": K}
             if name == "o" or name == "down":

@@ -513,12 +513,12 @@ static void kv_move(uintptr_t table, int layers, int slots, int slot, int n, int
   check_launch();
 }
 
-// ---------------------------------------------------------------------- skinny GEMM (M <= 256)
+// ---------------------------------------------------------------------- skinny GEMM (M <= SK_MAX_M)
 // C (+)= A . W^T for the small steps (skinny_kernels.h): split-K partials into
 // ws [S][M][N] fp32, then the finalize kernel (row scale, epilogue, bf16).
 static void skinny_gemm(uintptr_t a, uintptr_t w, uintptr_t c, int M, int N, int K, int epi, uintptr_t rs,
                         uintptr_t ws, int nsplit, uintptr_t stream) {
-  require(M >= 1 && M <= SK_MAX_M, "skinny_gemm: M must be in [1, 256]");
+  require(M >= 1 && M <= SK_MAX_M, "skinny_gemm: M must be in [1, SK_MAX_M]");
   require(N % SK_NB == 0, "skinny_gemm: N must be a multiple of 128");
   require(nsplit >= 1 && K % (SK_KS * nsplit) == 0, "skinny_gemm: K must be a multiple of 128 * S");
   require(epi == SK_EPI_STORE || epi == SK_EPI_RESID || epi == SK_EPI_SWIGLU, "skinny_gemm: unknown epilogue");

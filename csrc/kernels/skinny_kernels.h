@@ -47,7 +47,7 @@ enum { SK_EPI_STORE = 0, SK_EPI_RESID = 1, SK_EPI_SWIGLU = 2 };
 // of A (MT = 8; a chunk's A rows staged in two 64-row groups).  Every chunk re-reads its column block's weights, so the nm
 // chunks of a column block run on one XCD back to back (block b -> XCD b % 8:
 // chunk fastest within the XCD's share) and the repeats come from its L2.
-constexpr int SK_MAX_M = 256;
+constexpr int SK_MAX_M = 1024;           // up to 8 chunks (o / down at mid-size steps)
 
 template <int MT>
 __global__ void __launch_bounds__(256)

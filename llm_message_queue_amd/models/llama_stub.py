@@ -328,9 +328,11 @@ class LlamaStub:
         resid_o = small or nolib or tiles_ok
         rms = tiles_ok and self.fused_rms and G.RESID_EPI == G.EPI_RESID_LDS and not small
 
-        # skinny: o / down up to SKINNY_PROJ_MAX_M rows, gate/up (N = 28,672:
-        # enough tiles to fill the chip) only up to SKINNY_MAX_M
-        skinny = (small or nolib) and M <= (G.SKINNY_MAX_M if small else G.SKINNY_PROJ_MAX_M) \
+        # skinny: o / down up to SKINNY_RESID_MAX_M rows (past 256 its 128-row
+        # chunks still beat 256x256 tiles whose 32-64 tiles leave most CUs
+        # idle: profiles/r6_skinny_mid_m.jsonl), gate/up (N = 28,672: enough
+        # tiles to fill the chip) only up to SKINNY_MAX_M
+        skinny = (small or nolib) and M <= (G.SKINNY_MAX_M if small else G.SKINNY_RESID_MAX_M) \
             and self.row_scale_norm and self.fused_mlp
         skinny_gu = skinny and M <= G.SKINNY_MAX_M
 

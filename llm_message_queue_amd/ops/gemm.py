@@ -331,8 +331,9 @@ def qkv_rope(x: torch.Tensor, wqkv: torch.Tensor, pos: torch.Tensor, slot: torch
 
 # ---------------------------------------------------------------------- skinny small steps
 SKINNY_MAX_M = 64              # the model's gate/up on the skinny kernel up to this many rows
-SKINNY_PROJ_MAX_M = 256        # ... and qkv / o / down up to this many (profiles/r6_skinny_chunked.jsonl)
-SKINNY_CHUNKED_MAX_M = 256     # the kernel itself: 128-row chunks of A up to this many rows
+SKINNY_PROJ_MAX_M = 256        # ... and qkv up to this many (profiles/r6_skinny_chunked.jsonl)
+SKINNY_RESID_MAX_M = 512       # ... and o / down (into the residual) up to this many (profiles/r6_skinny_mid_m.jsonl)
+SKINNY_CHUNKED_MAX_M = 1024    # the kernel itself: 128-row chunks of A up to this many rows
 SK_STORE, SK_RESID, SK_SWIGLU = 0, 1, 2
 _SKINNY_WS = {}
 
@@ -354,7 +355,7 @@ def skinny_splits(N: int, K: int, cus: int, M: int = 1) -> int:
 
 def skinny(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, epi: int, row_scale=None, cus: int = 32,
            splits: int = 0):
-    """``out`` (+)= ``x`` [M <= 256][K] . ``w`` [N][K]^T on the skinny kernel
+    """``out`` (+)= ``x`` [M <= 1024][K] . ``w`` [N][K]^T on the skinny kernel
     (``csrc/kernels/skinny_kernels.h``): SK_STORE (out [M][N]), SK_RESID
     (out += ..., one rounding), SK_SWIGLU (``w`` swiglu-permuted, out [M][N/2]);
     ``row_scale`` multiplies row i of the product first (the folded RMSNorm).

@@ -531,7 +531,7 @@ def test_small_step_forward_matches_the_serving_path():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M", [1, 17, 40, 64, 65, 128, 129, 200, 256])
+@pytest.mark.parametrize("M", [1, 17, 40, 64, 65, 128, 129, 200, 256, 300, 640, 1000])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 14336), (6144, 512)])
 def test_skinny_gemm_matches_fp32(M, N, K):
     """The skinny kernel (M <= 64 in one block; up to 256 rows in 128-row
@@ -598,7 +598,7 @@ def test_library_free_residual_matches_fp32(T, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T", [1, 40, 165, 256, 300, 900])
+@pytest.mark.parametrize("T", [1, 40, 165, 256, 300, 512, 513, 900])
 def test_library_free_model_matches_the_default_routing(T):
     """``library_gemm=False`` (no hipBLASLt call in the forward) gives the
     same hidden rows as the default routing to bf16 tolerance and the same
